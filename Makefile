@@ -1,0 +1,22 @@
+# Build libpps_hip.so (gfx950) and the oracle's C restatement.
+# `python -c "import __graft_entry__ as g; g.build()"` drives the same recipe.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+SRCS := $(wildcard pps_amd/csrc/*.hip)
+OBJS := $(patsubst pps_amd/csrc/%.hip,build/%.o,$(SRCS))
+LIB := pps_amd/libpps_hip.so
+
+all: $(LIB)
+
+build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp include/pps_abi.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

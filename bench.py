@@ -1,0 +1,255 @@
+"""Benchmark: PPS re-ID inference + retrieval on MI355X (BASELINE.json metric
+"gallery images/sec + distmat GB/s; mAP/Rank-1 parity on Market-1501",
+workload configs[1]: Market-1501 ResNet-50 PPS, 1xMI355X, batch 64,
+3368q x 15913g L2 distmat).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step = one batch of 64 synthetic Market-sized images (uint8 BGR 128x64,
+resident in HBM) through the whole feature path: preprocess (mean-subtract +
+bicubic to 384x128) -> ResNet-50/stride-1 res5 -> part power set -> 31 heads
+-> L2 normalise.  value = images/s over all ranks (weak scaling: 64 per rank
+per step).  The retrieval stage (distance matrix + count-based mAP/CMC at
+Market sizes; gallery-sharded across ranks with an all-gather of queries) is
+timed after the step loop and reported as distmat_GBps etc.
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU, RCCL.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA)
+PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
+Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--batch', type=int, default=64)
+    p.add_argument('--no-graph', action='store_true', help='eager launches (no hipGraph)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--dist-reps', type=int, default=5)
+    return p.parse_args()
+
+
+def market_cfg():
+    from pps_amd import config
+    cfg = config.cfg
+    cfg.MODEL.NUM_CLASSES = 752
+    cfg.MODEL.USE_BN = True
+    cfg.RESNETS.RES5_STRIDE = 1
+    cfg.REID.SCALE = (128, 384)
+    cfg.REID.BPM_STRIP_NUM = 5
+    cfg.REID.BPM_DIM = 128
+    cfg.REID.NORMALIZE_FEATURE = True
+    cfg.REID.MAX_AVE_FEATURE = True
+    cfg.REID.RERANK = False
+    return cfg
+
+
+def synth_features(n, ids, gen, noise=4.0, n_ids=750):
+    """SURVEY §8(d) recipe on the device: centroid[id] + noise*N(0,1), L2 norm."""
+    cent = torch.randn((n_ids + 1, D_FEAT), generator=gen, device='cuda')
+    x = cent[ids] + noise * torch.randn((n, D_FEAT), generator=gen, device='cuda')
+    return (x / x.norm(dim=1, keepdim=True)).contiguous()
+
+
+def retrieval_stage(rank, world, reps):
+    """Distance matrix + mAP/CMC at Market sizes.  Gallery sharded over ranks,
+    queries all-gathered.  Returns timings (ms) and scores."""
+    from pps_amd import distributed as pdist
+    rng = np.random.RandomState(0)
+    qid = rng.randint(1, 751, Q_MARKET)
+    gid = np.concatenate([rng.randint(1, 751, G_MARKET - 2793), np.zeros(2793, int)])
+    qcam = rng.randint(1, 7, Q_MARKET)
+    gcam = rng.randint(1, 7, G_MARKET)
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(0)
+    # same global features on every rank (seeded), each rank keeps its shards
+    allf = synth_features(Q_MARKET + G_MARKET,
+                          torch.from_numpy(np.concatenate([qid, gid])).cuda(), gen)
+    qsl = pdist.shard_range(Q_MARKET, rank, world)
+    gsl = pdist.shard_range(G_MARKET, rank, world)
+    q_local = allf[qsl[0]:qsl[1]].contiguous()
+    g_local = allf[Q_MARKET + gsl[0]:Q_MARKET + gsl[1]].contiguous()
+    del allf
+    ev = pdist.ShardedEvaluator(qid, qcam, gid, gcam, rank, world)
+    # warm-up
+    res = ev.run(q_local, g_local)
+    torch.cuda.synchronize()
+    t_dist, t_rank, t_total = [], [], []
+    for _ in range(reps):
+        pdist.barrier(world)
+        torch.cuda.synchronize()
+        res = ev.run(q_local, g_local, timed=True)
+        torch.cuda.synchronize()
+        t_dist.append(res['t_distmat_ms'])
+        t_rank.append(res['t_rank_ms'])
+        t_total.append(res['t_total_ms'])
+    out = dict(distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
+               retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
+               cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
+               cmc10=float(res['cmc'][9]), G_local=gsl[1] - gsl[0])
+    return out
+
+
+def conv_roofline(m, x):
+    """Per-launch HIP events over one forward (same stream as the kernels)."""
+    timer = []
+    torch.cuda.synchronize()
+    m.forward(x, timer=timer)
+    torch.cuda.synchronize()
+    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in ('conv', 'heads'))
+    conv_flops = sum(f for _, op, f, _, _ in timer if op in ('conv', 'heads'))
+    n_launch = sum(1 for _, op, _, _, _ in timer if op in ('conv', 'heads'))
+    per = {}
+    for name, op, f, e0, e1 in timer:
+        per[name] = (op, f, e0.elapsed_time(e1))
+    achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+    return dict(bound='mfma', achieved=round(achieved, 2), peak=PEAK_FP32_MFMA_TFLOPS,
+                unit='TFLOP/s', frac=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (85 launches/forward)',
+                launches=n_launch, flops_per_forward=conv_flops,
+                avg_launch_us=round(conv_ms * 1e3 / n_launch, 2)), per
+
+
+def cpu_baseline(blobs, dist_sample=True):
+    """Oracle (CPU restatement) timed on this host's cores: bounded sample."""
+    from oracle import evaluator as ev
+    from oracle.forward import GraphForward
+    threads = torch.get_num_threads()
+    fw = GraphForward(blobs)
+    rng = np.random.RandomState(0)
+    n_img = 4
+    x = (rng.randn(n_img, 3, 384, 128) * 50).astype(np.float32)
+    fw(x[:1])  # warm-up
+    t0 = time.time()
+    fw(x)
+    fwd_s = time.time() - t0
+    out = dict(value=round(n_img / fwd_s, 3), unit='images/s', cores=threads, kind='port',
+               sample='%d images 384x128 through oracle/forward.py (recorded reference '
+                      'graph, torch CPU fp32, %d threads)' % (n_img, threads))
+    if dist_sample:
+        qs, gs = 1024, 4096
+        q = rng.randn(qs, D_FEAT).astype(np.float32)
+        g = rng.randn(gs, D_FEAT).astype(np.float32)
+        t0 = time.time()
+        ev.compute_dist(q, g)
+        ds = time.time() - t0
+        byt = (qs + gs) * D_FEAT * 4 + qs * gs * 4
+        out['distmat_GBps'] = round(byt / ds / 1e9, 3)
+        out['distmat_sample'] = '%dx%d D=%d NumPy fp32 (reference formula)' % (qs, gs, D_FEAT)
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from pps_amd import model, ops
+    from pps_amd import distributed as pdist
+    cfg = market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=0)
+    m = model.PPSModel(blobs)
+    B = args.batch
+    H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
+    g = torch.Generator(device='cuda')
+    g.manual_seed(1234 + rank)
+    imgs = torch.randint(0, 256, (B, 128, 64, 3), generator=g, device='cuda',
+                         dtype=torch.int64).to(torch.uint8)
+    xbuf = torch.empty((B, H, W, 4), dtype=torch.float32, device='cuda')
+    feat = torch.empty((B, m.feat_dim), dtype=torch.float32, device='cuda')
+    means = cfg.PIXEL_MEANS.ravel()
+
+    def step():
+        ops.preprocess_bgr(imgs, means, (H, W), xbuf)
+        m.forward(xbuf, out=feat)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        for _ in range(2):
+            graph.replay()
+        torch.cuda.synchronize()
+    run = graph.replay if graph is not None else step
+
+    pdist.barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    pdist.barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.max_over_ranks(elapsed, world)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * B * args.steps / elapsed
+
+    roof, per_layer = conv_roofline(m, xbuf)
+    ret = retrieval_stage(rank, world, args.dist_reps)
+    dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
+    dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
+    dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
+    # whole-job distmat GB/s: all ranks' shards / the slowest rank's time
+    dist_ms_max = pdist.max_over_ranks(ret['distmat_ms'], world)
+    total_bytes = (Q_MARKET + G_MARKET) * D_FEAT * 4 + Q_MARKET * G_MARKET * 4
+    out = {
+        'metric': 'gallery images/sec + distmat GB/s; mAP/Rank-1 parity on Market-1501',
+        'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic (uint8 images, seeded weights of the PPS R-50 architecture)',
+        'config': {'workload': 'Market-1501 ResNet-50 PPS (stride-1 res5, 31 part subsets), '
+                               'batch %d/GPU, 384x128, 3368q x 15913g L2 distmat' % B,
+                   'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': m.feat_dim,
+                   'parallelism': 'dp%d' % world, 'hipgraph': graph is not None},
+        'distmat_GBps': round(total_bytes / (dist_ms_max * 1e-3) / 1e9, 2),
+        'distmat_ms': round(dist_ms_max, 3),
+        'distmat_TFLOPs_per_gpu': round(dist_tflops, 2),
+        'rank_eval_ms': round(ret['rank_eval_ms'], 3),
+        'retrieval_ms': round(ret['retrieval_ms'], 3),
+        'mAP_synthetic': round(ret['mAP'], 6), 'cmc1_synthetic': round(ret['cmc1'], 6),
+        'roofline': roof,
+        'roofline_distmat': dict(bound='mfma', achieved=round(dist_tflops, 2),
+                                 peak=PEAK_FP32_MFMA_TFLOPS, unit='TFLOP/s',
+                                 frac=round(dist_tflops / PEAK_FP32_MFMA_TFLOPS, 4),
+                                 hbm_GBps=round(dist_bytes / (ret['distmat_ms'] * 1e-3) / 1e9, 2),
+                                 traffic=None, kernel='gemm_f32_kernel<128,128,2,2,EPI_DIST>'),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(blobs)
+    if rank == 0:
+        if os.environ.get('PPS_BENCH_LAYERS'):
+            with open(os.environ['PPS_BENCH_LAYERS'], 'w') as f:
+                json.dump({k: v for k, v in per_layer.items()}, f, indent=0)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

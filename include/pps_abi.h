@@ -1,0 +1,166 @@
+/*
+ * pps_abi.h -- C ABI of libpps_hip.so, the MI355X (gfx950) re-ID inference +
+ * retrieval path for PPS (shenyunhang/PPS).
+ *
+ * Conventions:
+ *   - Every buffer is caller-owned DEVICE memory (HBM), except where a
+ *     parameter is documented as host memory.  No entry point allocates,
+ *     frees or synchronises; all work is enqueued on `stream` (a hipStream_t
+ *     passed as void*; NULL = the legacy default stream), so a caller may
+ *     capture a sequence of calls into a hipGraph.
+ *   - Activations are NHWC float32.  Conv weights are packed [Cout][Kpad]
+ *     with K ordered (kh, kw, cin) and zero padded to Kpad (multiple of 16).
+ *   - Return value: PPS_OK (0) or a negative PPS_ERR_* code.  No C++
+ *     exception crosses the ABI.  pps_last_error() returns a thread-local,
+ *     ENFORCE-style message for the last failing call on this thread; the
+ *     Python layer raises it as RuntimeError, as Caffe2's CAFFE_ENFORCE
+ *     did (reference detectron/tests/test_zero_even_op.py:48-51).
+ *   - Re-entrant per stream; no global mutable state besides the
+ *     thread-local error string.
+ */
+#ifndef PPS_ABI_H_
+#define PPS_ABI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPS_OK 0
+#define PPS_ERR_INVALID_ARG -1   /* shape / pointer / alignment check failed */
+#define PPS_ERR_UNSUPPORTED -2   /* valid request outside what is built     */
+#define PPS_ERR_LAUNCH -3        /* hipGetLastError after launch != success  */
+#define PPS_ERR_CAPACITY -4      /* a fixed-capacity buffer was too small    */
+
+#define PPS_METRIC_EUCLIDEAN 0   /* sqrt(max(|q|^2 + |g|^2 - 2 q.g, 0))      */
+#define PPS_METRIC_SQEUCLIDEAN 1 /* max(|q|^2 + |g|^2 - 2 q.g, 0)            */
+#define PPS_METRIC_COSINE 2      /* 1 - q.g / (max(|q|,eps) max(|g|,eps))    */
+
+/* ---- library ------------------------------------------------------------ */
+int pps_abi_version(void);
+const char* pps_last_error(void);
+/* Names of the exported operator-registry entries, ';'-separated (host). */
+const char* pps_registered_ops(void);
+
+/* ---- retrieval: distance matrix ------------------------------------------
+ * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
+ * type)` (euclidean branch; cosine is defined as a true distance, the
+ * reference's cosine branch is broken).
+ * out[i*ldo + j] = metric(q[i,:], g[j,:]); q is [Q][ldq], g is [G][ldg],
+ * D valid columns, D % 4 == 0, ldq/ldg/ldo % 4 == 0, 16-B aligned pointers.
+ * FP32 MFMA (v_mfma_f32_32x32x2_f32) tiles; squared norms fused. */
+int pps_distmat(const float* q, int64_t Q, int64_t ldq,
+                const float* g, int64_t G, int64_t ldg, int D, int metric,
+                float* out, int64_t ldo, void* stream);
+
+/* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
+ * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
+ * The diagonal is exactly 0 as in the reference's difference form. */
+int pps_pairwise_distance(const float* X, int N, int D, float* Z,
+                          void* stream);
+
+/* ---- retrieval: rank / evaluation ----------------------------------------
+ * Count-based mAP/CMC (reid_dataset_evaluator.py:283-363 `cmc`, :366-439
+ * `mean_ap`): identical to sorting each row with a stable (distance, index)
+ * order, without materialising the sort.  Gallery may be a shard
+ * [g_offset, g_offset+G) of a global gallery.
+ *
+ * 1) pps_collect_positives: for each query row, list the gallery entries that
+ *    are true matches (gid == qid && gcam != qcam), as (distance, global
+ *    gallery index), in index order.  pos_cnt[q] may exceed Pmax, in which
+ *    case only Pmax entries are stored and the caller must retry larger. */
+int pps_collect_positives(const float* dist, int64_t Q, int64_t G,
+                          int64_t ldd, const int32_t* qid,
+                          const int32_t* qcam, const int32_t* gid,
+                          const int32_t* gcam, int64_t g_offset, int Pmax,
+                          float* pos_d, int32_t* pos_idx, int32_t* pos_cnt,
+                          void* stream);
+/* 2) pps_rank_counts: R positive lists ([R][Q][Pmax] entries, counts
+ *    [R][Q]) are merged and sorted per query by (distance, index) into
+ *    sorted_d [Q][R*Pmax] / sorted_idx (padding +inf / -1; pos_total[q] =
+ *    merged count); then for every valid gallery entry of
+ *    THIS shard (not same id & same cam) its distance is binned against the
+ *    sorted positives: hist[q][p] += 1 where p = first positive with
+ *    d_p >= d_i, and before[q] counts entries ordered before the first
+ *    positive.  hist / before are ADDITIVE over gallery shards (sum with an
+ *    all-reduce), and must be zeroed by the caller. */
+int pps_rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                    const int32_t* qid, const int32_t* qcam,
+                    const int32_t* gid, const int32_t* gcam, int64_t g_offset,
+                    int R, int Pmax, const float* pos_d,
+                    const int32_t* pos_idx, const int32_t* pos_cnt,
+                    float* sorted_d, int32_t* sorted_idx, int32_t* pos_total,
+                    int32_t* hist, int32_t* before, void* stream);
+/* 3) pps_ap_finalize: per query AP (sklearn >= 0.19 step-wise definition,
+ *    tie-grouped), validity flag and first-match rank from the summed
+ *    counts.  ap is float64 [Q]; first_rank int32 [Q] (-1 when invalid). */
+int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
+                    const int32_t* pos_total, const int32_t* hist,
+                    const int32_t* before, double* ap, int32_t* valid,
+                    int32_t* first_rank, void* stream);
+
+/* Stable per-row top-k (k <= 1024) of a distance matrix, ascending, ties by
+ * gallery index.  Replaces the `np.argsort(distmat, axis=1)[:, :k]` rank
+ * list (reid_dataset_evaluator.py:319,420). */
+int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k,
+             float* vals, int32_t* idx, void* stream);
+
+/* ---- feature extractor ----------------------------------------------------
+ * Implicit-GEMM convolution + test-mode SpatialBN + optional residual Sum +
+ * optional ReLU, fused (ResNet.py:246-256 stem conv, :276-333 bottleneck,
+ * :203-220 shortcut; detector.py:82-84,419-447 ConvAffine; reid_heads.py
+ * :42-76 head conv+bias+BN+ReLU via shift).
+ * y[p, co] = act(acc[p, co] * scale[co] + shift[co] (+ res[p, co])).
+ * x NHWC [N][H][W][ldx] (Cin valid channels, Cin % 4 == 0),
+ * w [Cout][Kpad], Kpad % 16 == 0, Kpad >= KH*KW*Cin,
+ * y NHWC [N][Ho][Wo][ldy] written at column offset 0. */
+int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+                      const float* w, int Cout, int Kpad, int KH, int KW,
+                      int stride, int pad, int dil, const float* scale,
+                      const float* shift, const float* residual, int relu,
+                      float* y, int Ho, int Wo, int ldy, void* stream);
+
+/* Batched variant for the 31 PPS head convs (reid_heads.py:42-79):
+ * for b in [0,B): Y[:, b*Cout:(b+1)*Cout] = relu?(X_b W_b^T * scale_b +
+ * shift_b); X_b = x + b*x_bstride ([M][K]), W_b = w + b*w_bstride
+ * ([Cout][K]), scale/shift + b*Cout, Y row stride ldy. */
+int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
+                            const float* w, int64_t w_bstride, int Cout,
+                            const float* scale, const float* shift, int relu,
+                            float* y, int ldy, int B, void* stream);
+
+/* MaxPool kernel k, stride s, pad p (padding never wins), NHWC
+ * (ResNet.py:255 `pool1`). */
+int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k,
+                  int stride, int pad, float* y, int Ho, int Wo,
+                  void* stream);
+
+/* Part power set (bpm_heads.py:18-55 + pps_heads.py:38-80): split H into
+ * `nstrip` strips of heights `splits` (HOST array), global ave + max pool per
+ * strip, then for every non-empty subset i = 1..2^S-1 (bit j => strip j):
+ * out[i-1][n][c] = mean_{j in i}(ave_j) + max_{j in i}(max_j)
+ * (max_ave = 1) or max_{j in i}(ave_j) (max_ave = 0, reference :70-76).
+ * x NHWC [N][H][W][C]; out [2^S-1][N][C]. */
+int pps_part_power_set(const float* x, int N, int H, int W, int C,
+                       const int32_t* splits, int nstrip, int max_ave,
+                       float* out, void* stream);
+
+/* Caffe2 `Normalize` along axis 1 (triplet_loss.py:17-19):
+ * y = x / max(||x||_2, 1e-12).  x, y [N][D] (may alias). */
+int pps_l2_normalize(const float* x, int64_t N, int D, float* y,
+                     void* stream);
+
+/* Image preprocessing (utils/blob.py:97-117 prep_im_for_blob,
+ * :65-94 im_list_to_blob): uint8 BGR HWC images [N][Hi][Wi][3] (device) ->
+ * subtract pixel means (HOST float[3]) -> bicubic resize (a = -0.75,
+ * half-pixel centres, border replicate, as cv2.INTER_CUBIC) to Ho x Wo ->
+ * NHWC float32 with 4 channels (4th = 0), the stem's packed layout. */
+int pps_preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi,
+                       const float* pixel_means, int Ho, int Wo, float* y,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPS_ABI_H_ */

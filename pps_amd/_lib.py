@@ -1,0 +1,90 @@
+"""ctypes binding of libpps_hip.so (the C ABI in include/pps_abi.h).
+
+This is the product path's only way to compute: there is no CPU or PyTorch
+fallback.  If the shared library is missing, `lib()` raises immediately.
+A negative status from any entry point is raised as RuntimeError carrying the
+library's ENFORCE-style message, mirroring how Caffe2's CAFFE_ENFORCE surfaced
+in Python (reference detectron/tests/test_zero_even_op.py:48-51).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libpps_hip.so')
+
+c_f32p = ctypes.c_void_p
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_ptr = ctypes.c_void_p
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    'pps_distmat': [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_int, c_int, c_ptr,
+                    c_i64, c_ptr],
+    'pps_pairwise_distance': [c_ptr, c_int, c_int, c_ptr, c_ptr],
+    'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
+                              c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
+                        c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                        c_ptr, c_ptr],
+    'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                        c_ptr],
+    'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_conv2d_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
+                          c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
+                          c_ptr, c_int, c_int, c_int, c_ptr],
+    'pps_gemm_bn_act_batched': [c_ptr, c_i64, c_int, c_int, c_ptr, c_i64, c_int, c_ptr,
+                                c_ptr, c_int, c_ptr, c_int, c_int, c_ptr],
+    'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                      c_int, c_int, c_ptr],
+    'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,
+                           c_ptr],
+    'pps_l2_normalize': [c_ptr, c_i64, c_int, c_ptr, c_ptr],
+    'pps_preprocess_bgr': [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr],
+}
+EXTRA = {
+    'pps_abi_version': ([], ctypes.c_int),
+    'pps_last_error': ([], ctypes.c_char_p),
+    'pps_registered_ops': ([], ctypes.c_char_p),
+}
+
+METRICS = {'euclidean': 0, 'sqeuclidean': 1, 'cosine': 2}
+
+_LIB = None
+
+
+def lib():
+    """Load (once) and return the configured CDLL. Raises if it is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            'libpps_hip.so not found at %s: build it with `make` or '
+            '`python -c "import __graft_entry__ as g; g.build()"`. There is no '
+            'CPU fallback on the product path.' % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    for name, (argtypes, res) in EXTRA.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+def call(name, *args):
+    """Invoke an entry point; raise RuntimeError on a negative status."""
+    L = lib()
+    status = getattr(L, name)(*args)
+    if status != 0:
+        msg = L.pps_last_error().decode('utf-8', 'replace')
+        raise RuntimeError('%s failed (status %d): %s' % (name, status, msg))
+    return status
+
+
+def exported_symbols():
+    return sorted(list(SIGNATURES) + list(EXTRA))

@@ -1,0 +1,215 @@
+// extern "C" entry points of libpps_hip.so (declared in include/pps_abi.h).
+// Each entry point validates shapes/alignment ENFORCE-style, fills the
+// launch parameters and enqueues on the caller's stream.  No allocation, no
+// synchronisation: every entry point is hipGraph-capturable.
+#include <string>
+
+#include "pps_internal.hpp"
+
+namespace pps {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int maxpool2d(const float*, int, int, int, int, int, int, int, float*, int, int,
+              hipStream_t);
+int part_power_set(const float*, int, int, int, int, const int32_t*, int, int, float*,
+                   hipStream_t);
+int l2_normalize(const float*, int64_t, int, float*, hipStream_t);
+int preprocess_bgr(const uint8_t*, int, int, int, const float*, int, int, float*,
+                   hipStream_t);
+int collect_positives(const float*, int64_t, int64_t, int64_t, const int32_t*,
+                      const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
+                      int32_t*, int32_t*, hipStream_t);
+int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const int32_t*,
+                const int32_t*, const int32_t*, int64_t, int, int, const float*,
+                const int32_t*, const int32_t*, float*, int32_t*, int32_t*, int32_t*,
+                int32_t*, hipStream_t);
+int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
+                const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
+int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+
+}  // namespace pps
+
+using namespace pps;
+
+extern "C" {
+
+int pps_abi_version(void) { return 1; }
+
+const char* pps_last_error(void) { return g_last_error.c_str(); }
+
+const char* pps_registered_ops(void) {
+  return "PairWiseDistance;Conv+SpatialBN+Sum+Relu;MaxPool;PartPowerSet;Normalize;"
+         "ComputeDist;RankCounts;TopK;PrepImForBlob";
+}
+
+int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
+                int64_t ldg, int D, int metric, float* out, int64_t ldo, void* stream) {
+  PPS_ENFORCE(q && g && out, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && D > 0, "bad shape");
+  PPS_ENFORCE(D % 4 == 0, "D must be a multiple of 4, got " + std::to_string(D));
+  PPS_ENFORCE(ldq % 4 == 0 && ldg % 4 == 0 && ldq >= D && ldg >= D, "bad leading dims");
+  PPS_ENFORCE(ldo >= G, "ldo < G");
+  PPS_ENFORCE(aligned16(q) && aligned16(g), "q/g must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  PPS_ENFORCE(Q < (1ll << 31) && G < (1ll << 31), "Q/G must fit int32");
+  GemmParams p{};
+  p.a = q; p.H = 1; p.W = (int)Q; p.Cin = D; p.lda = (int)ldq;
+  p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)Q;
+  p.M = (int)Q;
+  p.b = g; p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)G;
+  p.Kloop = (D + 15) / 16 * 16;
+  p.out = out; p.ldo = ldo; p.metric = metric;
+  return launch_gemm(p, EPI_DIST, 1, as_stream(stream));
+}
+
+int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
+  PPS_ENFORCE(X && Z, "null pointer");
+  PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
+  PPS_ENFORCE(aligned16(X), "X must be 16-byte aligned");
+  GemmParams p{};
+  p.a = X; p.H = 1; p.W = N; p.Cin = D; p.lda = D;
+  p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = N; p.M = N;
+  p.b = X; p.ldb = D; p.kb_valid = D; p.Ncol = N;
+  p.Kloop = (D + 15) / 16 * 16;
+  p.out = Z; p.ldo = N; p.metric = PPS_METRIC_SQEUCLIDEAN; p.zero_diag = 1;
+  return launch_gemm(p, EPI_DIST, 1, as_stream(stream));
+}
+
+int pps_collect_positives(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                          const int32_t* qid, const int32_t* qcam, const int32_t* gid,
+                          const int32_t* gcam, int64_t g_offset, int Pmax, float* pos_d,
+                          int32_t* pos_idx, int32_t* pos_cnt, void* stream) {
+  PPS_ENFORCE(dist && qid && qcam && gid && gcam && pos_d && pos_idx && pos_cnt,
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Pmax > 0, "bad shape");
+  return collect_positives(dist, Q, G, ldd, qid, qcam, gid, gcam, g_offset, Pmax, pos_d,
+                           pos_idx, pos_cnt, as_stream(stream));
+}
+
+int pps_rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                    const int32_t* qid, const int32_t* qcam, const int32_t* gid,
+                    const int32_t* gcam, int64_t g_offset, int R, int Pmax,
+                    const float* pos_d, const int32_t* pos_idx, const int32_t* pos_cnt,
+                    float* sorted_d, int32_t* sorted_idx, int32_t* pos_total,
+                    int32_t* hist, int32_t* before, void* stream) {
+  PPS_ENFORCE(dist && qid && qcam && gid && gcam && pos_d && pos_idx && pos_cnt &&
+                  sorted_d && sorted_idx && pos_total && hist && before,
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G, "bad shape");
+  PPS_ENFORCE(R >= 1 && R <= 64, "R must be in [1, 64]");
+  if ((int64_t)R * Pmax > 2048) {
+    set_error("merged positives per query R*Pmax=" + std::to_string((int64_t)R * Pmax) +
+              " exceeds the LDS capacity 2048");
+    return PPS_ERR_CAPACITY;
+  }
+  return rank_counts(dist, Q, G, ldd, qid, qcam, gid, gcam, g_offset, R, Pmax, pos_d,
+                     pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, hist, before,
+                     as_stream(stream));
+}
+
+int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* pos_total,
+                    const int32_t* hist, const int32_t* before, double* ap,
+                    int32_t* valid, int32_t* first_rank, void* stream) {
+  PPS_ENFORCE(sorted_d && pos_total && hist && before && ap && valid && first_rank,
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && Ptot >= 0, "bad shape");
+  return ap_finalize(Q, Ptot, sorted_d, pos_total, hist, before, ap, valid, first_rank,
+                     as_stream(stream));
+}
+
+int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* vals,
+             int32_t* idx, void* stream) {
+  PPS_ENFORCE(dist && vals && idx, "null pointer");
+  PPS_ENFORCE(k >= 1 && k <= 1024, "k must be in [1, 1024], got " + std::to_string(k));
+  PPS_ENFORCE(G >= k && ldd >= G, "need G >= k");
+  PPS_ENFORCE(G < (1ll << 31), "G must fit int32");
+  return topk(dist, Q, G, ldd, k, vals, idx, as_stream(stream));
+}
+
+int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+                      const float* w, int Cout, int Kpad, int KH, int KW, int stride,
+                      int pad, int dil, const float* scale, const float* shift,
+                      const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
+                      void* stream) {
+  PPS_ENFORCE(x && w && scale && shift && y, "null pointer");
+  PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "bad shape");
+  PPS_ENFORCE(Cin % 4 == 0 && ldx % 4 == 0 && ldx >= Cin,
+              "input channels must be a multiple of 4 (pad NHWC), got " +
+                  std::to_string(Cin));
+  PPS_ENFORCE(Kpad % 16 == 0 && Kpad >= KH * KW * Cin, "Kpad must be >= KH*KW*Cin, %16");
+  PPS_ENFORCE(stride >= 1 && dil >= 1 && pad >= 0, "bad stride/pad/dilation");
+  PPS_ENFORCE(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 &&
+                  Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
+              "output size does not match conv arithmetic");
+  PPS_ENFORCE(ldy >= Cout, "ldy < Cout");
+  PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
+  PPS_ENFORCE((int64_t)N * Ho * Wo < (1ll << 31), "too many output pixels");
+  GemmParams p{};
+  p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
+  p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = dil;
+  p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
+  p.b = w; p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
+  p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
+  p.out = y; p.ldo = ldy; p.relu = relu;
+  return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
+}
+
+int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
+                            const float* w, int64_t w_bstride, int Cout,
+                            const float* scale, const float* shift, int relu, float* y,
+                            int ldy, int B, void* stream) {
+  PPS_ENFORCE(x && w && scale && shift && y, "null pointer");
+  PPS_ENFORCE(M > 0 && K > 0 && Cout > 0 && B > 0, "bad shape");
+  PPS_ENFORCE(K % 16 == 0, "K must be a multiple of 16");
+  PPS_ENFORCE(x_bstride % 4 == 0 && w_bstride % 4 == 0, "batch strides must be %4");
+  PPS_ENFORCE(ldy >= B * Cout, "ldy < B*Cout");
+  PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
+  GemmParams p{};
+  p.a = x; p.a_bstride = x_bstride; p.H = 1; p.W = M; p.Cin = K; p.lda = K;
+  p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = M; p.M = M;
+  p.b = w; p.b_bstride = w_bstride; p.ldb = K; p.kb_valid = K; p.Ncol = Cout;
+  p.Kloop = K;
+  p.scale = scale; p.shift = shift; p.ss_bstride = Cout;
+  p.out = y; p.ldo = ldy; p.out_bstride = Cout; p.relu = relu;
+  return launch_gemm(p, EPI_CONV, B, as_stream(stream));
+}
+
+int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad,
+                  float* y, int Ho, int Wo, void* stream) {
+  PPS_ENFORCE(x && y, "null pointer");
+  PPS_ENFORCE(C % 4 == 0, "C must be a multiple of 4");
+  PPS_ENFORCE(Ho == (H + 2 * pad - k) / stride + 1 && Wo == (W + 2 * pad - k) / stride + 1,
+              "output size does not match pooling arithmetic (floor)");
+  PPS_ENFORCE(aligned16(x) && aligned16(y), "x/y must be 16-byte aligned");
+  return maxpool2d(x, N, H, W, C, k, stride, pad, y, Ho, Wo, as_stream(stream));
+}
+
+int pps_part_power_set(const float* x, int N, int H, int W, int C, const int32_t* splits,
+                       int nstrip, int max_ave, float* out, void* stream) {
+  PPS_ENFORCE(x && splits && out, "null pointer");
+  PPS_ENFORCE(nstrip >= 1 && nstrip <= 10, "nstrip must be in [1, 10]");
+  int sum = 0;
+  for (int j = 0; j < nstrip; ++j) {
+    PPS_ENFORCE(splits[j] > 0, "split heights must be positive");
+    sum += splits[j];
+  }
+  PPS_ENFORCE(sum == H, "split heights must sum to H (Split axis=2)");
+  return part_power_set(x, N, H, W, C, splits, nstrip, max_ave, out, as_stream(stream));
+}
+
+int pps_l2_normalize(const float* x, int64_t N, int D, float* y, void* stream) {
+  PPS_ENFORCE(x && y && D > 0 && N >= 0, "bad arguments");
+  return l2_normalize(x, N, D, y, as_stream(stream));
+}
+
+int pps_preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const float* means,
+                       int Ho, int Wo, float* y, void* stream) {
+  PPS_ENFORCE(img && means && y, "null pointer");
+  PPS_ENFORCE(N >= 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "bad shape");
+  PPS_ENFORCE(aligned16(y), "y must be 16-byte aligned");
+  return preprocess_bgr(img, N, Hi, Wi, means, Ho, Wo, y, as_stream(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+// Memory-bound feature-extractor kernels (HBM / L2 bound, no MFMA):
+//   max pooling (stem pool1), part-power-set strip pooling + subset combine,
+//   row L2 normalisation, image preprocessing (mean-subtract + bicubic).
+// All NHWC float32, 16-B vectorised along channels where the layout allows.
+#include "pps_internal.hpp"
+
+namespace pps {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- MaxPool k x k / s, pad p (ResNet.py:255) --------------------------------
+// One thread per (n, oh, ow, 4 channels).  Padding never wins (Caffe2 / cuDNN
+// max pooling ignores padded taps).
+__global__ void maxpool_nhwc_kernel(const float* __restrict__ x, int N, int H, int W,
+                                    int C, int k, int s, int pad,
+                                    float* __restrict__ y, int Ho, int Wo) {
+  const int C4 = C >> 2;
+  const int64_t total = (int64_t)N * Ho * Wo * C4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % C4);
+    int64_t r = t / C4;
+    const int ow = (int)(r % Wo);
+    r /= Wo;
+    const int oh = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    const int h0 = oh * s - pad, w0 = ow * s - pad;
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = h0 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = w0 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(
+            x + (((int64_t)n * H + ih) * W + iw) * C + c4 * 4);
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
+    }
+    *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oh) * Wo + ow) * C + c4 * 4) = m;
+  }
+}
+
+int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad,
+              float* y, int Ho, int Wo, hipStream_t st) {
+  const int64_t total = (int64_t)N * Ho * Wo * (C / 4);
+  const int block = 256;
+  const int64_t want = (total + block - 1) / block;
+  const int grid = (int)(want < 8192 ? want : 8192);
+  if (grid == 0) return PPS_OK;
+  hipLaunchKernelGGL(maxpool_nhwc_kernel, dim3(grid), dim3(block), 0, st, x, N, H, W, C,
+                     k, stride, pad, y, Ho, Wo);
+  PPS_CHECK_LAUNCH("maxpool_nhwc_kernel");
+  return PPS_OK;
+}
+
+// ---- Part power set (bpm_heads.py:18-55, pps_heads.py:38-80) ---------------
+// Thread per (n, c): strip-wise global average and max over the strip's
+// rows x W, then every non-empty subset i (bit j <=> strip j):
+//   max_ave: out = Mean(ave_j, j in i) + Max(max_j, j in i)
+//   else   : out = Max(ave_j, j in i)
+// Mean follows Caffe2's Mean op: sum in input order, then * (1/n).
+constexpr int kMaxStrips = 10;
+struct Splits {
+  int h[kMaxStrips];
+};
+
+__global__ void part_power_set_kernel(const float* __restrict__ x, int N, int H, int W,
+                                      int C, Splits sp, int S, int max_ave,
+                                      float* __restrict__ out) {
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float ave[kMaxStrips], mx[kMaxStrips];
+  const float* base = x + (int64_t)n * H * W * C + c;
+  int row = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxStrips; ++j) {
+    if (j >= S) break;
+    float sum = 0.f, m = -INFINITY;
+    for (int hh = 0; hh < sp.h[j]; ++hh, ++row) {
+      for (int ww = 0; ww < W; ++ww) {
+        const float v = base[((int64_t)row * W + ww) * C];
+        sum += v;
+        m = fmaxf(m, v);
+      }
+    }
+    ave[j] = sum / (float)(sp.h[j] * W);
+    mx[j] = m;
+  }
+  const int nsub = (1 << S) - 1;
+  for (int i = 1; i <= nsub; ++i) {
+    float v;
+    if (max_ave) {
+      float s = 0.f, m = -INFINITY;
+      int cnt = 0;
+      bool first = true;
+      for (int j = 0; j < S; ++j) {
+        if (i & (1 << j)) {
+          s = first ? ave[j] : s + ave[j];
+          first = false;
+          m = fmaxf(m, mx[j]);
+          ++cnt;
+        }
+      }
+      v = s * (1.f / (float)cnt) + m;
+    } else {
+      float m = -INFINITY;
+      for (int j = 0; j < S; ++j)
+        if (i & (1 << j)) m = fmaxf(m, ave[j]);
+      v = m;
+    }
+    out[((int64_t)(i - 1) * N + n) * C + c] = v;
+  }
+}
+
+int part_power_set(const float* x, int N, int H, int W, int C, const int32_t* splits,
+                   int S, int max_ave, float* out, hipStream_t st) {
+  Splits sp;
+  for (int j = 0; j < kMaxStrips; ++j) sp.h[j] = j < S ? splits[j] : 0;
+  dim3 block(256), grid((C + 255) / 256, N);
+  hipLaunchKernelGGL(part_power_set_kernel, grid, block, 0, st, x, N, H, W, C, sp, S,
+                     max_ave, out);
+  PPS_CHECK_LAUNCH("part_power_set_kernel");
+  return PPS_OK;
+}
+
+// ---- Normalize (triplet_loss.py:17-19 -> Caffe2 Normalize) -------------------
+__global__ void l2_normalize_kernel(const float* __restrict__ x, int D,
+                                    float* __restrict__ y) {
+  const int64_t row = blockIdx.x;
+  const float* xr = x + row * D;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) s += xr[i] * xr[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.f;
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) red[0] = t;
+  }
+  __syncthreads();
+  const float inv = 1.f / fmaxf(sqrtf(red[0]), 1e-12f);
+  float* yr = y + row * D;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) yr[i] = xr[i] * inv;
+}
+
+int l2_normalize(const float* x, int64_t N, int D, float* y, hipStream_t st) {
+  if (N <= 0) return PPS_OK;
+  hipLaunchKernelGGL(l2_normalize_kernel, dim3((unsigned)N), dim3(256), 0, st, x, D, y);
+  PPS_CHECK_LAUNCH("l2_normalize_kernel");
+  return PPS_OK;
+}
+
+// ---- Preprocess (utils/blob.py:97-117) ---------------------------------------
+// u8 BGR HWC -> float, minus PIXEL_MEANS, bicubic resize (cv2.INTER_CUBIC:
+// a = -0.75, src = (dst + 0.5) * scale - 0.5, replicate border) -> NHWC4.
+__device__ inline void cubic_coeffs(float x, float w[4]) {
+  const float A = -0.75f;
+  w[0] = ((A * (x + 1.f) - 5.f * A) * (x + 1.f) + 8.f * A) * (x + 1.f) - 4.f * A;
+  w[1] = ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f;
+  w[2] = ((A + 2.f) * (1.f - x) - (A + 3.f)) * (1.f - x) * (1.f - x) + 1.f;
+  w[3] = 1.f - w[0] - w[1] - w[2];
+}
+
+struct Means {
+  float m[3];
+};
+
+__global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ img, int N, int Hi,
+                                      int Wi, Means mean, int Ho, int Wo,
+                                      float* __restrict__ y) {
+  const int64_t total = (int64_t)N * Ho * Wo;
+  const float sx = (float)Wi / (float)Wo, sy = (float)Hi / (float)Ho;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int ox = (int)(t % Wo);
+    const int oy = (int)((t / Wo) % Ho);
+    const int n = (int)(t / ((int64_t)Wo * Ho));
+    const float fx = (ox + 0.5f) * sx - 0.5f;
+    const float fy = (oy + 0.5f) * sy - 0.5f;
+    const int x0 = (int)floorf(fx), y0 = (int)floorf(fy);
+    float wx[4], wy[4];
+    cubic_coeffs(fx - x0, wx);
+    cubic_coeffs(fy - y0, wy);
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+      const int yy = min(max(y0 - 1 + j, 0), Hi - 1);
+      float row[3] = {0.f, 0.f, 0.f};
+      for (int i = 0; i < 4; ++i) {
+        const int xx = min(max(x0 - 1 + i, 0), Wi - 1);
+        const uint8_t* px = img + (((int64_t)n * Hi + yy) * Wi + xx) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) row[c] += wx[i] * ((float)px[c] - mean.m[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += wy[j] * row[c];
+    }
+    *reinterpret_cast<f32x4*>(y + t * 4) = f32x4{acc[0], acc[1], acc[2], 0.f};
+  }
+}
+
+int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const float* means, int Ho,
+                   int Wo, float* y, hipStream_t st) {
+  Means m;
+  for (int c = 0; c < 3; ++c) m.m[c] = means[c];
+  const int64_t total = (int64_t)N * Ho * Wo;
+  const int64_t want = (total + 255) / 256;
+  const int grid = (int)(want < 8192 ? want : 8192);
+  if (grid == 0) return PPS_OK;
+  hipLaunchKernelGGL(preprocess_bgr_kernel, dim3(grid), dim3(256), 0, st, img, N, Hi, Wi,
+                     m, Ho, Wo, y);
+  PPS_CHECK_LAUNCH("preprocess_bgr_kernel");
+  return PPS_OK;
+}
+
+}  // namespace pps

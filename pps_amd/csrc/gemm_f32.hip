@@ -1,0 +1,293 @@
+// FP32 MFMA GEMM core for gfx950 (CDNA4): implicit-GEMM convolution over NHWC
+// activations and the query x gallery distance matrix share this kernel.
+//
+//   C[m][n] = sum_k A[m][k] * B[n][k]       (both operands K-contiguous)
+//
+// * v_mfma_f32_32x32x2_f32 (exact f32 in, f32 accumulate): the only way to
+//   keep the reference's fp32 numerics (SURVEY §7 "Precision vs parity").
+// * Block tile BM x BN x 16, 64*WM*WN threads, each wave owns
+//   (BM/WM) x (BN/WN) as TMxTN 32x32 accumulators (16 f32 regs each).
+// * K is permuted inside a 16-chunk: at MFMA step s (0..7) lane half h
+//   contributes k = 8h + s, so each lane reads its 8 k-values of a row with
+//   two ds_read_b128 from a K-contiguous LDS row.  Row stride 20 floats
+//   (80 B) makes those reads bank-conflict free for all four b128 lane groups.
+// * Register-staged global->LDS pipeline, 2 LDS buffers, ONE barrier per
+//   K-chunk: the loads for chunk t+1 are issued before the MFMAs on chunk t.
+// * XCD-aware bijective block remap: consecutive tiles along N (sharing the
+//   same A panel) land on the same XCD / L2.
+// * Epilogues: EPI_CONV = per-column scale/shift (folded test-mode BN,
+//   conv bias) + residual + ReLU; EPI_DIST = |q|^2 + |g|^2 - 2 q.g with the
+//   squared norms accumulated from the same LDS fragments, clamp, sqrt.
+#include "pps_internal.hpp"
+
+namespace pps {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 16;
+constexpr int LSTR = BK + 4;  // LDS row stride in floats
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN)
+gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int T = 64 * WM * WN;
+  constexpr int AL = BM * BK / 4 / T;  // f32x4 loads per thread (A)
+  constexpr int BL = BN * BK / 4 / T;  // f32x4 loads per thread (B)
+  constexpr int ROWS_PER_PASS = T / 4;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  static_assert(AL >= 1 && BL >= 1, "tile too small for thread count");
+  static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+
+  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LSTR];
+  float* As = lds;                       // [2][BM][LSTR]
+  float* Bs = lds + 2 * BM * LSTR;       // [2][BN][LSTR]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  // ---- XCD-aware bijective remap of the flat block id -------------------
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  }
+  const int tile_m = bid / tiles_n;
+  const int tile_n = bid - tile_m * tiles_n;
+  const int m0 = tile_m * BM;
+  const int n0 = tile_n * BN;
+  const int batch = blockIdx.y;
+
+  const float* __restrict__ A = p.a + batch * p.a_bstride;
+  const float* __restrict__ B = p.b + batch * p.b_bstride;
+
+  // ---- per-thread A-row geometry ----------------------------------------
+  const int c4 = tid & 3;
+  const float* abase[AL];
+  int ih0[AL], iw0[AL];
+  bool arow_ok[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int row = m0 + (tid >> 2) + i * ROWS_PER_PASS;
+    arow_ok[i] = row < p.M;
+    const int rowc = arow_ok[i] ? row : 0;
+    const int hw = p.Ho * p.Wo;
+    const int n = rowc / hw;
+    const int rem = rowc - n * hw;
+    const int oh = rem / p.Wo;
+    const int ow = rem - oh * p.Wo;
+    ih0[i] = oh * p.stride - p.pad;
+    iw0[i] = ow * p.stride - p.pad;
+    abase[i] = A + (int64_t)n * p.H * p.W * p.lda;
+  }
+  // tap tracking for k = chunk*BK + c4*4 : (kh, kw, c)
+  int tc = c4 * 4, tkh = 0, tkw = 0;
+  while (tc >= p.Cin) {
+    tc -= p.Cin;
+    if (++tkw == p.KW) { tkw = 0; ++tkh; }
+  }
+  const float* bbase[BL];
+  bool bcol_ok[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int col = n0 + (tid >> 2) + i * ROWS_PER_PASS;
+    bcol_ok[i] = col < p.Ncol;
+    bbase[i] = B + (int64_t)(bcol_ok[i] ? col : 0) * p.ldb + c4 * 4;
+  }
+
+  f32x4 ra[AL], rb[BL];
+  auto load_chunk = [&](int kc) {
+    const bool tap_ok = tkh < p.KH;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int ih = ih0[i] + tkh * p.dil;
+      const int iw = iw0[i] + tkw * p.dil;
+      const bool ok = arow_ok[i] && tap_ok && (unsigned)ih < (unsigned)p.H &&
+                      (unsigned)iw < (unsigned)p.W;
+      ra[i] = ok ? *reinterpret_cast<const f32x4*>(
+                       abase[i] + ((int64_t)ih * p.W + iw) * p.lda + tc)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int kb = kc * BK + c4 * 4;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const bool ok = bcol_ok[i] && kb < p.kb_valid;
+      rb[i] = ok ? *reinterpret_cast<const f32x4*>(bbase[i] + kc * BK)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // advance the tap tracker by one chunk
+    tc += BK;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      if (++tkw == p.KW) { tkw = 0; ++tkh; }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float na[TM], nb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) na[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) nb[j] = 0.f;
+
+  const int nchunks = p.Kloop / BK;
+  load_chunk(0);
+  int buf = 0;
+  for (int kc = 0; kc < nchunks; ++kc) {
+    float* as = As + buf * BM * LSTR;
+    float* bs = Bs + buf * BN * LSTR;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+      *reinterpret_cast<f32x4*>(as + ((tid >> 2) + i * ROWS_PER_PASS) * LSTR + c4 * 4) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      *reinterpret_cast<f32x4*>(bs + ((tid >> 2) + i * ROWS_PER_PASS) * LSTR + c4 * 4) = rb[i];
+    __syncthreads();
+    if (kc + 1 < nchunks) load_chunk(kc + 1);
+
+    f32x4 fa[TM][2], fb[TN][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* src = as + (wm * (BM / WM) + i * 32 + r32) * LSTR + h * 8;
+      fa[i][0] = *reinterpret_cast<const f32x4*>(src);
+      fa[i][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* src = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + h * 8;
+      fb[j][0] = *reinterpret_cast<const f32x4*>(src);
+      fb[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+    if (EPI == EPI_DIST) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        na[i] += fa[i][0].x * fa[i][0].x + fa[i][0].y * fa[i][0].y +
+                 fa[i][0].z * fa[i][0].z + fa[i][0].w * fa[i][0].w +
+                 fa[i][1].x * fa[i][1].x + fa[i][1].y * fa[i][1].y +
+                 fa[i][1].z * fa[i][1].z + fa[i][1].w * fa[i][1].w;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        nb[j] += fb[j][0].x * fb[j][0].x + fb[j][0].y * fb[j][0].y +
+                 fb[j][0].z * fb[j][0].z + fb[j][0].w * fb[j][0].w +
+                 fb[j][1].x * fb[j][1].x + fb[j][1].y * fb[j][1].y +
+                 fb[j][1].z * fb[j][1].z + fb[j][1].w * fb[j][1].w;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float av = (s < 4) ? fa[i][0][s] : fa[i][1][s - 4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float bv = (s < 4) ? fb[j][0][s] : fb[j][1][s - 4];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  // ---- epilogue ------------------------------------------------------------
+  float* __restrict__ out = p.out + batch * p.out_bstride;
+  if (EPI == EPI_CONV) {
+    const float* sc = p.scale + batch * p.ss_bstride;
+    const float* sh = p.shift + batch * p.ss_bstride;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * (BN / WN) + j * 32 + r32;
+      if (col >= p.Ncol) continue;
+      const float s_ = sc[col];
+      const float t_ = sh[col];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rbase = m0 + wm * (BM / WM) + i * 32 + 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rbase + (r & 3) + 8 * (r >> 2);
+          if (row < p.M) {
+            float v = acc[i][j][r] * s_ + t_;
+            if (p.residual) v += p.residual[(int64_t)row * p.ldr + col];
+            if (p.relu) v = fmaxf(v, 0.f);
+            out[(int64_t)row * p.ldo + col] = v;
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) na[i] += __shfl_xor(na[i], 32);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) nb[j] += __shfl_xor(nb[j], 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float qn[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) qn[r] = __shfl(na[i], (r & 3) + 8 * (r >> 2) + 4 * h);
+      const int rbase = m0 + wm * (BM / WM) + i * 32 + 4 * h;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * (BN / WN) + j * 32 + r32;
+        if (col >= p.Ncol) continue;
+        const float gn = nb[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rbase + (r & 3) + 8 * (r >> 2);
+          if (row < p.M) {
+            const float dot = acc[i][j][r];
+            float v;
+            if (p.metric == PPS_METRIC_COSINE) {
+              const float den = fmaxf(sqrtf(qn[r]), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
+              v = 1.f - dot / den;
+            } else {
+              // reference order: (-2 * a.b) + |a|^2 + |b|^2, clamp at 0
+              v = (-2.f * dot + qn[r]) + gn;
+              v = fmaxf(v, 0.f);
+              if (p.metric == PPS_METRIC_EUCLIDEAN) v = sqrtf(v);
+            }
+            if (p.zero_diag && row == col) v = 0.f;
+            out[(int64_t)row * p.ldo + col] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_tile(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.Ncol + BN - 1) / BN;
+  dim3 grid(tiles_m * tiles_n, batch);
+  dim3 block(64 * WM * WN);
+  if (epi == EPI_CONV)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI_CONV>), grid, block, 0,
+                       stream, p, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI_DIST>), grid, block, 0,
+                       stream, p, tiles_m, tiles_n);
+  PPS_CHECK_LAUNCH("gemm_f32_kernel");
+  return PPS_OK;
+}
+
+int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  if (p.M <= 0 || p.Ncol <= 0 || batch <= 0) return PPS_OK;
+  if (p.Ncol <= 64) return launch_tile<128, 64, 4, 1>(p, epi, batch, stream);
+  if (p.M <= 64) return launch_tile<64, 128, 1, 4>(p, epi, batch, stream);
+  return launch_tile<128, 128, 2, 2>(p, epi, batch, stream);
+}
+
+}  // namespace pps

@@ -1,0 +1,72 @@
+// Internal helpers shared by the libpps_hip.so translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/pps_abi.h"
+
+namespace pps {
+
+// Thread-local ENFORCE-style error message (pps_last_error()).
+void set_error(const std::string& msg);
+
+#define PPS_ENFORCE(cond, msg)                                              \
+  do {                                                                      \
+    if (!(cond)) {                                                          \
+      ::pps::set_error(std::string("[enforce fail at ") + __func__ + "] " + \
+                       #cond + ". " + (msg));                               \
+      return PPS_ERR_INVALID_ARG;                                           \
+    }                                                                       \
+  } while (0)
+
+#define PPS_CHECK_LAUNCH(name)                                               \
+  do {                                                                       \
+    hipError_t e_ = hipGetLastError();                                       \
+    if (e_ != hipSuccess) {                                                  \
+      ::pps::set_error(std::string(name) + ": " + hipGetErrorString(e_));    \
+      return PPS_ERR_LAUNCH;                                                 \
+    }                                                                        \
+  } while (0)
+
+inline bool aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- GEMM core (gemm_f32.hip) ----------------------------------------------
+enum Epi { EPI_CONV = 0, EPI_DIST = 1 };
+
+struct GemmParams {
+  // A operand: implicit im2col over an NHWC tensor (plain rows: H=1, W=M,
+  // KH=KW=1).  Row m <-> output pixel (n, oh, ow).
+  const float* a;
+  int64_t a_bstride;
+  int H, W, Cin, lda;
+  int KH, KW, stride, pad, dil;
+  int Ho, Wo;
+  int M;
+  // B operand: [Ncol][ldb], K contiguous; k >= kb_valid reads as zero.
+  const float* b;
+  int64_t b_bstride;
+  int ldb, kb_valid;
+  int Ncol;
+  int Kloop;  // K extent iterated, multiple of 16
+  // epilogue
+  const float* scale;
+  const float* shift;
+  int64_t ss_bstride;
+  const float* residual;
+  int64_t ldr;
+  float* out;
+  int64_t ldo;
+  int64_t out_bstride;
+  int relu;
+  int metric;
+  int zero_diag;
+};
+
+int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
+
+}  // namespace pps

@@ -1,0 +1,347 @@
+// Retrieval ranking and evaluation kernels.
+//
+// The reference sorts every query row (np.argsort, reid_dataset_evaluator.py
+// :319,:420) and then walks it in Python.  mAP and CMC only need, for each
+// true match p of a query, how many valid gallery entries rank before it, so
+// these kernels compute exactly that by counting against the (few) positives'
+// distances -- one streaming read of the distance row, no sort.  The result
+// equals a stable (distance, gallery index) sort; counts are additive over
+// gallery shards, which is what the multi-GPU path all-reduces.
+#include "pps_internal.hpp"
+
+namespace pps {
+
+constexpr int kEvalThreads = 256;
+constexpr int kPosCap = 2048;  // max merged positives per query in LDS
+
+// ---- 1) collect positives ------------------------------------------------------
+__global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t G,
+                                         int64_t ldd, const int32_t* __restrict__ qid,
+                                         const int32_t* __restrict__ qcam,
+                                         const int32_t* __restrict__ gid,
+                                         const int32_t* __restrict__ gcam,
+                                         int64_t g_offset, int Pmax,
+                                         float* __restrict__ pos_d,
+                                         int32_t* __restrict__ pos_idx,
+                                         int32_t* __restrict__ pos_cnt) {
+  const int64_t q = blockIdx.x;
+  const int qi = qid[q], qc = qcam[q];
+  const float* row = dist + q * ldd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ int wtot[kEvalThreads / 64];
+  int base = 0;
+  for (int64_t t0 = 0; t0 < G; t0 += kEvalThreads) {
+    const int64_t i = t0 + threadIdx.x;
+    const bool flag = i < G && gid[i] == qi && gcam[i] != qc;
+    const unsigned long long bal = __ballot(flag);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[wave] = __popcll(bal);
+    __syncthreads();
+    int wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kEvalThreads / 64; ++w) {
+      wbase += (w < wave) ? wtot[w] : 0;
+      tot += wtot[w];
+    }
+    const int slot = base + wbase + pre;
+    if (flag && slot < Pmax) {
+      pos_d[q * Pmax + slot] = row[i];
+      pos_idx[q * Pmax + slot] = (int32_t)(g_offset + i);
+    }
+    base += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pos_cnt[q] = base;
+}
+
+int collect_positives(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                      const int32_t* qid, const int32_t* qcam, const int32_t* gid,
+                      const int32_t* gcam, int64_t g_offset, int Pmax, float* pos_d,
+                      int32_t* pos_idx, int32_t* pos_cnt, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  hipLaunchKernelGGL(collect_positives_kernel, dim3((unsigned)Q), dim3(kEvalThreads), 0,
+                     st, dist, G, ldd, qid, qcam, gid, gcam, g_offset, Pmax, pos_d,
+                     pos_idx, pos_cnt);
+  PPS_CHECK_LAUNCH("collect_positives_kernel");
+  return PPS_OK;
+}
+
+// ---- 2) rank counts -------------------------------------------------------------
+__device__ inline bool key_less(float da, int ia, float db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+__global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, int64_t G,
+                                   int64_t ldd, const int32_t* __restrict__ qid,
+                                   const int32_t* __restrict__ qcam,
+                                   const int32_t* __restrict__ gid,
+                                   const int32_t* __restrict__ gcam, int64_t g_offset,
+                                   int R, int Pmax, const float* __restrict__ pos_d,
+                                   const int32_t* __restrict__ pos_idx,
+                                   const int32_t* __restrict__ pos_cnt,
+                                   float* __restrict__ sorted_d,
+                                   int32_t* __restrict__ sorted_idx,
+                                   int32_t* __restrict__ pos_total,
+                                   int32_t* __restrict__ hist,
+                                   int32_t* __restrict__ before) {
+  const int64_t q = blockIdx.x;
+  const int Ptot = R * Pmax;
+  const int qi = qid[q], qc = qcam[q];
+  __shared__ float ud[kPosCap];
+  __shared__ int ui[kPosCap];
+  __shared__ float sd[kPosCap];
+  __shared__ int si[kPosCap];
+  __shared__ int hs[kPosCap];
+  __shared__ int offs[65];
+  __shared__ int red[kEvalThreads / 64];
+  // merged list layout: list r occupies [offs[r], offs[r+1])
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int r = 0; r < R; ++r) {
+      offs[r] = o;
+      const int c = pos_cnt[(int64_t)r * Q + q];
+      o += c < Pmax ? c : Pmax;
+    }
+    offs[R] = o;
+  }
+  __syncthreads();
+  const int P = offs[R];
+  for (int r = 0; r < R; ++r) {
+    const int n = offs[r + 1] - offs[r];
+    for (int p = threadIdx.x; p < n; p += blockDim.x) {
+      ud[offs[r] + p] = pos_d[((int64_t)r * Q + q) * Pmax + p];
+      ui[offs[r] + p] = pos_idx[((int64_t)r * Q + q) * Pmax + p];
+    }
+  }
+  for (int p = threadIdx.x; p < P; p += blockDim.x) hs[p] = 0;
+  __syncthreads();
+  // rank-by-counting sort of the positives (P is small: tens per query)
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const float d = ud[p];
+    const int ix = ui[p];
+    int rk = 0;
+    for (int o = 0; o < P; ++o) rk += key_less(ud[o], ui[o], d, ix) ? 1 : 0;
+    sd[rk] = d;
+    si[rk] = ix;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < Ptot; p += blockDim.x) {
+    sorted_d[q * Ptot + p] = p < P ? sd[p] : INFINITY;
+    sorted_idx[q * Ptot + p] = p < P ? si[p] : -1;
+  }
+  if (threadIdx.x == 0) pos_total[q] = P;
+  const float df = P > 0 ? sd[0] : 0.f;
+  const int64_t idf = P > 0 ? si[0] : 0;
+  const float* row = dist + q * ldd;
+  int nbefore = 0;
+  if (P > 0) {
+    for (int64_t i = threadIdx.x; i < G; i += blockDim.x) {
+      if (gid[i] == qi && gcam[i] == qc) continue;  // junk: same id, same cam
+      const float d = row[i];
+      int lo = 0, hi = P;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sd[mid] < d) lo = mid + 1; else hi = mid;
+      }
+      if (lo < P) atomicAdd(&hs[lo], 1);
+      nbefore += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) nbefore += __shfl_xor(nbefore, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nbefore;
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x) hist[q * Ptot + p] += hs[p];
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < kEvalThreads / 64; ++w) s += red[w];
+    before[q] += s;
+  }
+}
+
+int rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int32_t* qid,
+                const int32_t* qcam, const int32_t* gid, const int32_t* gcam,
+                int64_t g_offset, int R, int Pmax, const float* pos_d,
+                const int32_t* pos_idx, const int32_t* pos_cnt, float* sorted_d,
+                int32_t* sorted_idx, int32_t* pos_total, int32_t* hist, int32_t* before,
+                hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  hipLaunchKernelGGL(rank_counts_kernel, dim3((unsigned)Q), dim3(kEvalThreads), 0, st,
+                     dist, Q, G, ldd, qid, qcam, gid, gcam, g_offset, R, Pmax, pos_d,
+                     pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, hist, before);
+  PPS_CHECK_LAUNCH("rank_counts_kernel");
+  return PPS_OK;
+}
+
+// ---- 3) AP / first-match finalisation -----------------------------------------
+// One wave per query.  le[p] = prefix sum of hist (valid entries with
+// d <= d_p); pos_le[p] = #positives with d <= d_p (upper bound, so tied
+// positives share the precision at the end of their tie group, as sklearn's
+// precision_recall_curve does on distinct thresholds).
+__global__ void ap_finalize_kernel(int64_t Q, int Ptot, const float* __restrict__ sorted_d,
+                                   const int32_t* __restrict__ pos_total,
+                                   const int32_t* __restrict__ hist,
+                                   const int32_t* __restrict__ before,
+                                   double* __restrict__ ap, int32_t* __restrict__ valid,
+                                   int32_t* __restrict__ first_rank) {
+  const int64_t q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int P = pos_total[q];
+  const float* sd = sorted_d + q * Ptot;
+  const int32_t* hq = hist + q * Ptot;
+  double acc = 0.0;
+  int carry = 0;
+  for (int p0 = 0; p0 < P; p0 += 64) {
+    const int p = p0 + lane;
+    int v = p < P ? hq[p] : 0;
+    // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o);
+      if (lane >= o) v += t;
+    }
+    const int le = carry + v;
+    carry += __shfl(v, 63);
+    if (p < P) {
+      const float d = sd[p];
+      int lo = p, hi = P;  // upper_bound of d in sd[p..P)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sd[mid] <= d) lo = mid + 1; else hi = mid;
+      }
+      acc += (double)lo / (double)le;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    ap[q] = P > 0 ? acc / (double)P : 0.0;
+    valid[q] = P > 0 ? 1 : 0;
+    first_rank[q] = P > 0 ? before[q] : -1;
+  }
+}
+
+int ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* pos_total,
+                const int32_t* hist, const int32_t* before, double* ap, int32_t* valid,
+                int32_t* first_rank, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  hipLaunchKernelGGL(ap_finalize_kernel, dim3((unsigned)Q), dim3(64), 0, st, Q, Ptot,
+                     sorted_d, pos_total, hist, before, ap, valid, first_rank);
+  PPS_CHECK_LAUNCH("ap_finalize_kernel");
+  return PPS_OK;
+}
+
+// ---- stable per-row top-k ---------------------------------------------------------
+// Radix select (4 x 8-bit digits of the order-preserving key) finds the k-th
+// smallest key K*; entries with key < K*, then entries == K* in index order,
+// are compacted into LDS and bitonic-sorted as 64-bit (key << 32 | index).
+__device__ inline uint32_t float_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float key_float(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+constexpr int kTopkThreads = 256;
+constexpr int kTopkCap = 1024;
+
+__global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
+                            float* __restrict__ vals, int32_t* __restrict__ idx) {
+  const int64_t q = blockIdx.x;
+  const float* row = dist + q * ldd;
+  __shared__ int hist[256];
+  __shared__ uint32_t s_prefix;
+  __shared__ int s_rem;
+  __shared__ unsigned long long cand[kTopkCap];
+  __shared__ int wtot[kTopkThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t prefix = 0, pmask = 0;
+  int rem = k;  // rank (1-based) of K* among entries matching the prefix
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < G; i += blockDim.x) {
+      const uint32_t key = float_key(row[i]);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int c = 0, b = 0;
+      for (; b < 256; ++b) {
+        if (c + hist[b] >= rem) break;
+        c += hist[b];
+      }
+      s_prefix = prefix | ((uint32_t)b << shift);
+      s_rem = rem - c;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    rem = s_rem;
+    pmask |= 255u << shift;
+    __syncthreads();
+  }
+  const uint32_t kstar = prefix;  // k-th smallest key; `rem` of its ties are kept
+  // ordered compaction: key < K* (any order) and the first `rem` ties by index
+  int nless = 0, nties = 0;
+  for (int64_t t0 = 0; t0 < G; t0 += blockDim.x) {
+    const int64_t i = t0 + threadIdx.x;
+    uint32_t key = 0;
+    bool less = false, tie = false;
+    if (i < G) {
+      key = float_key(row[i]);
+      less = key < kstar;
+      tie = key == kstar;
+    }
+    const unsigned long long bl = __ballot(less), bt = __ballot(tie);
+    const int pl = __popcll(bl & ((1ull << lane) - 1ull));
+    const int pt = __popcll(bt & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[wave] = (__popcll(bl) << 16) | __popcll(bt);
+    __syncthreads();
+    int bl_off = 0, bt_off = 0, tl = 0, tt = 0;
+    for (int w = 0; w < kTopkThreads / 64; ++w) {
+      const int v = wtot[w];
+      if (w < wave) { bl_off += v >> 16; bt_off += v & 0xffff; }
+      tl += v >> 16;
+      tt += v & 0xffff;
+    }
+    const unsigned long long packed = ((unsigned long long)key << 32) | (uint32_t)i;
+    if (less) cand[nless + bl_off + pl] = packed;
+    const int tslot = nties + bt_off + pt;
+    if (tie && tslot < rem) cand[(k - rem) + tslot] = packed;
+    nless += tl;
+    nties += tt;
+    __syncthreads();
+  }
+  // bitonic sort of k candidates (padded to a power of two with +inf keys)
+  int n2 = 1;
+  while (n2 < k) n2 <<= 1;
+  for (int i = threadIdx.x + k; i < n2; i += blockDim.x) cand[i] = ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
+        const int i = 2 * stride * (t / stride) + (t % stride);
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        const unsigned long long a = cand[i], b = cand[j];
+        if ((a > b) == up) { cand[i] = b; cand[j] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const unsigned long long v = cand[i];
+    vals[q * k + i] = key_float((uint32_t)(v >> 32));
+    idx[q * k + i] = (int32_t)(v & 0xffffffffu);
+  }
+}
+
+int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* vals,
+         int32_t* idx, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
+                     ldd, k, vals, idx);
+  PPS_CHECK_LAUNCH("topk_kernel");
+  return PPS_OK;
+}
+
+}  // namespace pps

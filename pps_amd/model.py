@@ -1,0 +1,368 @@
+"""PPS feature extractor on MI355X: ResNet-50 (stride-1 res5) + part power set
++ 31 reid heads, executed as hand-written HIP kernels through libpps_hip.so.
+
+The layer plan is produced by builders that mirror the reference graph
+builders one for one, with the same blob and parameter names:
+
+  add_ResNet50_conv5_body   detectron/modeling/ResNet.py:39-40,91-126
+    basic_bn_stem           ResNet.py:246-256
+    add_stage               ResNet.py:60-88
+    add_residual_block      ResNet.py:153-195 (stride rule :169-171)
+    bottleneck_transformation ResNet.py:276-333 (STRIDE_1X1 :290)
+    basic_bn_shortcut       ResNet.py:203-220
+  add_pps_part_head         detectron/modeling/pps_heads.py:38-96
+    add_uniform_partition   detectron/modeling/bpm_heads.py:18-55
+  add_reid_outputs          detectron/modeling/reid_heads.py:34-127
+
+Differences by design: NHWC activations; test-mode
+SpatialBN folded into the conv epilogue as per-channel scale/shift; residual
+Sum and ReLU fused into branch2c's epilogue; the 31 head convs run as one
+batched GEMM; the unused FC logits (reid_heads.py:84-90) are not computed;
+batch N instead of the reference's batch-1 Reshape([1,-1]).
+"""
+import numpy as np
+import torch
+
+from . import ops
+from .config import cfg
+
+BN_EPS = 1e-5  # Caffe2 SpatialBN default epsilon (pytorch v1.0.1)
+
+
+# ---------------------------------------------------------------------------
+# Plan builders (structure only; no device work)
+# ---------------------------------------------------------------------------
+class Plan(object):
+    def __init__(self):
+        self.layers = []       # dicts, executed in order
+        self.params = {}       # name -> shape (Detectron naming)
+
+    def conv(self, blob_in, prefix, dim_in, dim_out, k, stride, pad, dilation=1,
+             relu=False, residual=None, out=None, bias=False, bn=None):
+        self.params[prefix + '_w'] = (dim_out, dim_in, k, k)
+        if bias:
+            self.params[prefix + '_b'] = (dim_out,)
+        bn = bn or prefix + '_bn'
+        for s in ('_s', '_b', '_rm', '_riv'):
+            self.params[bn + s] = (dim_out,)
+        out = out or bn
+        self.layers.append(dict(op='conv', name=prefix, bn=bn, input=blob_in,
+                                output=out, cin=dim_in, cout=dim_out, k=k,
+                                stride=stride, pad=pad, dil=dilation, relu=relu,
+                                residual=residual))
+        return out
+
+
+def basic_bn_stem(plan, data):
+    """ResNet.py:246-256: conv1 7x7/2 -> res_conv1_bn -> Relu -> pool1."""
+    p = plan.conv(data, 'conv1', 3, 64, 7, 2, 3, relu=True, bn='res_conv1_bn')
+    plan.layers.append(dict(op='maxpool', input=p, output='pool1', k=3, stride=2,
+                            pad=1))
+    return 'pool1', 64
+
+
+def bottleneck_transformation(plan, blob_in, dim_in, dim_out, stride, prefix,
+                              dim_inner, dilation=1, shortcut=None, out=None):
+    """ResNet.py:276-333 (+ the Sum/Relu of add_residual_block :186-195)."""
+    str1x1, str3x3 = (stride, 1) if cfg.RESNETS.STRIDE_1X1 else (1, stride)
+    cur = plan.conv(blob_in, prefix + '_branch2a', dim_in, dim_inner, 1, str1x1,
+                    0, relu=True)
+    cur = plan.conv(cur, prefix + '_branch2b', dim_inner, dim_inner, 3, str3x3,
+                    dilation, dilation=dilation, relu=True)
+    cur = plan.conv(cur, prefix + '_branch2c', dim_inner, dim_out, 1, 1, 0,
+                    relu=True, residual=shortcut, out=out)
+    return cur
+
+
+def basic_bn_shortcut(plan, prefix, blob_in, dim_in, dim_out, stride):
+    """ResNet.py:203-220."""
+    if dim_in == dim_out:
+        return blob_in
+    return plan.conv(blob_in, prefix + '_branch1', dim_in, dim_out, 1, stride, 0)
+
+
+def add_residual_block(plan, prefix, blob_in, dim_in, dim_out, dim_inner,
+                       dilation, stride_init=2, inplace_sum=False):
+    """ResNet.py:153-195."""
+    stride = stride_init if (dim_in != dim_out and dim_in != 64 and
+                             dilation == 1) else 1
+    sc = basic_bn_shortcut(plan, prefix, blob_in, dim_in, dim_out, stride)
+    # :190-193 -- in-place Sum into branch2c_bn except for a stage's last block
+    out = prefix + ('_branch2c_bn' if inplace_sum else '_sum')
+    return bottleneck_transformation(plan, blob_in, dim_in, dim_out, stride,
+                                     prefix, dim_inner, dilation, shortcut=sc,
+                                     out=out)
+
+
+def add_stage(plan, prefix, blob_in, n, dim_in, dim_out, dim_inner, dilation,
+              stride_init=2):
+    """ResNet.py:60-88."""
+    for i in range(n):
+        blob_in = add_residual_block(plan, '{}_{}'.format(prefix, i), blob_in,
+                                     dim_in, dim_out, dim_inner, dilation,
+                                     stride_init, inplace_sum=i < n - 1)
+        dim_in = dim_out
+    return blob_in, dim_in
+
+
+def add_ResNet50_conv5_body(plan):
+    """ResNet.py:39-40 -> add_ResNet_convX_body :91-126."""
+    p, dim_in = basic_bn_stem(plan, 'data')
+    dim_b = cfg.RESNETS.NUM_GROUPS * cfg.RESNETS.WIDTH_PER_GROUP
+    s, dim_in = add_stage(plan, 'res2', p, 3, dim_in, 256, dim_b, 1)
+    s, dim_in = add_stage(plan, 'res3', s, 4, dim_in, 512, dim_b * 2, 1)
+    s, dim_in = add_stage(plan, 'res4', s, 6, dim_in, 1024, dim_b * 4, 1)
+    s, dim_in = add_stage(plan, 'res5', s, 3, dim_in, 2048, dim_b * 8,
+                          cfg.RESNETS.RES5_DILATION,
+                          stride_init=cfg.RESNETS.RES5_STRIDE)
+    return s, dim_in, 1. / 16. * cfg.RESNETS.RES5_DILATION / cfg.RESNETS.RES5_STRIDE
+
+
+def uniform_partition_split(spatial_scale):
+    """bpm_heads.py:18-35: strip heights along H."""
+    strip_num = cfg.REID.BPM_STRIP_NUM
+    table = {7: [3, 3, 4, 4, 4, 3, 3], 5: [5, 5, 4, 5, 5],
+             9: [2, 3, 3, 3, 3, 3, 3, 2, 2], 10: [2, 2, 2, 3, 3, 3, 3, 2, 2, 2]}
+    if strip_num in table and cfg.REID.SCALE[1] == 16 * 24:
+        scale = 16 * spatial_scale
+        return [int(s * scale) for s in table[strip_num]]
+    strip_h = int(cfg.REID.SCALE[1] * spatial_scale / strip_num)
+    return [strip_h] * strip_num
+
+
+def subset_prefixes(strip_num, preprefix='pps'):
+    """pps_heads.py:47-64: subset i = bits of i; blob prefix pps + digits."""
+    out = []
+    for i in range(1, 1 << strip_num):
+        comb = [j for j in range(strip_num) if i & (1 << j)]
+        out.append(preprefix + ''.join(str(c) for c in comb))
+    return out
+
+
+def add_pps_part_head(plan, blob_in, dim_in, spatial_scale, preprefix='pps'):
+    """pps_heads.py:38-96 (+ bpm_heads.add_uniform_partition)."""
+    split = uniform_partition_split(spatial_scale)
+    prefixes = subset_prefixes(cfg.REID.BPM_STRIP_NUM, preprefix)
+    plan.layers.append(dict(op='pps', input=blob_in, output=preprefix + '_pool2_all',
+                            split=split, max_ave=bool(cfg.REID.MAX_AVE_FEATURE),
+                            prefixes=prefixes, dim=dim_in))
+    return prefixes, dim_in
+
+
+def add_reid_outputs(plan, prefixes, dim, preprefix='reid'):
+    """reid_heads.py:34-127 (test branch; FC logits skipped, never fetched)."""
+    dim_inner = cfg.REID.BPM_DIM
+    for p in prefixes:
+        plan.params[p + '_conv_w'] = (dim_inner, dim, 1, 1)
+        plan.params[p + '_conv_b'] = (dim_inner,)
+        for s in ('_s', '_b', '_rm', '_riv'):
+            plan.params[p + '_bn' + s] = (dim_inner,)
+    out = preprefix + '_feature_concat'
+    plan.layers.append(dict(op='heads', input=plan.layers[-1]['output'],
+                            prefixes=prefixes, dim=dim, dim_inner=dim_inner,
+                            output=out))
+    if cfg.REID.NORMALIZE_FEATURE:
+        plan.layers.append(dict(op='normalize', input=out,
+                                output=preprefix + '_feature_concat_norm'))
+        out = preprefix + '_feature_concat_norm'
+    return out
+
+
+def build_plan():
+    """model_builder.py:242 build_generic_reid_model (test, single GPU)."""
+    assert not cfg.FPN.FPN_ON, 'FPN_reid variant is not built yet (SURVEY §8(a) gated row)'
+    plan = Plan()
+    blob, dim, scale = add_ResNet50_conv5_body(plan)
+    prefixes, d = add_pps_part_head(plan, blob, dim, scale)
+    plan.output = add_reid_outputs(plan, prefixes, d)
+    plan.spatial_scale = scale
+    plan.feat_dim = len(prefixes) * cfg.REID.BPM_DIM
+    return plan
+
+
+# ---------------------------------------------------------------------------
+# Weights
+# ---------------------------------------------------------------------------
+def synthetic_weights(plan, seed=0):
+    """Seeded Detectron-format weights: He-normal convs, BN
+    _s ~ U(0.5,1.5), _b ~ N(0,0.1), _rm ~ N(0,0.1), _riv ~ U(0.5,1.5).  The
+    branch2c / branch1 BN scales are drawn smaller (U(0.05,0.15)) so that the
+    residual stream stays O(1) through 16 blocks with untrained weights."""
+    rng = np.random.RandomState(seed)
+    blobs = {}
+    for name in sorted(plan.params):
+        shape = plan.params[name]
+        if name.endswith('_w') and len(shape) == 4:
+            fan_in = shape[1] * shape[2] * shape[3]
+            blobs[name] = (rng.randn(*shape) * np.sqrt(2.0 / fan_in)).astype(np.float32)
+        elif name.endswith('_conv_b'):
+            blobs[name] = (0.01 * rng.randn(*shape)).astype(np.float32)
+        elif name.endswith('_s'):
+            lo, hi = (0.05, 0.15) if ('branch2c' in name or 'branch1' in name) else (0.5, 1.5)
+            blobs[name] = rng.uniform(lo, hi, size=shape).astype(np.float32)
+        elif name.endswith('_riv'):
+            blobs[name] = rng.uniform(0.5, 1.5, size=shape).astype(np.float32)
+        elif name.endswith('_rm') or name.endswith('_b'):
+            blobs[name] = (0.1 * rng.randn(*shape)).astype(np.float32)
+        else:
+            raise KeyError(name)
+    return blobs
+
+
+def fold_bn(blobs, bn, conv_bias=None):
+    """Test-mode SpatialBN y = (x - rm) * s / sqrt(riv + eps) + b as
+    y = x * scale + shift (conv bias folded into shift)."""
+    s = blobs[bn + '_s'].astype(np.float64)
+    b = blobs[bn + '_b'].astype(np.float64)
+    rm = blobs[bn + '_rm'].astype(np.float64)
+    riv = blobs[bn + '_riv'].astype(np.float64)
+    scale = s / np.sqrt(riv + BN_EPS)
+    cb = 0.0 if conv_bias is None else conv_bias.astype(np.float64)
+    shift = (cb - rm) * scale + b
+    return scale.astype(np.float32), shift.astype(np.float32)
+
+
+def pack_conv_weight(w, cin_pad=None):
+    """[Cout][Cin][KH][KW] -> [Cout][Kpad], K ordered (kh, kw, cin), Kpad % 16."""
+    cout, cin, kh, kw = w.shape
+    cin_p = cin_pad or cin
+    t = np.zeros((cout, kh, kw, cin_p), np.float32)
+    t[..., :cin] = w.transpose(0, 2, 3, 1)
+    k = kh * kw * cin_p
+    kpad = (k + 15) // 16 * 16
+    out = np.zeros((cout, kpad), np.float32)
+    out[:, :k] = t.reshape(cout, k)
+    return out, kpad
+
+
+# ---------------------------------------------------------------------------
+# Device model
+# ---------------------------------------------------------------------------
+class PPSModel(object):
+    """Device-resident PPS extractor.  forward(x_nhwc4) -> [N, 3968] features.
+
+    x_nhwc4: float32 [N, H, W, 4] (BGR minus PIXEL_MEANS, 4th channel zero)
+    on the current CUDA device, H x W = REID.SCALE[::-1].
+    """
+
+    def __init__(self, blobs, device='cuda', plan=None):
+        self.plan = plan or build_plan()
+        self.device = torch.device(device)
+        missing = [n for n in self.plan.params if n not in blobs
+                   and not n.endswith('_conv_b')]
+        if missing:
+            raise KeyError('weights missing %d blobs, e.g. %s' % (len(missing), missing[:5]))
+        self.layers = []
+        dev = self.device
+        for L in self.plan.layers:
+            L = dict(L)
+            if L['op'] == 'conv':
+                cin_pad = 4 if L['cin'] == 3 else None
+                w, kpad = pack_conv_weight(blobs[L['name'] + '_w'], cin_pad)
+                sc, sh = fold_bn(blobs, L['bn'], blobs.get(L['name'] + '_b'))
+                L.update(w=torch.from_numpy(w).to(dev), kpad=kpad,
+                         scale=torch.from_numpy(sc).to(dev),
+                         shift=torch.from_numpy(sh).to(dev),
+                         cin_eff=cin_pad or L['cin'])
+            elif L['op'] == 'heads':
+                ws, scs, shs = [], [], []
+                for p in L['prefixes']:
+                    w = blobs[p + '_conv_w'].reshape(L['dim_inner'], L['dim'])
+                    sc, sh = fold_bn(blobs, p + '_bn', blobs.get(p + '_conv_b'))
+                    ws.append(w)
+                    scs.append(sc)
+                    shs.append(sh)
+                L.update(w=torch.from_numpy(np.stack(ws).astype(np.float32)).to(dev),
+                         scale=torch.from_numpy(np.concatenate(scs)).to(dev),
+                         shift=torch.from_numpy(np.concatenate(shs)).to(dev))
+            elif L['op'] == 'pps':
+                L['split_arr'] = np.array(L['split'], np.int32)
+            self.layers.append(L)
+        self.feat_dim = self.plan.feat_dim
+        self._bufs = {}
+        self._batch = None
+
+    # -- activation buffers (allocated once per batch size) -----------------
+    def _alloc(self, N, H, W):
+        shapes = {'data': (N, H, W, 4)}
+        for L in self.layers:
+            if L['op'] == 'conv':
+                n, h, w, _ = shapes[L['input']]
+                ho = (h + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
+                wo = (w + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
+                shapes[L['output']] = (n, ho, wo, L['cout'])
+            elif L['op'] == 'maxpool':
+                n, h, w, c = shapes[L['input']]
+                ho = (h + 2 * L['pad'] - L['k']) // L['stride'] + 1
+                wo = (w + 2 * L['pad'] - L['k']) // L['stride'] + 1
+                shapes[L['output']] = (n, ho, wo, c)
+            elif L['op'] == 'pps':
+                n, h, w, c = shapes[L['input']]
+                shapes[L['output']] = (len(L['prefixes']), n, c)
+            elif L['op'] == 'heads':
+                shapes[L['output']] = (N, len(L['prefixes']) * L['dim_inner'])
+            elif L['op'] == 'normalize':
+                shapes[L['output']] = shapes[L['input']]
+        self._shapes = shapes
+        # algorithmic FLOPs per launch (2*M*Cout*K with the TRUE Cin: the
+        # stem's 4th packed channel is not counted) -- SURVEY §8(d)
+        for L in self.layers:
+            if L['op'] == 'conv':
+                n, ho, wo, co = shapes[L['output']]
+                L['flops'] = 2.0 * n * ho * wo * co * L['k'] * L['k'] * L['cin']
+            elif L['op'] == 'heads':
+                L['flops'] = 2.0 * N * len(L['prefixes']) * L['dim_inner'] * L['dim']
+            else:
+                L['flops'] = 0.0
+        self._bufs = {k: torch.empty(v, dtype=torch.float32, device=self.device)
+                      for k, v in shapes.items() if k != 'data'}
+        self._batch = (N, H, W)
+
+    def buffers(self):
+        return self._bufs
+
+    def flops_per_forward(self, kinds=('conv', 'heads')):
+        return sum(L['flops'] for L in self.layers if L['op'] in kinds)
+
+    def forward(self, x, out=None, timer=None):
+        """Run the plan.  `timer`, if a list, receives (layer, op, flops,
+        start_event, end_event) per layer, recorded on the current stream."""
+        assert x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+        assert x.shape[3] == 4, 'input must be NHWC with 4 channels (see preprocess)'
+        N, H, W, _ = x.shape
+        if self._batch != (N, H, W):
+            self._alloc(N, H, W)
+        bufs = dict(self._bufs)
+        bufs['data'] = x
+        for L in self.layers:
+            op = L['op']
+            if timer is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            if op == 'conv':
+                xi = bufs[L['input']]
+                y = bufs[L['output']]
+                res = bufs[L['residual']] if L['residual'] else None
+                ops.conv2d_bn_act(xi, L['cin_eff'], L['w'], L['kpad'], L['k'],
+                                  L['stride'], L['pad'], L['dil'], L['scale'],
+                                  L['shift'], res, L['relu'], y)
+            elif op == 'maxpool':
+                ops.maxpool2d(bufs[L['input']], L['k'], L['stride'], L['pad'],
+                              bufs[L['output']])
+            elif op == 'pps':
+                ops.part_power_set(bufs[L['input']], L['split_arr'], L['max_ave'],
+                                   bufs[L['output']])
+            elif op == 'heads':
+                xs = bufs[L['input']]
+                y = bufs[L['output']] if out is None or self.layers[-1] is not L else out
+                ops.gemm_bn_act_batched(xs, L['w'], L['scale'], L['shift'], True, y)
+                bufs[L['output']] = y
+            elif op == 'normalize':
+                y = out if out is not None else bufs[L['output']]
+                ops.l2_normalize(bufs[L['input']], y)
+                bufs[L['output']] = y
+            if timer is not None:
+                ev1.record()
+                timer.append((L.get('name', L['output']), op, L['flops'], ev0, ev1))
+        return bufs[self.plan.output]

@@ -1,0 +1,233 @@
+"""Device operators over torch CUDA tensors, backed by libpps_hip.so.
+
+torch is used only for device memory and the current HIP stream; every
+computation below is a libpps_hip.so kernel.  Each wrapper checks device,
+dtype and contiguity, then calls the C ABI on torch's current stream.
+
+Also hosts the operator registry that mirrors the reference's Caffe2 op names
+(`model.net.PairWiseDistance(X, Z)`, detectron/modeling/triplet_loss.py:145;
+registration detectron/ops/pairwise_distance_op.cu:124-127), so code written
+against that registry can look ops up by the same names.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import METRICS, call
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(t, name, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError('%s must be a torch.Tensor' % name)
+    if not t.is_cuda:
+        raise RuntimeError('%s must be a device (HIP) tensor; the product path has no '
+                           'CPU implementation' % name)
+    if t.dtype != dtype:
+        raise RuntimeError('%s must be %s, got %s' % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise RuntimeError('%s must be contiguous' % name)
+    return t.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+# Retrieval
+# ---------------------------------------------------------------------------
+def compute_dist(q, g, metric='euclidean', out=None):
+    """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244)."""
+    if q.dim() != 2 or g.dim() != 2 or q.shape[1] != g.shape[1]:
+        raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
+                           % (tuple(q.shape), tuple(g.shape)))
+    Q, D = q.shape
+    G = g.shape[0]
+    if out is None:
+        out = torch.empty((Q, G), dtype=torch.float32, device=q.device)
+    call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
+         _dev(out, 'out'), out.stride(0), _stream())
+    return out
+
+
+def pairwise_distance(X):
+    """Caffe2 PairWiseDistance: squared L2, [N,D] -> [N,N]."""
+    if X.dim() != 2:
+        raise RuntimeError('[enforce fail] X.dim() == 2 (got %d)' % X.dim())
+    N, D = X.shape
+    Z = torch.empty((N, N), dtype=torch.float32, device=X.device)
+    call('pps_pairwise_distance', _dev(X, 'X'), N, D, _dev(Z, 'Z'), _stream())
+    return Z
+
+
+def topk(dist, k):
+    """Stable ascending top-k per row -> (vals [Q,k] f32, idx [Q,k] i32)."""
+    Q, G = dist.shape
+    vals = torch.empty((Q, k), dtype=torch.float32, device=dist.device)
+    idx = torch.empty((Q, k), dtype=torch.int32, device=dist.device)
+    call('pps_topk', _dev(dist, 'dist'), Q, G, dist.stride(0), k, vals.data_ptr(),
+         idx.data_ptr(), _stream())
+    return vals, idx
+
+
+def collect_positives(dist, qid, qcam, gid, gcam, g_offset, Pmax):
+    Q, G = dist.shape
+    pos_d = torch.empty((Q, Pmax), dtype=torch.float32, device=dist.device)
+    pos_idx = torch.empty((Q, Pmax), dtype=torch.int32, device=dist.device)
+    pos_cnt = torch.empty((Q,), dtype=torch.int32, device=dist.device)
+    call('pps_collect_positives', _dev(dist, 'dist'), Q, G, dist.stride(0),
+         _dev(qid, 'qid', torch.int32), _dev(qcam, 'qcam', torch.int32),
+         _dev(gid, 'gid', torch.int32), _dev(gcam, 'gcam', torch.int32), int(g_offset),
+         Pmax, pos_d.data_ptr(), pos_idx.data_ptr(), pos_cnt.data_ptr(), _stream())
+    return pos_d, pos_idx, pos_cnt
+
+
+def rank_counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt,
+                hist=None, before=None):
+    """pos_* are [R,Q,Pmax] / [R,Q] merged lists.  hist/before accumulate."""
+    Q, G = dist.shape
+    R, _, Pmax = pos_d.shape
+    Ptot = R * Pmax
+    dev = dist.device
+    sorted_d = torch.empty((Q, Ptot), dtype=torch.float32, device=dev)
+    sorted_idx = torch.empty((Q, Ptot), dtype=torch.int32, device=dev)
+    pos_total = torch.empty((Q,), dtype=torch.int32, device=dev)
+    if hist is None:
+        hist = torch.zeros((Q, Ptot), dtype=torch.int32, device=dev)
+    if before is None:
+        before = torch.zeros((Q,), dtype=torch.int32, device=dev)
+    call('pps_rank_counts', _dev(dist, 'dist'), Q, G, dist.stride(0),
+         _dev(qid, 'qid', torch.int32), _dev(qcam, 'qcam', torch.int32),
+         _dev(gid, 'gid', torch.int32), _dev(gcam, 'gcam', torch.int32), int(g_offset),
+         R, Pmax, _dev(pos_d, 'pos_d'), _dev(pos_idx, 'pos_idx', torch.int32),
+         _dev(pos_cnt, 'pos_cnt', torch.int32), sorted_d.data_ptr(),
+         sorted_idx.data_ptr(), pos_total.data_ptr(), _dev(hist, 'hist', torch.int32),
+         _dev(before, 'before', torch.int32), _stream())
+    return sorted_d, sorted_idx, pos_total, hist, before
+
+
+def ap_finalize(sorted_d, pos_total, hist, before):
+    Q, Ptot = sorted_d.shape
+    dev = sorted_d.device
+    ap = torch.empty((Q,), dtype=torch.float64, device=dev)
+    valid = torch.empty((Q,), dtype=torch.int32, device=dev)
+    first = torch.empty((Q,), dtype=torch.int32, device=dev)
+    call('pps_ap_finalize', Q, Ptot, _dev(sorted_d, 'sorted_d'),
+         _dev(pos_total, 'pos_total', torch.int32), _dev(hist, 'hist', torch.int32),
+         _dev(before, 'before', torch.int32), ap.data_ptr(), valid.data_ptr(),
+         first.data_ptr(), _stream())
+    return ap, valid, first
+
+
+def max_positives(qid, qcam, gid, gcam):
+    """Host-side bound on true matches per query (metadata only, exact)."""
+    qid = np.asarray(qid, np.int64)
+    qcam = np.asarray(qcam, np.int64)
+    gid = np.asarray(gid, np.int64)
+    gcam = np.asarray(gcam, np.int64)
+    if len(qid) == 0 or len(gid) == 0:
+        return 0
+    ids, inv = np.unique(np.concatenate([qid, gid]), return_inverse=True)
+    qi, gi = inv[:len(qid)], inv[len(qid):]
+    per_id = np.bincount(gi, minlength=len(ids))
+    cams = np.unique(np.concatenate([qcam, gcam]), return_inverse=True)[1]
+    qc, gc = cams[:len(qcam)], cams[len(qcam):]
+    ncam = int(cams.max()) + 1
+    per_idcam = np.bincount(gi * ncam + gc, minlength=len(ids) * ncam)
+    cnt = per_id[qi] - per_idcam[qi * ncam + qc]
+    return int(cnt.max())
+
+
+# ---------------------------------------------------------------------------
+# Feature extractor
+# ---------------------------------------------------------------------------
+def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, relu, y):
+    N, H, W, ldx = x.shape
+    _, Ho, Wo, Cout = y.shape
+    rp = 0
+    if residual is not None:
+        if tuple(residual.shape) != tuple(y.shape):
+            raise RuntimeError('residual shape %s != output %s'
+                               % (tuple(residual.shape), tuple(y.shape)))
+        rp = _dev(residual, 'residual')
+    call('pps_conv2d_bn_act', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w, 'w'), Cout, kpad,
+         k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
+         int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, _stream())
+    return y
+
+
+def gemm_bn_act_batched(x, w, scale, shift, relu, y):
+    """x [B,M,K], w [B,Cout,K] -> y [M, B*Cout] (PPS head convs)."""
+    B, M, K = x.shape
+    Cout = w.shape[1]
+    call('pps_gemm_bn_act_batched', _dev(x, 'x'), M * K, M, K, _dev(w, 'w'), Cout * K,
+         Cout, _dev(scale, 'scale'), _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'),
+         y.stride(0), B, _stream())
+    return y
+
+
+def maxpool2d(x, k, stride, pad, y):
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = y.shape
+    call('pps_maxpool2d', _dev(x, 'x'), N, H, W, C, k, stride, pad, _dev(y, 'y'), Ho, Wo,
+         _stream())
+    return y
+
+
+def part_power_set(x, split, max_ave, out):
+    N, H, W, C = x.shape
+    split = np.ascontiguousarray(split, dtype=np.int32)
+    call('pps_part_power_set', _dev(x, 'x'), N, H, W, C,
+         split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
+         _dev(out, 'out'), _stream())
+    return out
+
+
+def l2_normalize(x, y=None):
+    N, D = x.shape
+    if y is None:
+        y = torch.empty_like(x)
+    call('pps_l2_normalize', _dev(x, 'x'), N, D, _dev(y, 'y'), _stream())
+    return y
+
+
+def preprocess_bgr(img_u8, pixel_means, out_hw, y=None):
+    """uint8 BGR [N,Hi,Wi,3] (device) -> NHWC4 float32 [N,Ho,Wo,4]."""
+    N, Hi, Wi, C = img_u8.shape
+    assert C == 3
+    Ho, Wo = out_hw
+    if y is None:
+        y = torch.empty((N, Ho, Wo, 4), dtype=torch.float32, device=img_u8.device)
+    m = np.ascontiguousarray(np.asarray(pixel_means, np.float32).ravel()[:3])
+    call('pps_preprocess_bgr', _dev(img_u8, 'img', torch.uint8), N, Hi, Wi,
+         m.ctypes.data_as(_lib.ctypes.c_void_p), Ho, Wo, _dev(y, 'y'), _stream())
+    return y
+
+
+# ---------------------------------------------------------------------------
+# Operator registry (reference Caffe2 op names)
+# ---------------------------------------------------------------------------
+def _op_pairwise_distance(inputs, **args):
+    (X,) = inputs
+    return [pairwise_distance(X)]
+
+
+def _op_normalize(inputs, axis=1, **args):
+    (X,) = inputs
+    if axis != 1 or X.dim() != 2:
+        raise RuntimeError('Normalize: only axis=1 on 2-D input is built')
+    return [l2_normalize(X)]
+
+
+OPS = {
+    'PairWiseDistance': _op_pairwise_distance,
+    'Normalize': _op_normalize,
+}
+
+
+def run_op(name, inputs, **args):
+    """Look up an operator by its reference (Caffe2) name and run it."""
+    if name not in OPS:
+        raise RuntimeError('Operator %s is not registered in pps_amd (have: %s)'
+                           % (name, ', '.join(sorted(OPS))))
+    return OPS[name](inputs, **args)

