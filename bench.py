@@ -120,7 +120,7 @@ def conv_roofline(m, x):
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     return dict(bound='mfma', achieved=round(achieved, 2), peak=PEAK_FP32_MFMA_TFLOPS,
                 unit='TFLOP/s', frac=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (85 launches/forward)',
+                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (54 launches/forward)',
                 launches=n_launch, flops_per_forward=conv_flops,
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2)), per
 
