@@ -43,6 +43,13 @@ const char* pps_last_error(void);
 /* Names of the exported operator-registry entries, ';'-separated (host). */
 const char* pps_registered_ops(void);
 
+/* GEMM tile configurations shared by pps_distmat / pps_conv2d_bn_act /
+ * pps_gemm_bn_act_batched (`tile` argument): 0 = built-in heuristic,
+ * 1 = 128x128 (4 waves), 2 = 128x64, 3 = 64x128, 4 = 64x64, 5 = 256x128
+ * (8 waves).  Results are identical for every tile (same per-element fp32
+ * MFMA accumulation order); only speed differs, so callers may autotune. */
+int pps_gemm_num_tiles(void);
+
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
  * type)` (euclidean branch; cosine is defined as a true distance, the
@@ -52,7 +59,7 @@ const char* pps_registered_ops(void);
  * FP32 MFMA (v_mfma_f32_32x32x2_f32) tiles; squared norms fused. */
 int pps_distmat(const float* q, int64_t Q, int64_t ldq,
                 const float* g, int64_t G, int64_t ldg, int D, int metric,
-                float* out, int64_t ldo, void* stream);
+                float* out, int64_t ldo, int tile, void* stream);
 
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
@@ -119,7 +126,8 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
                       const float* w, int Cout, int Kpad, int KH, int KW,
                       int stride, int pad, int dil, const float* scale,
                       const float* shift, const float* residual, int relu,
-                      float* y, int Ho, int Wo, int ldy, void* stream);
+                      float* y, int Ho, int Wo, int ldy, int tile,
+                      void* stream);
 
 /* Batched variant for the 31 PPS head convs (reid_heads.py:42-79):
  * for b in [0,B): Y[:, b*Cout:(b+1)*Cout] = relu?(X_b W_b^T * scale_b +
@@ -128,7 +136,7 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
 int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
                             const float* w, int64_t w_bstride, int Cout,
                             const float* scale, const float* shift, int relu,
-                            float* y, int ldy, int B, void* stream);
+                            float* y, int ldy, int B, int tile, void* stream);
 
 /* MaxPool kernel k, stride s, pad p (padding never wins), NHWC
  * (ResNet.py:255 `pool1`). */

@@ -20,7 +20,7 @@ c_ptr = ctypes.c_void_p
 # name -> argtypes (all return int status)
 SIGNATURES = {
     'pps_distmat': [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_int, c_int, c_ptr,
-                    c_i64, c_ptr],
+                    c_i64, c_int, c_ptr],
     'pps_pairwise_distance': [c_ptr, c_int, c_int, c_ptr, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
@@ -32,9 +32,9 @@ SIGNATURES = {
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
     'pps_conv2d_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                           c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
-                          c_ptr, c_int, c_int, c_int, c_ptr],
+                          c_ptr, c_int, c_int, c_int, c_int, c_ptr],
     'pps_gemm_bn_act_batched': [c_ptr, c_i64, c_int, c_int, c_ptr, c_i64, c_int, c_ptr,
-                                c_ptr, c_int, c_ptr, c_int, c_int, c_ptr],
+                                c_ptr, c_int, c_ptr, c_int, c_int, c_int, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
                       c_int, c_int, c_ptr],
     'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,
@@ -44,6 +44,7 @@ SIGNATURES = {
 }
 EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
+    'pps_gemm_num_tiles': ([], ctypes.c_int),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),
 }

@@ -44,8 +44,11 @@ const char* pps_registered_ops(void) {
          "ComputeDist;RankCounts;TopK;PrepImForBlob";
 }
 
+int pps_gemm_num_tiles(void) { return GEMM_NUM_TILES - 1; }
+
 int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t G,
-                int64_t ldg, int D, int metric, float* out, int64_t ldo, void* stream) {
+                int64_t ldg, int D, int metric, float* out, int64_t ldo, int tile,
+                void* stream) {
   PPS_ENFORCE(q && g && out, "null pointer");
   PPS_ENFORCE(Q >= 0 && G >= 0 && D > 0, "bad shape");
   PPS_ENFORCE(D % 4 == 0, "D must be a multiple of 4, got " + std::to_string(D));
@@ -60,7 +63,7 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t 
   p.M = (int)Q;
   p.b = g; p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)G;
   p.Kloop = (D + 15) / 16 * 16;
-  p.out = out; p.ldo = ldo; p.metric = metric;
+  p.out = out; p.ldo = ldo; p.metric = metric; p.tile = tile;
   return launch_gemm(p, EPI_DIST, 1, as_stream(stream));
 }
 
@@ -132,7 +135,7 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
                       const float* w, int Cout, int Kpad, int KH, int KW, int stride,
                       int pad, int dil, const float* scale, const float* shift,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
-                      void* stream) {
+                      int tile, void* stream) {
   PPS_ENFORCE(x && w && scale && shift && y, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "bad shape");
   PPS_ENFORCE(Cin % 4 == 0 && ldx % 4 == 0 && ldx >= Cin,
@@ -152,14 +155,14 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
   p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
   p.b = w; p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
-  p.out = y; p.ldo = ldy; p.relu = relu;
+  p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
 }
 
 int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
                             const float* w, int64_t w_bstride, int Cout,
                             const float* scale, const float* shift, int relu, float* y,
-                            int ldy, int B, void* stream) {
+                            int ldy, int B, int tile, void* stream) {
   PPS_ENFORCE(x && w && scale && shift && y, "null pointer");
   PPS_ENFORCE(M > 0 && K > 0 && Cout > 0 && B > 0, "bad shape");
   PPS_ENFORCE(K % 16 == 0, "K must be a multiple of 16");
@@ -172,7 +175,7 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
   p.b = w; p.b_bstride = w_bstride; p.ldb = K; p.kb_valid = K; p.Ncol = Cout;
   p.Kloop = K;
   p.scale = scale; p.shift = shift; p.ss_bstride = Cout;
-  p.out = y; p.ldo = ldy; p.out_bstride = Cout; p.relu = relu;
+  p.out = y; p.ldo = ldy; p.out_bstride = Cout; p.relu = relu; p.tile = tile;
   return launch_gemm(p, EPI_CONV, B, as_stream(stream));
 }
 

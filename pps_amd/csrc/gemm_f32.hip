@@ -172,19 +172,20 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
       fb[j][0] = *reinterpret_cast<const f32x4*>(src);
       fb[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
     }
-    if (EPI == EPI_DIST) {
+    if (EPI & EPI_DIST) {
+      // explicit fma chain: identical rounding for every tile configuration
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        na[i] += fa[i][0].x * fa[i][0].x + fa[i][0].y * fa[i][0].y +
-                 fa[i][0].z * fa[i][0].z + fa[i][0].w * fa[i][0].w +
-                 fa[i][1].x * fa[i][1].x + fa[i][1].y * fa[i][1].y +
-                 fa[i][1].z * fa[i][1].z + fa[i][1].w * fa[i][1].w;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) na[i] = __builtin_fmaf(fa[i][u][e], fa[i][u][e], na[i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        nb[j] += fb[j][0].x * fb[j][0].x + fb[j][0].y * fb[j][0].y +
-                 fb[j][0].z * fb[j][0].z + fb[j][0].w * fb[j][0].w +
-                 fb[j][1].x * fb[j][1].x + fb[j][1].y * fb[j][1].y +
-                 fb[j][1].z * fb[j][1].z + fb[j][1].w * fb[j][1].w;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) nb[j] = __builtin_fmaf(fb[j][u][e], fb[j][u][e], nb[j]);
     }
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -202,28 +203,45 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
 
   // ---- epilogue ------------------------------------------------------------
-  float* __restrict__ out = p.out + batch * p.out_bstride;
-  if (EPI == EPI_CONV) {
-    const float* sc = p.scale + batch * p.ss_bstride;
-    const float* sh = p.shift + batch * p.ss_bstride;
+  // Addresses are a wave-uniform 64-bit tile base + 32-bit per-lane offsets
+  // (SGPR-base global addressing): one VGPR per address, not two.
+  const int64_t tile_off = (int64_t)m0 * p.ldo + n0;
+  float* __restrict__ out = p.out + batch * p.out_bstride + tile_off;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;      // rows valid in this tile
+  const int nrem = p.Ncol - n0;   // cols valid in this tile
+  if (!(EPI & EPI_DIST)) {
+    constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
+    constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
+    const float* sc = p.scale + batch * p.ss_bstride + n0;
+    const float* sh = p.shift + batch * p.ss_bstride + n0;
+    const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+    const int ldr = (int)p.ldr;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * (BN / WN) + j * 32 + r32;
-      if (col >= p.Ncol) continue;
-      const float s_ = sc[col];
-      const float t_ = sh[col];
+      const int c = wn * (BN / WN) + j * 32 + r32;   // column within the tile
+      const bool col_ok = c < nrem;
+      const float s_ = col_ok ? sc[c] : 0.f;
+      const float t_ = col_ok ? sh[c] : 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int rbase = m0 + wm * (BM / WM) + i * 32 + 4 * h;
+        const int rb = wm * (BM / WM) + i * 32 + 4 * h;  // row within the tile
+        float rv[16];
+        if (HAS_RES) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = rb + (r & 3) + 8 * (r >> 2);
+            const bool ok = col_ok && rr < mrem;
+            rv[r] = ok ? res[rr * ldr + c] : 0.f;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < p.M) {
-            float v = acc[i][j][r] * s_ + t_;
-            if (p.residual) v += p.residual[(int64_t)row * p.ldr + col];
-            if (p.relu) v = fmaxf(v, 0.f);
-            out[(int64_t)row * p.ldo + col] = v;
-          }
+          const int rr = rb + (r & 3) + 8 * (r >> 2);
+          float v = __builtin_fmaf(acc[i][j][r], s_, t_);
+          if (HAS_RES) v += rv[r];
+          if (RELU) v = fmaxf(v, 0.f);
+          if (col_ok && rr < mrem) out[rr * ldo + c] = v;
         }
       }
     }
@@ -237,29 +255,29 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
       float qn[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) qn[r] = __shfl(na[i], (r & 3) + 8 * (r >> 2) + 4 * h);
-      const int rbase = m0 + wm * (BM / WM) + i * 32 + 4 * h;
+      const int rb = wm * (BM / WM) + i * 32 + 4 * h;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * (BN / WN) + j * 32 + r32;
-        if (col >= p.Ncol) continue;
+        const int c = wn * (BN / WN) + j * 32 + r32;
+        if (c >= nrem) continue;
         const float gn = nb[j];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < p.M) {
+          const int rr = rb + (r & 3) + 8 * (r >> 2);
+          if (rr < mrem) {
             const float dot = acc[i][j][r];
             float v;
             if (p.metric == PPS_METRIC_COSINE) {
               const float den = fmaxf(sqrtf(qn[r]), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
               v = 1.f - dot / den;
             } else {
-              // reference order: (-2 * a.b) + |a|^2 + |b|^2, clamp at 0
-              v = (-2.f * dot + qn[r]) + gn;
+              // (-2 a.b + |a|^2) + |b|^2 (reference order, fused), clamp at 0
+              v = __builtin_fmaf(-2.f, dot, qn[r]) + gn;
               v = fmaxf(v, 0.f);
               if (p.metric == PPS_METRIC_EUCLIDEAN) v = sqrtf(v);
             }
-            if (p.zero_diag && row == col) v = 0.f;
-            out[(int64_t)row * p.ldo + col] = v;
+            if (p.zero_diag && m0 + rr == n0 + c) v = 0.f;
+            out[rr * ldo + c] = v;
           }
         }
       }
@@ -267,27 +285,65 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
-static int launch_tile(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+template <int BM, int BN, int WM, int WN, int EPI>
+static void launch_one(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  dim3 grid(tiles_m * tiles_n, batch);
-  dim3 block(64 * WM * WN);
-  if (epi == EPI_CONV)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI_CONV>), grid, block, 0,
-                       stream, p, tiles_m, tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI_DIST>), grid, block, 0,
-                       stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>), dim3(tiles_m * tiles_n, batch),
+                     dim3(64 * WM * WN), 0, stream, p, tiles_m, tiles_n);
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_tile(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  switch (epi) {
+    case EPI_DIST: launch_one<BM, BN, WM, WN, EPI_DIST>(p, batch, stream); break;
+    case EPI_CONV: launch_one<BM, BN, WM, WN, EPI_CONV>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU:
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES:
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES | EPI_F_RELU:
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU>(p, batch, stream); break;
+    default:
+      set_error("unknown epilogue");
+      return PPS_ERR_INVALID_ARG;
+  }
   PPS_CHECK_LAUNCH("gemm_f32_kernel");
   return PPS_OK;
 }
 
+static int ntiles(const GemmParams& p, int bm, int bn, int batch) {
+  return ((p.M + bm - 1) / bm) * ((p.Ncol + bn - 1) / bn) * batch;
+}
+
+// Heuristic tile choice (tile == 0): enough workgroups to fill 256 CUs at
+// >= 2 per CU, else fall back to narrower tiles.  PPSModel.autotune()
+// measures every candidate per layer and passes the winner explicitly.
+int pick_tile(const GemmParams& p, int batch) {
+  if (p.Ncol <= 64) return GEMM_TILE_128x64;
+  if (p.M <= 64) return GEMM_TILE_64x128;
+  if (ntiles(p, 128, 128, batch) >= 512) return GEMM_TILE_128x128;
+  if (ntiles(p, 128, 64, batch) >= 512) return GEMM_TILE_128x64;
+  return GEMM_TILE_64x64;
+}
+
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   if (p.M <= 0 || p.Ncol <= 0 || batch <= 0) return PPS_OK;
-  if (p.Ncol <= 64) return launch_tile<128, 64, 4, 1>(p, epi, batch, stream);
-  if (p.M <= 64) return launch_tile<64, 128, 1, 4>(p, epi, batch, stream);
-  return launch_tile<128, 128, 2, 2>(p, epi, batch, stream);
+  if (!(epi & EPI_DIST)) {
+    if (p.residual) epi |= EPI_F_RES;
+    if (p.relu) epi |= EPI_F_RELU;
+  }
+  const int tile = p.tile ? p.tile : pick_tile(p, batch);
+  switch (tile) {
+    case GEMM_TILE_128x128: return launch_tile<128, 128, 2, 2>(p, epi, batch, stream);
+    case GEMM_TILE_128x64: return launch_tile<128, 64, 4, 1>(p, epi, batch, stream);
+    case GEMM_TILE_64x128: return launch_tile<64, 128, 1, 4>(p, epi, batch, stream);
+    case GEMM_TILE_64x64: return launch_tile<64, 64, 2, 2>(p, epi, batch, stream);
+    case GEMM_TILE_256x128: return launch_tile<256, 128, 4, 2>(p, epi, batch, stream);
+    default:
+      set_error("unknown GEMM tile id " + std::to_string(tile));
+      return PPS_ERR_INVALID_ARG;
+  }
 }
 
 }  // namespace pps

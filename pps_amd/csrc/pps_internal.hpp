@@ -36,7 +36,16 @@ inline bool aligned16(const void* p) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- GEMM core (gemm_f32.hip) ----------------------------------------------
-enum Epi { EPI_CONV = 0, EPI_DIST = 1 };
+enum Epi { EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4 };
+enum GemmTile {
+  GEMM_TILE_AUTO = 0,
+  GEMM_TILE_128x128 = 1,
+  GEMM_TILE_128x64 = 2,
+  GEMM_TILE_64x128 = 3,
+  GEMM_TILE_64x64 = 4,
+  GEMM_TILE_256x128 = 5,
+  GEMM_NUM_TILES = 6
+};
 
 struct GemmParams {
   // A operand: implicit im2col over an NHWC tensor (plain rows: H=1, W=M,
@@ -65,8 +74,10 @@ struct GemmParams {
   int relu;
   int metric;
   int zero_diag;
+  int tile;  // GemmTile; 0 = heuristic
 };
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
+int pick_tile(const GemmParams& p, int batch);
 
 }  // namespace pps

@@ -324,6 +324,30 @@ class PPSModel(object):
     def flops_per_forward(self, kinds=('conv', 'heads')):
         return sum(L['flops'] for L in self.layers if L['op'] in kinds)
 
+    def _run(self, L, bufs, out=None, tile=None):
+        op = L['op']
+        tile = L.get('tile', 0) if tile is None else tile
+        if op == 'conv':
+            res = bufs[L['residual']] if L['residual'] else None
+            ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+                              L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
+                              res, L['relu'], bufs[L['output']], tile=tile)
+        elif op == 'maxpool':
+            ops.maxpool2d(bufs[L['input']], L['k'], L['stride'], L['pad'],
+                          bufs[L['output']])
+        elif op == 'pps':
+            ops.part_power_set(bufs[L['input']], L['split_arr'], L['max_ave'],
+                               bufs[L['output']])
+        elif op == 'heads':
+            y = bufs[L['output']] if out is None or self.layers[-1] is not L else out
+            ops.gemm_bn_act_batched(bufs[L['input']], L['w'], L['scale'], L['shift'], True,
+                                    y, tile=tile)
+            bufs[L['output']] = y
+        elif op == 'normalize':
+            y = out if out is not None else bufs[L['output']]
+            ops.l2_normalize(bufs[L['input']], y)
+            bufs[L['output']] = y
+
     def forward(self, x, out=None, timer=None):
         """Run the plan.  `timer`, if a list, receives (layer, op, flops,
         start_event, end_event) per layer, recorded on the current stream."""
@@ -335,34 +359,42 @@ class PPSModel(object):
         bufs = dict(self._bufs)
         bufs['data'] = x
         for L in self.layers:
-            op = L['op']
             if timer is not None:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
-            if op == 'conv':
-                xi = bufs[L['input']]
-                y = bufs[L['output']]
-                res = bufs[L['residual']] if L['residual'] else None
-                ops.conv2d_bn_act(xi, L['cin_eff'], L['w'], L['kpad'], L['k'],
-                                  L['stride'], L['pad'], L['dil'], L['scale'],
-                                  L['shift'], res, L['relu'], y)
-            elif op == 'maxpool':
-                ops.maxpool2d(bufs[L['input']], L['k'], L['stride'], L['pad'],
-                              bufs[L['output']])
-            elif op == 'pps':
-                ops.part_power_set(bufs[L['input']], L['split_arr'], L['max_ave'],
-                                   bufs[L['output']])
-            elif op == 'heads':
-                xs = bufs[L['input']]
-                y = bufs[L['output']] if out is None or self.layers[-1] is not L else out
-                ops.gemm_bn_act_batched(xs, L['w'], L['scale'], L['shift'], True, y)
-                bufs[L['output']] = y
-            elif op == 'normalize':
-                y = out if out is not None else bufs[L['output']]
-                ops.l2_normalize(bufs[L['input']], y)
-                bufs[L['output']] = y
+            self._run(L, bufs, out)
             if timer is not None:
                 ev1.record()
-                timer.append((L.get('name', L['output']), op, L['flops'], ev0, ev1))
+                timer.append((L.get('name', L['output']), L['op'], L['flops'], ev0, ev1))
         return bufs[self.plan.output]
+
+    def autotune(self, x, reps=3, tiles=None):
+        """Pick the fastest GEMM tile per conv layer by timing every candidate
+        on this device (the cudnn_exhaustive_search analogue of the
+        reference's DetectionModelHelper, detector.py:58).  Results do not
+        depend on the tile (same per-element accumulation order)."""
+        self.forward(x)
+        torch.cuda.synchronize()
+        bufs = dict(self._bufs)
+        bufs['data'] = x
+        cands = list(tiles or range(1, ops.num_tiles() + 1))
+        report = {}
+        for L in self.layers:
+            if L['op'] not in ('conv', 'heads'):
+                continue
+            times = {}
+            for t in cands:
+                for _ in range(2):
+                    self._run(L, bufs, tile=t)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    self._run(L, bufs, tile=t)
+                e1.record()
+                e1.synchronize()
+                times[t] = e0.elapsed_time(e1) / reps
+            L['tile'] = min(times, key=times.get)
+            report[L.get('name', L['output'])] = (L['tile'], times)
+        return report

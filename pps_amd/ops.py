@@ -16,6 +16,10 @@ from . import _lib
 from ._lib import METRICS, call
 
 
+def num_tiles():
+    return _lib.lib().pps_gemm_num_tiles()
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -36,7 +40,7 @@ def _dev(t, name, dtype=torch.float32):
 # ---------------------------------------------------------------------------
 # Retrieval
 # ---------------------------------------------------------------------------
-def compute_dist(q, g, metric='euclidean', out=None):
+def compute_dist(q, g, metric='euclidean', out=None, tile=0):
     """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244)."""
     if q.dim() != 2 or g.dim() != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
@@ -46,7 +50,7 @@ def compute_dist(q, g, metric='euclidean', out=None):
     if out is None:
         out = torch.empty((Q, G), dtype=torch.float32, device=q.device)
     call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
-         _dev(out, 'out'), out.stride(0), _stream())
+         _dev(out, 'out'), out.stride(0), int(tile), _stream())
     return out
 
 
@@ -141,7 +145,8 @@ def max_positives(qid, qcam, gid, gcam):
 # ---------------------------------------------------------------------------
 # Feature extractor
 # ---------------------------------------------------------------------------
-def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, relu, y):
+def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, relu, y,
+                  tile=0):
     N, H, W, ldx = x.shape
     _, Ho, Wo, Cout = y.shape
     rp = 0
@@ -152,17 +157,17 @@ def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, 
         rp = _dev(residual, 'residual')
     call('pps_conv2d_bn_act', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w, 'w'), Cout, kpad,
          k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
-         int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, _stream())
+         int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile), _stream())
     return y
 
 
-def gemm_bn_act_batched(x, w, scale, shift, relu, y):
+def gemm_bn_act_batched(x, w, scale, shift, relu, y, tile=0):
     """x [B,M,K], w [B,Cout,K] -> y [M, B*Cout] (PPS head convs)."""
     B, M, K = x.shape
     Cout = w.shape[1]
     call('pps_gemm_bn_act_batched', _dev(x, 'x'), M * K, M, K, _dev(w, 'w'), Cout * K,
          Cout, _dev(scale, 'scale'), _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'),
-         y.stride(0), B, _stream())
+         y.stride(0), B, int(tile), _stream())
     return y
 
 

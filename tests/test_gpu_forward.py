@@ -45,10 +45,16 @@ def test_conv2d_bn_act(N, H, W, Cin, Cout, k, s, p, residual):
         res = _cuda(res_np.transpose(0, 2, 3, 1))
     ref = torch.clamp_min(ref, 0).numpy().transpose(0, 2, 3, 1)
     wp, kpad = model.pack_conv_weight(w)
-    y = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
-    ops.conv2d_bn_act(_cuda(x.transpose(0, 2, 3, 1)), Cin, _cuda(wp), kpad, k, s, p, 1,
-                      _cuda(scale), _cuda(shift), res, True, y)
-    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
+    outs = []
+    for tile in range(0, ops.num_tiles() + 1):
+        y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+        ops.conv2d_bn_act(_cuda(x.transpose(0, 2, 3, 1)), Cin, _cuda(wp), kpad, k, s, p, 1,
+                          _cuda(scale), _cuda(shift), res, True, y, tile=tile)
+        got = y.cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4, err_msg='tile %d' % tile)
+        outs.append(got)
+    for o in outs[1:]:   # tile choice must not change a single bit
+        np.testing.assert_array_equal(o, outs[0])
 
 
 def test_maxpool():

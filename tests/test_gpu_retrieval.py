@@ -36,9 +36,15 @@ def test_distmat_ragged_shapes(Q, G, D, metric):
     q = rng.randn(Q, D).astype(np.float32)
     g = rng.randn(G, D).astype(np.float32)
     ref = ev.compute_dist(q, g, metric)
-    d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric).cpu().numpy()
     scale = max(1.0, float(np.abs(ref).max()))
-    np.testing.assert_allclose(d, ref, rtol=0, atol=2e-5 * scale * np.sqrt(D / 128.0))
+    first = None
+    for tile in range(0, ops.num_tiles() + 1):
+        d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric, tile=tile).cpu().numpy()
+        np.testing.assert_allclose(d, ref, rtol=0, atol=2e-5 * scale * np.sqrt(D / 128.0),
+                                   err_msg='tile %d' % tile)
+        if first is None:
+            first = d
+        np.testing.assert_array_equal(d, first)
 
 
 def test_distmat_enforces_shapes():
