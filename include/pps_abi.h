@@ -167,6 +167,13 @@ int pps_l2_normalize(const float* x, int64_t N, int D, float* y,
 int pps_preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi,
                        const float* pixel_means, int Ho, int Wo, float* y,
                        void* stream);
+/* Same for a ragged batch of images of different sizes packed in one device
+ * blob: image n starts at byte offsets[n] and is heights[n] x widths[n] x 3
+ * (offsets / heights / widths are DEVICE arrays). */
+int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets,
+                              const int32_t* heights, const int32_t* widths,
+                              const float* pixel_means, int Ho, int Wo, float* y,
+                              void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,82 @@
+"""ORACLE (test infrastructure only) -- NumPy restatement of the count-based
+rank evaluation kernels in pps_amd/csrc/rank.hip, used as a CPU backend so the
+gallery-sharded collective logic (pps_amd/distributed.py) can be tested with
+torch.distributed gloo, world_size > 1, without a GPU.  Same semantics as the
+HIP kernels: positives = same id & different cam; junk = same id & same cam;
+stable (distance, global gallery index) order; counts additive over shards.
+"""
+import numpy as np
+import torch
+
+from oracle import evaluator as ev
+
+
+class CpuBackend(object):
+    device = 'cpu'
+
+    @staticmethod
+    def distmat(q, g, metric):
+        return torch.from_numpy(ev.compute_dist(q.numpy(), g.numpy(), metric))
+
+    @staticmethod
+    def collect(dist, qid, qcam, gid, gcam, g_offset, pmax):
+        d, qi, qc, gi, gc = (t.numpy() for t in (dist, qid, qcam, gid, gcam))
+        Q = d.shape[0]
+        pos_d = np.zeros((Q, pmax), np.float32)
+        pos_idx = np.zeros((Q, pmax), np.int32)
+        cnt = np.zeros(Q, np.int32)
+        for q in range(Q):
+            hit = np.nonzero((gi == qi[q]) & (gc != qc[q]))[0]
+            cnt[q] = len(hit)
+            k = min(len(hit), pmax)
+            pos_d[q, :k] = d[q, hit[:k]]
+            pos_idx[q, :k] = hit[:k] + g_offset
+        return torch.from_numpy(pos_d), torch.from_numpy(pos_idx), torch.from_numpy(cnt)
+
+    @staticmethod
+    def counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt):
+        d, qi, qc, gi, gc = (t.numpy() for t in (dist, qid, qcam, gid, gcam))
+        pd, px, pc = pos_d.numpy(), pos_idx.numpy(), pos_cnt.numpy()
+        R, Q, pmax = pd.shape
+        ptot = R * pmax
+        sd = np.full((Q, ptot), np.inf, np.float32)
+        si = np.full((Q, ptot), -1, np.int32)
+        total = np.zeros(Q, np.int32)
+        hist = np.zeros((Q, ptot), np.int32)
+        before = np.zeros(Q, np.int32)
+        G = d.shape[1]
+        gidx = np.arange(G) + g_offset
+        for q in range(Q):
+            vals = [(pd[r, q, p], px[r, q, p]) for r in range(R)
+                    for p in range(min(pc[r, q], pmax))]
+            vals.sort()
+            P = len(vals)
+            total[q] = P
+            if P == 0:
+                continue
+            sd[q, :P] = [v[0] for v in vals]
+            si[q, :P] = [v[1] for v in vals]
+            valid = ~((gi == qi[q]) & (gc == qc[q]))
+            dv = d[q, valid]
+            lb = np.searchsorted(sd[q, :P], dv, side='left')
+            np.add.at(hist[q], lb[lb < P], 1)
+            df, idf = sd[q, 0], si[q, 0]
+            before[q] = np.sum((dv < df) | ((dv == df) & (gidx[valid] < idf)))
+        return (torch.from_numpy(sd), torch.from_numpy(si), torch.from_numpy(total),
+                torch.from_numpy(hist), torch.from_numpy(before))
+
+    @staticmethod
+    def finalize(sorted_d, pos_total, hist, before):
+        sd, tot, h, b = (t.numpy() for t in (sorted_d, pos_total, hist, before))
+        Q = sd.shape[0]
+        ap = np.zeros(Q)
+        valid = (tot > 0).astype(np.int32)
+        first = np.where(tot > 0, b, -1).astype(np.int32)
+        for q in range(Q):
+            P = tot[q]
+            if P == 0:
+                continue
+            le = np.cumsum(h[q, :P])
+            pos_le = np.searchsorted(sd[q, :P], sd[q, :P], side='right')
+            ap[q] = np.sum(pos_le / le) / P
+        return torch.from_numpy(ap), torch.from_numpy(valid), torch.from_numpy(first)

@@ -41,6 +41,8 @@ SIGNATURES = {
                            c_ptr],
     'pps_l2_normalize': [c_ptr, c_i64, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr': [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr],
+    'pps_preprocess_bgr_ragged': [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int,
+                                  c_ptr, c_ptr],
 }
 EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),

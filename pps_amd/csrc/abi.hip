@@ -16,8 +16,8 @@ int maxpool2d(const float*, int, int, int, int, int, int, int, float*, int, int,
 int part_power_set(const float*, int, int, int, int, const int32_t*, int, int, float*,
                    hipStream_t);
 int l2_normalize(const float*, int64_t, int, float*, hipStream_t);
-int preprocess_bgr(const uint8_t*, int, int, int, const float*, int, int, float*,
-                   hipStream_t);
+int preprocess_bgr(const uint8_t*, int, int, int, const int64_t*, const int32_t*,
+                   const int32_t*, const float*, int, int, float*, hipStream_t);
 int collect_positives(const float*, int64_t, int64_t, int64_t, const int32_t*,
                       const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
                       int32_t*, int32_t*, hipStream_t);
@@ -212,7 +212,18 @@ int pps_preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const float* m
   PPS_ENFORCE(img && means && y, "null pointer");
   PPS_ENFORCE(N >= 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "bad shape");
   PPS_ENFORCE(aligned16(y), "y must be 16-byte aligned");
-  return preprocess_bgr(img, N, Hi, Wi, means, Ho, Wo, y, as_stream(stream));
+  return preprocess_bgr(img, N, Hi, Wi, nullptr, nullptr, nullptr, means, Ho, Wo, y,
+                        as_stream(stream));
+}
+
+int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets,
+                              const int32_t* heights, const int32_t* widths,
+                              const float* means, int Ho, int Wo, float* y, void* stream) {
+  PPS_ENFORCE(blob && offsets && heights && widths && means && y, "null pointer");
+  PPS_ENFORCE(N >= 0 && Ho > 0 && Wo > 0, "bad shape");
+  PPS_ENFORCE(aligned16(y), "y must be 16-byte aligned");
+  return preprocess_bgr(blob, N, 0, 0, offsets, heights, widths, means, Ho, Wo, y,
+                        as_stream(stream));
 }
 
 }  // extern "C"

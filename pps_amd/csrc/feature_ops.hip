@@ -172,16 +172,31 @@ struct Means {
   float m[3];
 };
 
-__global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ img, int N, int Hi,
-                                      int Wi, Means mean, int Ho, int Wo,
-                                      float* __restrict__ y) {
+// One thread per output pixel.  Images are either a dense [N][Hi][Wi][3]
+// batch (offsets == nullptr) or a ragged blob described per image by a byte
+// offset and its own height / width (device arrays), as decoded JPEGs of a
+// dataset with mixed sizes (DukeMTMC-reID) arrive.
+__global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, int Hi0,
+                                      int Wi0, const int64_t* __restrict__ offsets,
+                                      const int32_t* __restrict__ heights,
+                                      const int32_t* __restrict__ widths, Means mean,
+                                      int Ho, int Wo, float* __restrict__ y) {
   const int64_t total = (int64_t)N * Ho * Wo;
-  const float sx = (float)Wi / (float)Wo, sy = (float)Hi / (float)Ho;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int ox = (int)(t % Wo);
     const int oy = (int)((t / Wo) % Ho);
     const int n = (int)(t / ((int64_t)Wo * Ho));
+    int Hi = Hi0, Wi = Wi0;
+    const uint8_t* img;
+    if (offsets) {
+      Hi = heights[n];
+      Wi = widths[n];
+      img = blob + offsets[n];
+    } else {
+      img = blob + (int64_t)n * Hi * Wi * 3;
+    }
+    const float sx = (float)Wi / (float)Wo, sy = (float)Hi / (float)Ho;
     const float fx = (ox + 0.5f) * sx - 0.5f;
     const float fy = (oy + 0.5f) * sy - 0.5f;
     const int x0 = (int)floorf(fx), y0 = (int)floorf(fy);
@@ -194,7 +209,7 @@ __global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ img, int N, in
       float row[3] = {0.f, 0.f, 0.f};
       for (int i = 0; i < 4; ++i) {
         const int xx = min(max(x0 - 1 + i, 0), Wi - 1);
-        const uint8_t* px = img + (((int64_t)n * Hi + yy) * Wi + xx) * 3;
+        const uint8_t* px = img + ((int64_t)yy * Wi + xx) * 3;
 #pragma unroll
         for (int c = 0; c < 3; ++c) row[c] += wx[i] * ((float)px[c] - mean.m[c]);
       }
@@ -205,8 +220,9 @@ __global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ img, int N, in
   }
 }
 
-int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const float* means, int Ho,
-                   int Wo, float* y, hipStream_t st) {
+int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* offsets,
+                   const int32_t* heights, const int32_t* widths, const float* means,
+                   int Ho, int Wo, float* y, hipStream_t st) {
   Means m;
   for (int c = 0; c < 3; ++c) m.m[c] = means[c];
   const int64_t total = (int64_t)N * Ho * Wo;
@@ -214,7 +230,7 @@ int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const float* means
   const int grid = (int)(want < 8192 ? want : 8192);
   if (grid == 0) return PPS_OK;
   hipLaunchKernelGGL(preprocess_bgr_kernel, dim3(grid), dim3(256), 0, st, img, N, Hi, Wi,
-                     m, Ho, Wo, y);
+                     offsets, heights, widths, m, Ho, Wo, y);
   PPS_CHECK_LAUNCH("preprocess_bgr_kernel");
   return PPS_OK;
 }

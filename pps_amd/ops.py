@@ -236,3 +236,18 @@ def run_op(name, inputs, **args):
         raise RuntimeError('Operator %s is not registered in pps_amd (have: %s)'
                            % (name, ', '.join(sorted(OPS))))
     return OPS[name](inputs, **args)
+
+
+def preprocess_bgr_ragged(blob_u8, offsets, heights, widths, pixel_means, out_hw, y=None):
+    """Ragged batch: blob_u8 flat uint8 device tensor; offsets int64 [N],
+    heights/widths int32 [N] device tensors -> NHWC4 float32 [N,Ho,Wo,4]."""
+    N = offsets.shape[0]
+    Ho, Wo = out_hw
+    if y is None:
+        y = torch.empty((N, Ho, Wo, 4), dtype=torch.float32, device=blob_u8.device)
+    m = np.ascontiguousarray(np.asarray(pixel_means, np.float32).ravel()[:3])
+    call('pps_preprocess_bgr_ragged', _dev(blob_u8, 'blob', torch.uint8), N,
+         _dev(offsets, 'offsets', torch.int64), _dev(heights, 'heights', torch.int32),
+         _dev(widths, 'widths', torch.int32), m.ctypes.data_as(_lib.ctypes.c_void_p), Ho, Wo,
+         _dev(y, 'y'), _stream())
+    return y

@@ -1,0 +1,243 @@
+"""Test-time driver: images -> features -> retrieval metrics, on MI355X.
+
+Same entry points and signatures as the reference's
+detectron/core/test_engine.py:
+  run_inference(weights_file, ind_range=None, multi_gpu_testing=False,
+                gpu_id=0, check_expected_results=False)          :91-143
+  test_net_on_dataset(weights_file, dataset_name, proposal_file,
+                      output_dir, multi_gpu=False, gpu_id=0)      :146-181
+  test_net(weights_file, dataset_name, proposal_file, output_dir,
+           ind_range=None, gpu_id=0)  -> ndarray [N, 3968]          :259-370
+  initialize_model_from_cfg(weights_file, gpu_id=0)                 :390-405
+and the result dict of task_evaluation.py:54-60,345-359.
+
+MI355X-first differences (SURVEY §3.1 hot loop): the reference runs one image
+per RunNet with two host<->device copies per image (test.py:163-185).  Here a
+thread pool decodes JPEGs for batch b+1 while the GPU runs batch b; each batch
+is one pinned-memory H2D copy of the raw uint8 pixels, then the preprocessing
+kernel (mean-subtract + bicubic), the ResNet-50 / PPS kernels and the
+normalisation run on the device, and features stay in HBM for the
+evaluation.  Multi-GPU uses one process per GPU (torch.distributed over RCCL)
+instead of subprocess + pickle files (utils/subprocess.py:39-103).
+"""
+import concurrent.futures as futures
+import logging
+import os
+import time
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import distributed as pdist
+from . import model as pmodel
+from . import ops
+from . import reid_dataset_evaluator as rde
+from .config import cfg
+from .json_dataset import JsonDataset
+from .weights import check_complete, load_weights
+
+logger = logging.getLogger(__name__)
+
+
+def get_output_dir(dataset_name, training=False):
+    if os.sep in dataset_name:  # a json path used as the dataset name
+        dataset_name = os.path.splitext(os.path.basename(dataset_name))[0]
+    d = os.path.join(cfg.OUTPUT_DIR, 'test' if not training else 'train', dataset_name)
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def initialize_model_from_cfg(weights_file, gpu_id=0, trusted=False, blobs=None):
+    """test_engine.py:390-405: build the test net and load its weights."""
+    torch.cuda.set_device(gpu_id)
+    plan = pmodel.build_plan()
+    if blobs is None:
+        blobs = load_weights(weights_file, trusted=trusted)
+    check_complete(blobs, plan)
+    return pmodel.PPSModel(blobs, device='cuda:%d' % gpu_id, plan=plan)
+
+
+def _decode_bgr(path):
+    """cv2.imread(path, IMREAD_COLOR) equivalent: uint8 HxWx3, BGR order."""
+    from PIL import Image
+    with Image.open(path) as im:
+        rgb = np.asarray(im.convert('RGB'), dtype=np.uint8)
+    return np.ascontiguousarray(rgb[..., ::-1])
+
+
+class BatchFeeder(object):
+    """Decode on CPU threads, stage raw pixels in pinned memory, one async H2D
+    copy per batch, preprocess on the GPU.  `source(i)` returns image i as a
+    uint8 BGR array (a path list uses _decode_bgr)."""
+
+    def __init__(self, source, n, batch, workers=8):
+        self.source, self.n, self.batch = source, n, batch
+        self.pool = futures.ThreadPoolExecutor(max_workers=workers)
+        self.H, self.W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
+        self.means = np.asarray(cfg.PIXEL_MEANS, np.float32).ravel()
+        self.copy_stream = torch.cuda.Stream()
+
+    def _decode_batch(self, start):
+        idx = range(start, min(start + self.batch, self.n))
+        return list(self.pool.map(self.source, idx))
+
+    def _stage(self, ims):
+        sizes = [im.size for im in ims]
+        offs = np.zeros(len(ims), np.int64)
+        offs[1:] = np.cumsum(sizes)[:-1]
+        blob = torch.empty(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
+        view = blob.numpy()
+        for im, o in zip(ims, offs):
+            view[o:o + im.size] = im.ravel()
+        meta = torch.from_numpy(np.stack([offs, [im.shape[0] for im in ims],
+                                          [im.shape[1] for im in ims]])).pin_memory()
+        with torch.cuda.stream(self.copy_stream):
+            dblob = blob.to('cuda', non_blocking=True)
+            dmeta = meta.to('cuda', non_blocking=True)
+            done = torch.cuda.Event()
+            done.record()
+        return dblob, dmeta, done, blob, meta
+
+    def __iter__(self):
+        starts = list(range(0, self.n, self.batch))
+        pending = self.pool.submit(self._decode_batch, starts[0]) if starts else None
+        for k, s in enumerate(starts):
+            ims = pending.result()
+            if k + 1 < len(starts):
+                pending = self.pool.submit(self._decode_batch, starts[k + 1])
+            dblob, dmeta, done, _hb, _hm = self._stage(ims)
+            torch.cuda.current_stream().wait_event(done)
+            offs = dmeta[0].contiguous()
+            hs = dmeta[1].to(torch.int32).contiguous()
+            ws = dmeta[2].to(torch.int32).contiguous()
+            x = ops.preprocess_bgr_ragged(dblob, offs, hs, ws, self.means, (self.H, self.W))
+            dblob.record_stream(torch.cuda.current_stream())
+            yield s, x
+
+
+def extract_features(model, source, n, batch=None, out=None):
+    """Features [n, D] (device tensor) for images source(0..n-1)."""
+    batch = batch or int(cfg.TEST.get('IMS_PER_BATCH', 64))
+    feats = out if out is not None else torch.empty((n, model.feat_dim),
+                                                    dtype=torch.float32, device='cuda')
+    for s, x in BatchFeeder(source, n, batch):
+        f = model.forward(x)
+        feats[s:s + x.shape[0]].copy_(f)
+    return feats
+
+
+def get_roidb_and_dataset(dataset_name, ind_range):
+    """test_engine.py:408-425 (sorted roidb, optional [start, end) range)."""
+    dataset = JsonDataset(dataset_name)
+    roidb = dataset.get_roidb(gt=True)
+    if ind_range is not None:
+        start, end = ind_range
+        roidb = roidb[start:end]
+    else:
+        start, end = 0, len(roidb)
+    return roidb, dataset, start, end, len(roidb)
+
+
+def test_net(weights_file, dataset_name, proposal_file, output_dir, ind_range=None,
+             gpu_id=0, model=None, trusted=False):
+    """test_engine.py:259-370: features of every image in the (range of the)
+    dataset, [N, 3968] float32 on the host; also written to output_dir as
+    features.npy (the reference's features.pkl held {'all_feats', 'cfg'})."""
+    roidb, dataset, start, end, total = get_roidb_and_dataset(dataset_name, ind_range)
+    if model is None:
+        model = initialize_model_from_cfg(weights_file, gpu_id, trusted=trusted)
+    paths = [e['image'] for e in roidb]
+    t0 = time.time()
+    feats = extract_features(model, lambda i: _decode_bgr(paths[i]), len(paths))
+    torch.cuda.synchronize()
+    logger.info('im_detect: %d images in %.2fs (%.1f img/s)', len(paths),
+                time.time() - t0, len(paths) / max(time.time() - t0, 1e-9))
+    all_feats = feats.cpu().numpy()
+    name = 'features.npy' if ind_range is None else 'feature_range_%s_%s.npy' % (start, end)
+    np.save(os.path.join(output_dir, name), all_feats)
+    return all_feats
+
+
+def _split_qg(roidb):
+    info = [rde.get_info(e) for e in roidb]
+    ids = np.array([i[0] for i in info])
+    cams = np.array([i[1] for i in info])
+    marks = np.array([i[3] for i in info])
+    return ids, cams, marks
+
+
+def multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir, trusted=False):
+    """One process per GPU (already launched by torch.distributed.run).
+    Queries and gallery are split separately into contiguous shards; every
+    rank extracts its shards, then the gallery-sharded evaluator runs
+    (SURVEY §8(e)).  Returns (results dict on every rank)."""
+    rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
+    local = int(os.environ.get('LOCAL_RANK', rank))
+    roidb, dataset, _, _, _ = get_roidb_and_dataset(dataset_name, None)
+    ids, cams, marks = _split_qg(roidb)
+    model = initialize_model_from_cfg(weights_file, local, trusted=trusted)
+    q_idx, g_idx = np.nonzero(marks == 0)[0], np.nonzero(marks == 1)[0]
+    qa, qb = pdist.shard_range(len(q_idx), rank, world)
+    ga, gb = pdist.shard_range(len(g_idx), rank, world)
+    paths = [e['image'] for e in roidb]
+    qp = [paths[i] for i in q_idx[qa:qb]]
+    gp = [paths[i] for i in g_idx[ga:gb]]
+    qf = extract_features(model, lambda i: _decode_bgr(qp[i]), len(qp))
+    gf = extract_features(model, lambda i: _decode_bgr(gp[i]), len(gp))
+    ev = pdist.ShardedEvaluator(ids[q_idx], cams[q_idx], ids[g_idx], cams[g_idx], rank,
+                                world)
+    res = ev.run(qf, gf)
+    if rank == 0:
+        print('{:<30}'.format('Single Query:'), end='')
+        rde.print_scores(res['mAP'], res['cmc'])
+    return _reid_results(dataset.name, (res['mAP'], res['cmc'], None, None))
+
+
+def _reid_results(name, s):
+    """task_evaluation.py:345-359."""
+    r = OrderedDict([('mAP', -1), ('CMC1', -1), ('CMC5', -1), ('CMC10', -1),
+                     ('mq_mAP', -1), ('mq_CMC1', -1), ('mq_CMC5', -1), ('mq_CMC10', -1)])
+    r['mAP'], r['CMC1'], r['CMC5'], r['CMC10'] = s[0], s[1][0], s[1][4], s[1][9]
+    if s[2] is not None:
+        r['mq_mAP'] = s[2]
+    if s[3] is not None:
+        r['mq_CMC1'], r['mq_CMC5'], r['mq_CMC10'] = s[3][0], s[3][4], s[3][9]
+    return OrderedDict([(name, OrderedDict(ReID=r))])
+
+
+def evaluate_reid(dataset, all_feats, output_dir):
+    """task_evaluation.py:54-60."""
+    s = rde.evaluate(dataset, all_feats, output_dir)
+    return _reid_results(dataset.name, s)
+
+
+def test_net_on_dataset(weights_file, dataset_name, proposal_file, output_dir,
+                        multi_gpu=False, gpu_id=0, trusted=False):
+    """test_engine.py:146-181."""
+    if multi_gpu and torch.distributed.is_initialized() and \
+            torch.distributed.get_world_size() > 1:
+        return multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir,
+                                             trusted=trusted)
+    dataset = JsonDataset(dataset_name)
+    t0 = time.time()
+    all_feats = test_net(weights_file, dataset_name, proposal_file, output_dir,
+                         gpu_id=gpu_id, trusted=trusted)
+    logger.info('Total inference time: {:.3f}s'.format(time.time() - t0))
+    return evaluate_reid(dataset, all_feats, output_dir)
+
+
+def run_inference(weights_file, ind_range=None, multi_gpu_testing=False, gpu_id=0,
+                  check_expected_results=False, trusted=False):
+    """test_engine.py:91-143."""
+    if ind_range is not None:  # child case: features of one range only
+        name = cfg.TEST.DATASETS[0]
+        return test_net(weights_file, name, None, get_output_dir(name), ind_range=ind_range,
+                        gpu_id=gpu_id, trusted=trusted)
+    all_results = OrderedDict()
+    for name in cfg.TEST.DATASETS:
+        all_results.update(test_net_on_dataset(weights_file, name, None,
+                                               get_output_dir(name),
+                                               multi_gpu=multi_gpu_testing,
+                                               gpu_id=gpu_id, trusted=trusted))
+    return all_results

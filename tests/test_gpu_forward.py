@@ -154,3 +154,33 @@ def test_full_forward_vs_oracle():
                                kept['reid_feature_concat'].numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(out, ref.numpy(), rtol=0, atol=2e-5)
     np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
+
+
+def test_preprocess_vs_oracle():
+    from oracle import preprocess as pre
+    from pps_amd import ops
+    rng = np.random.RandomState(5)
+    imgs = rng.randint(0, 256, (3, 128, 64, 3)).astype(np.uint8)
+    y = ops.preprocess_bgr(torch.from_numpy(imgs).cuda(), pre.PIXEL_MEANS, (384, 128))
+    y = y.cpu().numpy()
+    assert np.all(y[..., 3] == 0)
+    for n in range(3):
+        ref = pre.prep_im_for_blob(imgs[n])
+        np.testing.assert_allclose(y[n, ..., :3], ref, rtol=0, atol=2e-3)
+
+
+def test_preprocess_ragged_matches_dense():
+    from oracle import preprocess as pre
+    from pps_amd import ops
+    rng = np.random.RandomState(6)
+    shapes = [(128, 64), (97, 41), (250, 100), (128, 64)]
+    ims = [rng.randint(0, 256, (h, w, 3)).astype(np.uint8) for h, w in shapes]
+    blob = np.concatenate([im.ravel() for im in ims])
+    offs = np.cumsum([0] + [im.size for im in ims])[:-1].astype(np.int64)
+    y = ops.preprocess_bgr_ragged(torch.from_numpy(blob).cuda(),
+                                  torch.from_numpy(offs).cuda(),
+                                  torch.tensor([s[0] for s in shapes], dtype=torch.int32).cuda(),
+                                  torch.tensor([s[1] for s in shapes], dtype=torch.int32).cuda(),
+                                  pre.PIXEL_MEANS, (384, 128)).cpu().numpy()
+    for n, im in enumerate(ims):
+        np.testing.assert_allclose(y[n, ..., :3], pre.prep_im_for_blob(im), rtol=0, atol=2e-3)
