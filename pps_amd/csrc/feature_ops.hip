@@ -196,9 +196,10 @@ __global__ void preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, i
     } else {
       img = blob + (int64_t)n * Hi * Wi * 3;
     }
-    const float sx = (float)Wi / (float)Wo, sy = (float)Hi / (float)Ho;
-    const float fx = (ox + 0.5f) * sx - 0.5f;
-    const float fy = (oy + 0.5f) * sy - 0.5f;
+    // source coordinate in double, then float (cv::resize computes its
+    // tap tables the same way: fx = (float)((dx + 0.5) * scale - 0.5))
+    const float fx = (float)((ox + 0.5) * ((double)Wi / (double)Wo) - 0.5);
+    const float fy = (float)((oy + 0.5) * ((double)Hi / (double)Ho) - 0.5);
     const int x0 = (int)floorf(fx), y0 = (int)floorf(fy);
     float wx[4], wy[4];
     cubic_coeffs(fx - x0, wx);
