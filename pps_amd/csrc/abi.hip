@@ -2,6 +2,7 @@
 // Each entry point validates shapes/alignment ENFORCE-style, fills the
 // launch parameters and enqueues on the caller's stream.  No allocation, no
 // synchronisation: every entry point is hipGraph-capturable.
+#include <algorithm>
 #include <string>
 
 #include "pps_internal.hpp"
@@ -56,15 +57,28 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t 
   PPS_ENFORCE(ldo >= G, "ldo < G");
   PPS_ENFORCE(aligned16(q) && aligned16(g), "q/g must be 16-byte aligned");
   PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
-  PPS_ENFORCE(Q < (1ll << 31) && G < (1ll << 31), "Q/G must fit int32");
-  GemmParams p{};
-  p.a = q; p.H = 1; p.W = (int)Q; p.Cin = D; p.lda = (int)ldq;
-  p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)Q;
-  p.M = (int)Q;
-  p.b = g; p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)G;
-  p.Kloop = (D + 15) / 16 * 16;
-  p.out = out; p.ldo = ldo; p.metric = metric; p.tile = tile;
-  return launch_gemm(p, EPI_DIST, 1, as_stream(stream));
+  PPS_ENFORCE(ldq * 4 < kMaxBufBytes && ldg * 4 < kMaxBufBytes, "rows too long");
+  // operands are addressed through 32-bit buffer offsets: split Q and G into
+  // blocks of < 2 GiB each (one launch per block pair, same results)
+  const int64_t qblk = std::min<int64_t>(Q, (kMaxBufBytes - 1) / (ldq * 4));
+  const int64_t gblk = std::min<int64_t>(G, (kMaxBufBytes - 1) / (ldg * 4));
+  for (int64_t q0 = 0; q0 < Q; q0 += qblk) {
+    for (int64_t g0 = 0; g0 < G; g0 += gblk) {
+      const int64_t qn = std::min(qblk, Q - q0), gn = std::min(gblk, G - g0);
+      GemmParams p{};
+      p.a = q + q0 * ldq; p.a_bytes = (uint32_t)(qn * ldq * 4);
+      p.H = 1; p.W = (int)qn; p.Cin = D; p.lda = (int)ldq;
+      p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)qn;
+      p.M = (int)qn;
+      p.b = g + g0 * ldg; p.b_bytes = (uint32_t)(gn * ldg * 4);
+      p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)gn;
+      p.Kloop = (D + 15) / 16 * 16;
+      p.out = out + q0 * ldo + g0; p.ldo = ldo; p.metric = metric; p.tile = tile;
+      const int rc = launch_gemm(p, EPI_DIST, 1, as_stream(stream));
+      if (rc != PPS_OK) return rc;
+    }
+  }
+  return PPS_OK;
 }
 
 int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
@@ -72,9 +86,10 @@ int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) 
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
   PPS_ENFORCE(aligned16(X), "X must be 16-byte aligned");
   GemmParams p{};
-  p.a = X; p.H = 1; p.W = N; p.Cin = D; p.lda = D;
+  PPS_ENFORCE((int64_t)N * D * 4 < kMaxBufBytes, "X larger than 2 GiB");
+  p.a = X; p.H = 1; p.W = N; p.Cin = D; p.lda = D; p.a_bytes = (uint32_t)((int64_t)N * D * 4);
   p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = N; p.M = N;
-  p.b = X; p.ldb = D; p.kb_valid = D; p.Ncol = N;
+  p.b = X; p.ldb = D; p.kb_valid = D; p.Ncol = N; p.b_bytes = p.a_bytes;
   p.Kloop = (D + 15) / 16 * 16;
   p.out = Z; p.ldo = N; p.metric = PPS_METRIC_SQEUCLIDEAN; p.zero_diag = 1;
   return launch_gemm(p, EPI_DIST, 1, as_stream(stream));
@@ -150,7 +165,12 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
   PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
   PPS_ENFORCE((int64_t)N * Ho * Wo < (1ll << 31), "too many output pixels");
   GemmParams p{};
+  PPS_ENFORCE(KH * KW <= 64, "at most 64 filter taps");
+  PPS_ENFORCE((int64_t)N * H * W * ldx * 4 < kMaxBufBytes, "input larger than 2 GiB");
+  PPS_ENFORCE((int64_t)Cout * Kpad * 4 < kMaxBufBytes, "weights larger than 2 GiB");
   p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
+  p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 4);
+  p.b_bytes = (uint32_t)((int64_t)Cout * Kpad * 4);
   p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = dil;
   p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
   p.b = w; p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
@@ -170,7 +190,11 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
   PPS_ENFORCE(ldy >= B * Cout, "ldy < B*Cout");
   PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
   GemmParams p{};
+  PPS_ENFORCE((int64_t)M * K * 4 < kMaxBufBytes && (int64_t)Cout * K * 4 < kMaxBufBytes,
+              "operands larger than 2 GiB");
   p.a = x; p.a_bstride = x_bstride; p.H = 1; p.W = M; p.Cin = K; p.lda = K;
+  p.a_bytes = (uint32_t)((int64_t)M * K * 4);
+  p.b_bytes = (uint32_t)((int64_t)Cout * K * 4);
   p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = M; p.M = M;
   p.b = w; p.b_bstride = w_bstride; p.ldb = K; p.kb_valid = K; p.Ncol = Cout;
   p.Kloop = K;

@@ -27,6 +27,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 16;
 constexpr int LSTR = BK + 4;  // LDS row stride in floats
+constexpr int kOOB = 0x7ffffff0;  // byte offset beyond any num_records -> reads 0
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ inline rsrc_t make_rsrc(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ inline f32x4 bload(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
 
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ void __launch_bounds__(64 * WM * WN)
@@ -65,68 +75,82 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int n0 = tile_n * BN;
   const int batch = blockIdx.y;
 
-  const float* __restrict__ A = p.a + batch * p.a_bstride;
-  const float* __restrict__ B = p.b + batch * p.b_bstride;
+  // ---- operand descriptors: buffer loads with 32-bit offsets ---------------
+  // Out-of-range offsets (>= num_records) read as zero in hardware, so padding
+  // taps, ragged rows/cols and K tails need no exec-mask branches.
+  const rsrc_t ra_src = make_rsrc(p.a + batch * p.a_bstride, p.a_bytes);
+  const rsrc_t rb_src = make_rsrc(p.b + batch * p.b_bstride, p.b_bytes);
 
-  // ---- per-thread A-row geometry ----------------------------------------
+  // ---- per-thread A-row geometry (once) -------------------------------------
+  // Element offset of (row, tap t, channel c) = rbase + tap_off(t) + c, valid
+  // iff bit t of the row's tap mask is set (input pixel inside the image).
   const int c4 = tid & 3;
-  const float* abase[AL];
-  int ih0[AL], iw0[AL];
-  bool arow_ok[AL];
+  int rbase[AL];
+  uint64_t tmask[AL];
+  const int ntaps = p.KH * p.KW;
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int row = m0 + (tid >> 2) + i * ROWS_PER_PASS;
-    arow_ok[i] = row < p.M;
-    const int rowc = arow_ok[i] ? row : 0;
+    const int rowc = row < p.M ? row : 0;
     const int hw = p.Ho * p.Wo;
     const int n = rowc / hw;
     const int rem = rowc - n * hw;
     const int oh = rem / p.Wo;
     const int ow = rem - oh * p.Wo;
-    ih0[i] = oh * p.stride - p.pad;
-    iw0[i] = ow * p.stride - p.pad;
-    abase[i] = A + (int64_t)n * p.H * p.W * p.lda;
+    const int ih0 = oh * p.stride - p.pad;
+    const int iw0 = ow * p.stride - p.pad;
+    rbase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda;
+    uint64_t m = 0;
+    for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
+      const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
+      if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1ull << t;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+    tmask[i] = row < p.M ? m : 0ull;
   }
-  // tap tracking for k = chunk*BK + c4*4 : (kh, kw, c)
-  int tc = c4 * 4, tkh = 0, tkw = 0;
-  while (tc >= p.Cin) {
-    tc -= p.Cin;
-    if (++tkw == p.KW) { tkw = 0; ++tkh; }
-  }
-  const float* bbase[BL];
-  bool bcol_ok[BL];
+  // tap tracker for this thread's k = chunk*BK + c4*4 -> (tap t, channel tc,
+  // element offset toff of the tap); all rows of the thread share it.
+  const int step_w = p.dil * p.lda;                    // kw -> kw+1
+  const int step_h = p.dil * p.lda * (p.W - p.KW);     // extra on kw wrap
+  int tc = c4 * 4, tt = 0, tkw = 0, toff = 0;
+  auto advance = [&](int by) {
+    tc += by;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      ++tt;
+      toff += step_w;
+      if (++tkw == p.KW) { tkw = 0; toff += step_h; }
+    }
+  };
+  advance(0);
+  int bbase[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int col = n0 + (tid >> 2) + i * ROWS_PER_PASS;
-    bcol_ok[i] = col < p.Ncol;
-    bbase[i] = B + (int64_t)(bcol_ok[i] ? col : 0) * p.ldb + c4 * 4;
+    bbase[i] = col < p.Ncol ? (col * p.ldb + c4 * 4) * 4 : kOOB;
   }
 
   f32x4 ra[AL], rb[BL];
   auto load_chunk = [&](int kc) {
-    const bool tap_ok = tkh < p.KH;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int ih = ih0[i] + tkh * p.dil;
-      const int iw = iw0[i] + tkw * p.dil;
-      const bool ok = arow_ok[i] && tap_ok && (unsigned)ih < (unsigned)p.H &&
-                      (unsigned)iw < (unsigned)p.W;
-      ra[i] = ok ? *reinterpret_cast<const f32x4*>(
-                       abase[i] + ((int64_t)ih * p.W + iw) * p.lda + tc)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = (tmask[i] >> tt) & 1ull;
+      ra[i] = bload(ra_src, ok ? (rbase[i] + toff + tc) * 4 : kOOB);
     }
     const int kb = kc * BK + c4 * 4;
+    const bool kok = kb < p.kb_valid;
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const bool ok = bcol_ok[i] && kb < p.kb_valid;
-      rb[i] = ok ? *reinterpret_cast<const f32x4*>(bbase[i] + kc * BK)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    // advance the tap tracker by one chunk
-    tc += BK;
-    while (tc >= p.Cin) {
-      tc -= p.Cin;
-      if (++tkw == p.KW) { tkw = 0; ++tkh; }
+    for (int i = 0; i < BL; ++i) rb[i] = bload(rb_src, kok ? bbase[i] + kc * BK * 4 : kOOB);
+    if (p.Cin >= BK) {  // uniform: at most one tap step per chunk
+      tc += BK;
+      if (tc >= p.Cin) {
+        tc -= p.Cin;
+        ++tt;
+        toff += step_w;
+        if (++tkw == p.KW) { tkw = 0; toff += step_h; }
+      }
+    } else {
+      advance(BK);
     }
   };
 

@@ -36,6 +36,7 @@ inline bool aligned16(const void* p) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- GEMM core (gemm_f32.hip) ----------------------------------------------
+constexpr int64_t kMaxBufBytes = (int64_t)1 << 31;  // buffer-resource addressing limit
 enum Epi { EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4 };
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
@@ -52,6 +53,7 @@ struct GemmParams {
   // KH=KW=1).  Row m <-> output pixel (n, oh, ow).
   const float* a;
   int64_t a_bstride;
+  uint32_t a_bytes;  // bytes addressable from a (+batch stride), < 2^31
   int H, W, Cin, lda;
   int KH, KW, stride, pad, dil;
   int Ho, Wo;
@@ -59,6 +61,7 @@ struct GemmParams {
   // B operand: [Ncol][ldb], K contiguous; k >= kb_valid reads as zero.
   const float* b;
   int64_t b_bstride;
+  uint32_t b_bytes;  // bytes addressable from b (+batch stride), < 2^31
   int ldb, kb_valid;
   int Ncol;
   int Kloop;  // K extent iterated, multiple of 16
