@@ -112,16 +112,16 @@ def conv_roofline(m, x):
     torch.cuda.synchronize()
     m.forward(x, timer=timer)
     torch.cuda.synchronize()
-    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in ('conv', 'heads'))
-    conv_flops = sum(f for _, op, f, _, _ in timer if op in ('conv', 'heads'))
-    n_launch = sum(1 for _, op, _, _, _ in timer if op in ('conv', 'heads'))
+    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in ('conv', 'conv_dual', 'heads'))
+    conv_flops = sum(f for _, op, f, _, _ in timer if op in ('conv', 'conv_dual', 'heads'))
+    n_launch = sum(1 for _, op, _, _, _ in timer if op in ('conv', 'conv_dual', 'heads'))
     per = {}
     for name, op, f, e0, e1 in timer:
         per[name] = (op, f, e0.elapsed_time(e1))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     return dict(bound='mfma', achieved=round(achieved, 2), peak=PEAK_FP32_MFMA_TFLOPS,
                 unit='TFLOP/s', frac=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (54 launches/forward)',
+                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (%d launches/forward)' % n_launch,
                 launches=n_launch, flops_per_forward=conv_flops,
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2)), per
 

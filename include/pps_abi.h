@@ -129,6 +129,20 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
                       float* y, int Ho, int Wo, int ldy, int tile,
                       void* stream);
 
+/* Fused bottleneck tail with projection shortcut (first block of a stage):
+ * y = relu?(conv_KHxKW(x; W1') + conv_1x1_stride2(x2; W2') + shift), where the
+ * BN scales are pre-multiplied into W1' (branch2c) and W2' (branch1) and
+ * shift = shift_2c + shift_1; i.e. ResNet.py:186-195 Sum + Relu of
+ * bottleneck branch2c (:320-332) and basic_bn_shortcut (:203-220) as ONE
+ * implicit GEMM over the concatenated K (no shortcut tensor in HBM).
+ * w [Cout][Kpad1 + Kpad2]; x2 NHWC [N][H2][W2][ldx2], Kpad2 == Cin2 % 16 == 0. */
+int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin,
+                           int ldx, int KH, int KW, int stride, int pad,
+                           const float* x2, int H2, int W2, int Cin2, int ldx2,
+                           int stride2, const float* w, int Cout, int Kpad1,
+                           int Kpad2, const float* shift, int relu, float* y,
+                           int Ho, int Wo, int ldy, int tile, void* stream);
+
 /* Batched variant for the 31 PPS head convs (reid_heads.py:42-79):
  * for b in [0,B): Y[:, b*Cout:(b+1)*Cout] = relu?(X_b W_b^T * scale_b +
  * shift_b); X_b = x + b*x_bstride ([M][K]), W_b = w + b*w_bstride
@@ -137,6 +151,19 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
                             const float* w, int64_t w_bstride, int Cout,
                             const float* scale, const float* shift, int relu,
                             float* y, int ldy, int B, int tile, void* stream);
+
+/* Split-K form of the batched head GEMM: raw partial products
+ * part[s][m][b*Cout + c] = sum_{k in slice s} X_b[m][k] W_b[c][k] for the
+ * `splitk` equal K slices (K % (16*splitk) == 0); x [B][M][K], w [B][Cout][K],
+ * part [splitk][M][B*Cout].  Fills the chip at small batch (M = images). */
+int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Cout,
+                            int B, int splitk, float* part, int tile, void* stream);
+/* y[m][j] = relu?(sum_s part[s][m][j] * scale[j] + shift[j]) (fixed order),
+ * then, if normalize, Caffe2 Normalize along axis 1: y[m] /= max(|y[m]|,1e-12)
+ * (reid_heads.py:58-76 BN + Relu, :96-127 Concat + Normalize). */
+int pps_splitk_bn_act_normalize(const float* part, int splitk, int M, int N,
+                                const float* scale, const float* shift, int relu,
+                                int normalize, float* y, void* stream);
 
 /* MaxPool kernel k, stride s, pad p (padding never wins), NHWC
  * (ResNet.py:255 `pool1`). */

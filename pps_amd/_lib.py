@@ -33,8 +33,16 @@ SIGNATURES = {
     'pps_conv2d_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                           c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
                           c_ptr, c_int, c_int, c_int, c_int, c_ptr],
+    'pps_conv2d_dual_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                               c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_int,
+                               c_int, c_int, c_ptr],
     'pps_gemm_bn_act_batched': [c_ptr, c_i64, c_int, c_int, c_ptr, c_i64, c_int, c_ptr,
                                 c_ptr, c_int, c_ptr, c_int, c_int, c_int, c_ptr],
+    'pps_gemm_splitk_batched': [c_ptr, c_int, c_int, c_ptr, c_int, c_int, c_int, c_ptr, c_int,
+                                c_ptr],
+    'pps_splitk_bn_act_normalize': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_int,
+                                    c_ptr, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
                       c_int, c_int, c_ptr],
     'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,

@@ -29,6 +29,8 @@ int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const i
 int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
                 const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
+                            const float*, int, int, float*, hipStream_t);
 
 }  // namespace pps
 
@@ -66,6 +68,7 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t 
     for (int64_t g0 = 0; g0 < G; g0 += gblk) {
       const int64_t qn = std::min(qblk, Q - q0), gn = std::min(gblk, G - g0);
       GemmParams p{};
+  p.splitk = 1;
       p.a = q + q0 * ldq; p.a_bytes = (uint32_t)(qn * ldq * 4);
       p.H = 1; p.W = (int)qn; p.Cin = D; p.lda = (int)ldq;
       p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)qn;
@@ -86,6 +89,7 @@ int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) 
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
   PPS_ENFORCE(aligned16(X), "X must be 16-byte aligned");
   GemmParams p{};
+  p.splitk = 1;
   PPS_ENFORCE((int64_t)N * D * 4 < kMaxBufBytes, "X larger than 2 GiB");
   p.a = X; p.H = 1; p.W = N; p.Cin = D; p.lda = D; p.a_bytes = (uint32_t)((int64_t)N * D * 4);
   p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = N; p.M = N;
@@ -165,7 +169,10 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
   PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
   PPS_ENFORCE((int64_t)N * Ho * Wo < (1ll << 31), "too many output pixels");
   GemmParams p{};
+  p.splitk = 1;
   PPS_ENFORCE(KH * KW <= 64, "at most 64 filter taps");
+  PPS_ENFORCE(Cin >= 16 || ((Cin & (Cin - 1)) == 0 && Kpad <= 64 * Cin),
+              "channels < 16 must be a power of two with Kpad <= 64*Cin");
   PPS_ENFORCE((int64_t)N * H * W * ldx * 4 < kMaxBufBytes, "input larger than 2 GiB");
   PPS_ENFORCE((int64_t)Cout * Kpad * 4 < kMaxBufBytes, "weights larger than 2 GiB");
   p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
@@ -176,6 +183,42 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
   p.b = w; p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
+}
+
+int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+                           int KH, int KW, int stride, int pad, const float* x2, int H2,
+                           int W2, int Cin2, int ldx2, int stride2, const float* w,
+                           int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
+                           float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
+  PPS_ENFORCE(x && x2 && w && shift && y, "null pointer");
+  PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cin2 > 0, "bad shape");
+  PPS_ENFORCE(Cin % 4 == 0 && ldx % 4 == 0 && Cin2 % 16 == 0 && ldx2 % 4 == 0,
+              "channel counts must be multiples of 4 (second operand: 16)");
+  PPS_ENFORCE(Kpad1 % 16 == 0 && Kpad1 >= KH * KW * Cin && Kpad2 == Cin2,
+              "Kpad1 >= KH*KW*Cin (%16), Kpad2 == Cin2");
+  PPS_ENFORCE(KH * KW <= 64, "at most 64 filter taps");
+  PPS_ENFORCE(Ho == (H + 2 * pad - (KH - 1) - 1) / stride + 1 &&
+                  Wo == (W + 2 * pad - (KW - 1) - 1) / stride + 1,
+              "output size does not match conv arithmetic");
+  PPS_ENFORCE(Ho == (H2 - 1) / stride2 + 1 && Wo == (W2 - 1) / stride2 + 1,
+              "second operand (1x1, stride2) does not map onto the output grid");
+  PPS_ENFORCE((int64_t)N * H * W * ldx * 4 < kMaxBufBytes &&
+                  (int64_t)N * H2 * W2 * ldx2 * 4 < kMaxBufBytes,
+              "input larger than 2 GiB");
+  PPS_ENFORCE(aligned16(x) && aligned16(x2) && aligned16(w), "16-byte alignment");
+  GemmParams p{};
+  p.splitk = 1;
+  p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
+  p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 4);
+  p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = 1;
+  p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
+  p.a2 = x2; p.a2_bytes = (uint32_t)((int64_t)N * H2 * W2 * ldx2 * 4);
+  p.H2 = H2; p.W2 = W2; p.lda2 = ldx2; p.stride2 = stride2; p.Kloop1 = Kpad1;
+  p.b = w; p.ldb = Kpad1 + Kpad2; p.kb_valid = Kpad1 + Kpad2; p.Ncol = Cout;
+  p.b_bytes = (uint32_t)((int64_t)Cout * (Kpad1 + Kpad2) * 4);
+  p.Kloop = Kpad1 + Kpad2;
+  p.scale = nullptr; p.shift = shift; p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
 }
 
@@ -190,6 +233,7 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
   PPS_ENFORCE(ldy >= B * Cout, "ldy < B*Cout");
   PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
   GemmParams p{};
+  p.splitk = 1;
   PPS_ENFORCE((int64_t)M * K * 4 < kMaxBufBytes && (int64_t)Cout * K * 4 < kMaxBufBytes,
               "operands larger than 2 GiB");
   p.a = x; p.a_bstride = x_bstride; p.H = 1; p.W = M; p.Cin = K; p.lda = K;
@@ -201,6 +245,36 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
   p.scale = scale; p.shift = shift; p.ss_bstride = Cout;
   p.out = y; p.ldo = ldy; p.out_bstride = Cout; p.relu = relu; p.tile = tile;
   return launch_gemm(p, EPI_CONV, B, as_stream(stream));
+}
+
+int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Cout, int B,
+                            int splitk, float* part, int tile, void* stream) {
+  PPS_ENFORCE(x && w && part, "null pointer");
+  PPS_ENFORCE(M > 0 && K > 0 && Cout > 0 && B > 0 && splitk >= 1, "bad shape");
+  PPS_ENFORCE(K % (16 * splitk) == 0, "K must be a multiple of 16*splitk");
+  PPS_ENFORCE((int64_t)M * K * 4 < kMaxBufBytes && (int64_t)Cout * K * 4 < kMaxBufBytes,
+              "operands larger than 2 GiB");
+  PPS_ENFORCE(aligned16(x) && aligned16(w), "x/w must be 16-byte aligned");
+  GemmParams p{};
+  p.splitk = splitk;
+  p.a = x; p.a_bstride = (int64_t)M * K; p.H = 1; p.W = M; p.Cin = K / splitk; p.lda = K;
+  p.a_bytes = (uint32_t)((int64_t)M * K * 4);
+  p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = M; p.M = M;
+  p.b = w; p.b_bstride = (int64_t)Cout * K; p.ldb = K; p.kb_valid = K / splitk;
+  p.b_bytes = (uint32_t)((int64_t)Cout * K * 4); p.Ncol = Cout;
+  p.Kloop = K / splitk;
+  p.out = part; p.ldo = (int64_t)B * Cout; p.out_bstride = Cout;
+  p.out_sstride = (int64_t)M * B * Cout; p.tile = tile;
+  return launch_gemm(p, EPI_CONV | EPI_F_RAW, B, as_stream(stream));
+}
+
+int pps_splitk_bn_act_normalize(const float* part, int splitk, int M, int N,
+                                const float* scale, const float* shift, int relu,
+                                int normalize, float* y, void* stream) {
+  PPS_ENFORCE(part && scale && shift && y, "null pointer");
+  PPS_ENFORCE(splitk >= 1 && M >= 0 && N > 0, "bad shape");
+  return splitk_bn_act_normalize(part, splitk, (int64_t)M * N, M, N, scale, shift, relu,
+                                 normalize, y, as_stream(stream));
 }
 
 int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad,

@@ -117,14 +117,19 @@ __global__ void part_power_set_kernel(const float* __restrict__ x, int N, int H,
   }
 }
 
+constexpr int kPpsC_fwd = 64;
+__global__ void part_power_set_v2_kernel(const float* __restrict__ x, int N, int H, int W,
+                                         int C, Splits sp, int S, int max_ave,
+                                         float* __restrict__ out);
+
 int part_power_set(const float* x, int N, int H, int W, int C, const int32_t* splits,
                    int S, int max_ave, float* out, hipStream_t st) {
   Splits sp;
   for (int j = 0; j < kMaxStrips; ++j) sp.h[j] = j < S ? splits[j] : 0;
-  dim3 block(256), grid((C + 255) / 256, N);
-  hipLaunchKernelGGL(part_power_set_kernel, grid, block, 0, st, x, N, H, W, C, sp, S,
+  dim3 block(kPpsC_fwd * S), grid((C + kPpsC_fwd - 1) / kPpsC_fwd, N);
+  hipLaunchKernelGGL(part_power_set_v2_kernel, grid, block, 0, st, x, N, H, W, C, sp, S,
                      max_ave, out);
-  PPS_CHECK_LAUNCH("part_power_set_kernel");
+  PPS_CHECK_LAUNCH("part_power_set_v2_kernel");
   return PPS_OK;
 }
 
@@ -155,6 +160,158 @@ int l2_normalize(const float* x, int64_t N, int D, float* y, hipStream_t st) {
   hipLaunchKernelGGL(l2_normalize_kernel, dim3((unsigned)N), dim3(256), 0, st, x, D, y);
   PPS_CHECK_LAUNCH("l2_normalize_kernel");
   return PPS_OK;
+}
+
+// ---- split-K reduce + BN + ReLU + Normalize (reid_heads.py:42-127) ---------
+// One block per feature row: y[m][j] = relu(sum_s part[s][m][j] * scale[j] +
+// shift[j]) over the S partial GEMM slices in fixed order (deterministic),
+// then optionally y[m] /= max(||y[m]||, 1e-12) (Caffe2 Normalize axis 1).
+__global__ void splitk_bn_act_normalize_kernel(const float* __restrict__ part, int S,
+                                               int64_t sstride, int N,
+                                               const float* __restrict__ scale,
+                                               const float* __restrict__ shift, int relu,
+                                               int normalize, float* __restrict__ y) {
+  const int64_t m = blockIdx.x;
+  float* yr = y + m * N;
+  float ss = 0.f;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    float v = part[m * N + j];
+    for (int s = 1; s < S; ++s) v += part[s * sstride + m * N + j];
+    v = __builtin_fmaf(v, scale[j], shift[j]);
+    if (relu) v = fmaxf(v, 0.f);
+    yr[j] = v;
+    ss += v * v;
+  }
+  if (!normalize) return;
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.f;
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) red[0] = t;
+  }
+  __syncthreads();
+  const float inv = 1.f / fmaxf(sqrtf(red[0]), 1e-12f);
+  for (int j = threadIdx.x; j < N; j += blockDim.x) yr[j] *= inv;
+}
+
+// Vectorised single-pass form for N % 4 == 0, N <= 4096: one float4 column
+// group per thread, kept in registers between the norm and the scaling.
+__global__ void __launch_bounds__(1024)
+splitk_bn_act_normalize_v4_kernel(const float* __restrict__ part, int S, int64_t sstride,
+                                  int N, const float* __restrict__ scale,
+                                  const float* __restrict__ shift, int relu, int normalize,
+                                  float* __restrict__ y) {
+  const int64_t m = blockIdx.x;
+  const int j = threadIdx.x * 4;
+  const bool on = j < N;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    v = *reinterpret_cast<const f32x4*>(part + m * N + j);
+    for (int s = 1; s < S; ++s)
+      v += *reinterpret_cast<const f32x4*>(part + s * sstride + m * N + j);
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + j);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = __builtin_fmaf(v[e], sc[e], sh[e]);
+      v[e] = relu ? fmaxf(t, 0.f) : t;
+    }
+  }
+  float inv = 1.f;
+  if (normalize) {
+    float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    __shared__ float red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float t = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.f;
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (threadIdx.x == 0) red[0] = t;
+    }
+    __syncthreads();
+    inv = 1.f / fmaxf(sqrtf(red[0]), 1e-12f);
+  }
+  if (on) *reinterpret_cast<f32x4*>(y + m * N + j) = v * inv;
+}
+
+int splitk_bn_act_normalize(const float* part, int S, int64_t sstride, int M, int N,
+                            const float* scale, const float* shift, int relu, int normalize,
+                            float* y, hipStream_t st) {
+  if (M <= 0) return PPS_OK;
+  if (N % 4 == 0 && N <= 4096 && ((reinterpret_cast<uintptr_t>(part) |
+                                   reinterpret_cast<uintptr_t>(y) |
+                                   reinterpret_cast<uintptr_t>(scale) |
+                                   reinterpret_cast<uintptr_t>(shift)) & 15) == 0) {
+    const int threads = ((N / 4 + 63) / 64) * 64;
+    hipLaunchKernelGGL(splitk_bn_act_normalize_v4_kernel, dim3(M), dim3(threads), 0, st,
+                       part, S, sstride, N, scale, shift, relu, normalize, y);
+    PPS_CHECK_LAUNCH("splitk_bn_act_normalize_v4_kernel");
+    return PPS_OK;
+  }
+  hipLaunchKernelGGL(splitk_bn_act_normalize_kernel, dim3(M), dim3(256), 0, st, part, S,
+                     sstride, N, scale, shift, relu, normalize, y);
+  PPS_CHECK_LAUNCH("splitk_bn_act_normalize_kernel");
+  return PPS_OK;
+}
+
+// ---- part power set, strip-parallel variant ----------------------------------
+// Block = (image n, 64 channels); thread (strip j, channel c) reduces its
+// strip (rows x W values) -> LDS; then all threads emit the 2^S-1 subsets.
+constexpr int kPpsC = 64;
+__global__ void part_power_set_v2_kernel(const float* __restrict__ x, int N, int H, int W,
+                                         int C, Splits sp, int S, int max_ave,
+                                         float* __restrict__ out) {
+  __shared__ float s_ave[kMaxStrips][kPpsC];
+  __shared__ float s_max[kMaxStrips][kPpsC];
+  const int n = blockIdx.y;
+  const int c0 = blockIdx.x * kPpsC;
+  const int cl = threadIdx.x % kPpsC;
+  const int j = threadIdx.x / kPpsC;
+  const int c = c0 + cl;
+  if (j < S && c < C) {
+    int r0 = 0;
+    for (int t = 0; t < j; ++t) r0 += sp.h[t];
+    const float* base = x + (((int64_t)n * H + r0) * W) * C + c;
+    float sum = 0.f, m = -INFINITY;
+    const int cnt = sp.h[j] * W;
+    for (int e = 0; e < cnt; ++e) {  // rows of the strip, row-major: (hh, ww)
+      const float v = base[(int64_t)e * C];
+      sum += v;
+      m = fmaxf(m, v);
+    }
+    s_ave[j][cl] = sum / (float)cnt;
+    s_max[j][cl] = m;
+  }
+  __syncthreads();
+  const int nsub = (1 << S) - 1;
+  for (int o = threadIdx.x; o < nsub * kPpsC; o += blockDim.x) {
+    const int i = o / kPpsC + 1, cc = o % kPpsC;
+    if (c0 + cc >= C) continue;
+    float v;
+    if (max_ave) {
+      float s = 0.f, m = -INFINITY;
+      int k = 0;
+      bool first = true;
+      for (int t = 0; t < S; ++t)
+        if (i & (1 << t)) {
+          s = first ? s_ave[t][cc] : s + s_ave[t][cc];
+          first = false;
+          m = fmaxf(m, s_max[t][cc]);
+          ++k;
+        }
+      v = s * (1.f / (float)k) + m;
+    } else {
+      float m = -INFINITY;
+      for (int t = 0; t < S; ++t)
+        if (i & (1 << t)) m = fmaxf(m, s_ave[t][cc]);
+      v = m;
+    }
+    out[((int64_t)(i - 1) * N + n) * C + c0 + cc] = v;
+  }
 }
 
 // ---- Preprocess (utils/blob.py:97-117) ---------------------------------------

@@ -50,7 +50,9 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   static_assert(AL >= 1 && BL >= 1, "tile too small for thread count");
   static_assert(TM >= 1 && TN >= 1, "wave tile too small");
 
-  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LSTR];
+  // one LDS array (2 operand buffers + the 64-entry tap-offset table)
+  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LSTR + 64];
+  int* s_tapoff = reinterpret_cast<int*>(lds + 2 * (BM + BN) * LSTR);
   float* As = lds;                       // [2][BM][LSTR]
   float* Bs = lds + 2 * BM * LSTR;       // [2][BN][LSTR]
 
@@ -73,13 +75,17 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int tile_n = bid - tile_m * tiles_n;
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;
-  const int batch = blockIdx.y;
+  // blockIdx.y enumerates (batch, K-slice) pairs; K-slice s covers
+  // [s*Kloop, (s+1)*Kloop) of a K = splitk*Kloop reduction (raw partials)
+  const int batch = blockIdx.y / p.splitk;
+  const int kslice = blockIdx.y - batch * p.splitk;
 
   // ---- operand descriptors: buffer loads with 32-bit offsets ---------------
   // Out-of-range offsets (>= num_records) read as zero in hardware, so padding
   // taps, ragged rows/cols and K tails need no exec-mask branches.
-  const rsrc_t ra_src = make_rsrc(p.a + batch * p.a_bstride, p.a_bytes);
-  const rsrc_t rb_src = make_rsrc(p.b + batch * p.b_bstride, p.b_bytes);
+  const int64_t kofs0 = (int64_t)kslice * p.Kloop;
+  const rsrc_t ra_src = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
+  const rsrc_t rb_src = make_rsrc(p.b + batch * p.b_bstride + kofs0, p.b_bytes);
 
   // ---- per-thread A-row geometry (once) -------------------------------------
   // Element offset of (row, tap t, channel c) = rbase + tap_off(t) + c, valid
@@ -123,6 +129,40 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
     }
   };
   advance(0);
+  // narrow-channel inputs (the stem's packed 4-channel image): a 16-wide K
+  // chunk spans several taps, so look tap offsets up in LDS instead of
+  // stepping the tracker (Cin a power of two < 16).
+  const bool narrow = p.Cin < BK;
+  int cin_shift = 0;
+  while ((1 << cin_shift) < p.Cin) ++cin_shift;
+  if (narrow) {
+    for (int t = tid; t < 64; t += T) {
+      const int kh = t / p.KW, kw = t - (t / p.KW) * p.KW;
+      s_tapoff[t] = (kh * p.dil * p.W + kw * p.dil) * p.lda;
+    }
+    __syncthreads();
+  }
+  // second A operand (EPI_F_DUAL): a 1x1 conv of another tensor appended
+  // along K (the fused projection shortcut, ResNet.py:203-220)
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+  rsrc_t ra2_src = ra_src;
+  int rbase2[AL];
+  if (DUAL) {
+    ra2_src = make_rsrc(p.a2, p.a2_bytes);
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int row = m0 + (tid >> 2) + i * ROWS_PER_PASS;
+      const int hw = p.Ho * p.Wo;
+      const int n = row / hw;
+      const int rem = row - n * hw;
+      const int oh = rem / p.Wo;
+      const int ow = rem - oh * p.Wo;
+      rbase2[i] = row < p.M ? (((n * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.lda2 +
+                               c4 * 4) * 4
+                            : kOOB;
+    }
+  }
+  const int nch1 = DUAL ? p.Kloop1 / BK : (1 << 30);
   int bbase[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
@@ -132,16 +172,34 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
 
   f32x4 ra[AL], rb[BL];
   auto load_chunk = [&](int kc) {
+    if (DUAL && kc >= nch1) {
+      const int kofs = (kc - nch1) * BK * 4;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const bool ok = (tmask[i] >> tt) & 1ull;
-      ra[i] = bload(ra_src, ok ? (rbase[i] + toff + tc) * 4 : kOOB);
+      for (int i = 0; i < AL; ++i) ra[i] = bload(ra2_src, rbase2[i] == kOOB ? kOOB : rbase2[i] + kofs);
+    } else if (narrow) {
+      const int k = kc * BK + c4 * 4;
+      const int t = k >> cin_shift;
+      const int c = k & (p.Cin - 1);
+      const int off = t < 64 ? s_tapoff[t] + c : 0;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const bool ok = t < 64 && ((tmask[i] >> t) & 1ull);
+        ra[i] = bload(ra_src, ok ? (rbase[i] + off) * 4 : kOOB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const bool ok = (tmask[i] >> tt) & 1ull;
+        ra[i] = bload(ra_src, ok ? (rbase[i] + toff + tc) * 4 : kOOB);
+      }
     }
     const int kb = kc * BK + c4 * 4;
     const bool kok = kb < p.kb_valid;
 #pragma unroll
     for (int i = 0; i < BL; ++i) rb[i] = bload(rb_src, kok ? bbase[i] + kc * BK * 4 : kOOB);
-    if (p.Cin >= BK) {  // uniform: at most one tap step per chunk
+    if (narrow) {
+      // taps come from the LDS table
+    } else if (p.Cin >= BK) {  // uniform: at most one tap step per chunk
       tc += BK;
       if (tc >= p.Cin) {
         tc -= p.Cin;
@@ -230,23 +288,24 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // Addresses are a wave-uniform 64-bit tile base + 32-bit per-lane offsets
   // (SGPR-base global addressing): one VGPR per address, not two.
   const int64_t tile_off = (int64_t)m0 * p.ldo + n0;
-  float* __restrict__ out = p.out + batch * p.out_bstride + tile_off;
+  float* __restrict__ out = p.out + batch * p.out_bstride + kslice * p.out_sstride + tile_off;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;      // rows valid in this tile
   const int nrem = p.Ncol - n0;   // cols valid in this tile
   if (!(EPI & EPI_DIST)) {
     constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
     constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
-    const float* sc = p.scale + batch * p.ss_bstride + n0;
-    const float* sh = p.shift + batch * p.ss_bstride + n0;
+    constexpr bool RAW = (EPI & EPI_F_RAW) != 0;  // split-K partials: store acc
+    const float* sc = (DUAL || RAW) ? nullptr : p.scale + batch * p.ss_bstride + n0;
+    const float* sh = RAW ? nullptr : p.shift + batch * p.ss_bstride + n0;
     const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
     const int ldr = (int)p.ldr;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int c = wn * (BN / WN) + j * 32 + r32;   // column within the tile
       const bool col_ok = c < nrem;
-      const float s_ = col_ok ? sc[c] : 0.f;
-      const float t_ = col_ok ? sh[c] : 0.f;
+      const float s_ = (DUAL || RAW) ? 1.f : (col_ok ? sc[c] : 0.f);  // DUAL: folded in w
+      const float t_ = RAW ? 0.f : (col_ok ? sh[c] : 0.f);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int rb = wm * (BM / WM) + i * 32 + 4 * h;  // row within the tile
@@ -262,7 +321,7 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rr = rb + (r & 3) + 8 * (r >> 2);
-          float v = __builtin_fmaf(acc[i][j][r], s_, t_);
+          float v = RAW ? acc[i][j][r] : __builtin_fmaf(acc[i][j][r], s_, t_);
           if (HAS_RES) v += rv[r];
           if (RELU) v = fmaxf(v, 0.f);
           if (col_ok && rr < mrem) out[rr * ldo + c] = v;
@@ -313,7 +372,8 @@ template <int BM, int BN, int WM, int WN, int EPI>
 static void launch_one(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>), dim3(tiles_m * tiles_n, batch),
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>),
+                     dim3(tiles_m * tiles_n, batch * p.splitk),
                      dim3(64 * WM * WN), 0, stream, p, tiles_m, tiles_n);
 }
 
@@ -328,6 +388,10 @@ static int launch_tile(const GemmParams& p, int epi, int batch, hipStream_t stre
       launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RES | EPI_F_RELU:
       launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RAW:
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL>(p, batch, stream); break;
     default:
       set_error("unknown epilogue");
       return PPS_ERR_INVALID_ARG;
@@ -353,9 +417,14 @@ int pick_tile(const GemmParams& p, int batch) {
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   if (p.M <= 0 || p.Ncol <= 0 || batch <= 0) return PPS_OK;
-  if (!(epi & EPI_DIST)) {
+  if (p.splitk < 1) {
+    set_error("splitk must be >= 1");
+    return PPS_ERR_INVALID_ARG;
+  }
+  if (!(epi & EPI_DIST) && !(epi & EPI_F_RAW)) {
     if (p.residual) epi |= EPI_F_RES;
     if (p.relu) epi |= EPI_F_RELU;
+    if (p.a2) epi |= EPI_F_DUAL;
   }
   const int tile = p.tile ? p.tile : pick_tile(p, batch);
   switch (tile) {

@@ -37,7 +37,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // ---- GEMM core (gemm_f32.hip) ----------------------------------------------
 constexpr int64_t kMaxBufBytes = (int64_t)1 << 31;  // buffer-resource addressing limit
-enum Epi { EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4 };
+enum Epi { EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16 };
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
   GEMM_TILE_128x128 = 1,
@@ -65,6 +65,11 @@ struct GemmParams {
   int ldb, kb_valid;
   int Ncol;
   int Kloop;  // K extent iterated, multiple of 16
+  // optional second A operand (1x1 conv, stride2, no padding) for K >= Kloop1
+  const float* a2;
+  uint32_t a2_bytes;
+  int H2, W2, lda2, stride2;
+  int Kloop1;
   // epilogue
   const float* scale;
   const float* shift;
@@ -78,6 +83,8 @@ struct GemmParams {
   int metric;
   int zero_diag;
   int tile;  // GemmTile; 0 = heuristic
+  int splitk;           // >= 1; K slices enumerated with the batch on grid.y
+  int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)
 };
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);

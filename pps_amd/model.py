@@ -27,6 +27,7 @@ from . import ops
 from .config import cfg
 
 BN_EPS = 1e-5  # Caffe2 SpatialBN default epsilon (pytorch v1.0.1)
+HEAD_SPLITK = 8  # K=2048 head GEMMs split 8 ways: 31 x 8 x 2 workgroups at batch 64
 
 
 # ---------------------------------------------------------------------------
@@ -245,7 +246,7 @@ class PPSModel(object):
     on the current CUDA device, H x W = REID.SCALE[::-1].
     """
 
-    def __init__(self, blobs, device='cuda', plan=None):
+    def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True):
         self.plan = plan or build_plan()
         self.device = torch.device(device)
         missing = [n for n in self.plan.params if n not in blobs
@@ -254,8 +255,31 @@ class PPSModel(object):
             raise KeyError('weights missing %d blobs, e.g. %s' % (len(missing), missing[:5]))
         self.layers = []
         dev = self.device
+        # projection shortcuts fused into their block's branch2c GEMM (K concat)
+        shortcut_of = {}
+        if fuse_shortcut:
+            for L in self.plan.layers:
+                if L['op'] == 'conv' and L['name'].endswith('_branch1') and L['k'] == 1:
+                    shortcut_of[L['output']] = L
         for L in self.plan.layers:
             L = dict(L)
+            if L['op'] == 'conv' and L['output'] in shortcut_of:
+                continue  # computed inside the consuming branch2c
+            if L['op'] == 'conv' and L.get('residual') in shortcut_of:
+                sc_L = shortcut_of[L['residual']]
+                w1, kpad1 = pack_conv_weight(blobs[L['name'] + '_w'])
+                s1, h1 = fold_bn(blobs, L['bn'])
+                w2, kpad2 = pack_conv_weight(blobs[sc_L['name'] + '_w'])
+                s2, h2 = fold_bn(blobs, sc_L['bn'])
+                assert kpad2 == sc_L['cin'] and kpad1 == L['cin']
+                w = np.concatenate([w1 * s1[:, None], w2 * s2[:, None]], axis=1)
+                L.update(op='conv_dual', w=torch.from_numpy(w.astype(np.float32)).to(dev),
+                         kpad=kpad1, shift=torch.from_numpy((h1 + h2).astype(np.float32)).to(dev),
+                         cin_eff=L['cin'], input2=sc_L['input'], stride2=sc_L['stride'],
+                         residual=None, fused_shortcut=sc_L['name'],
+                         shortcut_cin=sc_L['cin'])
+                self.layers.append(L)
+                continue
             if L['op'] == 'conv':
                 cin_pad = 4 if L['cin'] == 3 else None
                 w, kpad = pack_conv_weight(blobs[L['name'] + '_w'], cin_pad)
@@ -277,6 +301,12 @@ class PPSModel(object):
                          shift=torch.from_numpy(np.concatenate(shs)).to(dev))
             elif L['op'] == 'pps':
                 L['split_arr'] = np.array(L['split'], np.int32)
+            elif L['op'] == 'normalize' and self.layers and self.layers[-1]['op'] == 'heads':
+                # heads GEMM as split-K partials + one reduce/BN/ReLU/Normalize pass
+                H = self.layers[-1]
+                H['normalize'] = True
+                H['output'] = L['output']
+                continue
             self.layers.append(L)
         self.feat_dim = self.plan.feat_dim
         self._bufs = {}
@@ -286,7 +316,7 @@ class PPSModel(object):
     def _alloc(self, N, H, W):
         shapes = {'data': (N, H, W, 4)}
         for L in self.layers:
-            if L['op'] == 'conv':
+            if L['op'] in ('conv', 'conv_dual'):
                 n, h, w, _ = shapes[L['input']]
                 ho = (h + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
                 wo = (w + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
@@ -301,15 +331,18 @@ class PPSModel(object):
                 shapes[L['output']] = (len(L['prefixes']), n, c)
             elif L['op'] == 'heads':
                 shapes[L['output']] = (N, len(L['prefixes']) * L['dim_inner'])
+                shapes[L['output'] + '_partials'] = (HEAD_SPLITK, N,
+                                                     len(L['prefixes']) * L['dim_inner'])
             elif L['op'] == 'normalize':
                 shapes[L['output']] = shapes[L['input']]
         self._shapes = shapes
         # algorithmic FLOPs per launch (2*M*Cout*K with the TRUE Cin: the
         # stem's 4th packed channel is not counted) -- SURVEY §8(d)
         for L in self.layers:
-            if L['op'] == 'conv':
+            if L['op'] in ('conv', 'conv_dual'):
                 n, ho, wo, co = shapes[L['output']]
-                L['flops'] = 2.0 * n * ho * wo * co * L['k'] * L['k'] * L['cin']
+                L['flops'] = 2.0 * n * ho * wo * co * (L['k'] * L['k'] * L['cin'] +
+                                                      L.get('shortcut_cin', 0))
             elif L['op'] == 'heads':
                 L['flops'] = 2.0 * N * len(L['prefixes']) * L['dim_inner'] * L['dim']
             else:
@@ -321,7 +354,7 @@ class PPSModel(object):
     def buffers(self):
         return self._bufs
 
-    def flops_per_forward(self, kinds=('conv', 'heads')):
+    def flops_per_forward(self, kinds=('conv', 'conv_dual', 'heads')):
         return sum(L['flops'] for L in self.layers if L['op'] in kinds)
 
     def _run(self, L, bufs, out=None, tile=None):
@@ -332,6 +365,11 @@ class PPSModel(object):
             ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
                               L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                               res, L['relu'], bufs[L['output']], tile=tile)
+        elif op == 'conv_dual':
+            ops.conv2d_dual_bn_act(bufs[L['input']], L['cin_eff'], L['k'], L['stride'],
+                                   L['pad'], bufs[L['input2']], L['stride2'], L['w'],
+                                   L['kpad'], L['shift'], L['relu'], bufs[L['output']],
+                                   tile=tile)
         elif op == 'maxpool':
             ops.maxpool2d(bufs[L['input']], L['k'], L['stride'], L['pad'],
                           bufs[L['output']])
@@ -340,8 +378,10 @@ class PPSModel(object):
                                bufs[L['output']])
         elif op == 'heads':
             y = bufs[L['output']] if out is None or self.layers[-1] is not L else out
-            ops.gemm_bn_act_batched(bufs[L['input']], L['w'], L['scale'], L['shift'], True,
-                                    y, tile=tile)
+            part = bufs[L['output'] + '_partials']
+            ops.gemm_splitk_batched(bufs[L['input']], L['w'], HEAD_SPLITK, part, tile=tile)
+            ops.splitk_bn_act_normalize(part, L['scale'], L['shift'], True,
+                                        L.get('normalize', False), y)
             bufs[L['output']] = y
         elif op == 'normalize':
             y = out if out is not None else bufs[L['output']]
@@ -381,7 +421,7 @@ class PPSModel(object):
         cands = list(tiles or range(1, ops.num_tiles() + 1))
         report = {}
         for L in self.layers:
-            if L['op'] not in ('conv', 'heads'):
+            if L['op'] not in ('conv', 'conv_dual', 'heads'):
                 continue
             times = {}
             for t in cands:

@@ -161,6 +161,19 @@ def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, 
     return y
 
 
+def conv2d_dual_bn_act(x, cin, k, stride, pad, x2, stride2, w, kpad1, shift, relu, y,
+                       tile=0):
+    """relu?(conv_k(x) + conv_1x1/stride2(x2) + shift), BN scales folded in w."""
+    N, H, W, ldx = x.shape
+    _, H2, W2, C2 = x2.shape
+    _, Ho, Wo, Cout = y.shape
+    call('pps_conv2d_dual_bn_act', _dev(x, 'x'), N, H, W, cin, ldx, k, k, stride, pad,
+         _dev(x2, 'x2'), H2, W2, C2, C2, stride2, _dev(w, 'w'), Cout, kpad1, C2,
+         _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile),
+         _stream())
+    return y
+
+
 def gemm_bn_act_batched(x, w, scale, shift, relu, y, tile=0):
     """x [B,M,K], w [B,Cout,K] -> y [M, B*Cout] (PPS head convs)."""
     B, M, K = x.shape
@@ -168,6 +181,22 @@ def gemm_bn_act_batched(x, w, scale, shift, relu, y, tile=0):
     call('pps_gemm_bn_act_batched', _dev(x, 'x'), M * K, M, K, _dev(w, 'w'), Cout * K,
          Cout, _dev(scale, 'scale'), _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'),
          y.stride(0), B, int(tile), _stream())
+    return y
+
+
+def gemm_splitk_batched(x, w, splitk, part, tile=0):
+    """x [B,M,K], w [B,Cout,K] -> raw partials part [splitk, M, B*Cout]."""
+    B, M, K = x.shape
+    Cout = w.shape[1]
+    call('pps_gemm_splitk_batched', _dev(x, 'x'), M, K, _dev(w, 'w'), Cout, B, splitk,
+         _dev(part, 'part'), int(tile), _stream())
+    return part
+
+
+def splitk_bn_act_normalize(part, scale, shift, relu, normalize, y):
+    S, M, N = part.shape
+    call('pps_splitk_bn_act_normalize', _dev(part, 'part'), S, M, N, _dev(scale, 'scale'),
+         _dev(shift, 'shift'), int(bool(relu)), int(bool(normalize)), _dev(y, 'y'), _stream())
     return y
 
 
