@@ -113,6 +113,18 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
 int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k,
              float* vals, int32_t* idx, void* stream);
 
+/* k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519): out [Q][G] =
+ * re_ranking(q_g, q_q, g_g, k1, k2, lambda) with the reference's float32
+ * operand order for V, V_qe and the Jaccard sums; ties in the initial rank use
+ * the stable (distance, index) order.  q_g [Q][G], q_q [Q][Q], g_g [G][G]
+ * (euclidean distances, as compute_dist returns them).  Workspace: a caller
+ * device buffer of pps_rerank_workspace_bytes(Q, G, k1, k2) bytes
+ * (dominated by the dense N x N normalised distance, N = Q + G <= 40960). */
+int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2);
+int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                   int64_t G, int k1, int k2, double lambda_value, void* workspace,
+                   int64_t ws_bytes, float* out, void* stream);
+
 /* ---- feature extractor ----------------------------------------------------
  * Implicit-GEMM convolution + test-mode SpatialBN + optional residual Sum +
  * optional ReLU, fused (ResNet.py:246-256 stem conv, :276-333 bottleneck,

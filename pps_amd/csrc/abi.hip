@@ -29,6 +29,9 @@ int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const i
 int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
                 const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int, double,
+           void*, size_t, float*, hipStream_t);
+size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
 int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
                             const float*, int, int, float*, hipStream_t);
 
@@ -148,6 +151,28 @@ int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float*
   PPS_ENFORCE(G >= k && ldd >= G, "need G >= k");
   PPS_ENFORCE(G < (1ll << 31), "G must fit int32");
   return topk(dist, Q, G, ldd, k, vals, idx, as_stream(stream));
+}
+
+int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
+  if (Q < 0 || G < 0 || k1 < 1 || k2 < 1) return -1;
+  return (int64_t)rerank_workspace_bytes(Q, G, k1, k2);
+}
+
+int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                   int64_t G, int k1, int k2, double lambda_value, void* workspace,
+                   int64_t ws_bytes, float* out, void* stream) {
+  PPS_ENFORCE(q_g && q_q && g_g && workspace && out, "null pointer");
+  PPS_ENFORCE(Q > 0 && G > 0, "bad shape");
+  PPS_ENFORCE(k1 >= 1 && k1 + 1 <= 64, "k1 + 1 must be <= 64");
+  PPS_ENFORCE(k2 >= 1 && k2 <= k1 + 1, "k2 must be in [1, k1 + 1]");
+  const int K1 = k1 + 1, Kh = (int)lrint(k1 / 2.0) + 1;
+  PPS_ENFORCE(K1 + K1 * Kh <= 1024, "expansion bound (k1+1)(round(k1/2)+2) must be <= 1024");
+  PPS_ENFORCE(k2 * (K1 + K1 * Kh <= 256 ? 256 : (K1 + K1 * Kh <= 512 ? 512 : 1024)) <= 4096,
+              "k2 * V row capacity must be <= 4096");
+  PPS_ENFORCE((Q + G) * 4 <= 160 * 1024, "Q + G must be <= 40960 (LDS accumulator)");
+  PPS_ENFORCE(Q + G <= Q + G && (Q + G) >= K1, "need Q + G >= k1 + 1");
+  return rerank(q_g, q_q, g_g, Q, G, k1, k2, lambda_value, workspace, (size_t)ws_bytes, out,
+                as_stream(stream));
 }
 
 int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,

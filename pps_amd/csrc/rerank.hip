@@ -1,0 +1,408 @@
+// k-reciprocal re-ranking on the GPU (Zhong et al., CVPR 2017), as the
+// reference evaluator applies it: reid_dataset_evaluator.py:442-519
+// `re_ranking(q_g_dist, q_q_dist, g_g_dist, k1=20, k2=6, lambda_value=0.3)`.
+//
+// The reference materialises four N x N matrices (N = Q + G) and walks them
+// with Python loops.  Here only the normalised squared-distance matrix OD is
+// dense; the k-reciprocal weights V are sparse rows (at most (k1+1)(r+2)
+// entries, r = round(k1/2)), the query-expanded V_qe rows are merges of k2
+// sparse rows, and the Jaccard term is accumulated per query in LDS through
+// an inverted (column) index of V_qe, in the same column order as the
+// reference, so every float32 sum has the reference's operand order.
+//
+//  1. rerank_colmax / rerank_build_od : OD[i][j] = M[j][i]^2 / max_r M[r][i]^2
+//     with M = [[qq, qg], [qg^T, gg]]                          (:447-454)
+//  2. pps_topk (rank.hip) on OD, k = k1 + 1 -> initial_rank      (:456)
+//  3. rerank_v_rows  : k-reciprocal sets, expansion, exp weights  (:462-488)
+//  4. rerank_vqe     : V_qe[i] = mean of V rows initial_rank[i,:k2] (:490-494)
+//  5. rerank_csc_*   : inverted index of V_qe                     (:497-499)
+//  6. rerank_jaccard : temp_min, jaccard, lambda blend, [Q][G] out (:501-518)
+#include "pps_internal.hpp"
+
+namespace pps {
+
+// M[r][c] of the concatenated distance matrix (before squaring)
+__device__ inline float rr_m(const float* qg, const float* qq, const float* gg, int64_t Q,
+                             int64_t G, int64_t r, int64_t c) {
+  if (r < Q) return c < Q ? qq[r * Q + c] : qg[r * G + (c - Q)];
+  return c < Q ? qg[c * G + (r - Q)] : gg[(r - Q) * G + (c - Q)];
+}
+
+// column max of M^2 (np.max(original_dist, axis=0) after np.power(.., 2))
+__global__ void rerank_colmax_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
+                                     const float* __restrict__ gg, int64_t Q, int64_t G,
+                                     float* __restrict__ colmax) {
+  const int64_t N = Q + G;
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float m = -INFINITY;
+  for (int64_t r = 0; r < N; ++r) {
+    const float v = rr_m(qg, qq, gg, Q, G, r, c);
+    m = fmaxf(m, v * v);
+  }
+  colmax[c] = m;
+}
+
+// OD[i][j] = M[j][i]^2 / colmax[i], via 32x32 LDS tiles (the transpose of :454)
+__global__ void rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
+                                       const float* __restrict__ gg, int64_t Q, int64_t G,
+                                       const float* __restrict__ colmax, float* __restrict__ od) {
+  __shared__ float tile[32][33];
+  const int64_t N = Q + G;
+  const int64_t i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: ty 0..7
+  for (int k = ty; k < 32; k += 8) {  // read M[j0+k][i0+tx] (row j, col i)
+    const int64_t r = j0 + k, c = i0 + tx;
+    float v = 0.f;
+    if (r < N && c < N) {
+      const float m = rr_m(qg, qq, gg, Q, G, r, c);
+      v = m * m;
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {  // write OD[i0+k][j0+tx] = tile[tx][k] / colmax
+    const int64_t i = i0 + k, j = j0 + tx;
+    if (i < N && j < N) od[i * N + j] = tile[tx][k] / colmax[i];
+  }
+}
+
+// ---- 3) V rows -----------------------------------------------------------------
+// One 64-lane wave per row i.  rank: [N][K1] (K1 = k1 + 1 <= 64), rank[i][0..K1).
+constexpr int kVCap = 1024;  // max expansion entries per row (bound checked on host)
+
+__device__ inline bool in_row(const int32_t* rank, int K1, int row, int len, int x) {
+  const int32_t* r = rank + (int64_t)row * K1;
+  for (int t = 0; t < len; ++t)
+    if (r[t] == x) return true;
+  return false;
+}
+
+__global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N,
+                                     const int32_t* __restrict__ rank, int K1, int Kh,
+                                     int vcap, int32_t* __restrict__ v_idx,
+                                     float* __restrict__ v_val, int32_t* __restrict__ v_cnt) {
+  __shared__ int32_t exp_[kVCap];
+  __shared__ int32_t R[64];
+  __shared__ int32_t s_n;
+  const int64_t i = blockIdx.x;
+  const int lane = threadIdx.x;
+  // k-reciprocal neighbours of i: forward k1+1 list, kept if i is in their list
+  int f = lane < K1 ? rank[i * K1 + lane] : -1;
+  bool rec = lane < K1 && in_row(rank, K1, f, K1, (int)i);
+  unsigned long long bal = __ballot(rec);
+  const int nR = __popcll(bal);
+  const int pos = __popcll(bal & ((1ull << lane) - 1ull));
+  if (rec) {
+    R[pos] = f;
+    exp_[pos] = f;
+  }
+  if (lane == 0) s_n = nR;
+  __syncthreads();
+  // expansion: candidates' own k-reciprocal sets over round(k1/2)+1 neighbours
+  for (int jc = 0; jc < nR; ++jc) {
+    const int cand = R[jc];
+    int cf = lane < Kh ? rank[(int64_t)cand * K1 + lane] : -1;
+    bool crec = lane < Kh && in_row(rank, K1, cf, Kh, cand);
+    unsigned long long cb = __ballot(crec);
+    const int ncr = __popcll(cb);
+    bool inR = false;
+    if (crec)
+      for (int t = 0; t < nR; ++t) inR |= (R[t] == cf);
+    const int inter = __popcll(__ballot(crec && inR));
+    if (3 * inter > 2 * ncr) {  // len(intersect) > 2/3 * len(candidate set)
+      const int base = s_n;
+      const int p = __popcll(cb & ((1ull << lane) - 1ull));
+      if (crec && base + p < kVCap) exp_[base + p] = cf;
+      __syncthreads();
+      if (lane == 0) s_n = base + ncr;
+    }
+    __syncthreads();
+  }
+  const int n = min(s_n, kVCap);
+  // np.unique: sort (bitonic over the next power of two) and drop repeats
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (int t = n + lane; t < n2; t += 64) exp_[t] = 0x7fffffff;
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = lane; t < n2 / 2; t += 64) {
+        const int a = 2 * stride * (t / stride) + (t % stride), b = a + stride;
+        const bool up = (a & size) == 0;
+        const int x = exp_[a], y = exp_[b];
+        if ((x > y) == up) { exp_[a] = y; exp_[b] = x; }
+      }
+      __syncthreads();
+    }
+  // compact unique entries (lane 0, n <= 1024: cheap) and weight them
+  if (lane == 0) {
+    int u = 0;
+    for (int t = 0; t < n; ++t)
+      if (t == 0 || exp_[t] != exp_[t - 1]) exp_[u++] = exp_[t];
+    s_n = u;
+  }
+  __syncthreads();
+  const int u = s_n;
+  float wsum = 0.f;
+  if (lane == 0) {
+    // weight = exp(-OD[i, idx]); V = weight / sum(weight) (float32, in index order)
+    for (int t = 0; t < u; ++t) wsum += expf(-od[i * N + exp_[t]]);
+  }
+  wsum = __shfl(wsum, 0);
+  const int cap = min(u, vcap);
+  for (int t = lane; t < cap; t += 64) {
+    const float w = expf(-od[i * N + exp_[t]]);
+    v_idx[i * vcap + t] = exp_[t];
+    v_val[i * vcap + t] = w / wsum;
+  }
+  if (lane == 0) v_cnt[i] = u;
+}
+
+// ---- 4) V_qe rows: mean of k2 sparse rows (row order = initial_rank order) ----
+constexpr int kQeCap = 4096;
+
+__global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int k2,
+                                  const int32_t* __restrict__ v_idx,
+                                  const float* __restrict__ v_val,
+                                  const int32_t* __restrict__ v_cnt, int vcap, int qcap,
+                                  int32_t* __restrict__ q_idx, float* __restrict__ q_val,
+                                  int32_t* __restrict__ q_cnt) {
+  __shared__ unsigned long long key[kQeCap];  // (column << 32) | (t << 16) | slot
+  __shared__ float val[kQeCap];
+  __shared__ int s_n;
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  for (int t = 0; t < k2; ++t) {
+    const int r = rank[i * K1 + t];
+    const int c = min(v_cnt[r], vcap);
+    const int base = s_n;
+    for (int e = tid; e < c; e += nt) {
+      if (base + e < kQeCap) {
+        key[base + e] = ((unsigned long long)(uint32_t)v_idx[(int64_t)r * vcap + e] << 32) |
+                        ((unsigned long long)t << 16) | (unsigned)(base + e);
+        val[base + e] = v_val[(int64_t)r * vcap + e];
+      }
+    }
+    __syncthreads();
+    if (tid == 0) s_n = base + c;
+    __syncthreads();
+  }
+  const int n = min(s_n, kQeCap);
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (int e = n + tid; e < n2; e += nt) key[e] = ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = tid; e < n2 / 2; e += nt) {
+        const int a = 2 * stride * (e / stride) + (e % stride), b = a + stride;
+        const bool up = (a & size) == 0;
+        const unsigned long long x = key[a], y = key[b];
+        if ((x > y) == up) { key[a] = y; key[b] = x; }
+      }
+      __syncthreads();
+    }
+  // segmented sums per column in row order t (key order), then / k2
+  if (tid == 0) {
+    int u = 0;
+    int e = 0;
+    while (e < n) {
+      const uint32_t col = (uint32_t)(key[e] >> 32);
+      float s = val[key[e] & 0xffff];
+      int f = e + 1;
+      while (f < n && (uint32_t)(key[f] >> 32) == col) {
+        s += val[key[f] & 0xffff];
+        ++f;
+      }
+      if (u < qcap) {
+        q_idx[i * qcap + u] = (int32_t)col;
+        q_val[i * qcap + u] = s / (float)k2;
+      }
+      ++u;
+      e = f;
+    }
+    q_cnt[i] = u;
+  }
+}
+
+// ---- 5) inverted index (CSC) of V_qe ------------------------------------------
+__global__ void rerank_csc_count_kernel(int64_t N, const int32_t* __restrict__ q_idx,
+                                        const float* __restrict__ q_val,
+                                        const int32_t* __restrict__ q_cnt, int qcap,
+                                        int32_t* __restrict__ col_cnt) {
+  const int64_t i = blockIdx.x;
+  const int c = min(q_cnt[i], qcap);
+  for (int e = threadIdx.x; e < c; e += blockDim.x)
+    if (q_val[i * qcap + e] != 0.f) atomicAdd(&col_cnt[q_idx[i * qcap + e]], 1);
+}
+
+__global__ void rerank_scan_kernel(int64_t N, const int32_t* __restrict__ cnt,
+                                   int32_t* __restrict__ start) {
+  // single block exclusive scan (N <= ~100k: cheap next to the rest)
+  __shared__ int32_t part[1024];
+  const int tid = threadIdx.x;
+  const int64_t per = (N + 1023) / 1024;
+  const int64_t a = tid * per, b = min(N, a + per);
+  int32_t s = 0;
+  for (int64_t e = a; e < b; ++e) s += cnt[e];
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int32_t run = 0;
+    for (int t = 0; t < 1024; ++t) {
+      const int32_t v = part[t];
+      part[t] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  int32_t run = part[tid];
+  for (int64_t e = a; e < b; ++e) {
+    start[e] = run;
+    run += cnt[e];
+  }
+  if (tid == 1023) start[N] = run;
+}
+
+__global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_idx,
+                                       const float* __restrict__ q_val,
+                                       const int32_t* __restrict__ q_cnt, int qcap,
+                                       const int32_t* __restrict__ start,
+                                       int32_t* __restrict__ fill, int32_t* __restrict__ csc_row,
+                                       float* __restrict__ csc_val) {
+  const int64_t i = blockIdx.x;
+  const int c = min(q_cnt[i], qcap);
+  for (int e = threadIdx.x; e < c; e += blockDim.x) {
+    const float v = q_val[i * qcap + e];
+    if (v == 0.f) continue;
+    const int col = q_idx[i * qcap + e];
+    const int slot = start[col] + atomicAdd(&fill[col], 1);
+    csc_row[slot] = (int32_t)i;
+    csc_val[slot] = v;
+  }
+}
+
+// ---- 6) Jaccard + blend for the query rows ------------------------------------
+__global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restrict__ od,
+                                      const int32_t* __restrict__ q_idx,
+                                      const float* __restrict__ q_val,
+                                      const int32_t* __restrict__ q_cnt, int qcap,
+                                      const int32_t* __restrict__ start,
+                                      const int32_t* __restrict__ csc_row,
+                                      const float* __restrict__ csc_val, float lam,
+                                      float one_m_lam, float* __restrict__ out) {
+  extern __shared__ float tm[];  // [N] temp_min accumulator
+  const int64_t i = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) tm[j] = 0.f;
+  __syncthreads();
+  const int c = min(q_cnt[i], qcap);
+  for (int e = 0; e < c; ++e) {  // nonzero columns of V_qe[i] in increasing order
+    const float a = q_val[i * qcap + e];
+    if (a == 0.f) continue;
+    const int col = q_idx[i * qcap + e];
+    const int s0 = start[col], s1 = start[col + 1];
+    for (int s = s0 + threadIdx.x; s < s1; s += blockDim.x)
+      tm[csc_row[s]] = tm[csc_row[s]] + fminf(a, csc_val[s]);  // one row per column entry
+    __syncthreads();
+  }
+  for (int64_t j = Q + threadIdx.x; j < N; j += blockDim.x) {
+    const float t = tm[j];
+    const float jac = 1.f - __fdiv_rn(t, 2.f - t);
+    out[i * (N - Q) + (j - Q)] = __fadd_rn(__fmul_rn(jac, one_m_lam),
+                                           __fmul_rn(od[i * N + j], lam));
+  }
+}
+
+int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+
+int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t G, int k1,
+           int k2, double lambda, void* ws, size_t ws_bytes, float* out, hipStream_t st) {
+  // NumPy (NEP 50) casts the Python-float factors to float32: lambda and 1-lambda
+  const float lam = (float)lambda, one_m_lam = (float)(1.0 - lambda);
+  const int64_t N = Q + G;
+  const int K1 = k1 + 1;
+  const int Kh = (int)lrint(k1 / 2.0) + 1;  // int(np.around(k1 / 2.)) + 1
+  const int vbound = K1 + K1 * Kh;
+  const int vcap = vbound <= 256 ? 256 : (vbound <= 512 ? 512 : 1024);
+  const int qcap = k2 * vcap;
+  // workspace carve-up (all 256-B aligned)
+  char* p = reinterpret_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += (bytes + 255) / 256 * 256;
+    return r;
+  };
+  float* od = reinterpret_cast<float*>(take(sizeof(float) * N * N));
+  float* colmax = reinterpret_cast<float*>(take(sizeof(float) * N));
+  float* topv = reinterpret_cast<float*>(take(sizeof(float) * N * K1));
+  int32_t* rank = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * K1));
+  int32_t* v_idx = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * vcap));
+  float* v_val = reinterpret_cast<float*>(take(sizeof(float) * N * vcap));
+  int32_t* v_cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N));
+  int32_t* q_idx = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * qcap));
+  float* q_val = reinterpret_cast<float*>(take(sizeof(float) * N * qcap));
+  int32_t* q_cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N));
+  int32_t* col_cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (N + 1)));
+  int32_t* start = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (N + 1)));
+  int32_t* fill = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (N + 1)));
+  int32_t* csc_row = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * qcap));
+  float* csc_val = reinterpret_cast<float*>(take(sizeof(float) * N * qcap));
+  if ((size_t)(p - reinterpret_cast<char*>(ws)) > ws_bytes) {
+    set_error("rerank workspace too small: need " +
+              std::to_string((size_t)(p - reinterpret_cast<char*>(ws))) + " bytes");
+    return PPS_ERR_CAPACITY;
+  }
+  hipLaunchKernelGGL(rerank_colmax_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
+                     qg, qq, gg, Q, G, colmax);
+  hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 31) / 32),
+                                                  (unsigned)((N + 31) / 32)),
+                     dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od);
+  PPS_CHECK_LAUNCH("rerank_build_od_kernel");
+  int rc = topk(od, N, N, N, K1, topv, rank, st);
+  if (rc != PPS_OK) return rc;
+  hipLaunchKernelGGL(rerank_v_rows_kernel, dim3((unsigned)N), dim3(64), 0, st, od, N, rank,
+                     K1, Kh, vcap, v_idx, v_val, v_cnt);
+  PPS_CHECK_LAUNCH("rerank_v_rows_kernel");
+  if (k2 != 1) {
+    hipLaunchKernelGGL(rerank_vqe_kernel, dim3((unsigned)N), dim3(256), 0, st, N, rank, K1, k2,
+                       v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
+    PPS_CHECK_LAUNCH("rerank_vqe_kernel");
+  } else {
+    (void)hipMemcpyAsync(q_idx, v_idx, sizeof(int32_t) * N * vcap, hipMemcpyDeviceToDevice, st);
+    (void)hipMemcpyAsync(q_val, v_val, sizeof(float) * N * vcap, hipMemcpyDeviceToDevice, st);
+    (void)hipMemcpyAsync(q_cnt, v_cnt, sizeof(int32_t) * N, hipMemcpyDeviceToDevice, st);
+  }
+  const int qc = k2 != 1 ? qcap : vcap;
+  (void)hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * (N + 1), st);
+  (void)hipMemsetAsync(fill, 0, sizeof(int32_t) * (N + 1), st);
+  hipLaunchKernelGGL(rerank_csc_count_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
+                     q_val, q_cnt, qc, col_cnt);
+  hipLaunchKernelGGL(rerank_scan_kernel, dim3(1), dim3(1024), 0, st, N, col_cnt, start);
+  hipLaunchKernelGGL(rerank_csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
+                     q_val, q_cnt, qc, start, fill, csc_row, csc_val);
+  PPS_CHECK_LAUNCH("rerank_csc_fill_kernel");
+  hipLaunchKernelGGL(rerank_jaccard_kernel, dim3((unsigned)Q), dim3(256), sizeof(float) * N, st,
+                     Q, N, od, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam, one_m_lam,
+                     out);
+  PPS_CHECK_LAUNCH("rerank_jaccard_kernel");
+  return PPS_OK;
+}
+
+size_t rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
+  const int64_t N = Q + G;
+  const int K1 = k1 + 1;
+  const int Kh = (int)lrint(k1 / 2.0) + 1;
+  const int vbound = K1 + K1 * Kh;
+  const int vcap = vbound <= 256 ? 256 : (vbound <= 512 ? 512 : 1024);
+  const int64_t qcap = (int64_t)k2 * vcap;
+  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+  size_t s = 0;
+  s += r(4 * N * N) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
+  s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
+  return s;
+}
+
+}  // namespace pps

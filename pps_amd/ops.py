@@ -123,6 +123,20 @@ def ap_finalize(sorted_d, pos_total, hist, before):
     return ap, valid, first
 
 
+def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3):
+    """k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519) -> [Q, G]."""
+    Q, G = q_g.shape
+    assert tuple(q_q.shape) == (Q, Q) and tuple(g_g.shape) == (G, G)
+    nbytes = _lib.lib().pps_rerank_workspace_bytes(Q, G, k1, k2)
+    if nbytes < 0:
+        raise RuntimeError('bad re-ranking arguments')
+    ws = torch.empty((int(nbytes),), dtype=torch.uint8, device=q_g.device)
+    out = torch.empty((Q, G), dtype=torch.float32, device=q_g.device)
+    call('pps_re_ranking', _dev(q_g, 'q_g'), _dev(q_q, 'q_q'), _dev(g_g, 'g_g'), Q, G, k1, k2,
+         float(lambda_value), ws.data_ptr(), int(nbytes), out.data_ptr(), _stream())
+    return out
+
+
 def max_positives(qid, qcam, gid, gcam):
     """Host-side bound on true matches per query (metadata only, exact)."""
     qid = np.asarray(qid, np.int64)

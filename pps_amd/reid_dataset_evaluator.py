@@ -191,7 +191,34 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
             print_scores(mq_mAP, mq_cmc)
 
     if cfg.REID.RERANK:
-        raise NotImplementedError(
-            'REID.RERANK: k-reciprocal re-ranking on the GPU is the next §8(f) row; '
-            'every shipped PPS config sets RERANK: False')
+        # :161-207 -- re-ranked scores overwrite the plain ones
+        with measure_time('Re-ranking distance...', verbose):
+            q_q = ops.compute_dist(qf, qf, metric=metric)
+            g_g = ops.compute_dist(gf, gf, metric=metric)
+            rr = ops.re_ranking(q_g, q_q, g_g)
+        with measure_time('Computing scores for re-ranked distance...', verbose):
+            mAP, cmc_scores = compute_score(rr, ids[q_inds], ids[g_inds], cams[q_inds],
+                                            cams[g_inds])
+        if verbose:
+            print('{:<30}'.format('Re-ranked Single Query:'), end='')
+            print_scores(mAP, cmc_scores)
+        if mq_inds.any():
+            with measure_time('Multi Query, Re-ranking distance...', verbose):
+                mq_mq = ops.compute_dist(pooled, pooled, metric=metric)
+                rr_mq = ops.re_ranking(mq_g, mq_mq, g_g)
+            with measure_time('Multi Query, Computing scores for re-ranked distance...',
+                              verbose):
+                mq_mAP, mq_cmc = compute_score(rr_mq, keys[:, 0], ids[g_inds], keys[:, 1],
+                                               cams[g_inds])
+            if verbose:
+                print('{:<30}'.format('Re-ranked Multi Query:'), end='')
+                print_scores(mq_mAP, mq_cmc)
     return mAP, cmc_scores, mq_mAP, mq_cmc
+
+
+def re_ranking(q_g_dist, q_q_dist, g_g_dist, k1=20, k2=6, lambda_value=0.3):
+    """:442-519 on the GPU; NumPy in -> NumPy out, CUDA tensors in -> tensor out."""
+    as_numpy = not isinstance(q_g_dist, torch.Tensor)
+    out = ops.re_ranking(_to_dev(q_g_dist), _to_dev(q_q_dist), _to_dev(g_g_dist), k1, k2,
+                         lambda_value)
+    return out.cpu().numpy() if as_numpy else out

@@ -155,3 +155,37 @@ def test_evaluate_vs_golden(golden):
                                           verbose=False)
     assert abs(mAP - float(g['mAP'])) < 1e-9
     np.testing.assert_allclose(cmc, g['cmc'], atol=1e-12)
+
+
+def test_re_ranking_vs_golden(golden):
+    """k-reciprocal re-ranking on the GPU vs the reference's own output."""
+    from pps_amd import reid_dataset_evaluator as gev
+    g = golden('rerank')
+    rr = gev.re_ranking(g['q_g'], g['q_q'], g['g_g'], k1=20, k2=6, lambda_value=0.3)
+    np.testing.assert_allclose(rr, g['rerank'], rtol=0, atol=1e-5)
+    m = gev.mean_ap(rr, g['qid'], g['gid'], g['qcam'], g['gcam'])
+    assert abs(m - float(g['mAP'])) < 1e-6
+
+
+@pytest.mark.parametrize('k1,k2', [(20, 6), (10, 1), (6, 3)])
+def test_re_ranking_vs_oracle_params(k1, k2):
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(k1 + k2)
+    x = rng.randn(150, 32).astype(np.float32)
+    q, g = x[:30], x[30:]
+    qg, qq, gg = ev.compute_dist(q, g), ev.compute_dist(q, q), ev.compute_dist(g, g)
+    ref = ev.re_ranking(qg, qq, gg, k1=k1, k2=k2, lambda_value=0.3)
+    rr = gev.re_ranking(qg, qq, gg, k1=k1, k2=k2, lambda_value=0.3)
+    np.testing.assert_allclose(rr, ref, rtol=0, atol=1e-5)
+
+
+def test_evaluate_with_rerank_vs_oracle(golden):
+    from pps_amd import reid_dataset_evaluator as gev
+    from pps_amd.config import cfg
+    g = golden('evaluate')
+    cfg.REID.RERANK = True
+    mAP, cmc, _, _ = gev.evaluate_arrays(g['feat'], g['ids'], g['cams'], g['marks'],
+                                         verbose=False)
+    ref = ev.evaluate_arrays(g['feat'], g['ids'], g['cams'], g['marks'], rerank=True)
+    assert abs(mAP - ref[0]) < 1e-6
+    np.testing.assert_allclose(cmc, ref[1], atol=1e-9)

@@ -9,7 +9,7 @@ from tests.conftest import ROOT
 def _declared():
     with open(os.path.join(ROOT, 'include', 'pps_abi.h')) as f:
         src = f.read()
-    return sorted(set(re.findall(r'^(?:int|const char\*)\s+(pps_\w+)\s*\(', src, re.M)))
+    return sorted(set(re.findall(r'^(?:int64_t|int|const char\*)\s+(pps_\w+)\s*\(', src, re.M)))
 
 
 def test_header_declares_entry_points():
