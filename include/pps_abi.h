@@ -198,6 +198,12 @@ int pps_part_power_set(const float* x, int N, int H, int W, int C,
 int pps_l2_normalize(const float* x, int64_t N, int D, float* y,
                      void* stream);
 
+/* Multi-query pooling (reid_dataset_evaluator.py:132-143, pool_type
+ * 'average'): out[g][:] = mean of x[members[offsets[g]..offsets[g+1])][:],
+ * summed in member order (device arrays; every group non-empty). */
+int pps_group_mean(const float* x, int D, const int32_t* offsets,
+                   const int32_t* members, int ngroups, float* out, void* stream);
+
 /* Image preprocessing (utils/blob.py:97-117 prep_im_for_blob,
  * :65-94 im_list_to_blob): uint8 BGR HWC images [N][Hi][Wi][3] (device) ->
  * subtract pixel means (HOST float[3]) -> bicubic resize (a = -0.75,

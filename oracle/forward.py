@@ -16,6 +16,7 @@ restated with the Caffe2 (pytorch v1.0.1) NCHW semantics the reference ran on
   Split        axis 2 by `split`
   FC           x W^T + b        Concat axis 1        Reshape [1,-1] -> [N,-1]
   Normalize    x / max(||x||_2, 1e-12) along axis 1
+  UpsampleNearest  integer nearest-neighbour upsampling (FPN top-down path)
 
 torch on CPU is used as the fp32 array library.  Only tests/, smoke() and
 bench.py's cpu_baseline may use this module.
@@ -113,6 +114,8 @@ class GraphForward(object):
             return [cat, torch.tensor([v.shape[a['axis']] for v in x])]
         if t == 'Reshape':
             return [x[0].reshape(x[0].shape[0], -1), torch.tensor(a['shape'])]
+        if t == 'UpsampleNearest':
+            return [F.interpolate(x[0], scale_factor=a['scale'], mode='nearest')]
         if t == 'Normalize':
             v = x[0]
             n = torch.sqrt(torch.sum(v * v, dim=1, keepdim=True))

@@ -50,6 +50,7 @@ SIGNATURES = {
     'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,
                            c_ptr],
     'pps_l2_normalize': [c_ptr, c_i64, c_int, c_ptr, c_ptr],
+    'pps_group_mean': [c_ptr, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr': [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr_ragged': [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int,
                                   c_ptr, c_ptr],

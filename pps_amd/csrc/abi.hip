@@ -17,6 +17,7 @@ int maxpool2d(const float*, int, int, int, int, int, int, int, float*, int, int,
 int part_power_set(const float*, int, int, int, int, const int32_t*, int, int, float*,
                    hipStream_t);
 int l2_normalize(const float*, int64_t, int, float*, hipStream_t);
+int group_mean(const float*, int, const int32_t*, const int32_t*, int, float*, hipStream_t);
 int preprocess_bgr(const uint8_t*, int, int, int, const int64_t*, const int32_t*,
                    const int32_t*, const float*, int, int, float*, hipStream_t);
 int collect_positives(const float*, int64_t, int64_t, int64_t, const int32_t*,
@@ -323,6 +324,12 @@ int pps_part_power_set(const float* x, int N, int H, int W, int C, const int32_t
   }
   PPS_ENFORCE(sum == H, "split heights must sum to H (Split axis=2)");
   return part_power_set(x, N, H, W, C, splits, nstrip, max_ave, out, as_stream(stream));
+}
+
+int pps_group_mean(const float* x, int D, const int32_t* offsets, const int32_t* members,
+                   int ngroups, float* out, void* stream) {
+  PPS_ENFORCE(x && offsets && members && out && D > 0 && ngroups >= 0, "bad arguments");
+  return group_mean(x, D, offsets, members, ngroups, out, as_stream(stream));
 }
 
 int pps_l2_normalize(const float* x, int64_t N, int D, float* y, void* stream) {

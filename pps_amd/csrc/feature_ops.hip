@@ -314,6 +314,31 @@ __global__ void part_power_set_v2_kernel(const float* __restrict__ x, int N, int
   }
 }
 
+// ---- multi-query pooling (reid_dataset_evaluator.py:132-143) ------------------
+// out[g] = mean of rows members[offsets[g] .. offsets[g+1]) of x, summed in
+// member order then divided by the count (np.mean over axis 0, float32).
+__global__ void group_mean_kernel(const float* __restrict__ x, int D,
+                                  const int32_t* __restrict__ offsets,
+                                  const int32_t* __restrict__ members,
+                                  float* __restrict__ out) {
+  const int g = blockIdx.x;
+  const int a = offsets[g], b = offsets[g + 1];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = x[(int64_t)members[a] * D + d];
+    for (int m = a + 1; m < b; ++m) s += x[(int64_t)members[m] * D + d];
+    out[(int64_t)g * D + d] = s / (float)(b - a);
+  }
+}
+
+int group_mean(const float* x, int D, const int32_t* offsets, const int32_t* members,
+               int ngroups, float* out, hipStream_t st) {
+  if (ngroups <= 0) return PPS_OK;
+  hipLaunchKernelGGL(group_mean_kernel, dim3(ngroups), dim3(256), 0, st, x, D, offsets,
+                     members, out);
+  PPS_CHECK_LAUNCH("group_mean_kernel");
+  return PPS_OK;
+}
+
 // ---- Preprocess (utils/blob.py:97-117) ---------------------------------------
 // u8 BGR HWC -> float, minus PIXEL_MEANS, bicubic resize (cv2.INTER_CUBIC:
 // a = -0.75, src = (dst + 0.5) * scale - 0.5, replicate border) -> NHWC4.

@@ -169,11 +169,30 @@ def add_reid_outputs(plan, prefixes, dim, preprefix='reid'):
     return out
 
 
+def add_fpn_coarsest_level(plan, blob, dim):
+    """FPN_reid.py:117-174 add_fpn, restricted to what the test net consumes:
+    with FPN_ON the PPS head reads only blob_in[0] (pps_heads.py:88-96), the
+    coarsest level = Conv 1x1 (bias) -> SpatialBN -> Relu on res5_2_sum
+    ('fpn_inner_res5_2_sum_bn').  The reference also computes the top-down /
+    lateral levels at test, whose outputs are never read (SURVEY Appendix A.6);
+    they are not built here.  No P6 level: max FPN level = 5 unless
+    MULTILEVEL_RPN/ROIS (FPN_reid.py:375-390, :272-283)."""
+    fpn_dim = cfg.FPN.DIM
+    if dim == fpn_dim:
+        return blob, dim
+    out = plan.conv(blob, 'fpn_inner_' + blob, dim, fpn_dim, 1, 1, 0, relu=True, bias=True,
+                    bn='fpn_inner_' + blob + '_bn')
+    return out, fpn_dim
+
+
 def build_plan():
     """model_builder.py:242 build_generic_reid_model (test, single GPU)."""
-    assert not cfg.FPN.FPN_ON, 'FPN_reid variant is not built yet (SURVEY §8(a) gated row)'
     plan = Plan()
     blob, dim, scale = add_ResNet50_conv5_body(plan)
+    if cfg.FPN.FPN_ON:
+        assert 'FPN_reid.add_fpn_ResNet50_conv5_body' in cfg.MODEL.CONV_BODY, \
+            'FPN_ON: only FPN_reid.add_fpn_ResNet50_conv5_body is built'
+        blob, dim = add_fpn_coarsest_level(plan, blob, dim)
     prefixes, d = add_pps_part_head(plan, blob, dim, scale)
     plan.output = add_reid_outputs(plan, prefixes, d)
     plan.spatial_scale = scale

@@ -231,6 +231,21 @@ def part_power_set(x, split, max_ave, out):
     return out
 
 
+def group_mean(x, groups):
+    """x [N,D] device; groups: list of index lists -> [len(groups), D] means."""
+    N, D = x.shape
+    offs = np.zeros(len(groups) + 1, np.int32)
+    offs[1:] = np.cumsum([len(g) for g in groups])
+    mem = np.concatenate([np.asarray(g, np.int32) for g in groups]) if groups else \
+        np.zeros(0, np.int32)
+    d_offs = torch.from_numpy(offs).to(x.device)
+    d_mem = torch.from_numpy(mem).to(x.device)
+    out = torch.empty((len(groups), D), dtype=torch.float32, device=x.device)
+    call('pps_group_mean', _dev(x, 'x'), D, d_offs.data_ptr(), d_mem.data_ptr(), len(groups),
+         out.data_ptr(), _stream())
+    return out
+
+
 def l2_normalize(x, y=None):
     N, D = x.shape
     if y is None:

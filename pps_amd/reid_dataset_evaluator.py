@@ -177,9 +177,8 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         groups = OrderedDict()
         for k, key in enumerate(zip(ids[mq_inds], cams[mq_inds])):
             groups.setdefault(key, []).append(k)
-        mqf = feat.index_select(0, torch.from_numpy(np.nonzero(mq_inds)[0]).cuda())
-        pooled = torch.stack([mqf[torch.tensor(v, device=mqf.device)].mean(0)
-                              for v in groups.values()]).contiguous()
+        mq_rows = np.nonzero(mq_inds)[0]
+        pooled = ops.group_mean(feat, [mq_rows[v] for v in groups.values()])
         keys = np.array(list(groups.keys()))
         with measure_time('Multi Query, Computing distance...', verbose):
             mq_g = ops.compute_dist(pooled, gf, metric=metric)

@@ -165,7 +165,12 @@ def record(cfg_file, overrides=()):
     import io
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
-        blob, dim, scale = ResNet.add_ResNet50_conv5_body(m)
+        if cfg.FPN.FPN_ON:
+            import detectron.modeling.FPN_reid as FPN_reid
+            body = cfg.MODEL.CONV_BODY.split('.')[-1]
+            blob, dim, scale = getattr(FPN_reid, body)(m)
+        else:
+            blob, dim, scale = ResNet.add_ResNet50_conv5_body(m)
         blobs, dims = pps_heads.add_pps_part_head(m, blob, dim, scale)
         reid_heads.add_reid_outputs(m, blobs, dims)
     out = 'reid_feature_concat_norm' if cfg.REID.NORMALIZE_FEATURE else 'reid_feature_concat'
@@ -177,19 +182,33 @@ def record(cfg_file, overrides=()):
         USE_BN=bool(cfg.MODEL.USE_BN), NUM_CLASSES=cfg.MODEL.NUM_CLASSES,
         PIXEL_MEANS=[float(v) for v in cfg.PIXEL_MEANS.ravel()],
         FPN_ON=bool(cfg.FPN.FPN_ON))
+    keys['CONV_BODY'] = cfg.MODEL.CONV_BODY
+    keys['FPN_DIM'] = cfg.FPN.DIM
     return dict(cfg_file=os.path.relpath(cfg_file, REF), cfg=keys, ops=m.ops,
-                params=m.params, output=out, spatial_scale=scale)
+                params=m.params, output=out,
+                spatial_scale=scale if not isinstance(scale, (list, tuple)) else list(scale),
+                overrides=list(overrides))
 
 
 def main():
     install_stubs()
-    g = record(os.path.join(REF, 'configs/market1501/pps_crm_triplet_R-50_1x.yaml'))
-    path = os.path.join(HERE, 'pps_graph_market1501.json')
-    with open(path, 'w') as f:
-        json.dump(g, f, indent=0, sort_keys=True)
     from collections import Counter
-    c = Counter(o['type'] for o in g['ops'])
-    print(path, len(g['ops']), 'ops', dict(c), len(g['params']), 'params')
+    from detectron.core.config import cfg
+    import copy
+    pristine = copy.deepcopy(cfg)
+    cases = [('pps_graph_market1501.json', ()),
+             # config-gated FPN_reid variant; not in a shipped config
+             ('pps_graph_market1501_fpn.json',
+              ('FPN.FPN_ON', 'True', 'MODEL.CONV_BODY', 'FPN_reid.add_fpn_ResNet50_conv5_body'))]
+    for name, over in cases:
+        cfg.clear()
+        cfg.update(copy.deepcopy(pristine))
+        g = record(os.path.join(REF, 'configs/market1501/pps_crm_triplet_R-50_1x.yaml'), over)
+        path = os.path.join(HERE, name)
+        with open(path, 'w') as f:
+            json.dump(g, f, indent=0, sort_keys=True)
+        c = Counter(o['type'] for o in g['ops'])
+        print(path, len(g['ops']), 'ops', dict(c), len(g['params']), 'params')
 
 
 if __name__ == '__main__':

@@ -241,3 +241,28 @@ def test_heads_splitk_bn_relu_normalize(splitk):
     ref = np.maximum(ref * sc + sh, 0)
     ref /= np.maximum(np.linalg.norm(ref, axis=1, keepdims=True), 1e-12)
     np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=0, atol=2e-6)
+
+
+def test_fpn_variant_forward_vs_oracle():
+    from oracle.forward import GraphForward, load_graph
+    from pps_amd import config, model
+    import os
+    _market_cfg()
+    config.merge_cfg_from_list(['FPN.FPN_ON', 'True', 'MODEL.CONV_BODY',
+                                'FPN_reid.add_fpn_ResNet50_conv5_body'])
+    g = load_graph(os.path.join(os.path.dirname(__file__), 'golden',
+                                'pps_graph_market1501_fpn.json'))
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=3)
+    # dead top-down params exist in the reference graph: give them values too
+    rng = np.random.RandomState(0)
+    for k, shp in g['params'].items():
+        if k not in blobs and '_fc_' not in k:
+            blobs[k] = (rng.rand(*shp) + 0.5).astype(np.float32) if k.endswith(('_s', '_riv')) \
+                else (0.05 * rng.randn(*shp)).astype(np.float32)
+    x = (rng.randn(2, 3, 384, 128) * 50).astype(np.float32)
+    ref = GraphForward(blobs, graph=g)(x).numpy()
+    xin = np.zeros((2, 384, 128, 4), np.float32)
+    xin[..., :3] = x.transpose(0, 2, 3, 1)
+    out = model.PPSModel(blobs, plan=plan).forward(_cuda(xin)).cpu().numpy()
+    np.testing.assert_allclose(out, ref, rtol=0, atol=2e-5)

@@ -189,3 +189,19 @@ def test_evaluate_with_rerank_vs_oracle(golden):
     ref = ev.evaluate_arrays(g['feat'], g['ids'], g['cams'], g['marks'], rerank=True)
     assert abs(mAP - ref[0]) < 1e-6
     np.testing.assert_allclose(cmc, ref[1], atol=1e-9)
+
+
+def test_multi_query_pooling_vs_oracle():
+    """marks == 2 (multi-query): per-(id, cam) mean features, then scores."""
+    from pps_amd import reid_dataset_evaluator as gev
+    from pps_amd.config import cfg
+    cfg.REID.RERANK = False
+    rng = np.random.RandomState(9)
+    x = rng.randn(200, 64).astype(np.float32)
+    ids = rng.randint(1, 15, 200)
+    cams = rng.randint(1, 4, 200)
+    marks = rng.choice([0, 1, 1, 2], 200)
+    res = gev.evaluate_arrays(x, ids, cams, marks, verbose=False)
+    ref = ev.evaluate_arrays(x, ids, cams, marks)
+    assert abs(res[0] - ref[0]) < 1e-9 and abs(res[2] - ref[2]) < 1e-9
+    np.testing.assert_allclose(res[3], ref[3], atol=1e-12)

@@ -68,3 +68,23 @@ def test_yaml_merge_and_overrides():
     import pytest
     with pytest.raises(AttributeError):
         cfg.REID.BPM_DIM = 3
+
+
+def test_fpn_variant_plan_is_reference_subset():
+    """FPN_reid (config-gated): the plan holds exactly the reference params the
+    test net reads; the rest of the reference graph is the dead top-down path."""
+    from pps_amd import config, model
+    _market()
+    config.merge_cfg_from_list(['FPN.FPN_ON', 'True', 'MODEL.CONV_BODY',
+                                'FPN_reid.add_fpn_ResNet50_conv5_body'])
+    plan = model.build_plan()
+    with open(os.path.join(GOLDEN, 'pps_graph_market1501_fpn.json')) as f:
+        g = json.load(f)
+    ref = {k: tuple(v) for k, v in g['params'].items() if '_fc_' not in k}
+    mine = {k: tuple(v) for k, v in plan.params.items()}
+    assert set(mine) <= set(ref)
+    assert all(ref[k] == v for k, v in mine.items())
+    dead = set(ref) - set(mine)
+    assert dead and all(k.startswith('fpn_inner_res4') or k.startswith('fpn_inner_res3') or
+                        k.startswith('fpn_inner_res2') for k in dead), sorted(dead)[:5]
+    assert mine['pps0_conv_w'] == (128, 256, 1, 1)
