@@ -25,8 +25,8 @@ namespace pps {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 16;
-constexpr int LSTR = BK + 4;  // LDS row stride in floats
+// K chunk per LDS stage is a template parameter BK (16 or 32); LDS rows hold
+// BK floats + 4 pad: 80 B or 144 B, both conflict-free for the fragment reads.
 constexpr int kOOB = 0x7ffffff0;  // byte offset beyond any num_records -> reads 0
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -38,13 +38,17 @@ __device__ inline f32x4 bload(rsrc_t r, int byte_off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int BK>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int T = 64 * WM * WN;
+  constexpr int LSTR = BK + 4;         // LDS row stride in floats
+  constexpr int V4 = BK / 4;           // float4 per LDS row
+  constexpr int HK = BK / 2;           // k values per lane half per chunk
   constexpr int AL = BM * BK / 4 / T;  // f32x4 loads per thread (A)
   constexpr int BL = BN * BK / 4 / T;  // f32x4 loads per thread (B)
-  constexpr int ROWS_PER_PASS = T / 4;
+  constexpr int ROWS_PER_PASS = T / V4;
+  static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   static_assert(AL >= 1 && BL >= 1, "tile too small for thread count");
@@ -90,13 +94,14 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // ---- per-thread A-row geometry (once) -------------------------------------
   // Element offset of (row, tap t, channel c) = rbase + tap_off(t) + c, valid
   // iff bit t of the row's tap mask is set (input pixel inside the image).
-  const int c4 = tid & 3;
+  const int c4 = tid % V4;   // float4 slot within the chunk row
+  const int trow = tid / V4;
   int rbase[AL];
   uint64_t tmask[AL];
   const int ntaps = p.KH * p.KW;
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int row = m0 + (tid >> 2) + i * ROWS_PER_PASS;
+    const int row = m0 + trow + i * ROWS_PER_PASS;
     const int rowc = row < p.M ? row : 0;
     const int hw = p.Ho * p.Wo;
     const int n = rowc / hw;
@@ -151,7 +156,7 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
     ra2_src = make_rsrc(p.a2, p.a2_bytes);
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int row = m0 + (tid >> 2) + i * ROWS_PER_PASS;
+      const int row = m0 + trow + i * ROWS_PER_PASS;
       const int hw = p.Ho * p.Wo;
       const int n = row / hw;
       const int rem = row - n * hw;
@@ -166,7 +171,7 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   int bbase[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
-    const int col = n0 + (tid >> 2) + i * ROWS_PER_PASS;
+    const int col = n0 + trow + i * ROWS_PER_PASS;
     bbase[i] = col < p.Ncol ? (col * p.ldb + c4 * 4) * 4 : kOOB;
   }
 
@@ -226,7 +231,7 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) nb[j] = 0.f;
 
-  const int nchunks = p.Kloop / BK;
+  const int nchunks = (p.Kloop + BK - 1) / BK;  // zero-filled tail half-chunk
   load_chunk(0);
   int buf = 0;
   for (int kc = 0; kc < nchunks; ++kc) {
@@ -234,50 +239,56 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
     float* bs = Bs + buf * BN * LSTR;
 #pragma unroll
     for (int i = 0; i < AL; ++i)
-      *reinterpret_cast<f32x4*>(as + ((tid >> 2) + i * ROWS_PER_PASS) * LSTR + c4 * 4) = ra[i];
+      *reinterpret_cast<f32x4*>(as + (trow + i * ROWS_PER_PASS) * LSTR + c4 * 4) = ra[i];
 #pragma unroll
     for (int i = 0; i < BL; ++i)
-      *reinterpret_cast<f32x4*>(bs + ((tid >> 2) + i * ROWS_PER_PASS) * LSTR + c4 * 4) = rb[i];
+      *reinterpret_cast<f32x4*>(bs + (trow + i * ROWS_PER_PASS) * LSTR + c4 * 4) = rb[i];
     __syncthreads();
     if (kc + 1 < nchunks) load_chunk(kc + 1);
 
-    f32x4 fa[TM][2], fb[TN][2];
+    // K order inside every 16-wide group g: MFMA step s, lane half h uses
+    // k = 16g + 8h + s.  BK=32 runs two groups per barrier with exactly the
+    // accumulation order of BK=16, so every tile / BK variant is bit-identical.
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* src = as + (wm * (BM / WM) + i * 32 + r32) * LSTR + h * 8;
-      fa[i][0] = *reinterpret_cast<const f32x4*>(src);
-      fa[i][1] = *reinterpret_cast<const f32x4*>(src + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* src = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + h * 8;
-      fb[j][0] = *reinterpret_cast<const f32x4*>(src);
-      fb[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
-    }
-    if (EPI & EPI_DIST) {
-      // explicit fma chain: identical rounding for every tile configuration
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) na[i] = __builtin_fmaf(fa[i][u][e], fa[i][u][e], na[i]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) nb[j] = __builtin_fmaf(fb[j][u][e], fb[j][u][e], nb[j]);
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int g = 0; g < BK / 16; ++g) {
+      f32x4 fa[TM][2], fb[TN][2];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float av = (s < 4) ? fa[i][0][s] : fa[i][1][s - 4];
+        const float* src = as + (wm * (BM / WM) + i * 32 + r32) * LSTR + g * 16 + h * 8;
+        fa[i][0] = *reinterpret_cast<const f32x4*>(src);
+        fa[i][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const float bv = (s < 4) ? fb[j][0][s] : fb[j][1][s - 4];
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {
+        const float* src = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + g * 16 + h * 8;
+        fb[j][0] = *reinterpret_cast<const f32x4*>(src);
+        fb[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+      if (EPI & EPI_DIST) {
+        // explicit fma chain: identical rounding for every tile configuration
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) na[i] = __builtin_fmaf(fa[i][u][e], fa[i][u][e], na[i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) nb[j] = __builtin_fmaf(fb[j][u][e], fb[j][u][e], nb[j]);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float av = (s < 4) ? fa[i][0][s] : fa[i][1][s - 4];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const float bv = (s < 4) ? fb[j][0][s] : fb[j][1][s - 4];
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+          }
         }
       }
     }
@@ -368,30 +379,30 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int BK>
 static void launch_one(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI>),
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, EPI, BK>),
                      dim3(tiles_m * tiles_n, batch * p.splitk),
                      dim3(64 * WM * WN), 0, stream, p, tiles_m, tiles_n);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK>
 static int launch_tile(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   switch (epi) {
-    case EPI_DIST: launch_one<BM, BN, WM, WN, EPI_DIST>(p, batch, stream); break;
-    case EPI_CONV: launch_one<BM, BN, WM, WN, EPI_CONV>(p, batch, stream); break;
+    case EPI_DIST: launch_one<BM, BN, WM, WN, EPI_DIST, BK>(p, batch, stream); break;
+    case EPI_CONV: launch_one<BM, BN, WM, WN, EPI_CONV, BK>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RELU:
-      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU>(p, batch, stream); break;
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU, BK>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RES:
-      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES>(p, batch, stream); break;
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES, BK>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RES | EPI_F_RELU:
-      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU>(p, batch, stream); break;
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU, BK>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RAW:
-      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW>(p, batch, stream); break;
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW, BK>(p, batch, stream); break;
     case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
-      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL>(p, batch, stream); break;
+      launch_one<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL, BK>(p, batch, stream); break;
     default:
       set_error("unknown epilogue");
       return PPS_ERR_INVALID_ARG;
@@ -426,13 +437,25 @@ int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
-  const int tile = p.tile ? p.tile : pick_tile(p, batch);
+  int tile = p.tile ? p.tile : pick_tile(p, batch);
+  // BK=32 needs the dual operand switch on a 32-chunk boundary and, for
+  // narrow inputs (Cin < 32), a power-of-two channel count
+  if (tile > GEMM_TILE_256x128) {
+    const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
+    const bool dual_ok = !p.a2 || p.Kloop1 % 32 == 0;
+    if (!narrow_ok || !dual_ok) tile -= 5;
+  }
   switch (tile) {
-    case GEMM_TILE_128x128: return launch_tile<128, 128, 2, 2>(p, epi, batch, stream);
-    case GEMM_TILE_128x64: return launch_tile<128, 64, 4, 1>(p, epi, batch, stream);
-    case GEMM_TILE_64x128: return launch_tile<64, 128, 1, 4>(p, epi, batch, stream);
-    case GEMM_TILE_64x64: return launch_tile<64, 64, 2, 2>(p, epi, batch, stream);
-    case GEMM_TILE_256x128: return launch_tile<256, 128, 4, 2>(p, epi, batch, stream);
+    case GEMM_TILE_128x128: return launch_tile<128, 128, 2, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_128x64: return launch_tile<128, 64, 4, 1, 16>(p, epi, batch, stream);
+    case GEMM_TILE_64x128: return launch_tile<64, 128, 1, 4, 16>(p, epi, batch, stream);
+    case GEMM_TILE_64x64: return launch_tile<64, 64, 2, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_256x128: return launch_tile<256, 128, 4, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_128x128_K32: return launch_tile<128, 128, 2, 2, 32>(p, epi, batch, stream);
+    case GEMM_TILE_128x64_K32: return launch_tile<128, 64, 4, 1, 32>(p, epi, batch, stream);
+    case GEMM_TILE_64x128_K32: return launch_tile<64, 128, 1, 4, 32>(p, epi, batch, stream);
+    case GEMM_TILE_64x64_K32: return launch_tile<64, 64, 2, 2, 32>(p, epi, batch, stream);
+    case GEMM_TILE_256x128_K32: return launch_tile<256, 128, 4, 2, 32>(p, epi, batch, stream);
     default:
       set_error("unknown GEMM tile id " + std::to_string(tile));
       return PPS_ERR_INVALID_ARG;

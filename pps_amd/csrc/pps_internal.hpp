@@ -45,7 +45,12 @@ enum GemmTile {
   GEMM_TILE_64x128 = 3,
   GEMM_TILE_64x64 = 4,
   GEMM_TILE_256x128 = 5,
-  GEMM_NUM_TILES = 6
+  GEMM_TILE_128x128_K32 = 6,  // same shapes with a 32-wide K chunk per barrier
+  GEMM_TILE_128x64_K32 = 7,
+  GEMM_TILE_64x128_K32 = 8,
+  GEMM_TILE_64x64_K32 = 9,
+  GEMM_TILE_256x128_K32 = 10,
+  GEMM_NUM_TILES = 11
 };
 
 struct GemmParams {
