@@ -61,6 +61,16 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq,
                 const float* g, int64_t G, int64_t ldg, int D, int metric,
                 float* out, int64_t ldo, int tile, void* stream);
 
+/* The distance matrix on bf16 matrix cores (same f32-level error as
+ * pps_distmat, see the "x3" block below): g3 = pps_split_bf16x3(g) as planes
+ * [3][G][ldg]; qsq / gsq = pps_row_sqnorm of q / g (a gallery index is
+ * split and normed once, then scored against any number of query batches). */
+int pps_row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out,
+                   void* stream);
+int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
+                   const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
+                   int metric, float* out, int64_t ldo, int tile, void* stream);
+
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
  * The diagonal is exactly 0 as in the reference's difference form. */
@@ -170,6 +180,35 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
  * part [splitk][M][B*Cout].  Fills the chip at small batch (M = images). */
 int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Cout,
                             int B, int splitk, float* part, int tile, void* stream);
+/* ---- f32 GEMMs on bf16 matrix cores ("x3") --------------------------------
+ * Same operations as pps_conv2d_bn_act / pps_conv2d_dual_bn_act /
+ * pps_gemm_splitk_batched, with the weights pre-split by pps_split_bf16x3
+ * into three bf16 planes (w = hi + mid + lo exactly) and the activations
+ * split the same way on the fly; products are summed from the six terms
+ * above 2^-24 relative weight on v_mfma_f32_32x32x16_bf16, so results carry
+ * f32-level error (not bf16) at 2.67x the f32-MFMA peak.  Identical bits for
+ * every tile; not bit-identical to the exact-f32 kernels (different
+ * rounding sequence).  Weight layouts: conv [3][Cout][Kpad], dual
+ * [3][Cout][Kpad1+Kpad2], split-K [B][3][Cout][K]. */
+int pps_split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out,
+                     void* stream); /* x [nbatch][n] -> out [nbatch][3][n] */
+int pps_conv2d_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
+                         const uint16_t* w3, int Cout, int Kpad, int KH, int KW,
+                         int stride, int pad, int dil, const float* scale,
+                         const float* shift, const float* residual, int relu,
+                         float* y, int Ho, int Wo, int ldy, int tile,
+                         void* stream);
+int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin,
+                              int ldx, int KH, int KW, int stride, int pad,
+                              const float* x2, int H2, int W2, int Cin2,
+                              int ldx2, int stride2, const uint16_t* w3,
+                              int Cout, int Kpad1, int Kpad2, const float* shift,
+                              int relu, float* y, int Ho, int Wo, int ldy,
+                              int tile, void* stream);
+int pps_gemm_splitk_batched_x3(const float* x, int M, int K, const uint16_t* w3,
+                               int Cout, int B, int splitk, float* part,
+                               int tile, void* stream);
+
 /* y[m][j] = relu?(sum_s part[s][m][j] * scale[j] + shift[j]) (fixed order),
  * then, if normalize, Caffe2 Normalize along axis 1: y[m] /= max(|y[m]|,1e-12)
  * (reid_heads.py:58-76 BN + Relu, :96-127 Concat + Normalize). */

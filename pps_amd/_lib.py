@@ -22,6 +22,9 @@ SIGNATURES = {
     'pps_distmat': [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_int, c_int, c_ptr,
                     c_i64, c_int, c_ptr],
     'pps_pairwise_distance': [c_ptr, c_int, c_int, c_ptr, c_ptr],
+    'pps_row_sqnorm': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr],
+    'pps_distmat_x3': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
+                       c_ptr, c_i64, c_int, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
@@ -41,6 +44,16 @@ SIGNATURES = {
                                 c_ptr, c_int, c_ptr, c_int, c_int, c_int, c_ptr],
     'pps_gemm_splitk_batched': [c_ptr, c_int, c_int, c_ptr, c_int, c_int, c_int, c_ptr, c_int,
                                 c_ptr],
+    'pps_split_bf16x3': [c_ptr, c_i64, c_int, c_ptr, c_ptr],
+    'pps_conv2d_bn_act_x3': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
+                             c_ptr, c_int, c_int, c_int, c_int, c_ptr],
+    'pps_conv2d_dual_bn_act_x3': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int,
+                                  c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int,
+                                  c_int, c_int, c_int, c_ptr],
+    'pps_gemm_splitk_batched_x3': [c_ptr, c_int, c_int, c_ptr, c_int, c_int, c_int, c_ptr,
+                                   c_int, c_ptr],
     'pps_splitk_bn_act_normalize': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_int,
                                     c_ptr, c_ptr],
     'pps_re_ranking': [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int, ctypes.c_double,

@@ -88,6 +88,48 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq, const float* g, int64_t 
   return PPS_OK;
 }
 
+int pps_row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out,
+                   void* stream) {
+  PPS_ENFORCE(x && out, "null pointer");
+  PPS_ENFORCE(rows >= 0 && D > 0 && D % 4 == 0 && ld >= D && ld % 4 == 0, "bad shape");
+  PPS_ENFORCE(aligned16(x), "x must be 16-byte aligned");
+  return row_sqnorm(x, rows, D, ld, out, as_stream(stream));
+}
+
+int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
+                   const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
+                   int metric, float* out, int64_t ldo, int tile, void* stream) {
+  PPS_ENFORCE(q && qsq && g3 && gsq && out, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && D > 0, "bad shape");
+  PPS_ENFORCE(D % 4 == 0, "D must be a multiple of 4, got " + std::to_string(D));
+  PPS_ENFORCE(ldq % 4 == 0 && ldg % 4 == 0 && ldq >= D && ldg >= D, "bad leading dims");
+  PPS_ENFORCE(ldo >= G, "ldo < G");
+  PPS_ENFORCE(aligned16(q) && aligned16(g3), "q/g3 must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  PPS_ENFORCE(ldq * 4 < kMaxBufBytes && ldg * 2 < kMaxBufBytes, "rows too long");
+  const int64_t qblk = std::min<int64_t>(Q, (kMaxBufBytes - 1) / (ldq * 4));
+  const int64_t gblk = std::min<int64_t>(G, (kMaxBufBytes - 1) / (ldg * 2));
+  for (int64_t q0 = 0; q0 < Q; q0 += qblk) {
+    for (int64_t g0 = 0; g0 < G; g0 += gblk) {
+      const int64_t qn = std::min(qblk, Q - q0), gn = std::min(gblk, G - g0);
+      GemmParams p{};
+      p.splitk = 1;
+      p.a = q + q0 * ldq; p.a_bytes = (uint32_t)(qn * ldq * 4);
+      p.H = 1; p.W = (int)qn; p.Cin = D; p.lda = (int)ldq;
+      p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)qn;
+      p.M = (int)qn;
+      p.b3 = g3 + g0 * ldg; p.b_plane = G * ldg; p.b_bytes = (uint32_t)(gn * ldg * 2);
+      p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)gn;
+      p.Kloop = (D + 15) / 16 * 16;
+      p.norm_a = qsq + q0; p.norm_b = gsq + g0;
+      p.out = out + q0 * ldo + g0; p.ldo = ldo; p.metric = metric; p.tile = tile;
+      const int rc = launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
+      if (rc != PPS_OK) return rc;
+    }
+  }
+  return PPS_OK;
+}
+
 int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
   PPS_ENFORCE(X && Z, "null pointer");
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
@@ -176,8 +218,9 @@ int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t
                 as_stream(stream));
 }
 
-int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
-                      const float* w, int Cout, int Kpad, int KH, int KW, int stride,
+// weights either f32 [Cout][Kpad] (x3 = 0) or bf16x3 planes [3][Cout][Kpad]
+static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
+                      const void* w, int x3, int Cout, int Kpad, int KH, int KW, int stride,
                       int pad, int dil, const float* scale, const float* shift,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
                       int tile, void* stream) {
@@ -200,21 +243,45 @@ int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
   PPS_ENFORCE(Cin >= 16 || ((Cin & (Cin - 1)) == 0 && Kpad <= 64 * Cin),
               "channels < 16 must be a power of two with Kpad <= 64*Cin");
   PPS_ENFORCE((int64_t)N * H * W * ldx * 4 < kMaxBufBytes, "input larger than 2 GiB");
-  PPS_ENFORCE((int64_t)Cout * Kpad * 4 < kMaxBufBytes, "weights larger than 2 GiB");
+  PPS_ENFORCE((int64_t)Cout * Kpad * 6 < kMaxBufBytes, "weights larger than 2 GiB");
   p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
   p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 4);
   p.b_bytes = (uint32_t)((int64_t)Cout * Kpad * 4);
   p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = dil;
   p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
-  p.b = w; p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
+  p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  if (x3) {
+    p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
+    p.b_bytes = (uint32_t)(p.b_plane * 2);
+    return launch_gemm_x3(p, EPI_CONV, 1, as_stream(stream));
+  }
+  p.b = static_cast<const float*>(w);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
 }
 
-int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+                      const float* w, int Cout, int Kpad, int KH, int KW, int stride,
+                      int pad, int dil, const float* scale, const float* shift,
+                      const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
+                      int tile, void* stream) {
+  return conv_impl(x, N, H, W, Cin, ldx, w, 0, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream);
+}
+
+int pps_conv2d_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
+                         const uint16_t* w3, int Cout, int Kpad, int KH, int KW, int stride,
+                         int pad, int dil, const float* scale, const float* shift,
+                         const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
+                         int tile, void* stream) {
+  return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream);
+}
+
+static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                            int KH, int KW, int stride, int pad, const float* x2, int H2,
-                           int W2, int Cin2, int ldx2, int stride2, const float* w,
+                           int W2, int Cin2, int ldx2, int stride2, const void* w, int x3,
                            int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
                            float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
   PPS_ENFORCE(x && x2 && w && shift && y, "null pointer");
@@ -241,11 +308,36 @@ int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx
   p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
   p.a2 = x2; p.a2_bytes = (uint32_t)((int64_t)N * H2 * W2 * ldx2 * 4);
   p.H2 = H2; p.W2 = W2; p.lda2 = ldx2; p.stride2 = stride2; p.Kloop1 = Kpad1;
-  p.b = w; p.ldb = Kpad1 + Kpad2; p.kb_valid = Kpad1 + Kpad2; p.Ncol = Cout;
-  p.b_bytes = (uint32_t)((int64_t)Cout * (Kpad1 + Kpad2) * 4);
+  p.ldb = Kpad1 + Kpad2; p.kb_valid = Kpad1 + Kpad2; p.Ncol = Cout;
   p.Kloop = Kpad1 + Kpad2;
   p.scale = nullptr; p.shift = shift; p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  PPS_ENFORCE((int64_t)Cout * (Kpad1 + Kpad2) * 6 < kMaxBufBytes, "weights larger than 2 GiB");
+  if (x3) {
+    p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * (Kpad1 + Kpad2);
+    p.b_bytes = (uint32_t)(p.b_plane * 2);
+    return launch_gemm_x3(p, EPI_CONV, 1, as_stream(stream));
+  }
+  p.b = static_cast<const float*>(w);
+  p.b_bytes = (uint32_t)((int64_t)Cout * (Kpad1 + Kpad2) * 4);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
+}
+
+int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
+                           int KH, int KW, int stride, int pad, const float* x2, int H2,
+                           int W2, int Cin2, int ldx2, int stride2, const float* w,
+                           int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
+                           float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
+  return dual_impl(x, N, H, W, Cin, ldx, KH, KW, stride, pad, x2, H2, W2, Cin2, ldx2, stride2,
+                   w, 0, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream);
+}
+
+int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
+                              int KH, int KW, int stride, int pad, const float* x2, int H2,
+                              int W2, int Cin2, int ldx2, int stride2, const uint16_t* w3,
+                              int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
+                              float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
+  return dual_impl(x, N, H, W, Cin, ldx, KH, KW, stride, pad, x2, H2, W2, Cin2, ldx2, stride2,
+                   w3, 1, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream);
 }
 
 int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
@@ -273,7 +365,7 @@ int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
   return launch_gemm(p, EPI_CONV, B, as_stream(stream));
 }
 
-int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Cout, int B,
+static int splitk_impl(const float* x, int M, int K, const void* w, int x3, int Cout, int B,
                             int splitk, float* part, int tile, void* stream) {
   PPS_ENFORCE(x && w && part, "null pointer");
   PPS_ENFORCE(M > 0 && K > 0 && Cout > 0 && B > 0 && splitk >= 1, "bad shape");
@@ -286,12 +378,35 @@ int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Co
   p.a = x; p.a_bstride = (int64_t)M * K; p.H = 1; p.W = M; p.Cin = K / splitk; p.lda = K;
   p.a_bytes = (uint32_t)((int64_t)M * K * 4);
   p.KH = p.KW = 1; p.stride = 1; p.dil = 1; p.Ho = 1; p.Wo = M; p.M = M;
-  p.b = w; p.b_bstride = (int64_t)Cout * K; p.ldb = K; p.kb_valid = K / splitk;
-  p.b_bytes = (uint32_t)((int64_t)Cout * K * 4); p.Ncol = Cout;
+  p.ldb = K; p.kb_valid = K / splitk; p.Ncol = Cout;
   p.Kloop = K / splitk;
   p.out = part; p.ldo = (int64_t)B * Cout; p.out_bstride = Cout;
   p.out_sstride = (int64_t)M * B * Cout; p.tile = tile;
+  if (x3) {
+    PPS_ENFORCE((int64_t)Cout * K * 6 < kMaxBufBytes, "weights larger than 2 GiB");
+    p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * K;
+    p.b_bstride = 3 * p.b_plane; p.b_bytes = (uint32_t)(p.b_plane * 2);
+    return launch_gemm_x3(p, EPI_CONV | EPI_F_RAW, B, as_stream(stream));
+  }
+  p.b = static_cast<const float*>(w); p.b_bstride = (int64_t)Cout * K;
+  p.b_bytes = (uint32_t)((int64_t)Cout * K * 4);
   return launch_gemm(p, EPI_CONV | EPI_F_RAW, B, as_stream(stream));
+}
+
+int pps_gemm_splitk_batched(const float* x, int M, int K, const float* w, int Cout, int B,
+                            int splitk, float* part, int tile, void* stream) {
+  return splitk_impl(x, M, K, w, 0, Cout, B, splitk, part, tile, stream);
+}
+
+int pps_gemm_splitk_batched_x3(const float* x, int M, int K, const uint16_t* w3, int Cout,
+                               int B, int splitk, float* part, int tile, void* stream) {
+  return splitk_impl(x, M, K, w3, 1, Cout, B, splitk, part, tile, stream);
+}
+
+int pps_split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, void* stream) {
+  PPS_ENFORCE(x && out, "null pointer");
+  PPS_ENFORCE(n > 0 && nbatch > 0, "bad shape");
+  return split_bf16x3(x, n, nbatch, out, as_stream(stream));
 }
 
 int pps_splitk_bn_act_normalize(const float* part, int splitk, int M, int N,

@@ -1,0 +1,228 @@
+// Device-side pieces shared by the two GEMM kernels -- gemm_f32.hip (exact
+// f32 MFMA) and gemm_x3.hip (f32 products from a three-way bf16 split):
+// buffer-resource loads, the XCD-aware block remap, the implicit-im2col A
+// gather and the convolution epilogue.
+#pragma once
+#include "pps_internal.hpp"
+
+namespace pps {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kOOB = 0x7ffffff0;  // byte offset beyond any num_records -> reads 0
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// A buffer descriptor must live in SGPRs.  The base and size are block-uniform
+// but reach here through the by-reference GemmParams, which the compiler
+// cannot prove uniform; without readfirstlane every buffer load becomes a
+// readfirstlane "waterfall" loop (v_readfirstlane x4 + v_cmp + exec loop).
+__device__ inline rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  void* ub = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+__device__ inline f32x4 bload(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ inline u32x2 bload64(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+
+// XCD-aware bijective remap of the flat block id: the hardware deals blocks
+// round-robin over the 8 XCDs; renumber so consecutive tiles (which share an
+// A panel) run on the same XCD / L2.
+__device__ inline int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+}
+
+// Implicit-im2col A operand over an NHWC tensor.  Each thread owns AL rows
+// (trow + i*RPP) and one float4 slot c4 of every BK-wide K chunk.  Element
+// offset of (row, tap t, channel c) = rbase + tap_off(t) + c, valid iff bit t
+// of the row's tap mask is set (input pixel inside the image); invalid loads
+// use the kOOB offset and read zero in hardware.
+//   DUAL: a second operand (1x1 conv of another NHWC tensor, stride2, no pad)
+//   appended along K from chunk Kloop1/BK on (the fused projection shortcut).
+template <int AL, int RPP, int BK, bool DUAL>
+struct AGather {
+  rsrc_t src, src2;
+  int rbase[AL];
+  uint64_t tmask[AL];
+  int rbase2[AL];
+  int tc, tt, tkw, toff, step_w, step_h, cin_shift, nch1;
+  bool narrow;
+
+  // s_tapoff: 64-int LDS table (narrow inputs); contains a barrier when used.
+  __device__ void init(const GemmParams& p, int batch, int64_t kofs0, int m0, int trow, int c4,
+                       int* s_tapoff, int tid, int T) {
+    src = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
+    const int ntaps = p.KH * p.KW;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int row = m0 + trow + i * RPP;
+      const int rowc = row < p.M ? row : 0;
+      const int hw = p.Ho * p.Wo;
+      const int n = rowc / hw;
+      const int rem = rowc - n * hw;
+      const int oh = rem / p.Wo;
+      const int ow = rem - oh * p.Wo;
+      const int ih0 = oh * p.stride - p.pad;
+      const int iw0 = ow * p.stride - p.pad;
+      rbase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda;
+      uint64_t m = 0;
+      for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
+        const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
+        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1ull << t;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
+      tmask[i] = row < p.M ? m : 0ull;
+    }
+    // tap tracker for k = chunk*BK + c4*4 -> (tap tt, channel tc, offset toff)
+    step_w = p.dil * p.lda;                 // kw -> kw+1
+    step_h = p.dil * p.lda * (p.W - p.KW);  // extra on kw wrap
+    tc = c4 * 4; tt = 0; tkw = 0; toff = 0;
+    advance(p, 0);
+    // narrow-channel inputs (the stem's packed 4-channel image): a K chunk
+    // spans several taps, so tap offsets come from an LDS table (Cin a power
+    // of two < BK)
+    narrow = p.Cin < BK;
+    cin_shift = 0;
+    while ((1 << cin_shift) < p.Cin) ++cin_shift;
+    if (narrow) {
+      for (int t = tid; t < 64; t += T) {
+        const int kh = t / p.KW, kw = t - (t / p.KW) * p.KW;
+        s_tapoff[t] = (kh * p.dil * p.W + kw * p.dil) * p.lda;
+      }
+      __syncthreads();
+    }
+    src2 = src;
+    nch1 = DUAL ? p.Kloop1 / BK : (1 << 30);
+    if (DUAL) {
+      src2 = make_rsrc(p.a2, p.a2_bytes);
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int row = m0 + trow + i * RPP;
+        const int hw = p.Ho * p.Wo;
+        const int n = row / hw;
+        const int rem = row - n * hw;
+        const int oh = rem / p.Wo;
+        const int ow = rem - oh * p.Wo;
+        rbase2[i] = row < p.M ? (((n * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.lda2 +
+                                 c4 * 4) * 4
+                              : kOOB;
+      }
+    }
+  }
+
+  __device__ void advance(const GemmParams& p, int by) {
+    tc += by;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      ++tt;
+      toff += step_w;
+      if (++tkw == p.KW) { tkw = 0; toff += step_h; }
+    }
+  }
+
+  // Loads chunk kc into ra and steps the tap tracker to chunk kc+1
+  // (chunks are loaded in order).
+  __device__ void load(const GemmParams& p, int kc, int c4, const int* s_tapoff, f32x4* ra) {
+    if (DUAL && kc >= nch1) {
+      const int kofs = (kc - nch1) * BK * 4;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) ra[i] = bload(src2, rbase2[i] == kOOB ? kOOB : rbase2[i] + kofs);
+    } else if (narrow) {
+      const int k = kc * BK + c4 * 4;
+      const int t = k >> cin_shift;
+      const int c = k & (p.Cin - 1);
+      const int off = t < 64 ? s_tapoff[t] + c : 0;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const bool ok = t < 64 && ((tmask[i] >> t) & 1ull);
+        ra[i] = bload(src, ok ? (rbase[i] + off) * 4 : kOOB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const bool ok = tt < 64 && ((tmask[i] >> tt) & 1ull);
+        ra[i] = bload(src, ok ? (rbase[i] + toff + tc) * 4 : kOOB);
+      }
+    }
+    if (narrow) {
+      // taps come from the LDS table
+    } else if (p.Cin >= BK) {  // uniform: at most one tap step per chunk
+      tc += BK;
+      if (tc >= p.Cin) {
+        tc -= p.Cin;
+        ++tt;
+        toff += step_w;
+        if (++tkw == p.KW) { tkw = 0; toff += step_h; }
+      }
+    } else {
+      advance(p, BK);
+    }
+  }
+};
+
+// Convolution epilogue on 32x32 accumulators (C/D layout of every 32x32
+// MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)):
+//   y = acc * scale + shift (folded test-mode BN / conv bias) [+ residual] [ReLU]
+//   DUAL: scale folded into the weights;  RAW: store acc (split-K partials).
+// Addresses are a wave-uniform 64-bit tile base + 32-bit per-lane offsets.
+template <int EPI, int BM, int BN, int WM, int WN>
+__device__ inline void conv_epilogue(const GemmParams& p,
+                                     f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int batch,
+                                     int kslice, int m0, int n0, int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+  constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
+  constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
+  constexpr bool RAW = (EPI & EPI_F_RAW) != 0;
+  const int64_t tile_off = (int64_t)m0 * p.ldo + n0;
+  float* __restrict__ out = p.out + batch * p.out_bstride + kslice * p.out_sstride + tile_off;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;
+  const int nrem = p.Ncol - n0;
+  const float* sc = (DUAL || RAW) ? nullptr : p.scale + batch * p.ss_bstride + n0;
+  const float* sh = RAW ? nullptr : p.shift + batch * p.ss_bstride + n0;
+  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+  const int ldr = (int)p.ldr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = wn * (BN / WN) + j * 32 + r32;  // column within the tile
+    const bool col_ok = c < nrem;
+    const float s_ = (DUAL || RAW) ? 1.f : (col_ok ? sc[c] : 0.f);
+    const float t_ = RAW ? 0.f : (col_ok ? sh[c] : 0.f);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wm * (BM / WM) + i * 32 + 4 * h;  // row within the tile
+      float rv[16];
+      if (HAS_RES) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = rb + (r & 3) + 8 * (r >> 2);
+          const bool ok = col_ok && rr < mrem;
+          rv[r] = ok ? res[rr * ldr + c] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = rb + (r & 3) + 8 * (r >> 2);
+        float v = RAW ? acc[i][j][r] : __builtin_fmaf(acc[i][j][r], s_, t_);
+        if (HAS_RES) v += rv[r];
+        if (RELU) v = fmaxf(v, 0.f);
+        if (col_ok && rr < mrem) out[rr * ldo + c] = v;
+      }
+    }
+  }
+}
+
+}  // namespace pps

@@ -5,9 +5,9 @@
 //
 // * v_mfma_f32_32x32x2_f32 (exact f32 in, f32 accumulate): the only way to
 //   keep the reference's fp32 numerics (SURVEY §7 "Precision vs parity").
-// * Block tile BM x BN x 16, 64*WM*WN threads, each wave owns
+// * Block tile BM x BN x BK (BK = 16 or 32), 64*WM*WN threads, each wave owns
 //   (BM/WM) x (BN/WN) as TMxTN 32x32 accumulators (16 f32 regs each).
-// * K is permuted inside a 16-chunk: at MFMA step s (0..7) lane half h
+// * K is permuted inside each 16-group: at MFMA step s (0..7) lane half h
 //   contributes k = 8h + s, so each lane reads its 8 k-values of a row with
 //   two ds_read_b128 from a K-contiguous LDS row.  Row stride 20 floats
 //   (80 B) makes those reads bank-conflict free for all four b128 lane groups.
@@ -18,33 +18,18 @@
 // * Epilogues: EPI_CONV = per-column scale/shift (folded test-mode BN,
 //   conv bias) + residual + ReLU; EPI_DIST = |q|^2 + |g|^2 - 2 q.g with the
 //   squared norms accumulated from the same LDS fragments, clamp, sqrt.
-#include "pps_internal.hpp"
+#include "gemm_common.hpp"
 
 namespace pps {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 // K chunk per LDS stage is a template parameter BK (16 or 32); LDS rows hold
 // BK floats + 4 pad: 80 B or 144 B, both conflict-free for the fragment reads.
-constexpr int kOOB = 0x7ffffff0;  // byte offset beyond any num_records -> reads 0
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-__device__ inline rsrc_t make_rsrc(const float* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-__device__ inline f32x4 bload(rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
-
 template <int BM, int BN, int WM, int WN, int EPI, int BK>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int T = 64 * WM * WN;
   constexpr int LSTR = BK + 4;         // LDS row stride in floats
   constexpr int V4 = BK / 4;           // float4 per LDS row
-  constexpr int HK = BK / 2;           // k values per lane half per chunk
   constexpr int AL = BM * BK / 4 / T;  // f32x4 loads per thread (A)
   constexpr int BL = BN * BK / 4 / T;  // f32x4 loads per thread (B)
   constexpr int ROWS_PER_PASS = T / V4;
@@ -69,12 +54,7 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int h = lane >> 5;
 
   // ---- XCD-aware bijective remap of the flat block id -------------------
-  const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg >> 3, rr = nwg & 7, xcd = bid & 7;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  }
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tile_m = bid / tiles_n;
   const int tile_n = bid - tile_m * tiles_n;
   const int m0 = tile_m * BM;
@@ -88,86 +68,12 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // Out-of-range offsets (>= num_records) read as zero in hardware, so padding
   // taps, ragged rows/cols and K tails need no exec-mask branches.
   const int64_t kofs0 = (int64_t)kslice * p.Kloop;
-  const rsrc_t ra_src = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
   const rsrc_t rb_src = make_rsrc(p.b + batch * p.b_bstride + kofs0, p.b_bytes);
-
-  // ---- per-thread A-row geometry (once) -------------------------------------
-  // Element offset of (row, tap t, channel c) = rbase + tap_off(t) + c, valid
-  // iff bit t of the row's tap mask is set (input pixel inside the image).
   const int c4 = tid % V4;   // float4 slot within the chunk row
   const int trow = tid / V4;
-  int rbase[AL];
-  uint64_t tmask[AL];
-  const int ntaps = p.KH * p.KW;
-#pragma unroll
-  for (int i = 0; i < AL; ++i) {
-    const int row = m0 + trow + i * ROWS_PER_PASS;
-    const int rowc = row < p.M ? row : 0;
-    const int hw = p.Ho * p.Wo;
-    const int n = rowc / hw;
-    const int rem = rowc - n * hw;
-    const int oh = rem / p.Wo;
-    const int ow = rem - oh * p.Wo;
-    const int ih0 = oh * p.stride - p.pad;
-    const int iw0 = ow * p.stride - p.pad;
-    rbase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda;
-    uint64_t m = 0;
-    for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
-      const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
-      if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1ull << t;
-      if (++kw == p.KW) { kw = 0; ++kh; }
-    }
-    tmask[i] = row < p.M ? m : 0ull;
-  }
-  // tap tracker for this thread's k = chunk*BK + c4*4 -> (tap t, channel tc,
-  // element offset toff of the tap); all rows of the thread share it.
-  const int step_w = p.dil * p.lda;                    // kw -> kw+1
-  const int step_h = p.dil * p.lda * (p.W - p.KW);     // extra on kw wrap
-  int tc = c4 * 4, tt = 0, tkw = 0, toff = 0;
-  auto advance = [&](int by) {
-    tc += by;
-    while (tc >= p.Cin) {
-      tc -= p.Cin;
-      ++tt;
-      toff += step_w;
-      if (++tkw == p.KW) { tkw = 0; toff += step_h; }
-    }
-  };
-  advance(0);
-  // narrow-channel inputs (the stem's packed 4-channel image): a 16-wide K
-  // chunk spans several taps, so look tap offsets up in LDS instead of
-  // stepping the tracker (Cin a power of two < 16).
-  const bool narrow = p.Cin < BK;
-  int cin_shift = 0;
-  while ((1 << cin_shift) < p.Cin) ++cin_shift;
-  if (narrow) {
-    for (int t = tid; t < 64; t += T) {
-      const int kh = t / p.KW, kw = t - (t / p.KW) * p.KW;
-      s_tapoff[t] = (kh * p.dil * p.W + kw * p.dil) * p.lda;
-    }
-    __syncthreads();
-  }
-  // second A operand (EPI_F_DUAL): a 1x1 conv of another tensor appended
-  // along K (the fused projection shortcut, ResNet.py:203-220)
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
-  rsrc_t ra2_src = ra_src;
-  int rbase2[AL];
-  if (DUAL) {
-    ra2_src = make_rsrc(p.a2, p.a2_bytes);
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int row = m0 + trow + i * ROWS_PER_PASS;
-      const int hw = p.Ho * p.Wo;
-      const int n = row / hw;
-      const int rem = row - n * hw;
-      const int oh = rem / p.Wo;
-      const int ow = rem - oh * p.Wo;
-      rbase2[i] = row < p.M ? (((n * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.lda2 +
-                               c4 * 4) * 4
-                            : kOOB;
-    }
-  }
-  const int nch1 = DUAL ? p.Kloop1 / BK : (1 << 30);
+  AGather<AL, ROWS_PER_PASS, BK, DUAL> ag;
+  ag.init(p, batch, kofs0, m0, trow, c4, s_tapoff, tid, T);
   int bbase[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
@@ -177,44 +83,11 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
 
   f32x4 ra[AL], rb[BL];
   auto load_chunk = [&](int kc) {
-    if (DUAL && kc >= nch1) {
-      const int kofs = (kc - nch1) * BK * 4;
-#pragma unroll
-      for (int i = 0; i < AL; ++i) ra[i] = bload(ra2_src, rbase2[i] == kOOB ? kOOB : rbase2[i] + kofs);
-    } else if (narrow) {
-      const int k = kc * BK + c4 * 4;
-      const int t = k >> cin_shift;
-      const int c = k & (p.Cin - 1);
-      const int off = t < 64 ? s_tapoff[t] + c : 0;
-#pragma unroll
-      for (int i = 0; i < AL; ++i) {
-        const bool ok = t < 64 && ((tmask[i] >> t) & 1ull);
-        ra[i] = bload(ra_src, ok ? (rbase[i] + off) * 4 : kOOB);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < AL; ++i) {
-        const bool ok = (tmask[i] >> tt) & 1ull;
-        ra[i] = bload(ra_src, ok ? (rbase[i] + toff + tc) * 4 : kOOB);
-      }
-    }
+    ag.load(p, kc, c4, s_tapoff, ra);
     const int kb = kc * BK + c4 * 4;
     const bool kok = kb < p.kb_valid;
 #pragma unroll
     for (int i = 0; i < BL; ++i) rb[i] = bload(rb_src, kok ? bbase[i] + kc * BK * 4 : kOOB);
-    if (narrow) {
-      // taps come from the LDS table
-    } else if (p.Cin >= BK) {  // uniform: at most one tap step per chunk
-      tc += BK;
-      if (tc >= p.Cin) {
-        tc -= p.Cin;
-        ++tt;
-        toff += step_w;
-        if (++tkw == p.KW) { tkw = 0; toff += step_h; }
-      }
-    } else {
-      advance(BK);
-    }
   };
 
   f32x16 acc[TM][TN];
@@ -296,50 +169,13 @@ gemm_f32_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
 
   // ---- epilogue ------------------------------------------------------------
-  // Addresses are a wave-uniform 64-bit tile base + 32-bit per-lane offsets
-  // (SGPR-base global addressing): one VGPR per address, not two.
-  const int64_t tile_off = (int64_t)m0 * p.ldo + n0;
-  float* __restrict__ out = p.out + batch * p.out_bstride + kslice * p.out_sstride + tile_off;
-  const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0;      // rows valid in this tile
-  const int nrem = p.Ncol - n0;   // cols valid in this tile
   if (!(EPI & EPI_DIST)) {
-    constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
-    constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
-    constexpr bool RAW = (EPI & EPI_F_RAW) != 0;  // split-K partials: store acc
-    const float* sc = (DUAL || RAW) ? nullptr : p.scale + batch * p.ss_bstride + n0;
-    const float* sh = RAW ? nullptr : p.shift + batch * p.ss_bstride + n0;
-    const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
-    const int ldr = (int)p.ldr;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = wn * (BN / WN) + j * 32 + r32;   // column within the tile
-      const bool col_ok = c < nrem;
-      const float s_ = (DUAL || RAW) ? 1.f : (col_ok ? sc[c] : 0.f);  // DUAL: folded in w
-      const float t_ = RAW ? 0.f : (col_ok ? sh[c] : 0.f);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int rb = wm * (BM / WM) + i * 32 + 4 * h;  // row within the tile
-        float rv[16];
-        if (HAS_RES) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rr = rb + (r & 3) + 8 * (r >> 2);
-            const bool ok = col_ok && rr < mrem;
-            rv[r] = ok ? res[rr * ldr + c] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = rb + (r & 3) + 8 * (r >> 2);
-          float v = RAW ? acc[i][j][r] : __builtin_fmaf(acc[i][j][r], s_, t_);
-          if (HAS_RES) v += rv[r];
-          if (RELU) v = fmaxf(v, 0.f);
-          if (col_ok && rr < mrem) out[rr * ldo + c] = v;
-        }
-      }
-    }
+    conv_epilogue<EPI, BM, BN, WM, WN>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
   } else {
+    float* __restrict__ out = p.out + batch * p.out_bstride + (int64_t)m0 * p.ldo + n0;
+    const int ldo = (int)p.ldo;
+    const int mrem = p.M - m0;
+    const int nrem = p.Ncol - n0;
 #pragma unroll
     for (int i = 0; i < TM; ++i) na[i] += __shfl_xor(na[i], 32);
 #pragma unroll

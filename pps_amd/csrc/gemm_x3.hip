@@ -1,0 +1,372 @@
+// FP32 GEMM from bf16 MFMA for gfx950: every f32 operand is split exactly
+// into three bf16 terms, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = x - x0 - x1, each step exact in f32), and the product is summed from
+// the six terms whose weight is >= 2^-16 of the leading one:
+//
+//   a.b ~= a0b0 + a1b0 + a0b1 + a2b0 + a1b1 + a0b2
+//
+// The dropped terms (a1b2, a2b1, a2b2) are below 2^-24 |ab|, i.e. under one
+// f32 rounding; every product of two bf16 is exact in the f32 accumulator.  So
+// the result carries f32-level error (tests/test_gpu_x3.py measures it against
+// an fp64 reference next to the exact-f32 MFMA kernel) at six
+// v_mfma_f32_32x32x16_bf16 (6 x 32 cycles per 32x32x16 block) instead of
+// eight v_mfma_f32_32x32x2_f32 (8 x 64 cycles): 2.67x the f32 MFMA roof.
+//
+// Layout (same implicit-GEMM conv as gemm_f32.hip, shared AGather/epilogue):
+// * A (activations, f32) is gathered exactly as in the f32 kernel, split in
+//   registers while it is written to LDS as three bf16 planes.
+// * B (weights) is split once at load time (pps_split_bf16x3): three bf16
+//   planes [3][Ncol][ldb] per batch, 6 bytes per weight.
+// * LDS rows hold BK + 8 bf16 (48 B / 80 B): the 16-byte fragment reads of a
+//   32x32x16 MFMA (lane (r, h) reads k = 16g + 8h .. +8 of row r) hit 16
+//   distinct 16-byte slots per 16-lane group, i.e. no bank conflicts.
+// * K order is fixed (16-groups ascending, the six terms in the order above)
+//   for every tile and BK, so all tile variants give identical bits.
+#include "gemm_common.hpp"
+
+namespace pps {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Two floats -> three packed bf16 pairs with x = hi + mid + lo exactly
+// (round-to-nearest-even splits; each remainder is exact in f32).
+__device__ inline void split2(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, u << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, u & 0xffff0000u);
+  const unsigned v = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
+  const float s0 = r0 - __builtin_bit_cast(float, v << 16);
+  const float s1 = r1 - __builtin_bit_cast(float, v & 0xffff0000u);
+  hi = u;
+  mid = v;
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){s0, s1}, bf16x2));
+}
+
+__device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Distance epilogue from precomputed squared row norms (pps_row_sqnorm):
+//   sqeuclid = (-2 q.g + |q|^2) + |g|^2 clamped at 0 [sqrt]; cosine = 1 - q.g/(|q||g|)
+template <int BM, int BN, int WM, int WN>
+__device__ inline void dist_epilogue(const GemmParams& p,
+                                     f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0,
+                                     int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;
+  const int nrem = p.Ncol - n0;
+  const float* qsq = p.norm_a + m0;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = wn * (BN / WN) + j * 32 + r32;
+    if (c >= nrem) continue;
+    const float gn = p.norm_b[n0 + c];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wm * (BM / WM) + i * 32 + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = rb + (r & 3) + 8 * (r >> 2);
+        if (rr < mrem) {
+          const float dot = acc[i][j][r];
+          const float qn = qsq[rr];
+          float v;
+          if (p.metric == PPS_METRIC_COSINE) {
+            const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
+            v = 1.f - dot / den;
+          } else {
+            v = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
+            if (p.metric == PPS_METRIC_EUCLIDEAN) v = sqrtf(v);
+          }
+          if (p.zero_diag && m0 + rr == n0 + c) v = 0.f;
+          out[rr * ldo + c] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int BK>
+__global__ void __launch_bounds__(64 * WM * WN)
+gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int T = 64 * WM * WN;
+  constexpr int LSTR = BK + 8;          // LDS row stride in bf16 elements
+  constexpr int V4 = BK / 4;            // 4-element slots per K chunk row
+  constexpr int AL = BM * BK / 4 / T;   // A float4 loads per thread
+  constexpr int BL = BN * BK / 4 / T;   // B 4-element (x3 planes) loads per thread
+  constexpr int RPP = T / V4;           // rows covered per load pass
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int APL = BM * LSTR;        // elements per A plane
+  constexpr int BPL = BN * LSTR;
+  constexpr int STAGE = 3 * (APL + BPL);
+  static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
+  static_assert(AL >= 1 && BL >= 1 && TM >= 1 && TN >= 1, "tile too small");
+  static_assert(2 * STAGE * 2 + 256 <= 160 * 1024, "LDS over 160 KB");
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * STAGE + 128];
+  int* s_tapoff = reinterpret_cast<int*>(lds + 2 * STAGE);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tile_m = bid / tiles_n;
+  const int tile_n = bid - tile_m * tiles_n;
+  const int m0 = tile_m * BM;
+  const int n0 = tile_n * BN;
+  const int batch = blockIdx.y / p.splitk;
+  const int kslice = blockIdx.y - batch * p.splitk;
+
+  const int64_t kofs0 = (int64_t)kslice * p.Kloop;
+  // one descriptor per bf16 plane: 32-bit offsets stay within a plane
+  const uint16_t* b3 = p.b3 + batch * p.b_bstride + kofs0;
+  const rsrc_t rb_src0 = make_rsrc(b3, p.b_bytes);
+  const rsrc_t rb_src1 = make_rsrc(b3 + p.b_plane, p.b_bytes);
+  const rsrc_t rb_src2 = make_rsrc(b3 + 2 * p.b_plane, p.b_bytes);
+  const int c4 = tid % V4;
+  const int trow = tid / V4;
+  AGather<AL, RPP, BK, DUAL> ag;
+  ag.init(p, batch, kofs0, m0, trow, c4, s_tapoff, tid, T);
+  unsigned bbase[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int col = n0 + trow + i * RPP;
+    bbase[i] = col < p.Ncol ? (unsigned)(col * p.ldb + c4 * 4) * 2u : (unsigned)kOOB;
+  }
+
+  // two register stages: chunk kc+2 is requested while chunk kc computes, so
+  // a load has two chunk-compute times to land (one was not enough at 2
+  // waves/SIMD: the MFMAs outrun a single stage's L2/HBM latency)
+  f32x4 ra0[AL], ra1[AL];
+  u32x2 rb0[BL][3], rb1[BL][3];
+  auto load_chunk = [&](int kc, f32x4 (&ra)[AL], u32x2 (&rb)[BL][3]) {
+    ag.load(p, kc, c4, s_tapoff, ra);
+    const bool kok = kc * BK + c4 * 4 < p.kb_valid;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const bool ok = kok && bbase[i] != (unsigned)kOOB;
+      const unsigned o = bbase[i] + (unsigned)(kc * BK * 2);
+      const int off = ok ? (int)o : kOOB;
+      rb[i][0] = bload64(rb_src0, off);
+      rb[i][1] = bload64(rb_src1, off);
+      rb[i][2] = bload64(rb_src2, off);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nchunks = (p.Kloop + BK - 1) / BK;
+  // one K chunk: registers -> LDS stage (A split into planes), barrier,
+  // request chunk kc+2 into the freed registers, MFMAs on the stage
+  auto step = [&](int kc, f32x4 (&ra)[AL], u32x2 (&rb)[BL][3], unsigned short* as) {
+    unsigned short* bs = as + 3 * APL;  // as: [3][BM][LSTR], bs: [3][BN][LSTR]
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      unsigned h0, m0_, l0, h1, m1, l1;
+      split2(ra[i][0], ra[i][1], h0, m0_, l0);
+      split2(ra[i][2], ra[i][3], h1, m1, l1);
+      const u32x2 hi = {h0, h1}, mid = {m0_, m1}, lo = {l0, l1};
+      unsigned short* d = as + (trow + i * RPP) * LSTR + c4 * 4;
+      *reinterpret_cast<u32x2*>(d) = hi;
+      *reinterpret_cast<u32x2*>(d + APL) = mid;
+      *reinterpret_cast<u32x2*>(d + 2 * APL) = lo;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      unsigned short* d = bs + (trow + i * RPP) * LSTR + c4 * 4;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x2*>(d + pl * BPL) = rb[i][pl];
+    }
+    __syncthreads();
+    if (kc + 2 < nchunks) load_chunk(kc + 2, ra, rb);
+
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned short* s = as + (wm * (BM / WM) + i * 32 + r32) * LSTR + g * 16 + h * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *reinterpret_cast<const bf16x8*>(s + pl * APL);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const unsigned short* s = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + g * 16 + h * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) fb[j][pl] = *reinterpret_cast<const bf16x8*>(s + pl * BPL);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x16 c = acc[i][j];
+          c = mfma_bf16(fa[i][0], fb[j][0], c);
+          c = mfma_bf16(fa[i][1], fb[j][0], c);
+          c = mfma_bf16(fa[i][0], fb[j][1], c);
+          c = mfma_bf16(fa[i][2], fb[j][0], c);
+          c = mfma_bf16(fa[i][1], fb[j][1], c);
+          c = mfma_bf16(fa[i][0], fb[j][2], c);
+          acc[i][j] = c;
+        }
+    }
+  };
+
+  load_chunk(0, ra0, rb0);
+  if (nchunks > 1) load_chunk(1, ra1, rb1);
+  for (int kc = 0; kc < nchunks; kc += 2) {
+    step(kc, ra0, rb0, lds);
+    if (kc + 1 < nchunks) step(kc + 1, ra1, rb1, lds + STAGE);
+  }
+
+  if (EPI & EPI_DIST)
+    dist_epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, r32, h);
+  else
+    conv_epilogue<EPI, BM, BN, WM, WN>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int BK>
+static void launch_one_x3(const GemmParams& p, int batch, hipStream_t stream) {
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.Ncol + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, EPI, BK>),
+                     dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream,
+                     p, tiles_m, tiles_n);
+}
+
+template <int BM, int BN, int WM, int WN, int BK>
+static int launch_tile_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  switch (epi) {
+    case EPI_DIST: launch_one_x3<BM, BN, WM, WN, EPI_DIST, BK>(p, batch, stream); break;
+    case EPI_CONV: launch_one_x3<BM, BN, WM, WN, EPI_CONV, BK>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU:
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU, BK>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES:
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES, BK>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES | EPI_F_RELU:
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU, BK>(p, batch, stream);
+      break;
+    case EPI_CONV | EPI_F_RAW:
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW, BK>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL, BK>(p, batch, stream);
+      break;
+    default:
+      set_error("unknown epilogue for the bf16x3 GEMM");
+      return PPS_ERR_INVALID_ARG;
+  }
+  PPS_CHECK_LAUNCH("gemm_x3_kernel");
+  return PPS_OK;
+}
+
+int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  if (p.M <= 0 || p.Ncol <= 0 || batch <= 0) return PPS_OK;
+  if (p.splitk < 1 || !p.b3) {
+    set_error("bf16x3 GEMM: splitk must be >= 1 and b3 set");
+    return PPS_ERR_INVALID_ARG;
+  }
+  if ((epi & EPI_DIST) && (!p.norm_a || !p.norm_b)) {
+    set_error("bf16x3 distance GEMM needs both squared-norm vectors");
+    return PPS_ERR_INVALID_ARG;
+  }
+  if (!(epi & EPI_DIST) && !(epi & EPI_F_RAW)) {
+    if (p.residual) epi |= EPI_F_RES;
+    if (p.relu) epi |= EPI_F_RELU;
+    if (p.a2) epi |= EPI_F_DUAL;
+  }
+  int tile = p.tile ? p.tile : pick_tile(p, batch);
+  if (tile == GEMM_TILE_256x128_K32) tile = GEMM_TILE_256x128;  // 184 KB of LDS: no
+  if (tile > GEMM_TILE_256x128) {
+    const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
+    const bool dual_ok = !p.a2 || p.Kloop1 % 32 == 0;
+    if (!narrow_ok || !dual_ok) tile -= 5;
+  }
+  switch (tile) {
+    case GEMM_TILE_128x128: return launch_tile_x3<128, 128, 2, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_128x64: return launch_tile_x3<128, 64, 4, 1, 16>(p, epi, batch, stream);
+    case GEMM_TILE_64x128: return launch_tile_x3<64, 128, 1, 4, 16>(p, epi, batch, stream);
+    case GEMM_TILE_64x64: return launch_tile_x3<64, 64, 2, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_256x128: return launch_tile_x3<256, 128, 4, 2, 16>(p, epi, batch, stream);
+    case GEMM_TILE_128x128_K32: return launch_tile_x3<128, 128, 2, 2, 32>(p, epi, batch, stream);
+    case GEMM_TILE_128x64_K32: return launch_tile_x3<128, 64, 4, 1, 32>(p, epi, batch, stream);
+    case GEMM_TILE_64x128_K32: return launch_tile_x3<64, 128, 1, 4, 32>(p, epi, batch, stream);
+    case GEMM_TILE_64x64_K32: return launch_tile_x3<64, 64, 2, 2, 32>(p, epi, batch, stream);
+    default:
+      set_error("unknown GEMM tile id " + std::to_string(tile));
+      return PPS_ERR_INVALID_ARG;
+  }
+}
+
+// ---- weight split: x[b][i] -> out[b][plane][i], x = hi + mid + lo ----------
+__global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t n, int nbatch,
+                                    unsigned short* __restrict__ out) {
+  const int64_t total = n * nbatch;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / n, i = e - b * n;
+    unsigned hi, mid, lo;
+    split2(x[e], 0.f, hi, mid, lo);
+    unsigned short* o = out + b * 3 * n + i;
+    o[0] = (unsigned short)hi;
+    o[n] = (unsigned short)mid;
+    o[2 * n] = (unsigned short)lo;
+  }
+}
+
+// ---- squared row norms: one wave per row, fixed lane order + xor tree -----
+__global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
+                                  float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* r = x + row * ld;
+  float s = 0.f;
+  for (int k = lane * 4; k < D; k += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
+    s = __builtin_fmaf(v[0], v[0], s);
+    s = __builtin_fmaf(v[1], v[1], s);
+    s = __builtin_fmaf(v[2], v[2], s);
+    s = __builtin_fmaf(v[3], v[3], s);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) out[row] = s;
+}
+
+int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream) {
+  if (rows <= 0) return PPS_OK;
+  const int64_t blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, rows,
+                     D, ld, out);
+  PPS_CHECK_LAUNCH("row_sqnorm_kernel");
+  return PPS_OK;
+}
+
+int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream) {
+  const int threads = 256;
+  const int64_t blocks = (n * nbatch + threads - 1) / threads;
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
+                     dim3(threads), 0, stream, x, n, nbatch,
+                     reinterpret_cast<unsigned short*>(out));
+  PPS_CHECK_LAUNCH("split_bf16x3_kernel");
+  return PPS_OK;
+}
+
+}  // namespace pps

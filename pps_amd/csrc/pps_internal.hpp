@@ -90,9 +90,20 @@ struct GemmParams {
   int tile;  // GemmTile; 0 = heuristic
   int splitk;           // >= 1; K slices enumerated with the batch on grid.y
   int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)
+  // bf16x3 GEMM (gemm_x3.hip): B as three bf16 planes [3][Ncol][ldb] per
+  // batch, b_plane elements apart; b_bstride counts bf16 elements and b_bytes
+  // the bytes addressable within ONE plane from its base
+  const uint16_t* b3;
+  int64_t b_plane;
+  // EPI_DIST in the bf16x3 GEMM: precomputed squared norms of A rows / B rows
+  const float* norm_a;
+  const float* norm_b;
 };
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
+int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream);
+int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream);
+int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
 
 }  // namespace pps

@@ -265,7 +265,13 @@ class PPSModel(object):
     on the current CUDA device, H x W = REID.SCALE[::-1].
     """
 
-    def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True):
+    def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True, math=None):
+        """math: 'x3' (default; f32 products on bf16 matrix cores, weights
+        split once into three bf16 planes -- gemm_x3.hip) or 'f32' (exact
+        f32 MFMA, gemm_f32.hip).  Env PPS_MATH overrides the default."""
+        self.math = math or ops.default_math()
+        if self.math not in ('x3', 'f32'):
+            raise ValueError("math must be 'x3' or 'f32', got %r" % self.math)
         self.plan = plan or build_plan()
         self.device = torch.device(device)
         missing = [n for n in self.plan.params if n not in blobs
@@ -327,6 +333,10 @@ class PPSModel(object):
                 H['output'] = L['output']
                 continue
             self.layers.append(L)
+        if self.math == 'x3':
+            for L in self.layers:
+                if L['op'] in ('conv', 'conv_dual', 'heads'):
+                    L['w'] = ops.split_bf16x3(L['w'], batched=L['op'] == 'heads')
         self.feat_dim = self.plan.feat_dim
         self._bufs = {}
         self._batch = None

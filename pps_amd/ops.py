@@ -9,6 +9,8 @@ Also hosts the operator registry that mirrors the reference's Caffe2 op names
 registration detectron/ops/pairwise_distance_op.cu:124-127), so code written
 against that registry can look ops up by the same names.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -40,17 +42,60 @@ def _dev(t, name, dtype=torch.float32):
 # ---------------------------------------------------------------------------
 # Retrieval
 # ---------------------------------------------------------------------------
-def compute_dist(q, g, metric='euclidean', out=None, tile=0):
-    """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244)."""
-    if q.dim() != 2 or g.dim() != 2 or q.shape[1] != g.shape[1]:
+def default_math():
+    """'x3' (f32 products on bf16 matrix cores, f32-level error) unless the
+    environment asks for the exact-f32 MFMA kernels with PPS_MATH=f32."""
+    m = os.environ.get('PPS_MATH', 'x3')
+    if m not in ('x3', 'f32'):
+        raise ValueError('PPS_MATH must be x3 or f32, got %r' % m)
+    return m
+
+
+def row_sqnorm(x):
+    """Squared L2 norm of every row of a [R, D] tensor (fixed summation order)."""
+    R, D = x.shape
+    out = torch.empty((R,), dtype=torch.float32, device=x.device)
+    call('pps_row_sqnorm', _dev(x, 'x'), R, D, x.stride(0), _dev(out, 'out'), _stream())
+    return out
+
+
+class GalleryIndex(object):
+    """A gallery prepared once for the bf16x3 distance GEMM: features split
+    into three bf16 planes + squared norms; score any number of query
+    batches against it with compute_dist(q, index)."""
+
+    def __init__(self, g):
+        if g.dim() != 2:
+            raise RuntimeError('gallery must be [G, D], got %s' % (tuple(g.shape),))
+        self.feats = g
+        self.planes = split_bf16x3(g)
+        self.sqnorm = row_sqnorm(g)
+
+    @property
+    def shape(self):
+        return self.feats.shape
+
+
+def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None):
+    """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244).
+    g may be a GalleryIndex (then the x3 kernel runs on its prepared planes)."""
+    math = 'x3' if isinstance(g, GalleryIndex) else (math or default_math())
+    if q.dim() != 2 or len(g.shape) != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
                            % (tuple(q.shape), tuple(g.shape)))
     Q, D = q.shape
     G = g.shape[0]
     if out is None:
         out = torch.empty((Q, G), dtype=torch.float32, device=q.device)
-    call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
-         _dev(out, 'out'), out.stride(0), int(tile), _stream())
+    if math == 'f32':
+        call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
+             _dev(out, 'out'), out.stride(0), int(tile), _stream())
+        return out
+    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g)
+    qsq = row_sqnorm(q)
+    call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
+         _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
+         METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
     return out
 
 
@@ -159,6 +204,26 @@ def max_positives(qid, qcam, gid, gcam):
 # ---------------------------------------------------------------------------
 # Feature extractor
 # ---------------------------------------------------------------------------
+def _weights(entry, w):
+    """f32 weights -> the exact-f32 MFMA entry; int16 (bf16x3 planes from
+    split_bf16x3) -> the `_x3` entry (f32 products on bf16 matrix cores)."""
+    if isinstance(w, torch.Tensor) and w.dtype == torch.int16:
+        return entry + '_x3', _dev(w, 'w', torch.int16)
+    return entry, _dev(w, 'w')
+
+
+def split_bf16x3(x, batched=False):
+    """f32 x -> int16 bf16 planes hi, mid, lo with x = hi + mid + lo exactly
+    (the weight format of the `_x3` GEMMs): shape (3,) + x.shape, or for
+    batched=True (x.shape[0], 3) + x.shape[1:]."""
+    nbatch = x.shape[0] if batched else 1
+    n = x.numel() // nbatch
+    shape = ((nbatch, 3) + tuple(x.shape[1:])) if batched else ((3,) + tuple(x.shape))
+    out = torch.empty(shape, dtype=torch.int16, device=x.device)
+    call('pps_split_bf16x3', _dev(x, 'x'), n, nbatch, _dev(out, 'out', torch.int16), _stream())
+    return out
+
+
 def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, relu, y,
                   tile=0):
     N, H, W, ldx = x.shape
@@ -169,7 +234,8 @@ def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, 
             raise RuntimeError('residual shape %s != output %s'
                                % (tuple(residual.shape), tuple(y.shape)))
         rp = _dev(residual, 'residual')
-    call('pps_conv2d_bn_act', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w, 'w'), Cout, kpad,
+    fn, wp = _weights('pps_conv2d_bn_act', w)
+    call(fn, _dev(x, 'x'), N, H, W, cin, ldx, wp, Cout, kpad,
          k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
          int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile), _stream())
     return y
@@ -181,8 +247,9 @@ def conv2d_dual_bn_act(x, cin, k, stride, pad, x2, stride2, w, kpad1, shift, rel
     N, H, W, ldx = x.shape
     _, H2, W2, C2 = x2.shape
     _, Ho, Wo, Cout = y.shape
-    call('pps_conv2d_dual_bn_act', _dev(x, 'x'), N, H, W, cin, ldx, k, k, stride, pad,
-         _dev(x2, 'x2'), H2, W2, C2, C2, stride2, _dev(w, 'w'), Cout, kpad1, C2,
+    fn, wp = _weights('pps_conv2d_dual_bn_act', w)
+    call(fn, _dev(x, 'x'), N, H, W, cin, ldx, k, k, stride, pad,
+         _dev(x2, 'x2'), H2, W2, C2, C2, stride2, wp, Cout, kpad1, C2,
          _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile),
          _stream())
     return y
@@ -199,11 +266,13 @@ def gemm_bn_act_batched(x, w, scale, shift, relu, y, tile=0):
 
 
 def gemm_splitk_batched(x, w, splitk, part, tile=0):
-    """x [B,M,K], w [B,Cout,K] -> raw partials part [splitk, M, B*Cout]."""
+    """x [B,M,K], w [B,Cout,K] (f32) or [B,3,Cout,K] (bf16x3 planes) -> raw
+    partials part [splitk, M, B*Cout]."""
     B, M, K = x.shape
-    Cout = w.shape[1]
-    call('pps_gemm_splitk_batched', _dev(x, 'x'), M, K, _dev(w, 'w'), Cout, B, splitk,
-         _dev(part, 'part'), int(tile), _stream())
+    Cout = w.shape[-2]
+    fn, wp = _weights('pps_gemm_splitk_batched', w)
+    call(fn, _dev(x, 'x'), M, K, wp, Cout, B, splitk, _dev(part, 'part'), int(tile),
+         _stream())
     return part
 
 

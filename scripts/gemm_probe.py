@@ -1,0 +1,69 @@
+"""Time single implicit-GEMM conv launches (x3 and f32 kernels) on PPS layer
+shapes, one tile at a time -- the unit used when tuning gemm_x3.hip /
+gemm_f32.hip and for PMC passes (scripts/pmc.sh CMD="python3 scripts/gemm_probe.py").
+
+  python scripts/gemm_probe.py [--layers res5b,res4b,...] [--tiles 1,5] [--math x3,f32]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+# name: (N, H, W, Cin, Cout, k, stride, pad) at batch 64, 384x128 input
+LAYERS = {
+    'res5b': (64, 24, 8, 512, 512, 3, 1, 1),
+    'res5a': (64, 24, 8, 2048, 512, 1, 1, 0),
+    'res5c': (64, 24, 8, 512, 2048, 1, 1, 0),
+    'res4b': (64, 24, 8, 256, 256, 3, 1, 1),
+    'res3b': (64, 48, 16, 128, 128, 3, 1, 1),
+    'res2b': (64, 96, 32, 64, 64, 3, 1, 1),
+    'res2c': (64, 96, 32, 64, 256, 1, 1, 0),
+    'stem': (64, 384, 128, 4, 64, 7, 2, 3),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--layers', default='res5b,res5a,res4b,res2b')
+    ap.add_argument('--tiles', default='1,2,3,4,5,6,7,8,9')
+    ap.add_argument('--math', default='x3,f32')
+    ap.add_argument('--reps', type=int, default=20)
+    a = ap.parse_args()
+    from pps_amd import model, ops
+    for name in a.layers.split(','):
+        N, H, W, Cin, Cout, k, s, p = LAYERS[name]
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N, H, W, Cin, device='cuda')
+        w = np.random.RandomState(0).randn(Cout, Cin, k, k).astype(np.float32) / np.sqrt(Cin * k * k)
+        wp, kpad = model.pack_conv_weight(w)
+        wf = torch.from_numpy(wp).cuda()
+        w3 = ops.split_bf16x3(wf)
+        sc = torch.ones(Cout, device='cuda')
+        sh = torch.zeros(Cout, device='cuda')
+        y = torch.empty(N, Ho, Wo, Cout, device='cuda')
+        flops = 2.0 * N * Ho * Wo * Cout * k * k * Cin
+        for math in a.math.split(','):
+            wt = w3 if math == 'x3' else wf
+            res = []
+            for tile in [int(t) for t in a.tiles.split(',')]:
+                ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, None, True, y, tile=tile)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, None, True, y,
+                                      tile=tile)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.reps
+                res.append('%d:%.3f(%.0f)' % (tile, ms, flops / ms / 1e9))
+            print('%-6s %-4s M=%d N=%d K=%d  %s' % (name, math, N * Ho * Wo, Cout, k * k * Cin,
+                                                    ' '.join(res)), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -130,7 +130,8 @@ def _market_cfg():
     return cfg
 
 
-def test_full_forward_vs_oracle():
+@pytest.mark.parametrize('math', ['x3', 'f32'])
+def test_full_forward_vs_oracle(math):
     from oracle.forward import GraphForward
     from pps_amd import model
     _market_cfg()
@@ -140,7 +141,7 @@ def test_full_forward_vs_oracle():
     x = (rng.randn(3, 3, 384, 128) * 50).astype(np.float32)
     ref, kept = GraphForward(blobs)(x, keep=('res2_2_sum', 'res3_3_sum', 'res4_5_sum',
                                              'res5_2_sum', 'reid_feature_concat'))
-    m = model.PPSModel(blobs)
+    m = model.PPSModel(blobs, math=math)
     xin = np.zeros((3, 384, 128, 4), np.float32)
     xin[..., :3] = x.transpose(0, 2, 3, 1)
     out = m.forward(_cuda(xin)).cpu().numpy()

@@ -18,11 +18,12 @@ def _cuda(x, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(x)).to(dtype).cuda()
 
 
+@pytest.mark.parametrize('math', ['x3', 'f32'])
 @pytest.mark.parametrize('case', ['market_small', 'full_dim'])
-def test_distmat_vs_golden(golden, case):
+def test_distmat_vs_golden(golden, case, math):
     from pps_amd import ops
     g = golden(case)
-    d = ops.compute_dist(_cuda(g['qf']), _cuda(g['gf'])).cpu().numpy()
+    d = ops.compute_dist(_cuda(g['qf']), _cuda(g['gf']), math=math).cpu().numpy()
     np.testing.assert_allclose(d, g['dist'], rtol=0, atol=1e-4)
     assert np.abs(d - g['dist']).max() < 5e-6
 
@@ -30,7 +31,8 @@ def test_distmat_vs_golden(golden, case):
 @pytest.mark.parametrize('Q,G,D', [(1, 1, 4), (3, 5, 8), (33, 65, 20), (127, 129, 132),
                                    (200, 300, 2048), (64, 1000, 3968)])
 @pytest.mark.parametrize('metric', ['euclidean', 'sqeuclidean', 'cosine'])
-def test_distmat_ragged_shapes(Q, G, D, metric):
+@pytest.mark.parametrize('math', ['x3', 'f32'])
+def test_distmat_ragged_shapes(Q, G, D, metric, math):
     from pps_amd import ops
     rng = np.random.RandomState(Q * 7 + G)
     q = rng.randn(Q, D).astype(np.float32)
@@ -39,12 +41,26 @@ def test_distmat_ragged_shapes(Q, G, D, metric):
     scale = max(1.0, float(np.abs(ref).max()))
     first = None
     for tile in range(0, ops.num_tiles() + 1):
-        d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric, tile=tile).cpu().numpy()
+        d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric, tile=tile,
+                             math=math).cpu().numpy()
         np.testing.assert_allclose(d, ref, rtol=0, atol=2e-5 * scale * np.sqrt(D / 128.0),
                                    err_msg='tile %d' % tile)
         if first is None:
             first = d
         np.testing.assert_array_equal(d, first)
+
+
+def test_gallery_index_matches_plain_x3():
+    from pps_amd import ops
+    rng = np.random.RandomState(11)
+    q = _cuda(rng.randn(70, 256).astype(np.float32))
+    g = _cuda(rng.randn(300, 256).astype(np.float32))
+    idx = ops.GalleryIndex(g)
+    a = ops.compute_dist(q, idx).cpu().numpy()
+    b = ops.compute_dist(q, g, math='x3').cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    sq = ops.row_sqnorm(g).cpu().numpy()
+    np.testing.assert_allclose(sq, (g.double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
 
 
 def test_distmat_enforces_shapes():

@@ -1,0 +1,145 @@
+"""The bf16x3 GEMM path (pps_amd/csrc/gemm_x3.hip): f32 products on bf16
+matrix cores.
+
+* the weight split is exact: hi + mid + lo == w bit for bit (fp64 sum);
+* results carry f32-level error: measured against an fp64 reference, the
+  x3 kernel's max error stays within 4x the exact-f32 MFMA kernel's max error
+  on the same data (tolerance written below), far from bf16 (~4e-3);
+* every tile configuration gives identical bits.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+X3_VS_F32 = 4.0      # max error of x3 <= X3_VS_F32 * max error of exact f32 (+ floor)
+ERR_FLOOR = 2e-7     # relative to max |ref|: one f32 ulp order of magnitude
+
+
+def _cuda(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+
+
+def _rel_err(got, ref):
+    return float(np.abs(got.astype(np.float64) - ref).max() / max(1e-30, np.abs(ref).max()))
+
+
+def test_split_bf16x3_exact():
+    from pps_amd import ops
+    rng = np.random.RandomState(0)
+    x = np.concatenate([rng.randn(4096), rng.randn(4096) * 1e-20, rng.randn(4096) * 1e20,
+                        [0.0, -0.0, 1.0, -1.0, 3.0e38, 1.17549435e-38]]).astype(np.float32)
+    planes = ops.split_bf16x3(_cuda(x))
+    assert planes.shape == (3, x.size) and planes.dtype == torch.int16
+    parts = planes.view(torch.bfloat16).double().cpu().numpy()
+    np.testing.assert_array_equal(parts.sum(0), x.astype(np.float64))
+    # the leading plane is round-to-nearest bf16 of x
+    np.testing.assert_array_equal(parts[0], torch.from_numpy(x).bfloat16().double().numpy())
+    hb = ops.split_bf16x3(_cuda(x[:12288].reshape(3, 64, 64)), batched=True)
+    assert hb.shape == (3, 3, 64, 64)
+    np.testing.assert_array_equal(hb.view(torch.bfloat16).double().sum(1).cpu().numpy(),
+                                  x[:12288].reshape(3, 64, 64))
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 96, 32, 64, 64, 1, 1, 0),
+    (2, 96, 32, 64, 64, 3, 1, 1),
+    (2, 48, 16, 256, 128, 1, 2, 0),
+    (1, 24, 8, 512, 512, 3, 1, 1),
+    (3, 7, 5, 32, 40, 3, 1, 1),        # ragged M and N
+    (1, 11, 9, 16, 33, 3, 2, 1),       # ragged, strided, Cin < 32 (BK32 falls back)
+    (1, 9, 7, 20, 24, 3, 1, 1),        # Cin not a power of two and < 32
+    (2, 384, 128, 4, 64, 7, 2, 3),     # stem conv1 (Cin 3 packed to 4)
+])
+@pytest.mark.parametrize('residual', [False, True])
+def test_conv_x3_error_and_tiles(N, H, W, Cin, Cout, k, s, p, residual):
+    from pps_amd import model, ops
+    rng = np.random.RandomState(N + H + Cin + Cout + k)
+    x = rng.randn(N, Cin, H, W).astype(np.float32)
+    if Cin == 4:
+        x[:, 3] = 0
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    scale = rng.uniform(0.5, 1.5, Cout).astype(np.float32)
+    shift = rng.randn(Cout).astype(np.float32) * 0.1
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w).double(), stride=s,
+                   padding=p)
+    ref = ref * torch.from_numpy(scale).double()[None, :, None, None] + \
+        torch.from_numpy(shift).double()[None, :, None, None]
+    res = None
+    if residual:
+        res_np = rng.randn(*ref.shape).astype(np.float32)
+        ref = ref + torch.from_numpy(res_np).double()
+        res = _cuda(res_np.transpose(0, 2, 3, 1))
+    ref = ref.numpy().transpose(0, 2, 3, 1)
+    wp, kpad = model.pack_conv_weight(w)
+    xd = _cuda(x.transpose(0, 2, 3, 1))
+    y = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.conv2d_bn_act(xd, Cin, _cuda(wp), kpad, k, s, p, 1, _cuda(scale), _cuda(shift), res,
+                      False, y)
+    e_f32 = _rel_err(y.cpu().numpy(), ref)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    outs = []
+    for tile in range(0, ops.num_tiles() + 1):
+        y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+        ops.conv2d_bn_act(xd, Cin, w3, kpad, k, s, p, 1, _cuda(scale), _cuda(shift), res,
+                          False, y, tile=tile)
+        outs.append(y.cpu().numpy())
+    e_x3 = _rel_err(outs[0], ref)
+    print('conv x3 err %.3g  f32 err %.3g' % (e_x3, e_f32))
+    assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
+    for t, o in enumerate(outs[1:], 1):
+        np.testing.assert_array_equal(o, outs[0], err_msg='tile %d' % t)
+
+
+@pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(2, 24, 8, 128, 256, 512, 2),
+                                                 (1, 24, 8, 512, 1024, 2048, 1),
+                                                 (3, 5, 7, 16, 32, 40, 1)])
+def test_conv_dual_x3(N, H, W, C1, C2, Cout, s2):
+    from pps_amd import model, ops
+    rng = np.random.RandomState(C1 + Cout)
+    x = rng.randn(N, C1, H, W).astype(np.float32)
+    x2 = rng.randn(N, C2, (H - 1) * s2 + 1, (W - 1) * s2 + 1).astype(np.float32)
+    w1 = (rng.randn(Cout, C1, 1, 1) / np.sqrt(C1)).astype(np.float32)
+    w2 = (rng.randn(Cout, C2, 1, 1) / np.sqrt(C2)).astype(np.float32)
+    sh = rng.randn(Cout).astype(np.float32)
+    p1, k1 = model.pack_conv_weight(w1)
+    p2, _ = model.pack_conv_weight(w2)
+    w = np.concatenate([p1, p2], 1)
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w1).double()) + \
+        F.conv2d(torch.from_numpy(x2).double(), torch.from_numpy(w2).double(), stride=s2) + \
+        torch.from_numpy(sh).double()[:, None, None]
+    ref = torch.clamp_min(ref, 0).numpy().transpose(0, 2, 3, 1)
+    xd, x2d = _cuda(x.transpose(0, 2, 3, 1)), _cuda(x2.transpose(0, 2, 3, 1))
+    y = torch.empty(ref.shape, device='cuda')
+    ops.conv2d_dual_bn_act(xd, C1, 1, 1, 0, x2d, s2, _cuda(w), k1, _cuda(sh), True, y)
+    e_f32 = _rel_err(y.cpu().numpy(), ref)
+    w3 = ops.split_bf16x3(_cuda(w))
+    outs = []
+    for tile in range(0, ops.num_tiles() + 1):
+        y = torch.full(ref.shape, float('nan'), device='cuda')
+        ops.conv2d_dual_bn_act(xd, C1, 1, 1, 0, x2d, s2, w3, k1, _cuda(sh), True, y,
+                               tile=tile)
+        outs.append(y.cpu().numpy())
+    e_x3 = _rel_err(outs[0], ref)
+    assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+
+
+@pytest.mark.parametrize('splitk', [1, 8])
+def test_heads_splitk_x3(splitk):
+    from pps_amd import ops
+    rng = np.random.RandomState(7)
+    B, M, K, C = 31, 6, 2048, 128
+    x = rng.randn(B, M, K).astype(np.float32)
+    w = (rng.randn(B, C, K) / 45).astype(np.float32)
+    ref = np.einsum('bmk,bck->mbc', x.astype(np.float64), w).reshape(M, B * C)
+    part = torch.empty((splitk, M, B * C), device='cuda')
+    ops.gemm_splitk_batched(_cuda(x), _cuda(w), splitk, part)
+    e_f32 = _rel_err(part.sum(0).cpu().numpy(), ref)
+    ops.gemm_splitk_batched(_cuda(x), ops.split_bf16x3(_cuda(w), batched=True), splitk, part)
+    e_x3 = _rel_err(part.sum(0).cpu().numpy(), ref)
+    assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
+
