@@ -46,7 +46,9 @@ const char* pps_registered_ops(void);
 /* GEMM tile configurations shared by pps_distmat / pps_conv2d_bn_act /
  * pps_gemm_bn_act_batched (`tile` argument): 0 = built-in heuristic,
  * 1 = 128x128 (4 waves), 2 = 128x64, 3 = 64x128, 4 = 64x64, 5 = 256x128
- * (8 waves), 6..10 = the same shapes with a 32-wide K chunk per barrier.  Results are identical for every tile (same per-element fp32
+ * (8 waves), 6..10 = the same shapes with a 32-wide K chunk per barrier,
+ * 11..20 = ids 1..10 with the `_x3` kernels' A operand kept f32 in LDS and
+ * split after the fragment read (the f32 kernels treat them as 1..10).  Results are identical for every tile (same per-element fp32
  * MFMA accumulation order); only speed differs, so callers may autotune. */
 int pps_gemm_num_tiles(void);
 

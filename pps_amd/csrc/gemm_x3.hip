@@ -91,7 +91,7 @@ __device__ inline void dist_epilogue(const GemmParams& p,
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int BK>
+template <int BM, int BN, int WM, int WN, int EPI, int BK, bool AF32>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int T = 64 * WM * WN;
@@ -104,7 +104,11 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int TN = BN / WN / 32;
   constexpr int APL = BM * LSTR;        // elements per A plane
   constexpr int BPL = BN * LSTR;
-  constexpr int STAGE = 3 * (APL + BPL);
+  // AF32: A stays f32 in LDS (rows of BK+4 floats, as in gemm_f32.hip) and is
+  // split after the fragment read -- 4 B instead of 6 B per element staged
+  constexpr int LSTRA = 2 * (BK + 4);   // A row stride in 16-bit units (AF32)
+  constexpr int AREG = AF32 ? BM * LSTRA : 3 * APL;
+  constexpr int STAGE = AREG + 3 * BPL;
   static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
   static_assert(AL >= 1 && BL >= 1 && TM >= 1 && TN >= 1, "tile too small");
   static_assert(2 * STAGE * 2 + 256 <= 160 * 1024, "LDS over 160 KB");
@@ -177,9 +181,13 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // one K chunk: registers -> LDS stage (A split into planes), barrier,
   // request chunk kc+2 into the freed registers, MFMAs on the stage
   auto step = [&](int kc, f32x4 (&ra)[AL], u32x2 (&rb)[BL][3], unsigned short* as) {
-    unsigned short* bs = as + 3 * APL;  // as: [3][BM][LSTR], bs: [3][BN][LSTR]
+    unsigned short* bs = as + AREG;  // as: [3][BM][LSTR] or [BM][BK+4] f32; bs: [3][BN][LSTR]
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
+      if (AF32) {
+        *reinterpret_cast<f32x4*>(as + (trow + i * RPP) * LSTRA + c4 * 8) = ra[i];
+        continue;
+      }
       unsigned h0, m0_, l0, h1, m1, l1;
       split2(ra[i][0], ra[i][1], h0, m0_, l0);
       split2(ra[i][2], ra[i][3], h1, m1, l1);
@@ -203,9 +211,25 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
       bf16x8 fa[TM][3], fb[TN][3];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const unsigned short* s = as + (wm * (BM / WM) + i * 32 + r32) * LSTR + g * 16 + h * 8;
+        const int row = wm * (BM / WM) + i * 32 + r32;
+        if (AF32) {
+          const float* s = reinterpret_cast<const float*>(as + row * LSTRA) + g * 16 + h * 8;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(s);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(s + 4);
+          u32x4 hi, mid, lo;
+          unsigned a, b, c;
+          split2(x0[0], x0[1], a, b, c); hi[0] = a; mid[0] = b; lo[0] = c;
+          split2(x0[2], x0[3], a, b, c); hi[1] = a; mid[1] = b; lo[1] = c;
+          split2(x1[0], x1[1], a, b, c); hi[2] = a; mid[2] = b; lo[2] = c;
+          split2(x1[2], x1[3], a, b, c); hi[3] = a; mid[3] = b; lo[3] = c;
+          fa[i][0] = __builtin_bit_cast(bf16x8, hi);
+          fa[i][1] = __builtin_bit_cast(bf16x8, mid);
+          fa[i][2] = __builtin_bit_cast(bf16x8, lo);
+        } else {
+          const unsigned short* s = as + row * LSTR + g * 16 + h * 8;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *reinterpret_cast<const bf16x8*>(s + pl * APL);
+          for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *reinterpret_cast<const bf16x8*>(s + pl * APL);
+        }
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -243,30 +267,36 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BK>
-static void launch_one_x3(const GemmParams& p, int batch, hipStream_t stream) {
+static void launch_one_x3(const GemmParams& p, int batch, hipStream_t stream, bool af32) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, EPI, BK>),
-                     dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream,
-                     p, tiles_m, tiles_n);
+  if (af32)
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, EPI, BK, true>),
+                       dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream,
+                       p, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, EPI, BK, false>),
+                       dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream,
+                       p, tiles_m, tiles_n);
 }
 
 template <int BM, int BN, int WM, int WN, int BK>
-static int launch_tile_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+static int launch_tile_x3(const GemmParams& p, int epi, int batch, hipStream_t stream,
+                          bool af32) {
   switch (epi) {
-    case EPI_DIST: launch_one_x3<BM, BN, WM, WN, EPI_DIST, BK>(p, batch, stream); break;
-    case EPI_CONV: launch_one_x3<BM, BN, WM, WN, EPI_CONV, BK>(p, batch, stream); break;
+    case EPI_DIST: launch_one_x3<BM, BN, WM, WN, EPI_DIST, BK>(p, batch, stream, af32); break;
+    case EPI_CONV: launch_one_x3<BM, BN, WM, WN, EPI_CONV, BK>(p, batch, stream, af32); break;
     case EPI_CONV | EPI_F_RELU:
-      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU, BK>(p, batch, stream); break;
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU, BK>(p, batch, stream, af32); break;
     case EPI_CONV | EPI_F_RES:
-      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES, BK>(p, batch, stream); break;
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES, BK>(p, batch, stream, af32); break;
     case EPI_CONV | EPI_F_RES | EPI_F_RELU:
-      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU, BK>(p, batch, stream);
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RES | EPI_F_RELU, BK>(p, batch, stream, af32);
       break;
     case EPI_CONV | EPI_F_RAW:
-      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW, BK>(p, batch, stream); break;
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RAW, BK>(p, batch, stream, af32); break;
     case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
-      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL, BK>(p, batch, stream);
+      launch_one_x3<BM, BN, WM, WN, EPI_CONV | EPI_F_RELU | EPI_F_DUAL, BK>(p, batch, stream, af32);
       break;
     default:
       set_error("unknown epilogue for the bf16x3 GEMM");
@@ -292,6 +322,10 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.a2) epi |= EPI_F_DUAL;
   }
   int tile = p.tile ? p.tile : pick_tile(p, batch);
+  // ids 11..20: the same shapes with A kept f32 in LDS and split after the
+  // fragment read (AF32); 1..10 split A while staging (three bf16 planes)
+  const bool af32 = tile > GEMM_TILE_256x128_K32;
+  if (af32) tile -= GEMM_TILE_256x128_K32;
   if (tile == GEMM_TILE_256x128_K32) tile = GEMM_TILE_256x128;  // 184 KB of LDS: no
   if (tile > GEMM_TILE_256x128) {
     const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
@@ -299,15 +333,15 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (!narrow_ok || !dual_ok) tile -= 5;
   }
   switch (tile) {
-    case GEMM_TILE_128x128: return launch_tile_x3<128, 128, 2, 2, 16>(p, epi, batch, stream);
-    case GEMM_TILE_128x64: return launch_tile_x3<128, 64, 4, 1, 16>(p, epi, batch, stream);
-    case GEMM_TILE_64x128: return launch_tile_x3<64, 128, 1, 4, 16>(p, epi, batch, stream);
-    case GEMM_TILE_64x64: return launch_tile_x3<64, 64, 2, 2, 16>(p, epi, batch, stream);
-    case GEMM_TILE_256x128: return launch_tile_x3<256, 128, 4, 2, 16>(p, epi, batch, stream);
-    case GEMM_TILE_128x128_K32: return launch_tile_x3<128, 128, 2, 2, 32>(p, epi, batch, stream);
-    case GEMM_TILE_128x64_K32: return launch_tile_x3<128, 64, 4, 1, 32>(p, epi, batch, stream);
-    case GEMM_TILE_64x128_K32: return launch_tile_x3<64, 128, 1, 4, 32>(p, epi, batch, stream);
-    case GEMM_TILE_64x64_K32: return launch_tile_x3<64, 64, 2, 2, 32>(p, epi, batch, stream);
+    case GEMM_TILE_128x128: return launch_tile_x3<128, 128, 2, 2, 16>(p, epi, batch, stream, af32);
+    case GEMM_TILE_128x64: return launch_tile_x3<128, 64, 4, 1, 16>(p, epi, batch, stream, af32);
+    case GEMM_TILE_64x128: return launch_tile_x3<64, 128, 1, 4, 16>(p, epi, batch, stream, af32);
+    case GEMM_TILE_64x64: return launch_tile_x3<64, 64, 2, 2, 16>(p, epi, batch, stream, af32);
+    case GEMM_TILE_256x128: return launch_tile_x3<256, 128, 4, 2, 16>(p, epi, batch, stream, af32);
+    case GEMM_TILE_128x128_K32: return launch_tile_x3<128, 128, 2, 2, 32>(p, epi, batch, stream, af32);
+    case GEMM_TILE_128x64_K32: return launch_tile_x3<128, 64, 4, 1, 32>(p, epi, batch, stream, af32);
+    case GEMM_TILE_64x128_K32: return launch_tile_x3<64, 128, 1, 4, 32>(p, epi, batch, stream, af32);
+    case GEMM_TILE_64x64_K32: return launch_tile_x3<64, 64, 2, 2, 32>(p, epi, batch, stream, af32);
     default:
       set_error("unknown GEMM tile id " + std::to_string(tile));
       return PPS_ERR_INVALID_ARG;

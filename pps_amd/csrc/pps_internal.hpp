@@ -50,7 +50,8 @@ enum GemmTile {
   GEMM_TILE_64x128_K32 = 8,
   GEMM_TILE_64x64_K32 = 9,
   GEMM_TILE_256x128_K32 = 10,
-  GEMM_NUM_TILES = 11
+  // 11..20: ids 1..10 with the bf16x3 kernel's A operand kept f32 in LDS
+  GEMM_NUM_TILES = 21
 };
 
 struct GemmParams {

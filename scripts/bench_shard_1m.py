@@ -1,0 +1,69 @@
+"""BASELINE.json configs[4] at the size one GPU owns: the synthetic 1M-gallery x
+10k-query, D=2048 sharded distance matrix is split
+8 ways, 125,000 gallery rows per GPU.  This times ONE shard on one GPU:
+build the gallery index (bf16x3 planes + norms), the [10k, 125k] L2 block
+(5.0 GB fp32) and the stable top-100 per query (the per-GPU output the
+8-way merge consumes).  Features: normalised Gaussian, seed 0 (§8(d)).
+
+  python scripts/bench_shard_1m.py [--queries 10000] [--shard 125000] [--math x3|f32]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--queries', type=int, default=10000)
+    ap.add_argument('--shard', type=int, default=125000)
+    ap.add_argument('--dim', type=int, default=2048)
+    ap.add_argument('--topk', type=int, default=100)
+    ap.add_argument('--math', default='x3')
+    ap.add_argument('--reps', type=int, default=3)
+    a = ap.parse_args()
+    from pps_amd import ops
+    g = torch.Generator(device='cuda')
+    g.manual_seed(0)
+    q = torch.randn(a.queries, a.dim, generator=g, device='cuda')
+    q /= q.norm(dim=1, keepdim=True)
+    gal = torch.randn(a.shard, a.dim, generator=g, device='cuda')
+    gal /= gal.norm(dim=1, keepdim=True)
+    out = torch.empty(a.queries, a.shard, device='cuda')
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    res = {}
+    for rep in range(a.reps + 1):
+        e = [ev() for _ in range(4)]
+        e[0].record()
+        idx = ops.GalleryIndex(gal) if a.math == 'x3' else gal
+        e[1].record()
+        ops.compute_dist(q, idx, out=out, math=a.math)
+        e[2].record()
+        vals, ids = ops.topk(out, a.topk)
+        e[3].record()
+        torch.cuda.synchronize()
+        if rep:  # first pass is warm-up
+            for k, (s, t) in dict(index_ms=(0, 1), distmat_ms=(1, 2), topk_ms=(2, 3)).items():
+                res.setdefault(k, []).append(e[s].elapsed_time(e[t]))
+    med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+    flops = 2.0 * a.queries * a.shard * a.dim
+    byt = (a.queries + a.shard) * a.dim * 4 + a.queries * a.shard * 4
+    print(json.dumps(dict(
+        config='synthetic %dq x %dg shard (1M/8), D=%d, math=%s' % (a.queries, a.shard, a.dim,
+                                                                   a.math),
+        index_ms=round(med['index_ms'], 3), distmat_ms=round(med['distmat_ms'], 3),
+        topk_ms=round(med['topk_ms'], 3),
+        distmat_TFLOPs=round(flops / med['distmat_ms'] / 1e9, 1),
+        distmat_GBps=round(byt / med['distmat_ms'] / 1e6, 1),
+        topk_GBps=round(a.queries * a.shard * 4 / med['topk_ms'] / 1e6, 1))), flush=True)
+
+
+if __name__ == '__main__':
+    main()
