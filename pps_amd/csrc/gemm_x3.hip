@@ -150,12 +150,15 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
     bbase[i] = col < p.Ncol ? (unsigned)(col * p.ldb + c4 * 4) * 2u : (unsigned)kOOB;
   }
 
-  // two register stages: chunk kc+2 is requested while chunk kc computes, so
-  // a load has two chunk-compute times to land (one was not enough at 2
-  // waves/SIMD: the MFMAs outrun a single stage's L2/HBM latency)
-  f32x4 ra0[AL], ra1[AL];
-  u32x2 rb0[BL][3], rb1[BL][3];
-  auto load_chunk = [&](int kc, f32x4 (&ra)[AL], u32x2 (&rb)[BL][3]) {
+  // One register stage, two LDS stages.  Iteration kc computes on stage kc&1
+  // while it writes chunk kc+1 (loaded one iteration earlier) into the other
+  // stage and requests chunk kc+2; one barrier closes the iteration.  The
+  // split / LDS-store work of the next chunk therefore sits between this
+  // chunk's MFMAs instead of in a separate phase that every wave of the
+  // block (synchronised by the barrier) would run at the same time.
+  f32x4 ra[AL];
+  u32x2 rb[BL][3];
+  auto load_chunk = [&](int kc) {
     ag.load(p, kc, c4, s_tapoff, ra);
     const bool kok = kc * BK + c4 * 4 < p.kb_valid;
 #pragma unroll
@@ -168,19 +171,8 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
       rb[i][2] = bload64(rb_src2, off);
     }
   };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nchunks = (p.Kloop + BK - 1) / BK;
-  // one K chunk: registers -> LDS stage (A split into planes), barrier,
-  // request chunk kc+2 into the freed registers, MFMAs on the stage
-  auto step = [&](int kc, f32x4 (&ra)[AL], u32x2 (&rb)[BL][3], unsigned short* as) {
+  // registers -> LDS stage `as` (A split into planes unless AF32)
+  auto store_chunk = [&](unsigned short* as) {
     unsigned short* bs = as + AREG;  // as: [3][BM][LSTR] or [BM][BK+4] f32; bs: [3][BN][LSTR]
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
@@ -203,61 +195,81 @@ gemm_x3_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x2*>(d + pl * BPL) = rb[i][pl];
     }
-    __syncthreads();
-    if (kc + 2 < nchunks) load_chunk(kc + 2, ra, rb);
-
-#pragma unroll
-    for (int g = 0; g < BK / 16; ++g) {
-      bf16x8 fa[TM][3], fb[TN][3];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / WM) + i * 32 + r32;
-        if (AF32) {
-          const float* s = reinterpret_cast<const float*>(as + row * LSTRA) + g * 16 + h * 8;
-          const f32x4 x0 = *reinterpret_cast<const f32x4*>(s);
-          const f32x4 x1 = *reinterpret_cast<const f32x4*>(s + 4);
-          u32x4 hi, mid, lo;
-          unsigned a, b, c;
-          split2(x0[0], x0[1], a, b, c); hi[0] = a; mid[0] = b; lo[0] = c;
-          split2(x0[2], x0[3], a, b, c); hi[1] = a; mid[1] = b; lo[1] = c;
-          split2(x1[0], x1[1], a, b, c); hi[2] = a; mid[2] = b; lo[2] = c;
-          split2(x1[2], x1[3], a, b, c); hi[3] = a; mid[3] = b; lo[3] = c;
-          fa[i][0] = __builtin_bit_cast(bf16x8, hi);
-          fa[i][1] = __builtin_bit_cast(bf16x8, mid);
-          fa[i][2] = __builtin_bit_cast(bf16x8, lo);
-        } else {
-          const unsigned short* s = as + row * LSTR + g * 16 + h * 8;
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *reinterpret_cast<const bf16x8*>(s + pl * APL);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const unsigned short* s = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + g * 16 + h * 8;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) fb[j][pl] = *reinterpret_cast<const bf16x8*>(s + pl * BPL);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          f32x16 c = acc[i][j];
-          c = mfma_bf16(fa[i][0], fb[j][0], c);
-          c = mfma_bf16(fa[i][1], fb[j][0], c);
-          c = mfma_bf16(fa[i][0], fb[j][1], c);
-          c = mfma_bf16(fa[i][2], fb[j][0], c);
-          c = mfma_bf16(fa[i][1], fb[j][1], c);
-          c = mfma_bf16(fa[i][0], fb[j][2], c);
-          acc[i][j] = c;
-        }
-    }
   };
 
-  load_chunk(0, ra0, rb0);
-  if (nchunks > 1) load_chunk(1, ra1, rb1);
-  for (int kc = 0; kc < nchunks; kc += 2) {
-    step(kc, ra0, rb0, lds);
-    if (kc + 1 < nchunks) step(kc + 1, ra1, rb1, lds + STAGE);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // MFMAs of one 16-wide K group of stage `as`
+  auto compute_group = [&](const unsigned short* as, int g) {
+    const unsigned short* bs = as + AREG;
+    bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * (BM / WM) + i * 32 + r32;
+      if (AF32) {
+        const float* s = reinterpret_cast<const float*>(as + row * LSTRA) + g * 16 + h * 8;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(s);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(s + 4);
+        u32x4 hi, mid, lo;
+        unsigned a, b, c;
+        split2(x0[0], x0[1], a, b, c); hi[0] = a; mid[0] = b; lo[0] = c;
+        split2(x0[2], x0[3], a, b, c); hi[1] = a; mid[1] = b; lo[1] = c;
+        split2(x1[0], x1[1], a, b, c); hi[2] = a; mid[2] = b; lo[2] = c;
+        split2(x1[2], x1[3], a, b, c); hi[3] = a; mid[3] = b; lo[3] = c;
+        fa[i][0] = __builtin_bit_cast(bf16x8, hi);
+        fa[i][1] = __builtin_bit_cast(bf16x8, mid);
+        fa[i][2] = __builtin_bit_cast(bf16x8, lo);
+      } else {
+        const unsigned short* s = as + row * LSTR + g * 16 + h * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *reinterpret_cast<const bf16x8*>(s + pl * APL);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned short* s = bs + (wn * (BN / WN) + j * 32 + r32) * LSTR + g * 16 + h * 8;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fb[j][pl] = *reinterpret_cast<const bf16x8*>(s + pl * BPL);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = mfma_bf16(fa[i][0], fb[j][0], c);
+        c = mfma_bf16(fa[i][1], fb[j][0], c);
+        c = mfma_bf16(fa[i][0], fb[j][1], c);
+        c = mfma_bf16(fa[i][2], fb[j][0], c);
+        c = mfma_bf16(fa[i][1], fb[j][1], c);
+        c = mfma_bf16(fa[i][0], fb[j][2], c);
+        acc[i][j] = c;
+      }
+  };
+
+  // Loads past the last chunk are harmless: they address beyond the tap /
+  // K ranges or num_records and read zero, and the stage they are written to
+  // is never read.  Keeping them unconditional keeps the store work and the
+  // MFMAs of an iteration in one basic block, so the scheduler interleaves them.
+  const int nchunks = (p.Kloop + BK - 1) / BK;
+  load_chunk(0);
+  store_chunk(lds);
+  load_chunk(1);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const unsigned short* cur = lds + (kc & 1) * STAGE;
+    unsigned short* nxt = lds + ((kc + 1) & 1) * STAGE;
+    compute_group(cur, 0);
+    store_chunk(nxt);
+#pragma unroll
+    for (int g = 1; g < BK / 16; ++g) compute_group(cur, g);
+    load_chunk(kc + 2);
+    __syncthreads();
   }
 
   if (EPI & EPI_DIST)
