@@ -28,6 +28,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA)
+PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # bf16 MFMA = 16x the f32 rate (~2.5 PF)
+# bf16x3 path: every f32 product costs 6 bf16 MFMA terms -> its own MFMA roof
+PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r01', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -42,6 +46,9 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--dist-reps', type=int, default=5)
     p.add_argument('--no-autotune', action='store_true')
+    p.add_argument('--tiles-file', default=None,
+                   help='JSON {layer: tile}: reuse (if present) or save the autotune result, '
+                        'so profiling passes run the same kernels as the timed run')
     return p.parse_args()
 
 
@@ -67,7 +74,7 @@ def synth_features(n, ids, gen, noise=4.0, n_ids=750):
     return (x / x.norm(dim=1, keepdim=True)).contiguous()
 
 
-def retrieval_stage(rank, world, reps):
+def retrieval_stage(rank, world, reps, tune=True):
     """Distance matrix + mAP/CMC at Market sizes.  Gallery sharded over ranks,
     queries all-gathered.  Returns timings (ms) and scores."""
     from pps_amd import distributed as pdist
@@ -87,6 +94,23 @@ def retrieval_stage(rank, world, reps):
     g_local = allf[Q_MARKET + gsl[0]:Q_MARKET + gsl[1]].contiguous()
     del allf
     ev = pdist.ShardedEvaluator(qid, qcam, gid, gcam, rank, world)
+    if tune:
+        # distance-GEMM tile choice on this shard's shape (outside the timed runs)
+        from pps_amd import ops
+        qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
+        best = None
+        for t in range(1, ops.num_tiles() + 1):
+            ops.compute_dist(qa, g_local, tile=t)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.compute_dist(qa, g_local, tile=t)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            if best is None or ms < best[1]:
+                best = (t, ms)
+        pdist.HipBackend.distmat_tile = best[0]
+        del qa
     # warm-up
     res = ev.run(q_local, g_local)
     torch.cuda.synchronize()
@@ -99,11 +123,28 @@ def retrieval_stage(rank, world, reps):
         t_dist.append(res['t_distmat_ms'])
         t_rank.append(res['t_rank_ms'])
         t_total.append(res['t_total_ms'])
-    out = dict(distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
+    out = dict(distmat_tile=pdist.HipBackend.distmat_tile,
+               distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
                retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
                cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
                cmc10=float(res['cmc'][9]), G_local=gsl[1] - gsl[0])
     return out
+
+
+def _pmc_traffic(key, math, batch):
+    """HBM bytes per launch measured by rocprofv3 PMC passes of this bench
+    (scripts/pmc_traffic.py -> profiles/r01/pmc_traffic.json): FETCH_SIZE x 2
+    (gfx950 reports half of wide streaming reads) + WRITE_SIZE, per launch.
+    None unless the file was measured for the same math and batch."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = t.get(key)
+    if not e or e.get('math') != math or e.get('batch', batch) != batch:
+        return None
+    return e.get('bytes_per_launch')
 
 
 def conv_roofline(m, x):
@@ -119,11 +160,19 @@ def conv_roofline(m, x):
     for name, op, f, e0, e1 in timer:
         per[name] = (op, f, e0.elapsed_time(e1))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
-    return dict(bound='mfma', achieved=round(achieved, 2), peak=PEAK_FP32_MFMA_TFLOPS,
-                unit='TFLOP/s', frac=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                traffic=None, kernel='gemm_f32_kernel<*,EPI_CONV> (%d launches/forward)' % n_launch,
+    if m.math == 'x3':
+        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3_kernel<*> implicit-GEMM conv, f32 products as 6 '
+                                        'bf16 MFMA terms (%d launches/forward)' % n_launch)
+    else:
+        peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '
+                                               '(%d launches/forward)' % n_launch)
+    return dict(bound='mfma', achieved=round(achieved, 2), peak=round(peak, 1),
+                unit='TFLOP/s', frac=round(achieved / peak, 4),
+                traffic=_pmc_traffic('conv', m.math, x.shape[0]), kernel=kernel,
                 launches=n_launch, flops_per_forward=conv_flops,
-                avg_launch_us=round(conv_ms * 1e3 / n_launch, 2)), per
+                algorithmic_bytes_per_launch=round(m.bytes_per_forward() / n_launch),
+                avg_launch_us=round(conv_ms * 1e3 / n_launch, 2),
+                frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
 
 
 def cpu_baseline(blobs, dist_sample=True):
@@ -185,7 +234,12 @@ def main():
         m.forward(xbuf, out=feat)
 
     ops.preprocess_bgr(imgs, means, (H, W), xbuf)
-    if not args.no_autotune:
+    if args.tiles_file and os.path.exists(args.tiles_file):
+        with open(args.tiles_file) as f:
+            saved = json.load(f)
+        m.set_tiles(saved)
+        pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
+    elif not args.no_autotune:
         m.autotune(xbuf)   # per-layer tile choice, outside the timed region
 
     for _ in range(max(1, args.warmup)):
@@ -214,10 +268,16 @@ def main():
     value = world * B * args.steps / elapsed
 
     roof, per_layer = conv_roofline(m, xbuf)
-    ret = retrieval_stage(rank, world, args.dist_reps)
+    tiles_saved = bool(args.tiles_file and os.path.exists(args.tiles_file))
+    ret = retrieval_stage(rank, world, args.dist_reps,
+                          tune=not (args.no_autotune or tiles_saved))
+    if args.tiles_file and not tiles_saved and rank == 0:
+        with open(args.tiles_file, 'w') as f:
+            json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile']), f, indent=0)
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
     dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
+    dist_math = ops.default_math()
     # whole-job distmat GB/s: all ranks' shards / the slowest rank's time
     dist_ms_max = pdist.max_over_ranks(ret['distmat_ms'], world)
     total_bytes = (Q_MARKET + G_MARKET) * D_FEAT * 4 + Q_MARKET * G_MARKET * 4
@@ -238,11 +298,18 @@ def main():
         'retrieval_ms': round(ret['retrieval_ms'], 3),
         'mAP_synthetic': round(ret['mAP'], 6), 'cmc1_synthetic': round(ret['cmc1'], 6),
         'roofline': roof,
-        'roofline_distmat': dict(bound='mfma', achieved=round(dist_tflops, 2),
-                                 peak=PEAK_FP32_MFMA_TFLOPS, unit='TFLOP/s',
-                                 frac=round(dist_tflops / PEAK_FP32_MFMA_TFLOPS, 4),
-                                 hbm_GBps=round(dist_bytes / (ret['distmat_ms'] * 1e-3) / 1e9, 2),
-                                 traffic=None, kernel='gemm_f32_kernel<128,128,2,2,EPI_DIST>'),
+        'roofline_distmat': dict(
+            bound='mfma', achieved=round(dist_tflops, 2),
+            peak=round(PEAK_X3_TFLOPS if dist_math == 'x3' else PEAK_FP32_MFMA_TFLOPS, 1),
+            unit='TFLOP/s',
+            frac=round(dist_tflops / (PEAK_X3_TFLOPS if dist_math == 'x3'
+                                      else PEAK_FP32_MFMA_TFLOPS), 4),
+            hbm_GBps=round(dist_bytes / (ret['distmat_ms'] * 1e-3) / 1e9, 2),
+            traffic=_pmc_traffic('distmat', dist_math, Q_MARKET),
+            algorithmic_bytes_per_launch=dist_bytes,
+            kernel='%s EPI_DIST, tile %d (+ split/norm of the gallery shard)' % (
+                'gemm_x3_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
+                ret['distmat_tile'])),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(blobs)

@@ -64,10 +64,11 @@ def all_gather_rows(x, sizes):
 class HipBackend(object):
     """libpps_hip.so kernels (the product path)."""
     device = 'cuda'
+    distmat_tile = 0   # GEMM tile for the distance matrix (0 = heuristic; bench tunes it)
 
-    @staticmethod
-    def distmat(q, g, metric):
-        return ops.compute_dist(q, g, metric=metric)
+    @classmethod
+    def distmat(cls, q, g, metric):
+        return ops.compute_dist(q, g, metric=metric, tile=cls.distmat_tile)
 
     @staticmethod
     def collect(dist, qid, qcam, gid, gcam, g_offset, pmax):

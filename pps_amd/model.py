@@ -376,6 +376,26 @@ class PPSModel(object):
                 L['flops'] = 2.0 * N * len(L['prefixes']) * L['dim_inner'] * L['dim']
             else:
                 L['flops'] = 0.0
+        # algorithmic HBM bytes per launch: every operand read once, the output
+        # written once (f32 activations; weights in the format the GEMM reads)
+        wbytes = 6 if self.math == 'x3' else 4
+        for L in self.layers:
+            if L['op'] in ('conv', 'conv_dual'):
+                n, ho, wo, co = shapes[L['output']]
+                b = 4 * np.prod(shapes[L['input']]) + 4 * n * ho * wo * co
+                b += wbytes * co * (L['k'] * L['k'] * L['cin'] + L.get('shortcut_cin', 0))
+                if L.get('residual'):
+                    b += 4 * n * ho * wo * co
+                if L['op'] == 'conv_dual':
+                    b += 4 * np.prod(shapes[L['input2']])
+                L['bytes'] = float(b)
+            elif L['op'] == 'heads':
+                nb = len(L['prefixes'])
+                L['bytes'] = float(4 * np.prod(shapes[L['input']]) +
+                                   wbytes * nb * L['dim_inner'] * L['dim'] +
+                                   4 * HEAD_SPLITK * N * nb * L['dim_inner'])
+            else:
+                L['bytes'] = 0.0
         self._bufs = {k: torch.empty(v, dtype=torch.float32, device=self.device)
                       for k, v in shapes.items() if k != 'data'}
         self._batch = (N, H, W)
@@ -385,6 +405,10 @@ class PPSModel(object):
 
     def flops_per_forward(self, kinds=('conv', 'conv_dual', 'heads')):
         return sum(L['flops'] for L in self.layers if L['op'] in kinds)
+
+    def bytes_per_forward(self, kinds=('conv', 'conv_dual', 'heads')):
+        """Algorithmic HBM bytes of the GEMM launches of one forward."""
+        return sum(L['bytes'] for L in self.layers if L['op'] in kinds)
 
     def _run(self, L, bufs, out=None, tile=None):
         op = L['op']
@@ -467,3 +491,15 @@ class PPSModel(object):
             L['tile'] = min(times, key=times.get)
             report[L.get('name', L['output'])] = (L['tile'], times)
         return report
+
+    def tiles(self):
+        """{layer name: tile id} of the GEMM layers (0 = heuristic)."""
+        return {L.get('name', L['output']): int(L.get('tile', 0)) for L in self.layers
+                if L['op'] in ('conv', 'conv_dual', 'heads')}
+
+    def set_tiles(self, tiles):
+        """Apply a tiles() mapping (e.g. a saved autotune result)."""
+        for L in self.layers:
+            k = L.get('name', L['output'])
+            if k in tiles:
+                L['tile'] = int(tiles[k])

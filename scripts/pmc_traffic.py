@@ -1,0 +1,57 @@
+"""HBM traffic per launch of the bench's dominant kernels from two rocprofv3
+PMC passes (FETCH_SIZE, WRITE_SIZE; separate passes, --kernel-trace only):
+
+  rocprofv3 --kernel-trace --pmc FETCH_SIZE -d <dir>/p1 -o run --output-format csv -- python3 bench.py ...
+  rocprofv3 --kernel-trace --pmc WRITE_SIZE -d <dir>/p2 -o run --output-format csv -- python3 bench.py ...
+  python scripts/pmc_traffic.py <dir> <math> <batch> <launches per forward> > profiles/rNN/pmc_traffic.json
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE (KB) counts half of
+the bytes of wide streaming reads -> x2; WRITE_SIZE (KB) is exact for 16-B
+stores.  Infinity-Cache hits are counted too, so this is memory-side
+traffic, an upper bound on HBM bytes.  conv = the last forward's implicit-GEMM
+launches (the bench's conv_roofline forward); distmat = the last EPI_DIST launch.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(path, counter):
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        if r['Counter_Name'] != counter:
+            continue
+        rows[int(r['Dispatch_Id'])] = (r['Kernel_Name'], float(r['Counter_Value']))
+    return [rows[k] for k in sorted(rows)]
+
+
+def epi_of(name):
+    args = name.split('<', 1)[1].split('>', 1)[0].split(',')
+    return int(args[4])
+
+
+def main():
+    d, math, batch, nconv = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    fetch = load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0], 'FETCH_SIZE')
+    write = load(glob.glob(os.path.join(d, 'p2', '*counter_collection.csv'))[0], 'WRITE_SIZE')
+    kname = 'gemm_x3_kernel' if math == 'x3' else 'gemm_f32_kernel'
+    out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
+                      'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
+    for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):
+        f = [v for nm, v in fetch if kname in nm and sel(epi_of(nm))][-n:]
+        w = [v for nm, v in write if kname in nm and sel(epi_of(nm))][-n:]
+        if len(f) < n or len(w) < n:
+            continue
+        fb = 2 * 1024 * sum(f)
+        wb = 1024 * sum(w)
+        out[key] = dict(math=math, launches=n, fetch_bytes=fb, write_bytes=wb,
+                        bytes_per_launch=round((fb + wb) / n))
+        if key == 'conv':
+            out[key]['batch'] = batch
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main()
