@@ -48,7 +48,9 @@ const char* pps_registered_ops(void);
  * 1 = 128x128 (4 waves), 2 = 128x64, 3 = 64x128, 4 = 64x64, 5 = 256x128
  * (8 waves), 6..10 = the same shapes with a 32-wide K chunk per barrier,
  * 11..20 = ids 1..10 with the `_x3` kernels' A operand kept f32 in LDS and
- * split after the fragment read (the f32 kernels treat them as 1..10).  Results are identical for every tile (same per-element fp32
+ * split after the fragment read (the f32 kernels treat them as 1..10),
+ * 21..28 = 192-row tiles of the `_x3` kernels (192x128 / 192x64, K chunk
+ * 16 / 32, A staged as planes / f32; the f32 kernels use 128-row tiles).  Results are identical for every tile (same per-element fp32
  * MFMA accumulation order); only speed differs, so callers may autotune. */
 int pps_gemm_num_tiles(void);
 

@@ -276,7 +276,12 @@ int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   int tile = p.tile ? p.tile : pick_tile(p, batch);
   // ids 11..20 select a bf16x3 staging variant (gemm_x3.hip); the f32 kernel
   // has one variant per shape
-  if (tile > GEMM_TILE_256x128_K32 && tile < GEMM_NUM_TILES) tile -= GEMM_TILE_256x128_K32;
+  if (tile >= GEMM_TILE_192_FIRST && tile < GEMM_NUM_TILES) {
+    const int v = tile - GEMM_TILE_192_FIRST;  // 192-row shapes -> nearest f32 shape
+    tile = (v & 1) ? ((v & 2) ? GEMM_TILE_128x64_K32 : GEMM_TILE_128x64)
+                   : ((v & 2) ? GEMM_TILE_128x128_K32 : GEMM_TILE_128x128);
+  }
+  if (tile > GEMM_TILE_256x128_K32 && tile < GEMM_TILE_192_FIRST) tile -= GEMM_TILE_256x128_K32;
   // BK=32 needs the dual operand switch on a 32-chunk boundary and, for
   // narrow inputs (Cin < 32), a power-of-two channel count
   if (tile > GEMM_TILE_256x128) {

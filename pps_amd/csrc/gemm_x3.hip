@@ -334,16 +334,26 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.a2) epi |= EPI_F_DUAL;
   }
   int tile = p.tile ? p.tile : pick_tile(p, batch);
+  const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
+  const bool dual_ok = !p.a2 || p.Kloop1 % 32 == 0;
+  if (tile >= GEMM_TILE_192_FIRST && tile < GEMM_NUM_TILES) {
+    // 192-row family (M = 12,288 / 49,152 / 196,608 at batch 64 are
+    // multiples of 192: fills 256 CUs without a partial last wave of tiles)
+    const int v = tile - GEMM_TILE_192_FIRST;
+    const bool af = v >= 4;
+    const bool k32 = (v & 2) && narrow_ok && dual_ok;
+    if (v & 1)
+      return k32 ? launch_tile_x3<192, 64, 2, 2, 32>(p, epi, batch, stream, af)
+                 : launch_tile_x3<192, 64, 2, 2, 16>(p, epi, batch, stream, af);
+    return k32 ? launch_tile_x3<192, 128, 2, 2, 32>(p, epi, batch, stream, af)
+               : launch_tile_x3<192, 128, 2, 2, 16>(p, epi, batch, stream, af);
+  }
   // ids 11..20: the same shapes with A kept f32 in LDS and split after the
   // fragment read (AF32); 1..10 split A while staging (three bf16 planes)
   const bool af32 = tile > GEMM_TILE_256x128_K32;
   if (af32) tile -= GEMM_TILE_256x128_K32;
   if (tile == GEMM_TILE_256x128_K32) tile = GEMM_TILE_256x128;  // 184 KB of LDS: no
-  if (tile > GEMM_TILE_256x128) {
-    const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
-    const bool dual_ok = !p.a2 || p.Kloop1 % 32 == 0;
-    if (!narrow_ok || !dual_ok) tile -= 5;
-  }
+  if (tile > GEMM_TILE_256x128 && (!narrow_ok || !dual_ok)) tile -= 5;
   switch (tile) {
     case GEMM_TILE_128x128: return launch_tile_x3<128, 128, 2, 2, 16>(p, epi, batch, stream, af32);
     case GEMM_TILE_128x64: return launch_tile_x3<128, 64, 4, 1, 16>(p, epi, batch, stream, af32);

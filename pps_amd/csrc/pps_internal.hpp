@@ -51,7 +51,10 @@ enum GemmTile {
   GEMM_TILE_64x64_K32 = 9,
   GEMM_TILE_256x128_K32 = 10,
   // 11..20: ids 1..10 with the bf16x3 kernel's A operand kept f32 in LDS
-  GEMM_NUM_TILES = 21
+  // 21..28 (bf16x3 kernel): 192x128 K16, 192x64 K16, 192x128 K32, 192x64 K32,
+  // then the same four with A kept f32 in LDS
+  GEMM_TILE_192_FIRST = 21,
+  GEMM_NUM_TILES = 29
 };
 
 struct GemmParams {

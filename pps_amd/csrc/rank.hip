@@ -15,6 +15,9 @@ constexpr int kEvalThreads = 256;
 constexpr int kPosCap = 2048;  // max merged positives per query in LDS
 
 // ---- 1) collect positives ------------------------------------------------------
+// One block per query; wave w scans its own contiguous quarter of the gallery
+// twice (count, then write at its offset), compacting with ballots -- no block
+// barrier inside the scan.  The list keeps ascending gallery order.
 __global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t G,
                                          int64_t ldd, const int32_t* __restrict__ qid,
                                          const int32_t* __restrict__ qcam,
@@ -28,30 +31,40 @@ __global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t
   const int qi = qid[q], qc = qcam[q];
   const float* row = dist + q * ldd;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ int wtot[kEvalThreads / 64];
-  int base = 0;
-  for (int64_t t0 = 0; t0 < G; t0 += kEvalThreads) {
-    const int64_t i = t0 + threadIdx.x;
-    const bool flag = i < G && gid[i] == qi && gcam[i] != qc;
-    const unsigned long long bal = __ballot(flag);
-    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wtot[wave] = __popcll(bal);
-    __syncthreads();
-    int wbase = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kEvalThreads / 64; ++w) {
-      wbase += (w < wave) ? wtot[w] : 0;
-      tot += wtot[w];
-    }
-    const int slot = base + wbase + pre;
-    if (flag && slot < Pmax) {
-      pos_d[q * Pmax + slot] = row[i];
-      pos_idx[q * Pmax + slot] = (int32_t)(g_offset + i);
-    }
-    base += tot;
-    __syncthreads();
+  constexpr int W = kEvalThreads / 64;
+  __shared__ int wtot[W];
+  const int64_t chunk = ((G + W - 1) / W + 63) / 64 * 64;
+  const int64_t beg = wave * chunk;
+  const int64_t end = beg + chunk < G ? beg + chunk : G;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int cnt = 0;
+  for (int64_t t0 = beg; t0 < end; t0 += 64) {
+    const int64_t i = t0 + lane;
+    const bool flag = i < end && gid[i] == qi && gcam[i] != qc;
+    cnt += __popcll(__ballot(flag));
   }
-  if (threadIdx.x == 0) pos_cnt[q] = base;
+  if (lane == 0) wtot[wave] = cnt;
+  __syncthreads();
+  int slot = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    slot += w < wave ? wtot[w] : 0;
+    total += wtot[w];
+  }
+  if (slot < Pmax && cnt > 0) {
+    for (int64_t t0 = beg; t0 < end; t0 += 64) {
+      const int64_t i = t0 + lane;
+      const bool flag = i < end && gid[i] == qi && gcam[i] != qc;
+      const unsigned long long bal = __ballot(flag);
+      const int s = slot + __popcll(bal & below);
+      if (flag && s < Pmax) {
+        pos_d[q * Pmax + s] = row[i];
+        pos_idx[q * Pmax + s] = (int32_t)(g_offset + i);
+      }
+      slot += __popcll(bal);
+    }
+  }
+  if (threadIdx.x == 0) pos_cnt[q] = total;
 }
 
 int collect_positives(const float* dist, int64_t Q, int64_t G, int64_t ldd,
@@ -135,9 +148,13 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
   const float* row = dist + q * ldd;
   int nbefore = 0;
   if (P > 0) {
-    for (int64_t i = threadIdx.x; i < G; i += blockDim.x) {
-      if (gid[i] == qi && gcam[i] == qc) continue;  // junk: same id, same cam
-      const float d = row[i];
+    // Entries farther than the farthest positive change neither the histogram
+    // (their bin would be P) nor the first-match count, so the common path
+    // reads only the distance; ids/cams are fetched for the few closer ones.
+    const float dmax = sd[P - 1];
+    auto visit = [&](int64_t i, float d) {
+      if (d > dmax) return;
+      if (gid[i] == qi && gcam[i] == qc) return;  // junk: same id, same cam
       int lo = 0, hi = P;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -145,6 +162,21 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
       }
       if (lo < P) atomicAdd(&hs[lo], 1);
       nbefore += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
+    };
+    constexpr int U = 4;  // independent row loads in flight per thread
+    const int64_t step = (int64_t)blockDim.x * U;
+    for (int64_t i0 = threadIdx.x; i0 < G; i0 += step) {
+      float d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * blockDim.x;
+        d[u] = i < G ? row[i] : INFINITY;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * blockDim.x;
+        if (i < G) visit(i, d[u]);
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) nbefore += __shfl_xor(nbefore, o);

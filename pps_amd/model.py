@@ -462,33 +462,39 @@ class PPSModel(object):
                 timer.append((L.get('name', L['output']), L['op'], L['flops'], ev0, ev1))
         return bufs[self.plan.output]
 
-    def autotune(self, x, reps=3, tiles=None):
+    def autotune(self, x, reps=3, tiles=None, finalists=4, final_reps=10):
         """Pick the fastest GEMM tile per conv layer by timing every candidate
         on this device (the cudnn_exhaustive_search analogue of the
-        reference's DetectionModelHelper, detector.py:58).  Results do not
-        depend on the tile (same per-element accumulation order)."""
+        reference's DetectionModelHelper, detector.py:58): a screening pass
+        over all tiles, then the `finalists` best re-timed with `final_reps`
+        launches each.  Results do not depend on the tile (same per-element
+        accumulation order)."""
         self.forward(x)
         torch.cuda.synchronize()
         bufs = dict(self._bufs)
         bufs['data'] = x
         cands = list(tiles or range(1, ops.num_tiles() + 1))
+
+        def time_tile(L, t, n):
+            for _ in range(2):
+                self._run(L, bufs, tile=t)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                self._run(L, bufs, tile=t)
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) / n
+
         report = {}
         for L in self.layers:
             if L['op'] not in ('conv', 'conv_dual', 'heads'):
                 continue
-            times = {}
-            for t in cands:
-                for _ in range(2):
-                    self._run(L, bufs, tile=t)
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(reps):
-                    self._run(L, bufs, tile=t)
-                e1.record()
-                e1.synchronize()
-                times[t] = e0.elapsed_time(e1) / reps
-            L['tile'] = min(times, key=times.get)
+            times = {t: time_tile(L, t, reps) for t in cands}
+            best = sorted(times, key=times.get)[:finalists]
+            final = {t: time_tile(L, t, final_reps) for t in best}
+            L['tile'] = min(final, key=final.get)
             report[L.get('name', L['output'])] = (L['tile'], times)
         return report
 
