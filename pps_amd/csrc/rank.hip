@@ -7,7 +7,7 @@
 // distances -- one streaming read of the distance row, no sort.  The result
 // equals a stable (distance, gallery index) sort; counts are additive over
 // gallery shards, which is what the multi-GPU path all-reduces.
-#include "pps_internal.hpp"
+#include "gemm_common.hpp"
 
 namespace pps {
 
@@ -165,13 +165,14 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
     };
     constexpr int U = 4;  // independent row loads in flight per thread
     const int64_t step = (int64_t)blockDim.x * U;
+    // buffer loads (tail reads zero without a branch; visit() skips it)
+    const rsrc_t rrow = make_rsrc(row, (uint32_t)(G * 4));
     for (int64_t i0 = threadIdx.x; i0 < G; i0 += step) {
       float d[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t i = i0 + (int64_t)u * blockDim.x;
-        d[u] = i < G ? row[i] : INFINITY;
-      }
+      for (int u = 0; u < U; ++u)
+        d[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rrow, (int)((i0 + (int64_t)u * blockDim.x) * 4), 0, 0));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * blockDim.x;
@@ -274,92 +275,98 @@ __device__ inline float key_float(uint32_t k) {
 }
 
 constexpr int kTopkThreads = 256;
-constexpr int kTopkCap = 1024;
+constexpr int kTopkCap = 1024;      // max k
+constexpr int kTopkBuf = 4096;      // candidate buffer (64-bit entries) in LDS
+constexpr int kTopkUnroll = 8;      // row elements per thread per chunk
+static_assert(kTopkCap + kTopkThreads * kTopkUnroll <= kTopkBuf,
+              "a cut buffer plus one chunk must fit");
 
-__global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
-                            float* __restrict__ vals, int32_t* __restrict__ idx) {
-  const int64_t q = blockIdx.x;
-  const float* row = dist + q * ldd;
-  __shared__ int hist[256];
-  __shared__ uint32_t s_prefix;
-  __shared__ int s_rem;
-  __shared__ unsigned long long cand[kTopkCap];
-  __shared__ int wtot[kTopkThreads / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t prefix = 0, pmask = 0;
-  int rem = k;  // rank (1-based) of K* among entries matching the prefix
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
-    __syncthreads();
-    for (int64_t i = threadIdx.x; i < G; i += blockDim.x) {
-      const uint32_t key = float_key(row[i]);
-      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int c = 0, b = 0;
-      for (; b < 256; ++b) {
-        if (c + hist[b] >= rem) break;
-        c += hist[b];
-      }
-      s_prefix = prefix | ((uint32_t)b << shift);
-      s_rem = rem - c;
-    }
-    __syncthreads();
-    prefix = s_prefix;
-    rem = s_rem;
-    pmask |= 255u << shift;
-    __syncthreads();
-  }
-  const uint32_t kstar = prefix;  // k-th smallest key; `rem` of its ties are kept
-  // ordered compaction: key < K* (any order) and the first `rem` ties by index
-  int nless = 0, nties = 0;
-  for (int64_t t0 = 0; t0 < G; t0 += blockDim.x) {
-    const int64_t i = t0 + threadIdx.x;
-    uint32_t key = 0;
-    bool less = false, tie = false;
-    if (i < G) {
-      key = float_key(row[i]);
-      less = key < kstar;
-      tie = key == kstar;
-    }
-    const unsigned long long bl = __ballot(less), bt = __ballot(tie);
-    const int pl = __popcll(bl & ((1ull << lane) - 1ull));
-    const int pt = __popcll(bt & ((1ull << lane) - 1ull));
-    if (lane == 0) wtot[wave] = (__popcll(bl) << 16) | __popcll(bt);
-    __syncthreads();
-    int bl_off = 0, bt_off = 0, tl = 0, tt = 0;
-    for (int w = 0; w < kTopkThreads / 64; ++w) {
-      const int v = wtot[w];
-      if (w < wave) { bl_off += v >> 16; bt_off += v & 0xffff; }
-      tl += v >> 16;
-      tt += v & 0xffff;
-    }
-    const unsigned long long packed = ((unsigned long long)key << 32) | (uint32_t)i;
-    if (less) cand[nless + bl_off + pl] = packed;
-    const int tslot = nties + bt_off + pt;
-    if (tie && tslot < rem) cand[(k - rem) + tslot] = packed;
-    nless += tl;
-    nties += tt;
-    __syncthreads();
-  }
-  // bitonic sort of k candidates (padded to a power of two with +inf keys)
-  int n2 = 1;
-  while (n2 < k) n2 <<= 1;
-  for (int i = threadIdx.x + k; i < n2; i += blockDim.x) cand[i] = ~0ull;
-  __syncthreads();
+// Bitonic sort (ascending) of buf[0, n2), n2 a power of two, by the block.
+__device__ inline void block_bitonic(unsigned long long* buf, int n2) {
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
         const int i = 2 * stride * (t / stride) + (t % stride);
         const int j = i + stride;
         const bool up = (i & size) == 0;
-        const unsigned long long a = cand[i], b = cand[j];
-        if ((a > b) == up) { cand[i] = b; cand[j] = a; }
+        const unsigned long long a = buf[i], b = buf[j];
+        if ((a > b) == up) { buf[i] = b; buf[j] = a; }
       }
       __syncthreads();
     }
   }
+}
+
+// One pass over the row.  Entries are packed as (order-preserving key << 32 |
+// index), so comparing packed values is the stable (distance, index) order.
+// An entry enters the LDS candidate buffer only if it beats the current
+// threshold = the k-th best packed value among the candidates kept so far;
+// when the buffer could overflow in the next chunk it is sorted and cut back
+// to its k best (rare after the first chunks: ~k*ln(G/k) insertions per row).
+__global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
+                            float* __restrict__ vals, int32_t* __restrict__ idx) {
+  const int64_t q = blockIdx.x;
+  const float* row = dist + q * ldd;
+  __shared__ unsigned long long cand[kTopkBuf];
+  __shared__ int s_n;
+  __shared__ unsigned long long s_thr;
+  if (threadIdx.x == 0) { s_n = 0; s_thr = ~0ull; }
+  __syncthreads();
+  const int64_t chunk = (int64_t)blockDim.x * kTopkUnroll;
+  auto cut = [&](int n) {  // sort the n candidates, keep the k best
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int i = n + threadIdx.x; i < n2; i += blockDim.x) cand[i] = ~0ull;
+    __syncthreads();
+    block_bitonic(cand, n2);
+    if (threadIdx.x == 0) {
+      s_n = n < k ? n : k;
+      s_thr = n >= k ? cand[k - 1] : ~0ull;
+    }
+    __syncthreads();
+  };
+  // the next chunk's row values are requested before this chunk is
+  // processed; the chunk-closing barrier is a raw s_barrier after an LDS-only
+  // wait, so those loads stay in flight across it (__syncthreads() would
+  // drain them with vmcnt(0))
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  // buffer loads: the row tail past G reads zero without exec-mask branches,
+  // which keeps the loads countable (a branchy guard makes hipcc wait vmcnt(0))
+  const rsrc_t rrow = make_rsrc(row, (uint32_t)(G * 4));
+  auto ld = [&](int64_t i) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rrow, (int)(i * 4), 0, 0));
+  };
+  float d[kTopkUnroll];
+#pragma unroll
+  for (int u = 0; u < kTopkUnroll; ++u) d[u] = ld((int64_t)u * blockDim.x + threadIdx.x);
+  for (int64_t c0 = 0; c0 < G; c0 += chunk) {
+    if (s_n + chunk > kTopkBuf) cut(s_n);  // uniform: s_n read after a barrier
+    const unsigned long long thr = s_thr;
+    float dn[kTopkUnroll];
+#pragma unroll
+    for (int u = 0; u < kTopkUnroll; ++u)
+      dn[u] = ld(c0 + chunk + (int64_t)u * blockDim.x + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < kTopkUnroll; ++u) {
+      const int64_t i = c0 + (int64_t)u * blockDim.x + threadIdx.x;
+      const unsigned long long packed =
+          ((unsigned long long)float_key(d[u]) << 32) | (uint32_t)i;
+      const bool take = i < G && packed < thr;
+      const unsigned long long bal = __ballot(take);  // one LDS atomic per wave
+      if (bal) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_n, __popcll(bal));
+        base = __shfl(base, 0);
+        if (take) cand[base + __popcll(bal & below)] = packed;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kTopkUnroll; ++u) d[u] = dn[u];
+    lds_barrier();
+  }
+  cut(s_n);
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const unsigned long long v = cand[i];
     vals[q * k + i] = key_float((uint32_t)(v >> 32));

@@ -1,0 +1,74 @@
+"""BASELINE.json configs[2] on one GPU: DukeMTMC-reID sizes (Q=2228, G=17661,
+D=3968) -- cosine distance matrix + k-reciprocal
+re-ranking (k1=20, k2=6, lambda=0.3; reid_dataset_evaluator.py:442-519) +
+mAP/CMC on the re-ranked distances.  Synthetic features of the §8(d)
+distribution (750-identity centroids + noise, L2-normalised, seed 0).
+
+  python scripts/bench_duke_rerank.py [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+Q, G, D = 2228, 17661, 3968
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reps', type=int, default=3)
+    a = ap.parse_args()
+    from pps_amd import ops
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(0)
+    qid = rng.randint(1, 703, Q)
+    gid = rng.randint(1, 703, G)
+    qcam = rng.randint(1, 9, Q)
+    gcam = rng.randint(1, 9, G)
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(0)
+    cent = torch.randn((703, D), generator=gen, device='cuda')
+    ids = torch.from_numpy(np.concatenate([qid, gid])).cuda()
+    x = cent[ids] + 4.0 * torch.randn((Q + G, D), generator=gen, device='cuda')
+    x = x / x.norm(dim=1, keepdim=True)
+    qf, gf = x[:Q].contiguous(), x[Q:].contiguous()
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    times = {}
+    for rep in range(a.reps + 1):
+        e = [ev() for _ in range(5)]
+        e[0].record()
+        q_g = ops.compute_dist(qf, gf, metric='cosine')
+        e[1].record()
+        q_q = ops.compute_dist(qf, qf, metric='cosine')
+        g_g = ops.compute_dist(gf, gf, metric='cosine')
+        e[2].record()
+        rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+        e[3].record()
+        res = gev.rank_eval(rr, qid, gid, qcam, gcam)
+        e[4].record()
+        torch.cuda.synchronize()
+        if rep:
+            for k, (s, t) in dict(q_g_ms=(0, 1), q_q_g_g_ms=(1, 2), rerank_ms=(2, 3),
+                                  rank_eval_ms=(3, 4), total_ms=(0, 4)).items():
+                times.setdefault(k, []).append(e[s].elapsed_time(e[t]))
+    mAP, cmc = gev.scores_from_ranks(*res)
+    mAP0, cmc0 = gev.scores_from_ranks(*gev.rank_eval(q_g, qid, gid, qcam, gcam))
+    out = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
+    out.update(config='Duke sizes Q=%d G=%d D=%d cosine + re-ranking (k1=20,k2=6,l=0.3), '
+                      'synthetic features' % (Q, G, D),
+               math=ops.default_math(), mAP_plain=round(mAP0, 6), cmc1_plain=round(float(cmc0[0]), 6),
+               mAP_reranked=round(mAP, 6), cmc1_reranked=round(float(cmc[0]), 6),
+               gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
