@@ -9,7 +9,7 @@ LIB := pps_amd/libpps_hip.so
 
 all: $(LIB)
 
-build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp pps_amd/csrc/gemm_common.hpp include/pps_abi.h
+build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp pps_amd/csrc/gemm_common.hpp pps_amd/csrc/gemm_x3_common.hpp include/pps_abi.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

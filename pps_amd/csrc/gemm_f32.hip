@@ -274,6 +274,7 @@ int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream) {
     if (p.a2) epi |= EPI_F_DUAL;
   }
   int tile = p.tile ? p.tile : pick_tile(p, batch);
+  if (tile >= GEMM_TILE_P_FIRST) tile = GEMM_TILE_128x128;  // pipelined ids: bf16x3 only
   // ids 11..20 select a bf16x3 staging variant (gemm_x3.hip); the f32 kernel
   // has one variant per shape
   if (tile >= GEMM_TILE_192_FIRST && tile < GEMM_NUM_TILES) {

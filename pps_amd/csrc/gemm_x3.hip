@@ -22,74 +22,9 @@
 //   distinct 16-byte slots per 16-lane group, i.e. no bank conflicts.
 // * K order is fixed (16-groups ascending, the six terms in the order above)
 //   for every tile and BK, so all tile variants give identical bits.
-#include "gemm_common.hpp"
+#include "gemm_x3_common.hpp"
 
 namespace pps {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Two floats -> three packed bf16 pairs with x = hi + mid + lo exactly
-// (round-to-nearest-even splits; each remainder is exact in f32).
-__device__ inline void split2(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
-  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
-  const float r0 = x0 - __builtin_bit_cast(float, u << 16);
-  const float r1 = x1 - __builtin_bit_cast(float, u & 0xffff0000u);
-  const unsigned v = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
-  const float s0 = r0 - __builtin_bit_cast(float, v << 16);
-  const float s1 = r1 - __builtin_bit_cast(float, v & 0xffff0000u);
-  hi = u;
-  mid = v;
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){s0, s1}, bf16x2));
-}
-
-__device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// Distance epilogue from precomputed squared row norms (pps_row_sqnorm):
-//   sqeuclid = (-2 q.g + |q|^2) + |g|^2 clamped at 0 [sqrt]; cosine = 1 - q.g/(|q||g|)
-template <int BM, int BN, int WM, int WN>
-__device__ inline void dist_epilogue(const GemmParams& p,
-                                     f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0,
-                                     int wm, int wn, int r32, int h) {
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
-  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
-  const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0;
-  const int nrem = p.Ncol - n0;
-  const float* qsq = p.norm_a + m0;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int c = wn * (BN / WN) + j * 32 + r32;
-    if (c >= nrem) continue;
-    const float gn = p.norm_b[n0 + c];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rb = wm * (BM / WM) + i * 32 + 4 * h;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = rb + (r & 3) + 8 * (r >> 2);
-        if (rr < mrem) {
-          const float dot = acc[i][j][r];
-          const float qn = qsq[rr];
-          float v;
-          if (p.metric == PPS_METRIC_COSINE) {
-            const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
-            v = 1.f - dot / den;
-          } else {
-            v = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
-            if (p.metric == PPS_METRIC_EUCLIDEAN) v = sqrtf(v);
-          }
-          if (p.zero_diag && m0 + rr == n0 + c) v = 0.f;
-          out[rr * ldo + c] = v;
-        }
-      }
-    }
-  }
-}
 
 template <int BM, int BN, int WM, int WN, int EPI, int BK, bool AF32>
 __global__ void __launch_bounds__(64 * WM * WN)
@@ -334,9 +269,15 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.a2) epi |= EPI_F_DUAL;
   }
   int tile = p.tile ? p.tile : pick_tile(p, batch);
+  if (tile >= GEMM_TILE_P_FIRST) {
+    // LDS-DMA pipelined family (gemm_x3p.hip); shapes it cannot stage
+    // (Cin % 32 != 0, unaligned rows) take the heuristic register-staged tile
+    if (x3p_eligible(p, epi)) return launch_gemm_x3p(p, epi, batch, stream, tile - GEMM_TILE_P_FIRST);
+    tile = pick_tile(p, batch);
+  }
   const bool narrow_ok = p.Cin >= 32 || (p.Cin & (p.Cin - 1)) == 0;
   const bool dual_ok = !p.a2 || p.Kloop1 % 32 == 0;
-  if (tile >= GEMM_TILE_192_FIRST && tile < GEMM_NUM_TILES) {
+  if (tile >= GEMM_TILE_192_FIRST && tile < GEMM_TILE_P_FIRST) {
     // 192-row family (M = 12,288 / 49,152 / 196,608 at batch 64 are
     // multiples of 192: fills 256 CUs without a partial last wave of tiles)
     const int v = tile - GEMM_TILE_192_FIRST;

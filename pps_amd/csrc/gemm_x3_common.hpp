@@ -1,0 +1,102 @@
+// Pieces shared by the two bf16x3 GEMM kernels (gemm_x3.hip: register-staged;
+// gemm_x3p.hip: LDS-DMA pipelined): the exact three-way bf16 split, the MFMA
+// wrapper and the distance epilogue.  Both kernels apply the six product
+// terms in the same order on the same 16-wide K groups, so they give
+// identical bits.
+#pragma once
+#include "gemm_common.hpp"
+
+namespace pps {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Two floats -> three packed bf16 pairs with x = hi + mid + lo exactly
+// (round-to-nearest-even splits; each remainder is exact in f32).
+__device__ inline void split2(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, u << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, u & 0xffff0000u);
+  const unsigned v = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
+  const float s0 = r0 - __builtin_bit_cast(float, v << 16);
+  const float s1 = r1 - __builtin_bit_cast(float, v & 0xffff0000u);
+  hi = u;
+  mid = v;
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){s0, s1}, bf16x2));
+}
+
+// Eight consecutive-K floats -> the three bf16x8 MFMA fragments.
+__device__ inline void split8(const f32x4& x0, const f32x4& x1, bf16x8& fhi, bf16x8& fmid,
+                              bf16x8& flo) {
+  u32x4 hi, mid, lo;
+  unsigned a, b, c;
+  split2(x0[0], x0[1], a, b, c); hi[0] = a; mid[0] = b; lo[0] = c;
+  split2(x0[2], x0[3], a, b, c); hi[1] = a; mid[1] = b; lo[1] = c;
+  split2(x1[0], x1[1], a, b, c); hi[2] = a; mid[2] = b; lo[2] = c;
+  split2(x1[2], x1[3], a, b, c); hi[3] = a; mid[3] = b; lo[3] = c;
+  fhi = __builtin_bit_cast(bf16x8, hi);
+  fmid = __builtin_bit_cast(bf16x8, mid);
+  flo = __builtin_bit_cast(bf16x8, lo);
+}
+
+__device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// The six product terms of one (A, B) fragment pair, fixed order:
+//   a0b0 + a1b0 + a0b1 + a2b0 + a1b1 + a0b2
+__device__ inline f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mfma_bf16(a[0], b[0], c);
+  c = mfma_bf16(a[1], b[0], c);
+  c = mfma_bf16(a[0], b[1], c);
+  c = mfma_bf16(a[2], b[0], c);
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[0], b[2], c);
+  return c;
+}
+
+// Distance epilogue from precomputed squared row norms (pps_row_sqnorm):
+//   sqeuclid = (-2 q.g + |q|^2) + |g|^2 clamped at 0 [sqrt]; cosine = 1 - q.g/(|q||g|)
+template <int BM, int BN, int WM, int WN>
+__device__ inline void dist_epilogue(const GemmParams& p,
+                                     f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0,
+                                     int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;
+  const int nrem = p.Ncol - n0;
+  const float* qsq = p.norm_a + m0;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = wn * (BN / WN) + j * 32 + r32;
+    if (c >= nrem) continue;
+    const float gn = p.norm_b[n0 + c];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wm * (BM / WM) + i * 32 + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = rb + (r & 3) + 8 * (r >> 2);
+        if (rr < mrem) {
+          const float dot = acc[i][j][r];
+          const float qn = qsq[rr];
+          float v;
+          if (p.metric == PPS_METRIC_COSINE) {
+            const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
+            v = 1.f - dot / den;
+          } else {
+            v = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
+            if (p.metric == PPS_METRIC_EUCLIDEAN) v = sqrtf(v);
+          }
+          if (p.zero_diag && m0 + rr == n0 + c) v = 0.f;
+          out[rr * ldo + c] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace pps

@@ -1,0 +1,470 @@
+// Pipelined bf16x3 GEMM for gfx950: the arithmetic of gemm_x3.hip (f32
+// operands split exactly into three bf16 terms, six MFMA terms per product,
+// same 16-wide K groups in the same order -> identical bits), restructured
+// around LDS-DMA so that several K chunks are in flight while one is
+// multiplied:
+//
+// * both operands travel global -> LDS by `buffer_load_dwordx4 ... lds`
+//   (16 B per lane, no VGPR staging, no ds_write): A as f32 rows (split into
+//   bf16 terms after the fragment read), B as the three bf16 weight planes;
+//   out-of-range taps / rows / K read zero in hardware (buffer bounds);
+// * NS LDS stages: chunk kc+NS-1 is requested right after the barrier that
+//   opens chunk kc, so up to NS-1 chunks are in flight.  The wait before the
+//   barrier is a COUNTED vmcnt and the barrier a raw s_barrier (a
+//   __syncthreads() would drain the DMA queue);
+// * the DMA image is lane-linear (LDS address = wave base + 16 * lane), so
+//   the bank-conflict swizzle goes on the per-lane SOURCE address and is
+//   undone on the fragment read: A rows (128 B) keep 16-byte chunk c in slot
+//   c ^ ((row >> 1) & 7), B rows (64 B) in slot c ^ ((row >> 2) & 3) -- each
+//   ds_read_b128 lane group then hits 16 distinct 16-byte slots;
+// * K chunk 32 and Cin % 32 == 0, so a chunk never straddles two im2col taps:
+//   the tap tracker is wave-uniform (scalar) and each lane keeps only a row
+//   base and a 64-bit tap-validity mask per DMA piece.
+#include "gemm_x3_common.hpp"
+
+namespace pps {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// One DMA piece: lane l's 16 bytes at buffer offset voff land at
+// lds_dst + 16 * l (lds_dst wave-uniform -> M0).
+__device__ inline void glds16(rsrc_t r, const unsigned char* lds_dst, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(uintptr_t)lds_dst, 16, voff, 0, 0,
+                                           0);
+}
+
+template <int N>
+__device__ inline void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// The six terms with the MFMA operands swapped (weights as the MFMA "A"):
+// the accumulator then holds the TRANSPOSED 32x32 block, i.e. lane l keeps
+// output row (l & 31) and, in register r = 4q + e, output column
+// 8q + 4(l >> 5) + e -- four consecutive columns per q, so the epilogue
+// moves 16-byte vectors (4 stores per block instead of 16).  Same products,
+// same term order.
+__device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mfma_bf16(b[0], a[0], c);
+  c = mfma_bf16(b[0], a[1], c);
+  c = mfma_bf16(b[1], a[0], c);
+  c = mfma_bf16(b[0], a[2], c);
+  c = mfma_bf16(b[1], a[1], c);
+  c = mfma_bf16(b[2], a[0], c);
+  return c;
+}
+
+// Convolution epilogue on transposed accumulators (see mfma_x3t):
+//   y = acc * scale + shift [+ residual] [ReLU]; DUAL: scale folded into the
+//   weights; RAW: store acc.  Needs Ncol, ldo (and ldr) % 4 == 0 (x3p_eligible).
+template <int EPI, int BM, int BN, int WM, int WN>
+__device__ inline void conv_epilogue_t(const GemmParams& p,
+                                       f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int batch,
+                                       int kslice, int m0, int n0, int wm, int wn, int r32,
+                                       int h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+  constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
+  constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
+  constexpr bool RAW = (EPI & EPI_F_RAW) != 0;
+  float* __restrict__ out =
+      p.out + batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;
+  const int nrem = p.Ncol - n0;
+  const float* sc = (DUAL || RAW) ? nullptr : p.scale + batch * p.ss_bstride + n0;
+  const float* sh = RAW ? nullptr : p.shift + batch * p.ss_bstride + n0;
+  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+  const int ldr = (int)p.ldr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cb = wn * (BN / WN) + j * 32 + 4 * h;
+    f32x4 s4[4], t4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = cb + 8 * q < nrem;
+      s4[q] = (DUAL || RAW || !ok) ? (f32x4){1.f, 1.f, 1.f, 1.f}
+                                   : *reinterpret_cast<const f32x4*>(sc + cb + 8 * q);
+      t4[q] = (RAW || !ok) ? (f32x4){0.f, 0.f, 0.f, 0.f}
+                           : *reinterpret_cast<const f32x4*>(sh + cb + 8 * q);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rr = wm * (BM / WM) + i * 32 + r32;
+      if (rr >= mrem) continue;
+      f32x4 rv[4];
+      if (HAS_RES) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          rv[q] = cb + 8 * q < nrem ? *reinterpret_cast<const f32x4*>(res + rr * ldr + cb + 8 * q)
+                                    : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (cb + 8 * q >= nrem) continue;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = RAW ? acc[i][j][4 * q + e] : __builtin_fmaf(acc[i][j][4 * q + e], s4[q][e], t4[q][e]);
+          if (HAS_RES) v[e] += rv[q][e];
+          if (RELU) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<f32x4*>(out + rr * ldo + cb + 8 * q) = v;
+      }
+    }
+  }
+}
+
+// Distance epilogue on transposed accumulators: same formulas as
+// dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
+template <int BM, int BN, int WM, int WN>
+__device__ inline void dist_epilogue_t(const GemmParams& p,
+                                       f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0,
+                                       int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0;
+  const int nrem = p.Ncol - n0;
+  const bool vec = (p.ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const float* qsq = p.norm_a + m0;
+  float qn[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * (BM / WM) + i * 32 + r32;
+    qn[i] = rr < mrem ? qsq[rr] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cb = wn * (BN / WN) + j * 32 + 4 * h;
+    float gn[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = cb + 8 * (r >> 2) + (r & 3);
+      gn[r] = c < nrem ? p.norm_b[n0 + c] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rr = wm * (BM / WM) + i * 32 + r32;
+      if (rr >= mrem) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = cb + 8 * q;
+        if (c >= nrem) continue;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float dot = acc[i][j][4 * q + e];
+          float d;
+          if (p.metric == PPS_METRIC_COSINE) {
+            const float den =
+                fmaxf(sqrtf(qn[i]), 1e-12f) * fmaxf(sqrtf(gn[4 * q + e]), 1e-12f);
+            d = 1.f - dot / den;
+          } else {
+            d = fmaxf(__builtin_fmaf(-2.f, dot, qn[i]) + gn[4 * q + e], 0.f);
+            if (p.metric == PPS_METRIC_EUCLIDEAN) d = sqrtf(d);
+          }
+          if (p.zero_diag && m0 + rr == n0 + c + e) d = 0.f;
+          v[e] = d;
+        }
+        float* o = out + rr * ldo + c;
+        if (vec && c + 3 < nrem) {
+          *reinterpret_cast<f32x4*>(o) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < nrem) o[e] = v[e];
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int NS>
+__global__ void __launch_bounds__(64 * WM * WN)
+gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int BK = 32;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int A_BYTES = BM * BK * 4;  // f32 rows of 128 B
+  constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
+  constexpr int STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int AI = BM / 8 / NW;       // A pieces (8 rows each) per wave and chunk
+  constexpr int BPW = BN / 16 / NW;     // B pieces (16 rows each) per wave, plane and chunk
+  constexpr int NLOAD = AI + 3 * BPW;   // DMA instructions per wave and chunk
+  static_assert(AI * 8 * NW == BM && BPW * 16 * NW == BN, "tile does not split into DMA pieces");
+  static_assert(TM >= 1 && TN >= 1 && (BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
+  static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
+  static_assert(NLOAD * (NS - 2) <= 63, "vmcnt range");
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NS * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tile_m = bid / tiles_n;
+  const int tile_n = bid - tile_m * tiles_n;
+  const int m0 = tile_m * BM;
+  const int n0 = tile_n * BN;
+  const int batch = blockIdx.y / p.splitk;
+  const int kslice = blockIdx.y - batch * p.splitk;
+  const int64_t kofs0 = (int64_t)kslice * p.Kloop;
+
+  // ---- A pieces: piece q = wave*AI + i covers tile rows 8q..8q+7; lane l
+  // takes row 8q + (l >> 3) and fills physical chunk l & 7 with logical
+  // chunk (l & 7) ^ ((row >> 1) & 7) (4 floats of the 32-wide K chunk)
+  const rsrc_t ra = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
+  rsrc_t ra2 = ra;
+  if (DUAL) ra2 = make_rsrc(p.a2, p.a2_bytes);
+  int abase[AI];
+  uint64_t amask[AI];
+  int abase2[AI];
+  {
+    const int hw = p.Ho * p.Wo;
+    const int ntaps = p.KH * p.KW;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int rt = (wave * AI + i) * 8 + (lane >> 3);
+      const int cl = (lane & 7) ^ ((rt >> 1) & 7);
+      const int row = m0 + rt;
+      const int rowc = row < p.M ? row : 0;
+      const int n = rowc / hw;
+      const int rem = rowc - n * hw;
+      const int oh = rem / p.Wo;
+      const int ow = rem - oh * p.Wo;
+      const int ih0 = oh * p.stride - p.pad;
+      const int iw0 = ow * p.stride - p.pad;
+      abase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda + cl * 4;
+      uint64_t m = 0;
+      for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
+        const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
+        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) m |= 1ull << t;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
+      amask[i] = row < p.M ? m : 0ull;
+      if (DUAL)
+        abase2[i] = row < p.M ? (((n * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.lda2 +
+                                 cl * 4) * 4
+                              : kOOB;
+    }
+  }
+
+  // ---- B pieces: plane pl, piece q = wave*BPW + j covers tile columns
+  // 16q..16q+15; lane l takes column 16q + (l >> 2) and fills physical chunk
+  // l & 3 with logical chunk (l & 3) ^ ((col >> 2) & 3) = (l & 3) ^ ((l >> 4) & 3)
+  const uint16_t* b3 = p.b3 + batch * p.b_bstride + kofs0;
+  const rsrc_t rb0 = make_rsrc(b3, p.b_bytes);
+  const rsrc_t rb1 = make_rsrc(b3 + p.b_plane, p.b_bytes);
+  const rsrc_t rb2 = make_rsrc(b3 + 2 * p.b_plane, p.b_bytes);
+  const int bcl = (lane & 3) ^ ((lane >> 4) & 3);
+  int boff[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int col = n0 + (wave * BPW + j) * 16 + (lane >> 2);
+    boff[j] = col < p.Ncol ? (col * p.ldb + bcl * 8) * 2 : kOOB;
+  }
+
+  // ---- wave-uniform im2col tracker of the next chunk to request
+  int tc = 0, tt = 0, tkw = 0, toff = 0;
+  const int step_w = p.dil * p.lda;
+  const int step_h = p.dil * p.lda * (p.W - p.KW);
+  const int nch1 = DUAL ? p.Kloop1 / BK : (1 << 30);
+  int kiss = 0;  // next chunk to request
+  int siss = 0;  // its LDS stage
+  auto issue = [&]() {
+    const unsigned char* st = lds + siss * STAGE;
+    if (DUAL && kiss >= nch1) {
+      const int kofs = (kiss - nch1) * BK * 4;
+#pragma unroll
+      for (int i = 0; i < AI; ++i)
+        glds16(ra2, st + (wave * AI + i) * 1024, abase2[i] == kOOB ? kOOB : abase2[i] + kofs);
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = tt < 64 && ((amask[i] >> tt) & 1ull);
+        glds16(ra, st + (wave * AI + i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
+      }
+      tc += BK;
+      if (tc >= p.Cin) {
+        tc = 0;
+        ++tt;
+        toff += step_w;
+        if (++tkw == p.KW) { tkw = 0; toff += step_h; }
+      }
+    }
+    const bool kok = kiss * BK + bcl * 8 < p.kb_valid;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int off = (kok && boff[j] != kOOB) ? boff[j] + kiss * BK * 2 : kOOB;
+      const unsigned char* d = st + A_BYTES + (wave * BPW + j) * 1024;
+      glds16(rb0, d, off);
+      glds16(rb1, d + B_PLANE, off);
+      glds16(rb2, d + 2 * B_PLANE, off);
+    }
+    ++kiss;
+    siss = siss + 1 == NS ? 0 : siss + 1;
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // Fragment reads of one 16-wide K group g of a stage, A split into its
+  // three bf16 terms.  The rows of this lane are r32 mod 32, so both
+  // swizzles are per-lane constants.
+  const int asw = (r32 >> 1) & 7;
+  const int bsw = (r32 >> 2) & 3;
+  auto read_split = [&](const unsigned char* st, int g, bf16x8 (&fa)[TM][3],
+                        bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const unsigned char* rp = st + (wm * (BM / WM) + i * 32 + r32) * 128;
+      const int c0 = 4 * g + 2 * h;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + ((c0 ^ asw) << 4));
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((c0 + 1) ^ asw) << 4));
+      split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const unsigned char* bp =
+          st + A_BYTES + (wn * (BN / WN) + j * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        fb[j][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
+    }
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_x3t(fa[i], fb[j], acc[i][j]);
+  };
+  // chunk kc has landed for every wave once each wave saw its own pieces
+  // retire (counted vmcnt: the NS-2 younger chunks stay in flight) and all
+  // waves passed the barrier; the barrier also retires every wave's reads of
+  // the stage the next request overwrites (lgkmcnt(0) before it)
+  auto chunk_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt<NLOAD * (NS - 2)>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // Software pipeline over 16-wide K groups (two per chunk): the reads and
+  // the split of group q+1 are issued in the same basic block as the MFMAs
+  // of group q, so the scheduler interleaves them.  Requests run NS-1 chunks
+  // ahead; requests past the last chunk read zeros into stages that are
+  // never consumed, which keeps every wait count uniform.
+  const int nchunks = (p.Kloop + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue();
+  chunk_barrier();
+  issue();
+  bf16x8 fa0[TM][3], fb0[TN][3], fa1[TM][3], fb1[TN][3];
+  read_split(lds, 0, fa0, fb0);
+  int scur = 0;
+  for (int kc = 0; kc < nchunks - 1; ++kc) {
+    const unsigned char* st = lds + scur * STAGE;
+    scur = scur + 1 == NS ? 0 : scur + 1;
+    read_split(st, 1, fa1, fb1);
+    mfmas(fa0, fb0);
+    chunk_barrier();
+    issue();
+    read_split(lds + scur * STAGE, 0, fa0, fb0);
+    mfmas(fa1, fb1);
+  }
+  read_split(lds + scur * STAGE, 1, fa1, fb1);
+  mfmas(fa0, fb0);
+  mfmas(fa1, fb1);
+  wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
+
+  if (EPI & EPI_DIST)
+    dist_epilogue_t<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, r32, h);
+  else
+    conv_epilogue_t<EPI, BM, BN, WM, WN>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI>
+static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.Ncol + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS>),
+                     dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p,
+                     tiles_m, tiles_n);
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  switch (epi) {
+    case EPI_DIST: launch_one_p<BM, BN, WM, WN, NS, EPI_DIST>(p, batch, stream); break;
+    case EPI_CONV: launch_one_p<BM, BN, WM, WN, NS, EPI_CONV>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU:
+      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RELU>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES:
+      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RES>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RES | EPI_F_RELU:
+      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RES | EPI_F_RELU>(p, batch, stream);
+      break;
+    case EPI_CONV | EPI_F_RAW:
+      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RAW>(p, batch, stream); break;
+    case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
+      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RELU | EPI_F_DUAL>(p, batch, stream);
+      break;
+    default:
+      set_error("unknown epilogue for the pipelined bf16x3 GEMM");
+      return PPS_ERR_INVALID_ARG;
+  }
+  PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+  return PPS_OK;
+}
+
+// The DMA pieces need 16-byte-aligned 4-float A slots, 8-element B slots and
+// a 32-wide K chunk inside one tap (and, with a fused shortcut, a K switch on
+// a chunk boundary).
+bool x3p_eligible(const GemmParams& p, int epi) {
+  if (p.Cin % 32 != 0 || p.lda % 4 != 0 || p.ldb % 8 != 0) return false;
+  if (p.a2 && (p.Kloop1 % 32 != 0 || (p.Kloop - p.Kloop1) % 32 != 0 || p.lda2 % 4 != 0))
+    return false;
+  // 16-byte epilogue vectors (the distance epilogue falls back per row)
+  if (!(epi & EPI_DIST)) {
+    if (p.Ncol % 4 != 0 || p.ldo % 4 != 0 || (reinterpret_cast<uintptr_t>(p.out) & 15) != 0)
+      return false;
+    if (p.residual && (p.ldr % 4 != 0 || (reinterpret_cast<uintptr_t>(p.residual) & 15) != 0))
+      return false;
+    if ((p.scale && (reinterpret_cast<uintptr_t>(p.scale) & 15) != 0) ||
+        (p.shift && (reinterpret_cast<uintptr_t>(p.shift) & 15) != 0) ||
+        p.out_bstride % 4 != 0 || p.out_sstride % 4 != 0 || p.ss_bstride % 4 != 0)
+      return false;
+  }
+  return true;
+}
+
+int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
+  switch (variant) {
+    case 0: return launch_tile_p<128, 128, 2, 2, 3>(p, epi, batch, stream);
+    case 1: return launch_tile_p<192, 128, 2, 2, 3>(p, epi, batch, stream);
+    case 2: return launch_tile_p<128, 64, 2, 2, 3>(p, epi, batch, stream);
+    case 3: return launch_tile_p<192, 64, 2, 2, 3>(p, epi, batch, stream);
+    case 4: return launch_tile_p<256, 128, 4, 2, 2>(p, epi, batch, stream);
+    case 5: return launch_tile_p<128, 256, 2, 4, 2>(p, epi, batch, stream);
+    case 6: return launch_tile_p<192, 256, 2, 4, 2>(p, epi, batch, stream);
+    default:
+      set_error("unknown pipelined GEMM variant " + std::to_string(variant));
+      return PPS_ERR_INVALID_ARG;
+  }
+}
+
+}  // namespace pps

@@ -54,7 +54,11 @@ enum GemmTile {
   // 21..28 (bf16x3 kernel): 192x128 K16, 192x64 K16, 192x128 K32, 192x64 K32,
   // then the same four with A kept f32 in LDS
   GEMM_TILE_192_FIRST = 21,
-  GEMM_NUM_TILES = 29
+  // 29..35 (bf16x3 only): LDS-DMA pipelined kernel (gemm_x3p.hip), K chunk 32:
+  // 128x128, 192x128, 128x64, 192x64 (4 waves, 3 stages), 256x128, 128x256,
+  // 192x256 (8 waves, 2 stages)
+  GEMM_TILE_P_FIRST = 29,
+  GEMM_NUM_TILES = 36
 };
 
 struct GemmParams {
@@ -106,6 +110,8 @@ struct GemmParams {
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
 int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream);
+bool x3p_eligible(const GemmParams& p, int epi);
+int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant);
 int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream);
 int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
