@@ -36,12 +36,16 @@ def main():
     d, math, batch, nconv = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
     fetch = load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0], 'FETCH_SIZE')
     write = load(glob.glob(os.path.join(d, 'p2', '*counter_collection.csv'))[0], 'WRITE_SIZE')
-    kname = 'gemm_x3_kernel' if math == 'x3' else 'gemm_f32_kernel'
+    # the x3 path launches both the register-staged and the pipelined family
+    knames = ('gemm_x3_kernel', 'gemm_x3p_kernel') if math == 'x3' else ('gemm_f32_kernel',)
+
+    def is_gemm(nm):
+        return any(k + '<' in nm for k in knames)
     out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
                       'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
     for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):
-        f = [v for nm, v in fetch if kname in nm and sel(epi_of(nm))][-n:]
-        w = [v for nm, v in write if kname in nm and sel(epi_of(nm))][-n:]
+        f = [v for nm, v in fetch if is_gemm(nm) and sel(epi_of(nm))][-n:]
+        w = [v for nm, v in write if is_gemm(nm) and sel(epi_of(nm))][-n:]
         if len(f) < n or len(w) < n:
             continue
         fb = 2 * 1024 * sum(f)
