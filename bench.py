@@ -161,7 +161,7 @@ def conv_roofline(m, x):
         per[name] = (op, f, e0.elapsed_time(e1))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if m.math == 'x3':
-        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3_kernel<*> implicit-GEMM conv, f32 products as 6 '
+        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv, f32 products as 6 '
                                         'bf16 MFMA terms (%d launches/forward)' % n_launch)
     else:
         peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '
@@ -238,6 +238,8 @@ def main():
         with open(args.tiles_file) as f:
             saved = json.load(f)
         m.set_tiles(saved)
+        if '__planes__' in saved:
+            m.set_planes(saved['__planes__'])
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
     elif not args.no_autotune:
         m.autotune(xbuf)   # per-layer tile choice, outside the timed region
@@ -273,7 +275,8 @@ def main():
                           tune=not (args.no_autotune or tiles_saved))
     if args.tiles_file and not tiles_saved and rank == 0:
         with open(args.tiles_file, 'w') as f:
-            json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile']), f, indent=0)
+            json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile'],
+                           __planes__=m.planes()), f, indent=0)
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
     dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
@@ -290,7 +293,8 @@ def main():
         'config': {'workload': 'Market-1501 ResNet-50 PPS (stride-1 res5, 31 part subsets), '
                                'batch %d/GPU, 384x128, 3368q x 15913g L2 distmat' % B,
                    'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': m.feat_dim,
-                   'parallelism': 'dp%d' % world, 'hipgraph': graph is not None},
+                   'parallelism': 'dp%d' % world, 'hipgraph': graph is not None,
+                   'act_plane_edges': len(m.planes())},
         'distmat_GBps': round(total_bytes / (dist_ms_max * 1e-3) / 1e9, 2),
         'distmat_ms': round(dist_ms_max, 3),
         'distmat_TFLOPs_per_gpu': round(dist_tflops, 2),
@@ -308,7 +312,7 @@ def main():
             traffic=_pmc_traffic('distmat', dist_math, Q_MARKET),
             algorithmic_bytes_per_launch=dist_bytes,
             kernel='%s EPI_DIST, tile %d (+ split/norm of the gallery shard)' % (
-                'gemm_x3_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
+                'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
                 ret['distmat_tile'])),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -50,7 +50,10 @@ const char* pps_registered_ops(void);
  * 11..20 = ids 1..10 with the `_x3` kernels' A operand kept f32 in LDS and
  * split after the fragment read (the f32 kernels treat them as 1..10),
  * 21..28 = 192-row tiles of the `_x3` kernels (192x128 / 192x64, K chunk
- * 16 / 32, A staged as planes / f32; the f32 kernels use 128-row tiles).  Results are identical for every tile (same per-element fp32
+ * 16 / 32, A staged as planes / f32; the f32 kernels use 128-row tiles),
+ * 29..35 = the `_x3` LDS-DMA pipelined tiles (128x128, 192x128, 128x64,
+ * 192x64, 256x128, 128x256, 192x256; K chunk 32; the f32 kernels use the
+ * heuristic).  Results are identical for every tile (same per-element fp32
  * MFMA accumulation order); only speed differs, so callers may autotune. */
 int pps_gemm_num_tiles(void);
 
@@ -74,6 +77,14 @@ int pps_row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out,
 int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
                    int metric, float* out, int64_t ldo, int tile, void* stream);
+/* pps_distmat_x3 with the queries ALSO pre-split into bf16x3 planes
+ * q3 [3][Q][ldq] (pps_split_bf16x3; plane stride Q*ldq): both operands are
+ * then staged by pure DMA.  Same bits as pps_distmat_x3.  Pipelined tiles
+ * only (tile 0 or >= 29); D % 32 == 0, ldq % 8 == 0, ldg % 8 == 0. */
+int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq,
+                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg,
+                    int D, int metric, float* out, int64_t ldo, int tile,
+                    void* stream);
 
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
@@ -202,6 +213,23 @@ int pps_conv2d_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
                          const float* shift, const float* residual, int relu,
                          float* y, int Ho, int Wo, int ldy, int tile,
                          void* stream);
+/* pps_conv2d_bn_act_x3 with bf16x3 ACTIVATION planes on either side
+ * (pipelined tiles only: tile 0 or >= 29).  Exactly one of x (f32 NHWC) /
+ * x3 (planes [3][N][H][W][ldx], plane stride x_plane elements) and one of
+ * y / y3 (planes [3][N][Ho][Wo][ldy], stride y_plane) is non-null.  A
+ * producer writes y = hi + mid + lo split exactly as the x3 GEMMs split an
+ * f32 operand, so a consumer reading x3 computes the same bits as from the
+ * f32 tensor while skipping the split in its K loop.  Used between the
+ * bottleneck convs branch2a -> 2b -> 2c (ResNet.py:276-333), whose
+ * intermediates have no other reader.  Needs Cin % 32 == 0, ldx % 8 == 0,
+ * Cout % 4 == 0, 16-byte aligned planes. */
+int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane,
+                          int N, int H, int W, int Cin, int ldx,
+                          const uint16_t* w3, int Cout, int Kpad, int KH, int KW,
+                          int stride, int pad, int dil, const float* scale,
+                          const float* shift, const float* residual, int relu,
+                          float* y, uint16_t* y3, int64_t y_plane, int Ho,
+                          int Wo, int ldy, int tile, void* stream);
 int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin,
                               int ldx, int KH, int KW, int stride, int pad,
                               const float* x2, int H2, int W2, int Cin2,

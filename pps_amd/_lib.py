@@ -25,6 +25,8 @@ SIGNATURES = {
     'pps_row_sqnorm': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr],
     'pps_distmat_x3': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
                        c_ptr, c_i64, c_int, c_ptr],
+    'pps_distmat_x3p': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
+                        c_ptr, c_i64, c_int, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
@@ -48,6 +50,10 @@ SIGNATURES = {
     'pps_conv2d_bn_act_x3': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
                              c_ptr, c_int, c_int, c_int, c_int, c_ptr],
+    'pps_conv2d_bn_act_x3p': [c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                              c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr,
+                              c_ptr, c_int, c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int,
+                              c_ptr],
     'pps_conv2d_dual_bn_act_x3': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int,
                                   c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int,

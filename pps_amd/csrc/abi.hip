@@ -130,6 +130,44 @@ int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
   return PPS_OK;
 }
 
+int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq,
+                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
+                    int metric, float* out, int64_t ldo, int tile, void* stream) {
+  PPS_ENFORCE(q3 && qsq && g3 && gsq && out, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && D > 0, "bad shape");
+  PPS_ENFORCE(D % 32 == 0, "D must be a multiple of 32, got " + std::to_string(D));
+  PPS_ENFORCE(ldq % 8 == 0 && ldg % 8 == 0 && ldq >= D && ldg >= D, "bad leading dims");
+  PPS_ENFORCE(ldo >= G, "ldo < G");
+  PPS_ENFORCE(aligned16(q3) && aligned16(g3), "q3/g3 must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  PPS_ENFORCE(tile == 0 || tile >= GEMM_TILE_P_FIRST,
+              "query planes need a pipelined tile (0 or >= " +
+                  std::to_string((int)GEMM_TILE_P_FIRST) + ")");
+  PPS_ENFORCE(ldq * 2 < kMaxBufBytes && ldg * 2 < kMaxBufBytes, "rows too long");
+  const int64_t qblk = std::min<int64_t>(Q, (kMaxBufBytes - 1) / (ldq * 2));
+  const int64_t gblk = std::min<int64_t>(G, (kMaxBufBytes - 1) / (ldg * 2));
+  for (int64_t q0 = 0; q0 < Q; q0 += qblk) {
+    for (int64_t g0 = 0; g0 < G; g0 += gblk) {
+      const int64_t qn = std::min(qblk, Q - q0), gn = std::min(gblk, G - g0);
+      GemmParams p{};
+      p.splitk = 1;
+      p.a3 = q3 + q0 * ldq; p.a_plane = Q * ldq; p.a_bytes = (uint32_t)(qn * ldq * 2);
+      p.H = 1; p.W = (int)qn; p.Cin = D; p.lda = (int)ldq;
+      p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)qn;
+      p.M = (int)qn;
+      p.b3 = g3 + g0 * ldg; p.b_plane = G * ldg; p.b_bytes = (uint32_t)(gn * ldg * 2);
+      p.ldb = (int)ldg; p.kb_valid = D; p.Ncol = (int)gn;
+      p.Kloop = D;
+      p.norm_a = qsq + q0; p.norm_b = gsq + g0;
+      p.out = out + q0 * ldo + g0; p.ldo = ldo; p.metric = metric;
+      p.tile = tile ? tile : GEMM_TILE_P_FIRST + 4;  // 256x128: the Market-shape winner
+      const int rc = launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
+      if (rc != PPS_OK) return rc;
+    }
+  }
+  return PPS_OK;
+}
+
 int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
   PPS_ENFORCE(X && Z, "null pointer");
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
@@ -219,11 +257,26 @@ int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t
 }
 
 // weights either f32 [Cout][Kpad] (x3 = 0) or bf16x3 planes [3][Cout][Kpad]
+// x3p: bf16x3 activation planes (x_pl / y_pl, plane strides in elements)
+// instead of f32 x / y -- gemm_x3p.hip tiles only
 static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       const void* w, int x3, int Cout, int Kpad, int KH, int KW, int stride,
                       int pad, int dil, const float* scale, const float* shift,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
-                      int tile, void* stream) {
+                      int tile, void* stream, const uint16_t* x_pl = nullptr,
+                      int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0) {
+  PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
+              "exactly one of x / x planes and one of y / y planes must be given");
+  if (x_pl || y_pl) {
+    PPS_ENFORCE(x3, "activation planes need the bf16x3 weights");
+    PPS_ENFORCE(tile == 0 || tile >= GEMM_TILE_P_FIRST,
+                "activation planes need a pipelined tile (0 or >= " +
+                    std::to_string((int)GEMM_TILE_P_FIRST) + ")");
+    if (x_pl) x = reinterpret_cast<const float*>(x_pl);  // for the shared checks below
+    if (y_pl) y = reinterpret_cast<float*>(y_pl);
+    PPS_ENFORCE(!x_pl || x_plane >= (int64_t)N * H * W * ldx, "x plane stride too small");
+    PPS_ENFORCE(!y_pl || y_plane >= (int64_t)N * Ho * Wo * ldy, "y plane stride too small");
+  }
   PPS_ENFORCE(x && w && scale && shift && y, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "bad shape");
   PPS_ENFORCE(Cin % 4 == 0 && ldx % 4 == 0 && ldx >= Cin,
@@ -252,10 +305,15 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  if (x_pl) {
+    p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
+    p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
+  }
+  if (y_pl) { p.out = nullptr; p.out3 = y_pl; p.out_plane = y_plane; }
   if (x3) {
     p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
     p.b_bytes = (uint32_t)(p.b_plane * 2);
-    return launch_gemm_x3(p, EPI_CONV, 1, as_stream(stream));
+    return launch_gemm_x3(p, y_pl ? EPI_CONV | EPI_F_PLANES : EPI_CONV, 1, as_stream(stream));
   }
   p.b = static_cast<const float*>(w);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
@@ -277,6 +335,17 @@ int pps_conv2d_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
                          int tile, void* stream) {
   return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
                    shift, residual, relu, y, Ho, Wo, ldy, tile, stream);
+}
+
+int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N, int H,
+                          int W, int Cin, int ldx, const uint16_t* w3, int Cout, int Kpad,
+                          int KH, int KW, int stride, int pad, int dil, const float* scale,
+                          const float* shift, const float* residual, int relu, float* y,
+                          uint16_t* y3, int64_t y_plane, int Ho, int Wo, int ldy, int tile,
+                          void* stream) {
+  return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x3, x_plane, y3,
+                   y_plane);
 }
 
 static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,

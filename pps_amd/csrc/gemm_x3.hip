@@ -268,6 +268,16 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
+  if (p.a3 || (epi & EPI_F_PLANES)) {
+    // bf16-plane activations exist only in the pipelined family
+    if (!x3p_eligible(p, epi)) {
+      set_error("bf16-plane activations: shape/alignment not eligible for the pipelined GEMM");
+      return PPS_ERR_INVALID_ARG;
+    }
+    const int v = p.tile >= GEMM_TILE_P_FIRST ? p.tile - GEMM_TILE_P_FIRST
+                                              : (p.M % 192 == 0 ? 1 : 0);
+    return launch_gemm_x3p(p, epi, batch, stream, v);
+  }
   int tile = p.tile ? p.tile : pick_tile(p, batch);
   if (tile >= GEMM_TILE_P_FIRST) {
     // LDS-DMA pipelined family (gemm_x3p.hip); shapes it cannot stage

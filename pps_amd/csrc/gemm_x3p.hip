@@ -56,7 +56,9 @@ __device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
 
 // Convolution epilogue on transposed accumulators (see mfma_x3t):
 //   y = acc * scale + shift [+ residual] [ReLU]; DUAL: scale folded into the
-//   weights; RAW: store acc.  Needs Ncol, ldo (and ldr) % 4 == 0 (x3p_eligible).
+//   weights; RAW: store acc; PLANES: write y as three bf16 planes (exact
+//   split, 8-byte stores per plane).  Needs Ncol, ldo (and ldr) % 4 == 0
+//   (x3p_eligible).
 template <int EPI, int BM, int BN, int WM, int WN>
 __device__ inline void conv_epilogue_t(const GemmParams& p,
                                        f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int batch,
@@ -68,8 +70,10 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool RAW = (EPI & EPI_F_RAW) != 0;
-  float* __restrict__ out =
-      p.out + batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
+  constexpr bool PLANES = (EPI & EPI_F_PLANES) != 0;
+  const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
+  float* __restrict__ out = PLANES ? nullptr : p.out + obase;
+  uint16_t* __restrict__ out3 = PLANES ? p.out3 + obase : nullptr;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;
   const int nrem = p.Ncol - n0;
@@ -110,7 +114,17 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
           if (HAS_RES) v[e] += rv[q][e];
           if (RELU) v[e] = fmaxf(v[e], 0.f);
         }
-        *reinterpret_cast<f32x4*>(out + rr * ldo + cb + 8 * q) = v;
+        if (PLANES) {
+          unsigned h0, m0_, l0, h1, m1, l1;
+          split2(v[0], v[1], h0, m0_, l0);
+          split2(v[2], v[3], h1, m1, l1);
+          uint16_t* o = out3 + rr * ldo + cb + 8 * q;
+          *reinterpret_cast<u32x2*>(o) = (u32x2){h0, h1};
+          *reinterpret_cast<u32x2*>(o + p.out_plane) = (u32x2){m0_, m1};
+          *reinterpret_cast<u32x2*>(o + 2 * p.out_plane) = (u32x2){l0, l1};
+        } else {
+          *reinterpret_cast<f32x4*>(out + rr * ldo + cb + 8 * q) = v;
+        }
       }
     }
   }
@@ -182,20 +196,28 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int NS>
+// A3 = false: A is f32 NHWC, staged as 128-byte f32 rows and split after the
+// fragment read.  A3 = true: A is three bf16 planes (written by a producer
+// epilogue with EPI_F_PLANES), staged like B as 64-byte rows per plane --
+// no split arithmetic in the main loop.
+template <int BM, int BN, int WM, int WN, int EPI, int NS, bool A3>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int BK = 32;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
-  constexpr int A_BYTES = BM * BK * 4;  // f32 rows of 128 B
+  constexpr int A_PLANE = BM * BK * 2;  // A3: bf16 rows of 64 B per plane
+  constexpr int A_BYTES = A3 ? 3 * A_PLANE : BM * BK * 4;  // else f32 rows of 128 B
   constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
   constexpr int STAGE = A_BYTES + 3 * B_PLANE;
-  constexpr int AI = BM / 8 / NW;       // A pieces (8 rows each) per wave and chunk
+  constexpr int AROWS = A3 ? 16 : 8;    // rows per A piece (1 KiB)
+  constexpr int AI = BM / AROWS / NW;   // A pieces per wave and chunk (per plane if A3)
   constexpr int BPW = BN / 16 / NW;     // B pieces (16 rows each) per wave, plane and chunk
-  constexpr int NLOAD = AI + 3 * BPW;   // DMA instructions per wave and chunk
-  static_assert(AI * 8 * NW == BM && BPW * 16 * NW == BN, "tile does not split into DMA pieces");
+  constexpr int NLOAD = (A3 ? 3 : 1) * AI + 3 * BPW;  // DMA instructions per wave and chunk
+  static_assert(AI * AROWS * NW == BM && BPW * 16 * NW == BN,
+                "tile does not split into DMA pieces");
+  static_assert(!(A3 && (EPI & EPI_F_DUAL)), "fused shortcut reads f32 activations");
   static_assert(TM >= 1 && TN >= 1 && (BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
   static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
   static_assert(NLOAD * (NS - 2) <= 63, "vmcnt range");
@@ -221,10 +243,20 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 
   // ---- A pieces: piece q = wave*AI + i covers tile rows 8q..8q+7; lane l
   // takes row 8q + (l >> 3) and fills physical chunk l & 7 with logical
-  // chunk (l & 7) ^ ((row >> 1) & 7) (4 floats of the 32-wide K chunk)
-  const rsrc_t ra = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
-  rsrc_t ra2 = ra;
-  if (DUAL) ra2 = make_rsrc(p.a2, p.a2_bytes);
+  // chunk (l & 7) ^ ((row >> 1) & 7) (4 floats of the 32-wide K chunk).
+  // A3: 16 rows per piece and plane, lane row 16q + (l >> 2), physical chunk
+  // l & 3 holding logical chunk (l & 3) ^ ((row >> 2) & 3) (8 bf16)
+  rsrc_t ra, ra1, ra2;
+  if (A3) {
+    const uint16_t* a3 = p.a3 + batch * p.a_bstride + kofs0;
+    ra = make_rsrc(a3, p.a_bytes);
+    ra1 = make_rsrc(a3 + p.a_plane, p.a_bytes);
+    ra2 = make_rsrc(a3 + 2 * p.a_plane, p.a_bytes);
+  } else {
+    ra = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
+    ra1 = ra;
+    ra2 = DUAL ? make_rsrc(p.a2, p.a2_bytes) : ra;
+  }
   int abase[AI];
   uint64_t amask[AI];
   int abase2[AI];
@@ -233,8 +265,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     const int ntaps = p.KH * p.KW;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int rt = (wave * AI + i) * 8 + (lane >> 3);
-      const int cl = (lane & 7) ^ ((rt >> 1) & 7);
+      const int rt = A3 ? (wave * AI + i) * 16 + (lane >> 2) : (wave * AI + i) * 8 + (lane >> 3);
+      // first element (of the 32-wide K chunk) this lane fetches
+      const int ce = A3 ? 8 * ((lane & 3) ^ ((rt >> 2) & 3)) : 4 * ((lane & 7) ^ ((rt >> 1) & 7));
       const int row = m0 + rt;
       const int rowc = row < p.M ? row : 0;
       const int n = rowc / hw;
@@ -243,7 +276,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const int ow = rem - oh * p.Wo;
       const int ih0 = oh * p.stride - p.pad;
       const int iw0 = ow * p.stride - p.pad;
-      abase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda + cl * 4;
+      abase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda + ce;
       uint64_t m = 0;
       for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
         const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
@@ -253,7 +286,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       amask[i] = row < p.M ? m : 0ull;
       if (DUAL)
         abase2[i] = row < p.M ? (((n * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.lda2 +
-                                 cl * 4) * 4
+                                 ce) * 4
                               : kOOB;
     }
   }
@@ -291,7 +324,15 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const bool ok = tt < 64 && ((amask[i] >> tt) & 1ull);
-        glds16(ra, st + (wave * AI + i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
+        if (A3) {
+          const int off = ok ? (abase[i] + toff + tc) * 2 : kOOB;
+          const unsigned char* d = st + (wave * AI + i) * 1024;
+          glds16(ra, d, off);
+          glds16(ra1, d + A_PLANE, off);
+          glds16(ra2, d + 2 * A_PLANE, off);
+        } else {
+          glds16(ra, st + (wave * AI + i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
+        }
       }
       tc += BK;
       if (tc >= p.Cin) {
@@ -331,11 +372,19 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
                         bf16x8 (&fb)[TN][3]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const unsigned char* rp = st + (wm * (BM / WM) + i * 32 + r32) * 128;
-      const int c0 = 4 * g + 2 * h;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + ((c0 ^ asw) << 4));
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((c0 + 1) ^ asw) << 4));
-      split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+      if (A3) {
+        const unsigned char* ap =
+            st + (wm * (BM / WM) + i * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * A_PLANE);
+      } else {
+        const unsigned char* rp = st + (wm * (BM / WM) + i * 32 + r32) * 128;
+        const int c0 = 4 * g + 2 * h;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + ((c0 ^ asw) << 4));
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((c0 + 1) ^ asw) << 4));
+        split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -397,32 +446,52 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     conv_epilogue_t<EPI, BM, BN, WM, WN>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3>
 static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS>),
+  hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS, A3>),
                      dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p,
                      tiles_m, tiles_n);
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+// NSF / NSP: LDS stages with f32 / bf16-plane A operands (NSP = 0: the tile
+// does not take plane activations)
+template <int BM, int BN, int WM, int WN, int NSF, int NSP>
 static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
+  if constexpr (NSP == 0) {
+    if (p.a3) {
+      set_error("tile not built for bf16-plane activations");
+      return PPS_ERR_INVALID_ARG;
+    }
+  } else if (p.a3) {
+    switch (epi) {
+      case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSP, EPI_DIST, true>(p, batch, stream); break;
+      case C: launch_one_p<BM, BN, WM, WN, NSP, C, true>(p, batch, stream); break;
+      case C | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RL, true>(p, batch, stream); break;
+      case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL, true>(p, batch, stream); break;
+      case C | PL: launch_one_p<BM, BN, WM, WN, NSP, C | PL, true>(p, batch, stream); break;
+      case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSP, C | RL | PL, true>(p, batch, stream); break;
+      default:
+        set_error("epilogue not built for bf16-plane activations");
+        return PPS_ERR_INVALID_ARG;
+    }
+    PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+    return PPS_OK;
+  }
   switch (epi) {
-    case EPI_DIST: launch_one_p<BM, BN, WM, WN, NS, EPI_DIST>(p, batch, stream); break;
-    case EPI_CONV: launch_one_p<BM, BN, WM, WN, NS, EPI_CONV>(p, batch, stream); break;
-    case EPI_CONV | EPI_F_RELU:
-      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RELU>(p, batch, stream); break;
-    case EPI_CONV | EPI_F_RES:
-      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RES>(p, batch, stream); break;
-    case EPI_CONV | EPI_F_RES | EPI_F_RELU:
-      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RES | EPI_F_RELU>(p, batch, stream);
-      break;
-    case EPI_CONV | EPI_F_RAW:
-      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RAW>(p, batch, stream); break;
-    case EPI_CONV | EPI_F_RELU | EPI_F_DUAL:
-      launch_one_p<BM, BN, WM, WN, NS, EPI_CONV | EPI_F_RELU | EPI_F_DUAL>(p, batch, stream);
-      break;
+    case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSF, EPI_DIST, false>(p, batch, stream); break;
+    case C: launch_one_p<BM, BN, WM, WN, NSF, C, false>(p, batch, stream); break;
+    case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL, false>(p, batch, stream); break;
+    case C | RS: launch_one_p<BM, BN, WM, WN, NSF, C | RS, false>(p, batch, stream); break;
+    case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL, false>(p, batch, stream); break;
+    case C | EPI_F_RAW:
+      launch_one_p<BM, BN, WM, WN, NSF, C | EPI_F_RAW, false>(p, batch, stream); break;
+    case C | RL | EPI_F_DUAL:
+      launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL, false>(p, batch, stream); break;
+    case C | PL: launch_one_p<BM, BN, WM, WN, NSF, C | PL, false>(p, batch, stream); break;
+    case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | PL, false>(p, batch, stream); break;
     default:
       set_error("unknown epilogue for the pipelined bf16x3 GEMM");
       return PPS_ERR_INVALID_ARG;
@@ -431,22 +500,24 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
   return PPS_OK;
 }
 
-// The DMA pieces need 16-byte-aligned 4-float A slots, 8-element B slots and
-// a 32-wide K chunk inside one tap (and, with a fused shortcut, a K switch on
-// a chunk boundary).
+// The DMA pieces need 16-byte-aligned 4-float (or 8-bf16) A slots, 8-element
+// B slots and a 32-wide K chunk inside one tap (and, with a fused shortcut, a
+// K switch on a chunk boundary); the epilogue moves 4-column vectors.
+static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 bool x3p_eligible(const GemmParams& p, int epi) {
-  if (p.Cin % 32 != 0 || p.lda % 4 != 0 || p.ldb % 8 != 0) return false;
+  if (p.Cin % 32 != 0 || p.ldb % 8 != 0) return false;
+  if (p.a3 ? (p.lda % 8 != 0 || p.a2 || !al16(p.a3) || p.a_plane % 8 != 0) : p.lda % 4 != 0)
+    return false;
   if (p.a2 && (p.Kloop1 % 32 != 0 || (p.Kloop - p.Kloop1) % 32 != 0 || p.lda2 % 4 != 0))
     return false;
   // 16-byte epilogue vectors (the distance epilogue falls back per row)
   if (!(epi & EPI_DIST)) {
-    if (p.Ncol % 4 != 0 || p.ldo % 4 != 0 || (reinterpret_cast<uintptr_t>(p.out) & 15) != 0)
+    if (p.Ncol % 4 != 0 || p.ldo % 4 != 0) return false;
+    if ((epi & EPI_F_PLANES) ? (!p.out3 || !al16(p.out3) || p.out_plane % 4 != 0) : !al16(p.out))
       return false;
-    if (p.residual && (p.ldr % 4 != 0 || (reinterpret_cast<uintptr_t>(p.residual) & 15) != 0))
-      return false;
-    if ((p.scale && (reinterpret_cast<uintptr_t>(p.scale) & 15) != 0) ||
-        (p.shift && (reinterpret_cast<uintptr_t>(p.shift) & 15) != 0) ||
-        p.out_bstride % 4 != 0 || p.out_sstride % 4 != 0 || p.ss_bstride % 4 != 0)
+    if (p.residual && (p.ldr % 4 != 0 || !al16(p.residual))) return false;
+    if ((p.scale && !al16(p.scale)) || (p.shift && !al16(p.shift)) || p.out_bstride % 4 != 0 ||
+        p.out_sstride % 4 != 0 || p.ss_bstride % 4 != 0)
       return false;
   }
   return true;
@@ -454,13 +525,15 @@ bool x3p_eligible(const GemmParams& p, int epi) {
 
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
   switch (variant) {
-    case 0: return launch_tile_p<128, 128, 2, 2, 3>(p, epi, batch, stream);
-    case 1: return launch_tile_p<192, 128, 2, 2, 3>(p, epi, batch, stream);
-    case 2: return launch_tile_p<128, 64, 2, 2, 3>(p, epi, batch, stream);
-    case 3: return launch_tile_p<192, 64, 2, 2, 3>(p, epi, batch, stream);
-    case 4: return launch_tile_p<256, 128, 4, 2, 2>(p, epi, batch, stream);
-    case 5: return launch_tile_p<128, 256, 2, 4, 2>(p, epi, batch, stream);
-    case 6: return launch_tile_p<192, 256, 2, 4, 2>(p, epi, batch, stream);
+    case 0: return launch_tile_p<128, 128, 2, 2, 3, 3>(p, epi, batch, stream);
+    case 1: return launch_tile_p<192, 128, 2, 2, 3, 2>(p, epi, batch, stream);
+    case 2: return launch_tile_p<128, 64, 2, 2, 3, 3>(p, epi, batch, stream);
+    case 3: return launch_tile_p<192, 64, 2, 2, 3, 3>(p, epi, batch, stream);
+    case 4: return launch_tile_p<256, 128, 4, 2, 2, 2>(p, epi, batch, stream);
+    case 5: return launch_tile_p<128, 256, 2, 4, 2, 2>(p, epi, batch, stream);
+    case 6:  // 192x256 with plane A needs 168 KB for two stages: 128x256 instead
+      if (p.a3) return launch_tile_p<128, 256, 2, 4, 2, 2>(p, epi, batch, stream);
+      return launch_tile_p<192, 256, 2, 4, 2, 0>(p, epi, batch, stream);
     default:
       set_error("unknown pipelined GEMM variant " + std::to_string(variant));
       return PPS_ERR_INVALID_ARG;

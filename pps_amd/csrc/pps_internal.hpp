@@ -37,7 +37,10 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // ---- GEMM core (gemm_f32.hip) ----------------------------------------------
 constexpr int64_t kMaxBufBytes = (int64_t)1 << 31;  // buffer-resource addressing limit
-enum Epi { EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16 };
+enum Epi {
+  EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16,
+  EPI_F_PLANES = 32  // gemm_x3p.hip: result written as three bf16 planes (out3)
+};
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
   GEMM_TILE_128x128 = 1,
@@ -106,6 +109,14 @@ struct GemmParams {
   // EPI_DIST in the bf16x3 GEMM: precomputed squared norms of A rows / B rows
   const float* norm_a;
   const float* norm_b;
+  // bf16x3 activation planes (gemm_x3p.hip only): A read from three bf16
+  // planes a3 + k * a_plane with the NHWC indexing of `a` (x = sum of the
+  // planes exactly); with EPI_F_PLANES the result is written as three planes
+  // out3 + k * out_plane, indexed like `out`
+  const uint16_t* a3;
+  int64_t a_plane;
+  uint16_t* out3;
+  int64_t out_plane;
 };
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);

@@ -20,6 +20,8 @@ Sum and ReLU fused into branch2c's epilogue; the 31 head convs run as one
 batched GEMM; the unused FC logits (reid_heads.py:84-90) are not computed;
 batch N instead of the reference's batch-1 Reshape([1,-1]).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -265,10 +267,20 @@ class PPSModel(object):
     on the current CUDA device, H x W = REID.SCALE[::-1].
     """
 
-    def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True, math=None):
+    def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True, math=None,
+                 act_planes=None):
         """math: 'x3' (default; f32 products on bf16 matrix cores, weights
         split once into three bf16 planes -- gemm_x3.hip) or 'f32' (exact
-        f32 MFMA, gemm_f32.hip).  Env PPS_MATH overrides the default."""
+        f32 MFMA, gemm_f32.hip).  Env PPS_MATH overrides the default.
+
+        act_planes (x3 only; default on, env PPS_ACT_PLANES=0 disables):
+        a bottleneck intermediate read only by the next conv (branch2a ->
+        2b -> 2c) may be written by its producer's epilogue as bf16x3 planes
+        and read as such (ops.conv2d_bn_act_x3p), so the consumer's K loop
+        skips the operand split at the price of 6 instead of 4 bytes per
+        element.  Which edges use planes is a speed choice made per edge by
+        autotune() (heuristic before that: the 3x3 convs with Cin >= 256);
+        the bits are the same either way."""
         self.math = math or ops.default_math()
         if self.math not in ('x3', 'f32'):
             raise ValueError("math must be 'x3' or 'f32', got %r" % self.math)
@@ -337,9 +349,58 @@ class PPSModel(object):
             for L in self.layers:
                 if L['op'] in ('conv', 'conv_dual', 'heads'):
                     L['w'] = ops.split_bf16x3(L['w'], batched=L['op'] == 'heads')
-        self.feat_dim = self.plan.feat_dim
+        if act_planes is None:
+            act_planes = os.environ.get('PPS_ACT_PLANES', '1') != '0'
+        self.act_planes = bool(act_planes) and self.math == 'x3'
         self._bufs = {}
+        self._edges = self._plane_edges() if self.act_planes else []
+        self.set_planes([P['name'] for P, C in self._edges
+                         if C['k'] > 1 and C['cin'] >= 256])
+        self.feat_dim = self.plan.feat_dim
         self._batch = None
+
+    def _plane_edges(self):
+        """(producer, consumer) conv pairs whose tensor may travel as bf16x3
+        planes: the producer's output has exactly one reader, a plain conv
+        taking it as its main input with Cin % 32 == 0 (the pipelined GEMM's
+        staging unit) -- never a residual, shortcut or pooling input."""
+        readers = {}
+        for L in self.layers:
+            for key in ('input', 'input2', 'residual'):
+                if L.get(key):
+                    readers.setdefault(L[key], []).append((L, key))
+        edges = []
+        for L in self.layers:
+            rs = readers.get(L['output'], [])
+            if (L['op'] == 'conv' and L['cin_eff'] % 4 == 0 and L['cout'] % 4 == 0
+                    and L['output'] != self.plan.output and len(rs) == 1
+                    and rs[0][0]['op'] == 'conv' and rs[0][1] == 'input'
+                    and rs[0][0]['cin_eff'] % 32 == 0):
+                edges.append((L, rs[0][0]))
+        return edges
+
+    def _set_edge(self, P, C, on):
+        P['planes_out'] = C['planes_in'] = bool(on)
+        name = P['output']
+        if name in self._bufs:  # swap the one buffer if already allocated
+            old = self._bufs[name]
+            shape = tuple(old.shape[1:]) if old.dtype == torch.int16 else tuple(old.shape)
+            is_pl = old.dtype == torch.int16
+            if is_pl != bool(on):
+                self._bufs[name] = (ops.act_planes(shape, self.device) if on else
+                                    torch.empty(shape, dtype=torch.float32, device=self.device))
+
+    def planes(self):
+        """Names of the conv layers whose output travels as bf16x3 planes."""
+        return [P['name'] for P, C in self._edges if P.get('planes_out')]
+
+    def set_planes(self, producers):
+        names = set(producers)
+        known = {P['name'] for P, C in self._edges}
+        if names - known:
+            raise ValueError('not a plane-eligible producer: %s' % sorted(names - known)[:3])
+        for P, C in self._edges:
+            self._set_edge(P, C, P['name'] in names)
 
     # -- activation buffers (allocated once per batch size) -----------------
     def _alloc(self, N, H, W):
@@ -396,7 +457,9 @@ class PPSModel(object):
                                    4 * HEAD_SPLITK * N * nb * L['dim_inner'])
             else:
                 L['bytes'] = 0.0
-        self._bufs = {k: torch.empty(v, dtype=torch.float32, device=self.device)
+        planes = {L['output'] for L in self.layers if L.get('planes_out')}
+        self._bufs = {k: (ops.act_planes(v, self.device) if k in planes else
+                          torch.empty(v, dtype=torch.float32, device=self.device))
                       for k, v in shapes.items() if k != 'data'}
         self._batch = (N, H, W)
 
@@ -413,7 +476,13 @@ class PPSModel(object):
     def _run(self, L, bufs, out=None, tile=None):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
-        if op == 'conv':
+        if op == 'conv' and (L.get('planes_in') or L.get('planes_out')):
+            tile = tile if tile >= ops.TILE_P_FIRST else 0  # planes: pipelined tiles only
+            res = bufs[L['residual']] if L['residual'] else None
+            ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+                                  L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
+                                  res, L['relu'], bufs[L['output']], tile=tile)
+        elif op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
                               L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
@@ -462,20 +531,22 @@ class PPSModel(object):
                 timer.append((L.get('name', L['output']), L['op'], L['flops'], ev0, ev1))
         return bufs[self.plan.output]
 
-    def autotune(self, x, reps=3, tiles=None, finalists=4, final_reps=10):
+    def autotune(self, x, reps=3, tiles=None, finalists=4, final_reps=10, planes=True):
         """Pick the fastest GEMM tile per conv layer by timing every candidate
         on this device (the cudnn_exhaustive_search analogue of the
         reference's DetectionModelHelper, detector.py:58): a screening pass
         over all tiles, then the `finalists` best re-timed with `final_reps`
-        launches each.  Results do not depend on the tile (same per-element
-        accumulation order)."""
+        launches each.  Then (x3 with act_planes) each plane-eligible edge,
+        in forward order, is switched to bf16x3 planes and kept if its two
+        layers, re-tuned, get > 2 % faster.  Results do not depend on the
+        tile or the plane choice (same per-element accumulation order)."""
         self.forward(x)
         torch.cuda.synchronize()
-        bufs = dict(self._bufs)
-        bufs['data'] = x
         cands = list(tiles or range(1, ops.num_tiles() + 1))
 
         def time_tile(L, t, n):
+            bufs = dict(self._bufs)
+            bufs['data'] = x
             for _ in range(2):
                 self._run(L, bufs, tile=t)
             e0 = torch.cuda.Event(enable_timing=True)
@@ -487,15 +558,38 @@ class PPSModel(object):
             e1.synchronize()
             return e0.elapsed_time(e1) / n
 
-        report = {}
-        for L in self.layers:
-            if L['op'] not in ('conv', 'conv_dual', 'heads'):
-                continue
-            times = {t: time_tile(L, t, reps) for t in cands}
+        def tune(L):
+            lc = cands
+            if L.get('planes_in') or L.get('planes_out'):
+                lc = [t for t in cands if t >= ops.TILE_P_FIRST] or [0]
+            times = {t: time_tile(L, t, reps) for t in lc}
             best = sorted(times, key=times.get)[:finalists]
             final = {t: time_tile(L, t, final_reps) for t in best}
             L['tile'] = min(final, key=final.get)
+            return final[L['tile']], times
+
+        tune_planes = planes and self.act_planes
+        if tune_planes:
+            self.set_planes([])
+        report, cost = {}, {}
+        for L in self.layers:
+            if L['op'] not in ('conv', 'conv_dual', 'heads'):
+                continue
+            cost[id(L)], times = tune(L)
             report[L.get('name', L['output'])] = (L['tile'], times)
+        if tune_planes:
+            for P, C in self._edges:
+                before = cost[id(P)] + cost[id(C)]
+                saved = P['tile'], C['tile']
+                self._set_edge(P, C, True)
+                (cp, tp), (cc, tc) = tune(P), tune(C)
+                if cp + cc < 0.98 * before:
+                    cost[id(P)], cost[id(C)] = cp, cc
+                    report[P['name']] = (P['tile'], tp)
+                    report[C['name']] = (C['tile'], tc)
+                else:
+                    self._set_edge(P, C, False)
+                    P['tile'], C['tile'] = saved
         return report
 
     def tiles(self):

@@ -18,6 +18,9 @@ from . import _lib
 from ._lib import METRICS, call
 
 
+TILE_P_FIRST = 29  # first pipelined (gemm_x3p.hip) tile id, include/pps_abi.h
+
+
 def num_tiles():
     return _lib.lib().pps_gemm_num_tiles()
 
@@ -76,9 +79,14 @@ class GalleryIndex(object):
         return self.feats.shape
 
 
-def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None):
+def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes=None):
     """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244).
-    g may be a GalleryIndex (then the x3 kernel runs on its prepared planes)."""
+    g may be a GalleryIndex (then the x3 kernel runs on its prepared planes).
+    q_planes (x3): also split the queries into bf16x3 planes first so the
+    pipelined GEMM stages both operands by DMA (pps_distmat_x3p; pipelined
+    tiles only).  Same bits either way; measured at the Market shape it is
+    not faster (scripts/dist_probe.py: the split in the K loop is hidden),
+    so None = off."""
     math = 'x3' if isinstance(g, GalleryIndex) else (math or default_math())
     if q.dim() != 2 or len(g.shape) != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
@@ -93,6 +101,12 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None):
         return out
     idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g)
     qsq = row_sqnorm(q)
+    if q_planes:
+        q3 = split_bf16x3(q)
+        call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
+             _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
+             METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
+        return out
     call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
          METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
@@ -238,6 +252,50 @@ def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, 
     call(fn, _dev(x, 'x'), N, H, W, cin, ldx, wp, Cout, kpad,
          k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
          int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile), _stream())
+    return y
+
+
+def act_planes(shape, device):
+    """Buffer for a bf16x3 activation tensor: int16 [3, N, H, W, C] holding
+    hi, mid, lo planes with x = hi + mid + lo exactly (split as the x3 GEMMs
+    split f32 operands, so a consumer reading the planes gets the bits it
+    would have computed from the f32 tensor)."""
+    return torch.empty((3,) + tuple(shape), dtype=torch.int16, device=device)
+
+
+def _is_planes(t):
+    return isinstance(t, torch.Tensor) and t.dtype == torch.int16 and t.dim() == 5 \
+        and t.shape[0] == 3
+
+
+def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, residual, relu,
+                      y, tile=0):
+    """conv2d_bn_act on the pipelined bf16x3 GEMM where the input and/or the
+    output are bf16x3 activation planes (act_planes) instead of f32 NHWC:
+    x / y may each be either.  Same bits as the f32-activation call."""
+    xs = x.shape[1:] if _is_planes(x) else x.shape
+    ys = y.shape[1:] if _is_planes(y) else y.shape
+    N, H, W, ldx = xs
+    _, Ho, Wo, Cout = ys
+    if not (isinstance(w3, torch.Tensor) and w3.dtype == torch.int16):
+        raise RuntimeError('activation planes need bf16x3 weights (split_bf16x3)')
+    rp = 0
+    if residual is not None:
+        if tuple(residual.shape) != tuple(ys):
+            raise RuntimeError('residual shape %s != output %s'
+                               % (tuple(residual.shape), tuple(ys)))
+        rp = _dev(residual, 'residual')
+    if _is_planes(x):
+        xp, x3, xpl = 0, _dev(x, 'x planes', torch.int16), x[0].numel()
+    else:
+        xp, x3, xpl = _dev(x, 'x'), 0, 0
+    if _is_planes(y):
+        yp, y3, ypl = 0, _dev(y, 'y planes', torch.int16), y[0].numel()
+    else:
+        yp, y3, ypl = _dev(y, 'y'), 0, 0
+    call('pps_conv2d_bn_act_x3p', xp, x3, xpl, N, H, W, cin, ldx, _dev(w3, 'w', torch.int16),
+         Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
+         int(bool(relu)), yp, y3, ypl, Ho, Wo, Cout, int(tile), _stream())
     return y
 
 

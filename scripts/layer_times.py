@@ -42,9 +42,11 @@ def main():
         if op == 'conv':
             n, ho, wo, co = m._shapes[L['output']]
             shp = 'M=%d N=%d K=%d' % (n * ho * wo, co, L['k'] * L['k'] * L['cin'])
+        if L.get('planes_in') or L.get('planes_out'):
+            op += '/p' + ('i' if L.get('planes_in') else '') + ('o' if L.get('planes_out') else '')
         rows.append((name, op, shp, ms, f / (ms * 1e-3) / 1e12 if f else 0))
     for r in rows:
-        print('%-22s %-8s %-26s %8.3f ms %7.1f TF' % r)
+        print('%-22s %-11s %-26s %8.3f ms %7.1f TF' % r)
     print('total %.3f ms' % tot)
 
 

@@ -143,3 +143,108 @@ def test_heads_splitk_x3(splitk):
     e_x3 = _rel_err(part.sum(0).cpu().numpy(), ref)
     assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
 
+
+
+def _planes_of(t):
+    """f32 NHWC tensor -> bf16x3 activation planes [3, N, H, W, C]."""
+    from pps_amd import ops
+    return ops.split_bf16x3(t.contiguous().view(-1)).view((3,) + tuple(t.shape))
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 96, 32, 64, 64, 3, 1, 1),      # res2 branch2b
+    (2, 24, 8, 512, 2048, 1, 1, 0),    # res5 branch2c
+    (1, 24, 8, 512, 512, 3, 1, 1),     # res5 branch2b
+    (3, 7, 5, 32, 40, 3, 1, 1),        # ragged M and N
+    (1, 11, 9, 64, 36, 3, 2, 1),       # ragged, strided
+])
+@pytest.mark.parametrize('residual', [False, True])
+def test_conv_x3_activation_planes(N, H, W, Cin, Cout, k, s, p, residual):
+    """pps_conv2d_bn_act_x3p: planes in and/or out give the same bits as the
+    f32-activation call, on every pipelined tile; written planes sum exactly
+    to the f32 output."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(7 + N + H + Cin + Cout + k)
+    x = _cuda(rng.randn(N, H, W, Cin))
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    scale = _cuda(rng.uniform(0.5, 1.5, Cout))
+    shift = _cuda(rng.randn(Cout) * 0.1)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = _cuda(rng.randn(N, Ho, Wo, Cout)) if residual else None
+    y = torch.empty((N, Ho, Wo, Cout), dtype=torch.float32, device='cuda')
+    ops.conv2d_bn_act(x, Cin, w3, kpad, k, s, p, 1, scale, shift, res, True, y)
+    want = y.cpu().numpy()
+    xp = _planes_of(x)
+    for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+        yo = torch.full_like(y, float('nan'))
+        ops.conv2d_bn_act_x3p(xp, Cin, w3, kpad, k, s, p, 1, scale, shift, res, True, yo,
+                              tile=tile)
+        np.testing.assert_array_equal(yo.cpu().numpy(), want, err_msg='planes in, tile %d' % tile)
+        if residual:
+            continue  # plane outputs feed convs only (no residual epilogue with planes)
+        for src in (x, xp):
+            yp = ops.act_planes(y.shape, 'cuda').fill_(-1)
+            ops.conv2d_bn_act_x3p(src, Cin, w3, kpad, k, s, p, 1, scale, shift, None, True,
+                                  yp, tile=tile)
+            got = yp.view(torch.bfloat16).double().sum(0).cpu().numpy()
+            np.testing.assert_array_equal(got, want.astype(np.float64),
+                                          err_msg='planes out, tile %d' % tile)
+            np.testing.assert_array_equal(yp.cpu().numpy(), _planes_of(y).cpu().numpy())
+
+
+def test_conv_x3_planes_rejects_register_tiles():
+    from pps_amd import ops
+    x = torch.zeros((1, 4, 4, 32), device='cuda')
+    w3 = torch.zeros((3, 32, 32), dtype=torch.int16, device='cuda')
+    v = torch.zeros(32, device='cuda')
+    y = ops.act_planes((1, 4, 4, 32), 'cuda')
+    with pytest.raises(RuntimeError, match='pipelined tile'):
+        ops.conv2d_bn_act_x3p(x, 32, w3, 32, 1, 1, 0, 1, v, v, None, False, y, tile=1)
+
+
+def test_forward_act_planes_same_bits():
+    """The whole forward with bottleneck intermediates as planes equals the
+    f32-intermediate forward bit for bit."""
+    from pps_amd import config, model
+    cfg = config.cfg
+    cfg.MODEL.NUM_CLASSES = 752
+    cfg.MODEL.USE_BN = True
+    cfg.RESNETS.RES5_STRIDE = 1
+    cfg.REID.SCALE = (128, 384)
+    cfg.REID.BPM_STRIP_NUM = 5
+    cfg.REID.BPM_DIM = 128
+    cfg.REID.NORMALIZE_FEATURE = True
+    cfg.REID.MAX_AVE_FEATURE = True
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=1)
+    rng = np.random.RandomState(1)
+    x = np.zeros((4, 384, 128, 4), np.float32)
+    x[..., :3] = rng.randn(4, 384, 128, 3) * 50
+    xd = _cuda(x)
+    m_pl = model.PPSModel(blobs, math='x3', act_planes=True)
+    m_f = model.PPSModel(blobs, math='x3', act_planes=False)
+    m_pl.set_planes([P['name'] for P, C in m_pl._edges])
+    # 2a and 2b of every bottleneck but the 2b's feeding a fused shortcut
+    assert len(m_pl.planes()) == 28, m_pl.planes()
+    a = m_pl.forward(xd).cpu().numpy()
+    b = m_f.forward(xd).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('Q,G,D', [(300, 1000, 3968), (37, 501, 64), (1, 7, 2048)])
+def test_distmat_query_planes_same_bits(Q, G, D):
+    """pps_distmat_x3p (queries pre-split into planes) == pps_distmat_x3 bit
+    for bit on every pipelined tile, and within 1e-4 of the f32 formula."""
+    from oracle import evaluator as ev
+    from pps_amd import ops
+    rng = np.random.RandomState(Q + G)
+    qn = rng.randn(Q, D).astype(np.float32)
+    gn = rng.randn(G, D).astype(np.float32)
+    q, idx = _cuda(qn), ops.GalleryIndex(_cuda(gn))
+    want = ops.compute_dist(q, idx, q_planes=False, tile=ops.TILE_P_FIRST).cpu().numpy()
+    for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+        got = ops.compute_dist(q, idx, q_planes=True, tile=tile).cpu().numpy()
+        np.testing.assert_array_equal(got, want, err_msg='tile %d' % tile)
+    np.testing.assert_allclose(want, ev.compute_dist(qn, gn), rtol=0, atol=1e-4 * np.sqrt(D / 64))
