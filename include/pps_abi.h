@@ -53,8 +53,12 @@ const char* pps_registered_ops(void);
  * 16 / 32, A staged as planes / f32; the f32 kernels use 128-row tiles),
  * 29..35 = the `_x3` LDS-DMA pipelined tiles (128x128, 192x128, 128x64,
  * 192x64, 256x128, 128x256, 192x256; K chunk 32; the f32 kernels use the
- * heuristic).  Results are identical for every tile (same per-element fp32
- * MFMA accumulation order); only speed differs, so callers may autotune. */
+ * heuristic), 36..42 = the same pipelined tiles on 16x16x32 MFMA blocks
+ * (192x256 -> 128x256).  Results are identical for every tile below 36
+ * (same per-element fp32 MFMA accumulation order) and identical among the
+ * tiles from 36 on (one MFMA sums a 32-wide K chunk: a different rounding
+ * sequence, same f32-level error); only speed differs, so callers may
+ * autotune. */
 int pps_gemm_num_tiles(void);
 
 /* ---- retrieval: distance matrix ------------------------------------------

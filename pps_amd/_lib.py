@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libpps_hip.so')
+# PPS_LIB_PATH: load an alternative build (kernel experiments, scripts/)
+LIB_PATH = os.environ.get('PPS_LIB_PATH') or os.path.join(_HERE, 'libpps_hip.so')
 
 c_f32p = ctypes.c_void_p
 c_i64 = ctypes.c_int64

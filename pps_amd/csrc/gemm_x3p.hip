@@ -54,18 +54,43 @@ __device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
   return c;
 }
 
+// The same six terms on v_mfma_f32_16x16x32_bf16 (S = 16 tiles): one MFMA
+// covers a whole 32-wide K chunk, so its rounding differs from the 32x32x16
+// form -- S = 16 tiles agree bit for bit with each other, not with S = 32.
+// Transposed accumulator: lane l keeps output row (l & 15) and columns
+// 4 (l >> 4) + e, e = 0..3 (one 16-byte vector per block).
+__device__ inline f32x4 mfma16_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = mfma16_bf16(b[0], a[0], c);
+  c = mfma16_bf16(b[0], a[1], c);
+  c = mfma16_bf16(b[1], a[0], c);
+  c = mfma16_bf16(b[0], a[2], c);
+  c = mfma16_bf16(b[1], a[1], c);
+  c = mfma16_bf16(b[2], a[0], c);
+  return c;
+}
+
+template <int S> struct AccT { typedef f32x16 type; };
+template <> struct AccT<16> { typedef f32x4 type; };
+
 // Convolution epilogue on transposed accumulators (see mfma_x3t):
 //   y = acc * scale + shift [+ residual] [ReLU]; DUAL: scale folded into the
 //   weights; RAW: store acc; PLANES: write y as three bf16 planes (exact
 //   split, 8-byte stores per plane).  Needs Ncol, ldo (and ldr) % 4 == 0
 //   (x3p_eligible).
-template <int EPI, int BM, int BN, int WM, int WN>
+// S = MFMA block (32: 32x32x16, lane row l & 31, columns 8q + 4 (l >> 5) + e;
+// 16: 16x16x32, lane row l & 15, columns 4 (l >> 4) + e); r32 = l % S,
+// h = l / S.
+template <int EPI, int BM, int BN, int WM, int WN, int S = 32>
 __device__ inline void conv_epilogue_t(const GemmParams& p,
-                                       f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int batch,
-                                       int kslice, int m0, int n0, int wm, int wn, int r32,
-                                       int h) {
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
+                                       typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                       int batch, int kslice, int m0, int n0, int wm, int wn,
+                                       int r32, int h) {
+  constexpr int TM = BM / WM / S;
+  constexpr int TN = BN / WN / S;
+  constexpr int NQ = S * S / 256;  // 16-byte column groups per lane and block
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
@@ -83,10 +108,10 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   const int ldr = (int)p.ldr;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int cb = wn * (BN / WN) + j * 32 + 4 * h;
-    f32x4 s4[4], t4[4];
+    const int cb = wn * (BN / WN) + j * S + 4 * h;
+    f32x4 s4[NQ], t4[NQ];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const bool ok = cb + 8 * q < nrem;
       s4[q] = (DUAL || RAW || !ok) ? (f32x4){1.f, 1.f, 1.f, 1.f}
                                    : *reinterpret_cast<const f32x4*>(sc + cb + 8 * q);
@@ -95,17 +120,17 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int rr = wm * (BM / WM) + i * 32 + r32;
+      const int rr = wm * (BM / WM) + i * S + r32;
       if (rr >= mrem) continue;
-      f32x4 rv[4];
+      f32x4 rv[NQ];
       if (HAS_RES) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < NQ; ++q)
           rv[q] = cb + 8 * q < nrem ? *reinterpret_cast<const f32x4*>(res + rr * ldr + cb + 8 * q)
                                     : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         if (cb + 8 * q >= nrem) continue;
         f32x4 v;
 #pragma unroll
@@ -132,12 +157,13 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
 
 // Distance epilogue on transposed accumulators: same formulas as
 // dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int S = 32>
 __device__ inline void dist_epilogue_t(const GemmParams& p,
-                                       f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0,
-                                       int wm, int wn, int r32, int h) {
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
+                                       typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                       int m0, int n0, int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / S;
+  constexpr int TN = BN / WN / S;
+  constexpr int NQ = S * S / 256;
   float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;
@@ -147,24 +173,24 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
   float qn[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int rr = wm * (BM / WM) + i * 32 + r32;
+    const int rr = wm * (BM / WM) + i * S + r32;
     qn[i] = rr < mrem ? qsq[rr] : 0.f;
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int cb = wn * (BN / WN) + j * 32 + 4 * h;
-    float gn[16];
+    const int cb = wn * (BN / WN) + j * S + 4 * h;
+    float gn[4 * NQ];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 4 * NQ; ++r) {
       const int c = cb + 8 * (r >> 2) + (r & 3);
       gn[r] = c < nrem ? p.norm_b[n0 + c] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int rr = wm * (BM / WM) + i * 32 + r32;
+      const int rr = wm * (BM / WM) + i * S + r32;
       if (rr >= mrem) continue;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const int c = cb + 8 * q;
         if (c >= nrem) continue;
         f32x4 v;
@@ -200,13 +226,17 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
 // fragment read.  A3 = true: A is three bf16 planes (written by a producer
 // epilogue with EPI_F_PLANES), staged like B as 64-byte rows per plane --
 // no split arithmetic in the main loop.
-template <int BM, int BN, int WM, int WN, int EPI, int NS, bool A3>
+// S: MFMA block, 32 (v_mfma_f32_32x32x16_bf16, two 16-wide K groups per
+// chunk) or 16 (v_mfma_f32_16x16x32_bf16, one group per chunk; the wave's
+// column blocks are processed in two halves to keep the same pipeline).
+template <int BM, int BN, int WM, int WN, int EPI, int NS, bool A3, int S = 32>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int BK = 32;
   constexpr int NW = WM * WN;
-  constexpr int TM = BM / WM / 32;
-  constexpr int TN = BN / WN / 32;
+  constexpr int TM = BM / WM / S;
+  constexpr int TN = BN / WN / S;
+  static_assert(S == 32 || (S == 16 && TN % 2 == 0), "MFMA block");
   constexpr int A_PLANE = BM * BK * 2;  // A3: bf16 rows of 64 B per plane
   constexpr int A_BYTES = A3 ? 3 * A_PLANE : BM * BK * 4;  // else f32 rows of 128 B
   constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
@@ -218,7 +248,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   static_assert(AI * AROWS * NW == BM && BPW * 16 * NW == BN,
                 "tile does not split into DMA pieces");
   static_assert(!(A3 && (EPI & EPI_F_DUAL)), "fused shortcut reads f32 activations");
-  static_assert(TM >= 1 && TN >= 1 && (BM / WM) % 32 == 0 && (BN / WN) % 32 == 0, "wave tile");
+  static_assert(TM >= 1 && TN >= 1 && (BM / WM) % S == 0 && (BN / WN) % S == 0, "wave tile");
   static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
   static_assert(NLOAD * (NS - 2) <= 63, "vmcnt range");
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
@@ -229,8 +259,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN;
   const int wn = wave - wm * WN;
-  const int r32 = lane & 31;
-  const int h = lane >> 5;
+  const int r32 = lane & (S - 1);  // lane's row within an MFMA block
+  const int h = lane / S;          // its K slot (S = 16: 0..3) / column half (S = 32)
 
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tile_m = bid / tiles_n;
@@ -355,52 +385,18 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     siss = siss + 1 == NS ? 0 : siss + 1;
   };
 
-  f32x16 acc[TM][TN];
+  typename AccT<S>::type acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < S * S / 64; ++r) acc[i][j][r] = 0.f;
 
-  // Fragment reads of one 16-wide K group g of a stage, A split into its
-  // three bf16 terms.  The rows of this lane are r32 mod 32, so both
-  // swizzles are per-lane constants.
+  // Fragment reads: the rows of this lane are r32 mod S, so both swizzles
+  // are per-lane constants.
   const int asw = (r32 >> 1) & 7;
   const int bsw = (r32 >> 2) & 3;
-  auto read_split = [&](const unsigned char* st, int g, bf16x8 (&fa)[TM][3],
-                        bf16x8 (&fb)[TN][3]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (A3) {
-        const unsigned char* ap =
-            st + (wm * (BM / WM) + i * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * A_PLANE);
-      } else {
-        const unsigned char* rp = st + (wm * (BM / WM) + i * 32 + r32) * 128;
-        const int c0 = 4 * g + 2 * h;
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + ((c0 ^ asw) << 4));
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((c0 + 1) ^ asw) << 4));
-        split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const unsigned char* bp =
-          st + A_BYTES + (wn * (BN / WN) + j * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        fb[j][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
-    }
-  };
-  auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_x3t(fa[i], fb[j], acc[i][j]);
-  };
   // chunk kc has landed for every wave once each wave saw its own pieces
   // retire (counted vmcnt: the NS-2 younger chunks stay in flight) and all
   // waves passed the barrier; the barrier also retires every wave's reads of
@@ -412,52 +408,162 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     asm volatile("" ::: "memory");
   };
 
-  // Software pipeline over 16-wide K groups (two per chunk): the reads and
-  // the split of group q+1 are issued in the same basic block as the MFMAs
-  // of group q, so the scheduler interleaves them.  Requests run NS-1 chunks
-  // ahead; requests past the last chunk read zeros into stages that are
-  // never consumed, which keeps every wait count uniform.
+  // Requests run NS-1 chunks ahead; requests past the last chunk read zeros
+  // into stages that are never consumed, which keeps every wait count uniform.
   const int nchunks = (p.Kloop + BK - 1) / BK;
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue();
+  for (int st = 0; st < NS - 1; ++st) issue();
   chunk_barrier();
   issue();
-  bf16x8 fa0[TM][3], fb0[TN][3], fa1[TM][3], fb1[TN][3];
-  read_split(lds, 0, fa0, fb0);
-  int scur = 0;
-  for (int kc = 0; kc < nchunks - 1; ++kc) {
-    const unsigned char* st = lds + scur * STAGE;
-    scur = scur + 1 == NS ? 0 : scur + 1;
-    read_split(st, 1, fa1, fb1);
+  if constexpr (S == 32) {
+    // Fragment reads of one 16-wide K group g of a stage, A split into its
+    // three bf16 terms.
+    auto read_split = [&](const unsigned char* st, int g, bf16x8 (&fa)[TM][3],
+                          bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (A3) {
+          const unsigned char* ap =
+              st + (wm * (BM / WM) + i * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * A_PLANE);
+        } else {
+          const unsigned char* rp = st + (wm * (BM / WM) + i * 32 + r32) * 128;
+          const int c0 = 4 * g + 2 * h;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + ((c0 ^ asw) << 4));
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((c0 + 1) ^ asw) << 4));
+          split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const unsigned char* bp =
+            st + A_BYTES + (wn * (BN / WN) + j * 32 + r32) * 64 + (((2 * g + h) ^ bsw) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          fb[j][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
+      }
+    };
+    auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_x3t(fa[i], fb[j], acc[i][j]);
+    };
+    // Software pipeline over 16-wide K groups (two per chunk): the reads and
+    // the split of group q+1 are issued in the same basic block as the MFMAs
+    // of group q, so the scheduler interleaves them.
+    bf16x8 fa0[TM][3], fb0[TN][3], fa1[TM][3], fb1[TN][3];
+    read_split(lds, 0, fa0, fb0);
+    int scur = 0;
+    for (int kc = 0; kc < nchunks - 1; ++kc) {
+      const unsigned char* st = lds + scur * STAGE;
+      scur = scur + 1 == NS ? 0 : scur + 1;
+      read_split(st, 1, fa1, fb1);
+      mfmas(fa0, fb0);
+      chunk_barrier();
+      issue();
+      read_split(lds + scur * STAGE, 0, fa0, fb0);
+      mfmas(fa1, fb1);
+    }
+    read_split(lds + scur * STAGE, 1, fa1, fb1);
     mfmas(fa0, fb0);
-    chunk_barrier();
-    issue();
-    read_split(lds + scur * STAGE, 0, fa0, fb0);
     mfmas(fa1, fb1);
+  } else {
+    // S = 16: a chunk is one 32-wide K group.  Its A fragments serve both
+    // column halves, so A is double-buffered across chunks (fa0 / fa1
+    // alternate; the loop runs two chunks per trip) and B per half.
+    constexpr int TNH = TN / 2;
+    auto readA16 = [&](const unsigned char* st, bf16x8 (&fa)[TM][3]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (A3) {
+          const unsigned char* ap =
+              st + (wm * (BM / WM) + i * 16 + r32) * 64 + ((h ^ bsw) << 4);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * A_PLANE);
+        } else {
+          const unsigned char* rp = st + (wm * (BM / WM) + i * 16 + r32) * 128;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + (((2 * h) ^ asw) << 4));
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((2 * h + 1) ^ asw) << 4));
+          split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+        }
+      }
+    };
+    auto readB16 = [&](const unsigned char* st, int half, bf16x8 (&fb)[TNH][3]) {
+#pragma unroll
+      for (int jj = 0; jj < TNH; ++jj) {
+        const unsigned char* bp = st + A_BYTES +
+                                  (wn * (BN / WN) + (half * TNH + jj) * 16 + r32) * 64 +
+                                  ((h ^ bsw) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          fb[jj][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
+      }
+    };
+    auto mfmas16 = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TNH][3], int half) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TNH; ++jj)
+          acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
+    };
+    bf16x8 fa0[TM][3], fa1[TM][3], fb0[TNH][3], fb1[TNH][3];
+    readA16(lds, fa0);
+    readB16(lds, 0, fb0);
+    int scur = 0;
+    // one chunk: MFMAs of half 0 beside the reads of half 1, barrier +
+    // request, then the next chunk's A / half-0 B beside half 1's MFMAs
+    auto step = [&](bf16x8 (&fc)[TM][3], bf16x8 (&fn)[TM][3]) {
+      const unsigned char* st = lds + scur * STAGE;
+      scur = scur + 1 == NS ? 0 : scur + 1;
+      readB16(st, 1, fb1);
+      mfmas16(fc, fb0, 0);
+      chunk_barrier();
+      issue();
+      readA16(lds + scur * STAGE, fn);
+      readB16(lds + scur * STAGE, 0, fb0);
+      mfmas16(fc, fb1, 1);
+    };
+    auto tail = [&](bf16x8 (&fc)[TM][3]) {
+      readB16(lds + scur * STAGE, 1, fb1);
+      mfmas16(fc, fb0, 0);
+      mfmas16(fc, fb1, 1);
+    };
+    int kc = 0;
+    for (; kc + 2 < nchunks; kc += 2) {
+      step(fa0, fa1);
+      step(fa1, fa0);
+    }
+    if (kc + 1 < nchunks) {
+      step(fa0, fa1);
+      tail(fa1);
+    } else {
+      tail(fa0);
+    }
   }
-  read_split(lds + scur * STAGE, 1, fa1, fb1);
-  mfmas(fa0, fb0);
-  mfmas(fa1, fb1);
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
 
   if (EPI & EPI_DIST)
-    dist_epilogue_t<BM, BN, WM, WN>(p, acc, m0, n0, wm, wn, r32, h);
+    dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
   else
-    conv_epilogue_t<EPI, BM, BN, WM, WN>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
+    conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3, int S>
 static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS, A3>),
+  hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS, A3, S>),
                      dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p,
                      tiles_m, tiles_n);
 }
 
 // NSF / NSP: LDS stages with f32 / bf16-plane A operands (NSP = 0: the tile
 // does not take plane activations)
-template <int BM, int BN, int WM, int WN, int NSF, int NSP>
+template <int BM, int BN, int WM, int WN, int NSF, int NSP, int S>
 static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
   if constexpr (NSP == 0) {
@@ -467,12 +573,12 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
     }
   } else if (p.a3) {
     switch (epi) {
-      case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSP, EPI_DIST, true>(p, batch, stream); break;
-      case C: launch_one_p<BM, BN, WM, WN, NSP, C, true>(p, batch, stream); break;
-      case C | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RL, true>(p, batch, stream); break;
-      case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL, true>(p, batch, stream); break;
-      case C | PL: launch_one_p<BM, BN, WM, WN, NSP, C | PL, true>(p, batch, stream); break;
-      case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSP, C | RL | PL, true>(p, batch, stream); break;
+      case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSP, EPI_DIST, true, S>(p, batch, stream); break;
+      case C: launch_one_p<BM, BN, WM, WN, NSP, C, true, S>(p, batch, stream); break;
+      case C | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RL, true, S>(p, batch, stream); break;
+      case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL, true, S>(p, batch, stream); break;
+      case C | PL: launch_one_p<BM, BN, WM, WN, NSP, C | PL, true, S>(p, batch, stream); break;
+      case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSP, C | RL | PL, true, S>(p, batch, stream); break;
       default:
         set_error("epilogue not built for bf16-plane activations");
         return PPS_ERR_INVALID_ARG;
@@ -481,17 +587,17 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
     return PPS_OK;
   }
   switch (epi) {
-    case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSF, EPI_DIST, false>(p, batch, stream); break;
-    case C: launch_one_p<BM, BN, WM, WN, NSF, C, false>(p, batch, stream); break;
-    case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL, false>(p, batch, stream); break;
-    case C | RS: launch_one_p<BM, BN, WM, WN, NSF, C | RS, false>(p, batch, stream); break;
-    case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL, false>(p, batch, stream); break;
+    case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSF, EPI_DIST, false, S>(p, batch, stream); break;
+    case C: launch_one_p<BM, BN, WM, WN, NSF, C, false, S>(p, batch, stream); break;
+    case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL, false, S>(p, batch, stream); break;
+    case C | RS: launch_one_p<BM, BN, WM, WN, NSF, C | RS, false, S>(p, batch, stream); break;
+    case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL, false, S>(p, batch, stream); break;
     case C | EPI_F_RAW:
-      launch_one_p<BM, BN, WM, WN, NSF, C | EPI_F_RAW, false>(p, batch, stream); break;
+      launch_one_p<BM, BN, WM, WN, NSF, C | EPI_F_RAW, false, S>(p, batch, stream); break;
     case C | RL | EPI_F_DUAL:
-      launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL, false>(p, batch, stream); break;
-    case C | PL: launch_one_p<BM, BN, WM, WN, NSF, C | PL, false>(p, batch, stream); break;
-    case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | PL, false>(p, batch, stream); break;
+      launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL, false, S>(p, batch, stream); break;
+    case C | PL: launch_one_p<BM, BN, WM, WN, NSF, C | PL, false, S>(p, batch, stream); break;
+    case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | PL, false, S>(p, batch, stream); break;
     default:
       set_error("unknown epilogue for the pipelined bf16x3 GEMM");
       return PPS_ERR_INVALID_ARG;
@@ -523,21 +629,32 @@ bool x3p_eligible(const GemmParams& p, int epi) {
   return true;
 }
 
-int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
-  switch (variant) {
-    case 0: return launch_tile_p<128, 128, 2, 2, 3, 3>(p, epi, batch, stream);
-    case 1: return launch_tile_p<192, 128, 2, 2, 3, 2>(p, epi, batch, stream);
-    case 2: return launch_tile_p<128, 64, 2, 2, 3, 3>(p, epi, batch, stream);
-    case 3: return launch_tile_p<192, 64, 2, 2, 3, 3>(p, epi, batch, stream);
-    case 4: return launch_tile_p<256, 128, 4, 2, 2, 2>(p, epi, batch, stream);
-    case 5: return launch_tile_p<128, 256, 2, 4, 2, 2>(p, epi, batch, stream);
-    case 6:  // 192x256 with plane A needs 168 KB for two stages: 128x256 instead
-      if (p.a3) return launch_tile_p<128, 256, 2, 4, 2, 2>(p, epi, batch, stream);
-      return launch_tile_p<192, 256, 2, 4, 2, 0>(p, epi, batch, stream);
+// variants 0..6: 32x32x16 MFMA blocks (bit-identical to gemm_x3.hip);
+// 7..13: the same tiles on 16x16x32 MFMA blocks (bit-identical among
+// themselves, f32-level like the others).
+template <int S>
+static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t stream, int v) {
+  switch (v) {
+    case 0: return launch_tile_p<128, 128, 2, 2, 3, 3, S>(p, epi, batch, stream);
+    case 1: return launch_tile_p<192, 128, 2, 2, 3, 2, S>(p, epi, batch, stream);
+    case 2: return launch_tile_p<128, 64, 2, 2, 3, 3, S>(p, epi, batch, stream);
+    case 3: return launch_tile_p<192, 64, 2, 2, 3, 3, S>(p, epi, batch, stream);
+    case 4: return launch_tile_p<256, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
+    case 5: return launch_tile_p<128, 256, 2, 4, 2, 2, S>(p, epi, batch, stream);
+    case 6:
+      // 192x256 with plane A needs 168 KB for two stages, and on 16x16 blocks
+      // more than the 256 VGPRs of an 8-wave workgroup: 128x256 instead
+      if (p.a3 || S == 16) return launch_tile_p<128, 256, 2, 4, 2, 2, S>(p, epi, batch, stream);
+      if constexpr (S == 32) return launch_tile_p<192, 256, 2, 4, 2, 0, S>(p, epi, batch, stream);
     default:
-      set_error("unknown pipelined GEMM variant " + std::to_string(variant));
+      set_error("unknown pipelined GEMM variant " + std::to_string(v));
       return PPS_ERR_INVALID_ARG;
   }
+}
+
+int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
+  if (variant >= 7) return launch_variant<16>(p, epi, batch, stream, variant - 7);
+  return launch_variant<32>(p, epi, batch, stream, variant);
 }
 
 }  // namespace pps

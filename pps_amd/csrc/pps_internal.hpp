@@ -61,7 +61,9 @@ enum GemmTile {
   // 128x128, 192x128, 128x64, 192x64 (4 waves, 3 stages), 256x128, 128x256,
   // 192x256 (8 waves, 2 stages)
   GEMM_TILE_P_FIRST = 29,
-  GEMM_NUM_TILES = 36
+  // 36..42 (bf16x3 only): ids 29..35 on 16x16x32 MFMA blocks (own rounding)
+  GEMM_TILE_P16_FIRST = 36,
+  GEMM_NUM_TILES = 43
 };
 
 struct GemmParams {

