@@ -209,10 +209,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # PPS_DIST_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
+    # the devices there are (one-GPU box); the product path is nccl (= RCCL)
+    backend = os.environ.get('PPS_DIST_BACKEND', 'nccl')
+    if backend == 'gloo':
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     from pps_amd import model, ops
     from pps_amd import distributed as pdist
     cfg = market_cfg()
