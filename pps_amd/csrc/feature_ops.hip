@@ -447,16 +447,11 @@ struct Means {
 // batch (offsets == nullptr) or a ragged blob described per image by a byte
 // offset and its own height / width (device arrays), as decoded JPEGs of a
 // dataset with mixed sizes (DukeMTMC-reID) arrive.
-// LDS = true: the block first copies the 4 source rows its output row needs
-// (same clamped rows for every column) into LDS, so each pixel's 48 taps are
-// LDS reads instead of scattered byte loads.
-template <bool LDS>
 __global__ void __launch_bounds__(128)
 preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
                       const int64_t* __restrict__ offsets, const int32_t* __restrict__ heights,
                       const int32_t* __restrict__ widths, Means mean, int Ho, int Wo,
                       float* __restrict__ y) {
-  extern __shared__ uint8_t srows[];
   // block = (output row n*Ho + oy, 128 output columns): no 64-bit index math
   const int row = blockIdx.x;
   const int ox = blockIdx.y * blockDim.x + threadIdx.x;
@@ -479,13 +474,6 @@ preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
 #pragma unroll
   for (int j = 0; j < 4; ++j) yy[j] = min(max(y0 - 1 + j, 0), Hi - 1);
   const int rb = Wi * 3;
-  if (LDS) {
-    for (int t = threadIdx.x; t < 4 * rb; t += blockDim.x) {
-      const int j = t / rb;
-      srows[t] = img[(int64_t)yy[j] * rb + (t - j * rb)];
-    }
-    __syncthreads();
-  }
   if (ox >= Wo) return;
   const float fx = (float)((ox + 0.5) * ((double)Wi / (double)Wo) - 0.5);
   const int x0 = (int)floorf(fx);
@@ -498,7 +486,7 @@ preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
   float acc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint8_t* rowp = LDS ? srows + j * rb : img + (int64_t)yy[j] * rb;
+    const uint8_t* rowp = img + (int64_t)yy[j] * rb;
     float rowv[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -525,7 +513,7 @@ int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* off
   // LDS staging needs the widest image's 4 rows in LDS: known for a dense
   // batch; a ragged batch passes its maximum width as Wi (0 = unknown)
   // (staging the 4 source rows in LDS measured 1.9x slower: byte taps hit L1)
-  hipLaunchKernelGGL(preprocess_bgr_kernel<false>, dim3((unsigned)(N * Ho), (Wo + 127) / 128),
+  hipLaunchKernelGGL(preprocess_bgr_kernel, dim3((unsigned)(N * Ho), (Wo + 127) / 128),
                      dim3(128), 0, st, img, N, Hi, Wi, offsets, heights, widths, m, Ho, Wo, y);
   PPS_CHECK_LAUNCH("preprocess_bgr_kernel");
   return PPS_OK;
