@@ -3,6 +3,7 @@
 // launch parameters and enqueues on the caller's stream.  No allocation, no
 // synchronisation: every entry point is hipGraph-capturable.
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "pps_internal.hpp"
@@ -11,6 +12,13 @@ namespace pps {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = getenv("PPS_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 int maxpool2d(const float*, int, int, int, int, int, int, int, float*, int, int,
               hipStream_t);

@@ -278,7 +278,11 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
                                               : (p.M % 192 == 0 ? 1 : 0);
     return launch_gemm_x3p(p, epi, batch, stream, v);
   }
-  int tile = p.tile ? p.tile : pick_tile(p, batch);
+  // default for the distance matrix: the pipelined 256x128 tile on 16x16x32
+  // blocks (the Market / Duke / 1M-shard autotune winner, scripts/dist_probe.py)
+  int tile = p.tile ? p.tile
+                    : ((epi & EPI_DIST) && x3p_eligible(p, epi) ? GEMM_TILE_P16_FIRST + 4
+                                                                : pick_tile(p, batch));
   if (tile >= GEMM_TILE_P_FIRST) {
     // LDS-DMA pipelined family (gemm_x3p.hip); shapes it cannot stage
     // (Cin % 32 != 0, unaligned rows) take the heuristic register-staged tile

@@ -20,6 +20,21 @@ void set_error(const std::string& msg);
     }                                                                       \
   } while (0)
 
+// PPS_DEBUG_SYNC=1 (debug only; breaks hipGraph capture): synchronize after
+// each checked launch so an asynchronous fault is reported by the kernel
+// that caused it
+bool debug_sync();
+#define PPS_CHECK_LAUNCH_S(name, stream)                                     \
+  do {                                                                       \
+    PPS_CHECK_LAUNCH(name);                                                  \
+    if (::pps::debug_sync()) {                                               \
+      hipError_t s_ = hipStreamSynchronize(stream);                          \
+      if (s_ != hipSuccess) {                                                \
+        ::pps::set_error(std::string(name) + " (sync): " + hipGetErrorString(s_)); \
+        return PPS_ERR_LAUNCH;                                               \
+      }                                                                      \
+    }                                                                        \
+  } while (0)
 #define PPS_CHECK_LAUNCH(name)                                               \
   do {                                                                       \
     hipError_t e_ = hipGetLastError();                                       \

@@ -342,7 +342,12 @@ __global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t l
 #pragma unroll
   for (int u = 0; u < kTopkUnroll; ++u) d[u] = ld((int64_t)u * blockDim.x + threadIdx.x);
   for (int64_t c0 = 0; c0 < G; c0 += chunk) {
-    if (s_n + chunk > kTopkBuf) cut(s_n);  // uniform: s_n read after a barrier
+    // every wave must take the same cut decision: snapshot the count, then
+    // a barrier so that no wave's insertions of this chunk (atomicAdd on
+    // s_n) can land before a slower wave has read it
+    const int n_now = s_n;
+    lds_barrier();
+    if (n_now + chunk > kTopkBuf) cut(n_now);
     const unsigned long long thr = s_thr;
     float dn[kTopkUnroll];
 #pragma unroll

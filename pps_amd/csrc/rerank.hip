@@ -17,6 +17,8 @@
 //  4. rerank_vqe     : V_qe[i] = mean of V rows initial_rank[i,:k2] (:490-494)
 //  5. rerank_csc_*   : inverted index of V_qe                     (:497-499)
 //  6. rerank_jaccard : temp_min, jaccard, lambda blend, [Q][G] out (:501-518)
+#include <vector>
+
 #include "pps_internal.hpp"
 
 namespace pps {
@@ -357,19 +359,31 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   }
   hipLaunchKernelGGL(rerank_colmax_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
                      qg, qq, gg, Q, G, colmax);
+  PPS_CHECK_LAUNCH_S("rerank_colmax_kernel", st);
   hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 31) / 32),
                                                   (unsigned)((N + 31) / 32)),
                      dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od);
-  PPS_CHECK_LAUNCH("rerank_build_od_kernel");
+  PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
   int rc = topk(od, N, N, N, K1, topv, rank, st);
   if (rc != PPS_OK) return rc;
+  PPS_CHECK_LAUNCH_S("rerank topk", st);
+  if (debug_sync()) {  // every neighbour index must address a row of OD
+    std::vector<int32_t> h((size_t)(N * K1));
+    (void)hipMemcpy(h.data(), rank, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+    for (size_t t = 0; t < h.size(); ++t)
+      if (h[t] < 0 || h[t] >= N) {
+        set_error("rerank topk: rank[" + std::to_string(t / K1) + "][" +
+                  std::to_string(t % K1) + "] = " + std::to_string(h[t]));
+        return PPS_ERR_LAUNCH;
+      }
+  }
   hipLaunchKernelGGL(rerank_v_rows_kernel, dim3((unsigned)N), dim3(64), 0, st, od, N, rank,
                      K1, Kh, vcap, v_idx, v_val, v_cnt);
-  PPS_CHECK_LAUNCH("rerank_v_rows_kernel");
+  PPS_CHECK_LAUNCH_S("rerank_v_rows_kernel", st);
   if (k2 != 1) {
     hipLaunchKernelGGL(rerank_vqe_kernel, dim3((unsigned)N), dim3(256), 0, st, N, rank, K1, k2,
                        v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
-    PPS_CHECK_LAUNCH("rerank_vqe_kernel");
+    PPS_CHECK_LAUNCH_S("rerank_vqe_kernel", st);
   } else {
     (void)hipMemcpyAsync(q_idx, v_idx, sizeof(int32_t) * N * vcap, hipMemcpyDeviceToDevice, st);
     (void)hipMemcpyAsync(q_val, v_val, sizeof(float) * N * vcap, hipMemcpyDeviceToDevice, st);
@@ -380,14 +394,16 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   (void)hipMemsetAsync(fill, 0, sizeof(int32_t) * (N + 1), st);
   hipLaunchKernelGGL(rerank_csc_count_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
                      q_val, q_cnt, qc, col_cnt);
+  PPS_CHECK_LAUNCH_S("rerank_csc_count_kernel", st);
   hipLaunchKernelGGL(rerank_scan_kernel, dim3(1), dim3(1024), 0, st, N, col_cnt, start);
+  PPS_CHECK_LAUNCH_S("rerank_scan_kernel", st);
   hipLaunchKernelGGL(rerank_csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
                      q_val, q_cnt, qc, start, fill, csc_row, csc_val);
-  PPS_CHECK_LAUNCH("rerank_csc_fill_kernel");
+  PPS_CHECK_LAUNCH_S("rerank_csc_fill_kernel", st);
   hipLaunchKernelGGL(rerank_jaccard_kernel, dim3((unsigned)Q), dim3(256), sizeof(float) * N, st,
                      Q, N, od, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam, one_m_lam,
                      out);
-  PPS_CHECK_LAUNCH("rerank_jaccard_kernel");
+  PPS_CHECK_LAUNCH_S("rerank_jaccard_kernel", st);
   return PPS_OK;
 }
 

@@ -41,17 +41,28 @@ def main():
     def ev():
         return torch.cuda.Event(enable_timing=True)
 
+    debug = os.environ.get('PPS_DEBUG_SYNC') == '1'
+
+    def mark(what):  # debug: locate an asynchronous fault stage by stage
+        if debug:
+            torch.cuda.synchronize()
+            print('ok:', what, flush=True)
+
     times = {}
     for rep in range(a.reps + 1):
         e = [ev() for _ in range(5)]
         e[0].record()
         q_g = ops.compute_dist(qf, gf, metric='cosine')
         e[1].record()
+        mark('q_g')
         q_q = ops.compute_dist(qf, qf, metric='cosine')
+        mark('q_q')
         g_g = ops.compute_dist(gf, gf, metric='cosine')
+        mark('g_g')
         e[2].record()
         rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
         e[3].record()
+        mark('re_ranking')
         res = gev.rank_eval(rr, qid, gid, qcam, gcam)
         e[4].record()
         torch.cuda.synchronize()

@@ -25,6 +25,8 @@ def main():
     ap.add_argument('--topk', type=int, default=100)
     ap.add_argument('--math', default='x3')
     ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--tile', type=int, default=-1,
+                    help='distance-GEMM tile (-1: time the pipelined tiles once, keep the best)')
     a = ap.parse_args()
     from pps_amd import ops
     g = torch.Generator(device='cuda')
@@ -38,13 +40,29 @@ def main():
     def ev():
         return torch.cuda.Event(enable_timing=True)
 
+    tile = a.tile
+    if tile < 0:
+        idx0 = ops.GalleryIndex(gal) if a.math == 'x3' else gal
+        best = None
+        for t in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+            ops.compute_dist(q, idx0, out=out, math=a.math, tile=t)
+            e0, e1 = ev(), ev()
+            e0.record()
+            ops.compute_dist(q, idx0, out=out, math=a.math, tile=t)
+            e1.record()
+            e1.synchronize()
+            if best is None or e0.elapsed_time(e1) < best[1]:
+                best = (t, e0.elapsed_time(e1))
+        tile = best[0]
+        del idx0
+
     res = {}
     for rep in range(a.reps + 1):
         e = [ev() for _ in range(4)]
         e[0].record()
         idx = ops.GalleryIndex(gal) if a.math == 'x3' else gal
         e[1].record()
-        ops.compute_dist(q, idx, out=out, math=a.math)
+        ops.compute_dist(q, idx, out=out, math=a.math, tile=tile)
         e[2].record()
         vals, ids = ops.topk(out, a.topk)
         e[3].record()
@@ -58,7 +76,7 @@ def main():
     print(json.dumps(dict(
         config='synthetic %dq x %dg shard (1M/8), D=%d, math=%s' % (a.queries, a.shard, a.dim,
                                                                    a.math),
-        index_ms=round(med['index_ms'], 3), distmat_ms=round(med['distmat_ms'], 3),
+        tile=tile, index_ms=round(med['index_ms'], 3), distmat_ms=round(med['distmat_ms'], 3),
         topk_ms=round(med['topk_ms'], 3),
         distmat_TFLOPs=round(flops / med['distmat_ms'] / 1e9, 1),
         distmat_GBps=round(byt / med['distmat_ms'] / 1e6, 1),

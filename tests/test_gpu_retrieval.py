@@ -162,6 +162,23 @@ def test_topk_ties_and_negatives():
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize('k', [21, 100])
+def test_topk_many_rows_odd_stride(k):
+    """Re-ranking shapes (DukeMTMC: N = Q + G = 19,889 rows of OD, odd row
+    stride, k = k1 + 1 = 21): every row's stable top-k equals NumPy's.  Many
+    blocks per CU exercise the candidate-count snapshot (all waves must take
+    the same cut decision in every chunk)."""
+    from pps_amd import ops
+    rng = np.random.RandomState(k)
+    Q, G = 1536, 19889
+    d = rng.rand(Q, G).astype(np.float32)
+    d[::7, ::5] = 0.25  # ties
+    vals, idx = ops.topk(_cuda(d), k)
+    ref = np.argsort(d, axis=1, kind='stable')[:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, ref, axis=1))
+
+
 def test_evaluate_vs_golden(golden):
     from pps_amd import reid_dataset_evaluator as gev
     from pps_amd.config import cfg
