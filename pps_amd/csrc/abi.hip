@@ -168,7 +168,7 @@ int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq
       p.Kloop = D;
       p.norm_a = qsq + q0; p.norm_b = gsq + g0;
       p.out = out + q0 * ldo + g0; p.ldo = ldo; p.metric = metric;
-      p.tile = tile ? tile : GEMM_TILE_P_FIRST + 4;  // 256x128: the Market-shape winner
+      p.tile = tile ? tile : GEMM_TILE_P16_FIRST + 4;  // as pps_distmat_x3's default
       const int rc = launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
       if (rc != PPS_OK) return rc;
     }

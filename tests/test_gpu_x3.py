@@ -248,7 +248,7 @@ def test_distmat_query_planes_same_bits(Q, G, D):
     q, idx = _cuda(qn), ops.GalleryIndex(_cuda(gn))
     for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
         want = ops.compute_dist(q, idx, q_planes=False,
-                                tile=tile or ops.TILE_P_FIRST + 4).cpu().numpy()
+                                tile=tile or ops.TILE_P16_FIRST + 4).cpu().numpy()
         got = ops.compute_dist(q, idx, q_planes=True, tile=tile).cpu().numpy()
         np.testing.assert_array_equal(got, want, err_msg='tile %d' % tile)
     np.testing.assert_allclose(want, ev.compute_dist(qn, gn), rtol=0, atol=1e-4 * np.sqrt(D / 64))
