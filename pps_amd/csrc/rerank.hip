@@ -10,7 +10,7 @@
 // an inverted (column) index of V_qe, in the same column order as the
 // reference, so every float32 sum has the reference's operand order.
 //
-//  1. rerank_colmax / rerank_build_od : OD[i][j] = M[j][i]^2 / max_r M[r][i]^2
+//  1. rerank_colmax_sq / rowmax_sq / build_od : OD[i][j] = M[j][i]^2 / max_r M[r][i]^2
 //     with M = [[qq, qg], [qg^T, gg]]                          (:447-454)
 //  2. pps_topk (rank.hip) on OD, k = k1 + 1 -> initial_rank      (:456)
 //  3. rerank_v_rows  : k-reciprocal sets, expansion, exp weights  (:462-488)
@@ -30,19 +30,36 @@ __device__ inline float rr_m(const float* qg, const float* qq, const float* gg, 
   return c < Q ? qg[c * G + (r - Q)] : gg[(r - Q) * G + (c - Q)];
 }
 
-// column max of M^2 (np.max(original_dist, axis=0) after np.power(.., 2))
-__global__ void rerank_colmax_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
-                                     const float* __restrict__ gg, int64_t Q, int64_t G,
-                                     float* __restrict__ colmax) {
-  const int64_t N = Q + G;
+// The column maxima of M^2 by blocks: column c of M is column c of qq plus
+// row c of qg (c < Q), or column c-Q of qg plus column c-Q of gg (c >= Q).
+// Squares are >= 0, so their float bits order as unsigned integers and an
+// integer atomicMax into a zeroed vector is an exact, order-free max.
+constexpr int kCmRows = 256;  // rows per block of the column-max kernel
+__global__ void rerank_colmax_sq_kernel(const float* __restrict__ x, int64_t R, int64_t C,
+                                        int64_t ld, unsigned* __restrict__ out) {
   const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float m = -INFINITY;
-  for (int64_t r = 0; r < N; ++r) {
-    const float v = rr_m(qg, qq, gg, Q, G, r, c);
+  if (c >= C) return;
+  const int64_t r0 = blockIdx.y * (int64_t)kCmRows;
+  const int64_t r1 = r0 + kCmRows < R ? r0 + kCmRows : R;
+  float m = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float v = x[r * ld + c];
     m = fmaxf(m, v * v);
   }
-  colmax[c] = m;
+  atomicMax(out + c, __float_as_uint(m));
+}
+
+// max over row r of x^2 (one block per row)
+__global__ void rerank_rowmax_sq_kernel(const float* __restrict__ x, int64_t C, int64_t ld,
+                                        unsigned* __restrict__ out) {
+  const int64_t r = blockIdx.x;
+  float m = 0.f;
+  for (int64_t c = threadIdx.x; c < C; c += blockDim.x) {
+    const float v = x[r * ld + c];
+    m = fmaxf(m, v * v);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out + r, __float_as_uint(m));
 }
 
 // OD[i][j] = M[j][i]^2 / colmax[i], via 32x32 LDS tiles (the transpose of :454)
@@ -357,9 +374,21 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
               std::to_string((size_t)(p - reinterpret_cast<char*>(ws))) + " bytes");
     return PPS_ERR_CAPACITY;
   }
-  hipLaunchKernelGGL(rerank_colmax_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
-                     qg, qq, gg, Q, G, colmax);
-  PPS_CHECK_LAUNCH_S("rerank_colmax_kernel", st);
+  // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M
+  unsigned* cm = reinterpret_cast<unsigned*>(colmax);
+  (void)hipMemsetAsync(cm, 0, sizeof(unsigned) * N, st);
+  auto colmax_sq = [&](const float* x, int64_t R, int64_t C, unsigned* out) {
+    if (R <= 0 || C <= 0) return;
+    hipLaunchKernelGGL(rerank_colmax_sq_kernel,
+                       dim3((unsigned)((C + 255) / 256), (unsigned)((R + kCmRows - 1) / kCmRows)),
+                       dim3(256), 0, st, x, R, C, C, out);
+  };
+  colmax_sq(qq, Q, Q, cm);      // columns c < Q: rows r < Q
+  colmax_sq(qg, Q, G, cm + Q);  // columns c >= Q: rows r < Q
+  colmax_sq(gg, G, G, cm + Q);  // columns c >= Q: rows r >= Q
+  hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, G,
+                     cm);       // columns c < Q: rows r >= Q (qg^T)
+  PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
   hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 31) / 32),
                                                   (unsigned)((N + 31) / 32)),
                      dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od);
