@@ -635,10 +635,14 @@ bool x3p_eligible(const GemmParams& p, int epi) {
 template <int S>
 static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t stream, int v) {
   switch (v) {
-    case 0: return launch_tile_p<128, 128, 2, 2, 3, 3, S>(p, epi, batch, stream);
+    // 4-wave tiles up to 80 KB of LDS take two stages: two workgroups per CU,
+    // so one's epilogue overlaps the other's loads (measured 10-30 % faster
+    // than three stages at one workgroup per CU on every layer shape,
+    // scripts/gemm_probe.py); 192x128 needs 96 KB for two stages anyway
+    case 0: return launch_tile_p<128, 128, 2, 2, 2, 2, S>(p, epi, batch, stream);
     case 1: return launch_tile_p<192, 128, 2, 2, 3, 2, S>(p, epi, batch, stream);
-    case 2: return launch_tile_p<128, 64, 2, 2, 3, 3, S>(p, epi, batch, stream);
-    case 3: return launch_tile_p<192, 64, 2, 2, 3, 3, S>(p, epi, batch, stream);
+    case 2: return launch_tile_p<128, 64, 2, 2, 2, 2, S>(p, epi, batch, stream);
+    case 3: return launch_tile_p<192, 64, 2, 2, 2, 2, S>(p, epi, batch, stream);
     case 4: return launch_tile_p<256, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
     case 5: return launch_tile_p<128, 256, 2, 4, 2, 2, S>(p, epi, batch, stream);
     case 6:

@@ -23,6 +23,9 @@ LAYERS = {
     'res2b': (64, 96, 32, 64, 64, 3, 1, 1),
     'res2c': (64, 96, 32, 64, 256, 1, 1, 0),
     'stem': (64, 384, 128, 4, 64, 7, 2, 3),
+    'res3c': (64, 48, 16, 128, 512, 1, 1, 0),
+    'res4c': (64, 24, 8, 256, 1024, 1, 1, 0),
+    'res2a': (64, 96, 32, 256, 64, 1, 1, 0),
 }
 
 
@@ -32,6 +35,7 @@ def main():
     ap.add_argument('--tiles', default='1,2,3,4,5,6,7,8,9')
     ap.add_argument('--math', default='x3,f32')
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--residual', action='store_true', help='conv + BN + residual Sum + ReLU')
     a = ap.parse_args()
     from pps_amd import model, ops
     for name in a.layers.split(','):
@@ -45,17 +49,18 @@ def main():
         sc = torch.ones(Cout, device='cuda')
         sh = torch.zeros(Cout, device='cuda')
         y = torch.empty(N, Ho, Wo, Cout, device='cuda')
+        resid = torch.randn(N, Ho, Wo, Cout, device="cuda") if a.residual else None
         flops = 2.0 * N * Ho * Wo * Cout * k * k * Cin
         for math in a.math.split(','):
             wt = w3 if math == 'x3' else wf
             res = []
             for tile in [int(t) for t in a.tiles.split(',')]:
-                ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, None, True, y, tile=tile)
+                ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y, tile=tile)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
-                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, None, True, y,
+                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y,
                                       tile=tile)
                 e1.record()
                 torch.cuda.synchronize()
