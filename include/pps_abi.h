@@ -51,12 +51,13 @@ const char* pps_registered_ops(void);
  * split after the fragment read (the f32 kernels treat them as 1..10),
  * 21..28 = 192-row tiles of the `_x3` kernels (192x128 / 192x64, K chunk
  * 16 / 32, A staged as planes / f32; the f32 kernels use 128-row tiles),
- * 29..35 = the `_x3` LDS-DMA pipelined tiles (128x128, 192x128, 128x64,
- * 192x64, 256x128, 128x256, 192x256; K chunk 32; the f32 kernels use the
- * heuristic), 36..42 = the same pipelined tiles on 16x16x32 MFMA blocks
- * (192x256 -> 128x256).  Results are identical for every tile below 36
- * (same per-element fp32 MFMA accumulation order) and identical among the
- * tiles from 36 on (one MFMA sums a 32-wide K chunk: a different rounding
+ * 29..37 = the `_x3` LDS-DMA pipelined tiles (128x128, 192x128, 128x64,
+ * 192x64 with 4 waves; 256x128, 128x256, 192x256, 128x128, 192x128 with 8
+ * waves; K chunk 32; the f32 kernels use the heuristic), 38..46 = the same
+ * pipelined tiles on 16x16x32 MFMA blocks (192x256 -> 128x256).  Results
+ * are identical for every tile below 38 (same per-element fp32 MFMA
+ * accumulation order) and identical among the tiles from 38 on (one MFMA
+ * sums a 32-wide K chunk: a different rounding
  * sequence, same f32-level error); only speed differs, so callers may
  * autotune. */
 int pps_gemm_num_tiles(void);

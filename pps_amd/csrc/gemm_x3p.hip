@@ -629,8 +629,8 @@ bool x3p_eligible(const GemmParams& p, int epi) {
   return true;
 }
 
-// variants 0..6: 32x32x16 MFMA blocks (bit-identical to gemm_x3.hip);
-// 7..13: the same tiles on 16x16x32 MFMA blocks (bit-identical among
+// variants 0..8: 32x32x16 MFMA blocks (bit-identical to gemm_x3.hip);
+// 9..17: the same tiles on 16x16x32 MFMA blocks (bit-identical among
 // themselves, f32-level like the others).
 template <int S>
 static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t stream, int v) {
@@ -650,6 +650,13 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
       // more than the 256 VGPRs of an 8-wave workgroup: 128x256 instead
       if (p.a3 || S == 16) return launch_tile_p<128, 256, 2, 4, 2, 2, S>(p, epi, batch, stream);
       if constexpr (S == 32) return launch_tile_p<192, 256, 2, 4, 2, 0, S>(p, epi, batch, stream);
+    // 8-wave versions of 128x128 / 192x128 (two waves per SIMD in one
+    // workgroup; 128x128 also two workgroups per CU): res3/res4 3x3 and
+    // res4 2c run 6-10 % faster on them
+    case 7: return launch_tile_p<128, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
+    case 8:  // plane A: 192 rows do not split into 8 waves x 16-row pieces
+      if (p.a3) return launch_tile_p<128, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
+      return launch_tile_p<192, 128, 2, 4, 2, 0, S>(p, epi, batch, stream);
     default:
       set_error("unknown pipelined GEMM variant " + std::to_string(v));
       return PPS_ERR_INVALID_ARG;
@@ -657,7 +664,8 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 }
 
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
-  if (variant >= 7) return launch_variant<16>(p, epi, batch, stream, variant - 7);
+  constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;  // variants per block size
+  if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }
 

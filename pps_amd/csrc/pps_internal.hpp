@@ -76,9 +76,10 @@ enum GemmTile {
   // 128x128, 192x128, 128x64, 192x64 (4 waves, 3 stages), 256x128, 128x256,
   // 192x256 (8 waves, 2 stages)
   GEMM_TILE_P_FIRST = 29,
-  // 36..42 (bf16x3 only): ids 29..35 on 16x16x32 MFMA blocks (own rounding)
-  GEMM_TILE_P16_FIRST = 36,
-  GEMM_NUM_TILES = 43
+  // 36, 37: 128x128 and 192x128 with 8 waves
+  // 38..46 (bf16x3 only): ids 29..37 on 16x16x32 MFMA blocks (own rounding)
+  GEMM_TILE_P16_FIRST = 38,
+  GEMM_NUM_TILES = 47
 };
 
 struct GemmParams {
