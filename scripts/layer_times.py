@@ -18,7 +18,13 @@ def main():
     m = model.PPSModel(model.synthetic_weights(plan, 0))
     x = torch.randn((B, 384, 128, 4), device='cuda') * 50
     x[..., 3] = 0
-    if not os.environ.get('NO_AUTOTUNE'):
+    tf = os.environ.get('TILES_FILE')
+    if tf:
+        with open(tf) as f:
+            saved = json.load(f)
+        m.set_tiles(saved)
+        m.set_planes(saved.get('__planes__', m.planes()))
+    elif not os.environ.get('NO_AUTOTUNE'):
         rep = m.autotune(x)
         for k, (t, ts) in rep.items():
             print('%-22s tile %d  %s' % (k, t, ' '.join('%d:%.3f' % kv for kv in sorted(ts.items()))))
@@ -44,9 +50,10 @@ def main():
             shp = 'M=%d N=%d K=%d' % (n * ho * wo, co, L['k'] * L['k'] * L['cin'])
         if L.get('planes_in') or L.get('planes_out'):
             op += '/p' + ('i' if L.get('planes_in') else '') + ('o' if L.get('planes_out') else '')
+        op += ' t%d' % L.get('tile', 0) if op != 'pps' and op != 'maxpool' else ''
         rows.append((name, op, shp, ms, f / (ms * 1e-3) / 1e12 if f else 0))
     for r in rows:
-        print('%-22s %-11s %-26s %8.3f ms %7.1f TF' % r)
+        print('%-22s %-15s %-26s %8.3f ms %7.1f TF' % r)
     print('total %.3f ms' % tot)
 
 
