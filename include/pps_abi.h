@@ -90,6 +90,18 @@ int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq
                     const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg,
                     int D, int metric, float* out, int64_t ldo, int tile,
                     void* stream);
+/* Self-distance of one feature set x [N][ld] (the reference's
+ * compute_dist(g, g) / compute_dist(q, q) of re-ranking and multi-query,
+ * reid_dataset_evaluator.py:169-175, 195-206): out [N][N] from the
+ * upper-triangle tiles only, each strictly-upper tile also writing its
+ * mirror (half the MFMA work).  x3 = pps_split_bf16x3(x) planes, xsq =
+ * pps_row_sqnorm(x).  128x128 pipelined tiles (29, 36, 38, 45; 0 = 38);
+ * D % 32 == 0.  Entry (i, j), i <= j, equals pps_distmat_x3's on the same
+ * tile; the lower triangle holds exact copies (a symmetric matrix, unlike
+ * the rounding-asymmetric full product). */
+int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,
+                        const uint16_t* x3, int D, int metric, float* out,
+                        int64_t ldo, int tile, void* stream);
 
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].

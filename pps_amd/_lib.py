@@ -28,6 +28,8 @@ SIGNATURES = {
                        c_ptr, c_i64, c_int, c_ptr],
     'pps_distmat_x3p': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
                         c_ptr, c_i64, c_int, c_ptr],
+    'pps_distmat_x3_self': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_i64,
+                            c_int, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,

@@ -176,6 +176,31 @@ int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq
   return PPS_OK;
 }
 
+int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,
+                        const uint16_t* x3, int D, int metric, float* out, int64_t ldo,
+                        int tile, void* stream) {
+  PPS_ENFORCE(x && xsq && x3 && out, "null pointer");
+  PPS_ENFORCE(N >= 0 && D > 0 && D % 32 == 0, "D must be a positive multiple of 32");
+  PPS_ENFORCE(ld % 8 == 0 && ld >= D, "bad leading dim");
+  PPS_ENFORCE(ldo >= N, "ldo < N");
+  PPS_ENFORCE(aligned16(x) && aligned16(x3), "x/x3 must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  PPS_ENFORCE(N * ld * 4 < kMaxBufBytes, "self-distance operand larger than 2 GiB");
+  PPS_ENFORCE(N * ldo < (1ll << 31), "output larger than 2^31 elements");
+  GemmParams p{};
+  p.splitk = 1;
+  p.a = x; p.a_bytes = (uint32_t)(N * ld * 4);
+  p.H = 1; p.W = (int)N; p.Cin = D; p.lda = (int)ld;
+  p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)N;
+  p.M = (int)N;
+  p.b3 = x3; p.b_plane = N * ld; p.b_bytes = (uint32_t)(N * ld * 2);
+  p.ldb = (int)ld; p.kb_valid = D; p.Ncol = (int)N;
+  p.Kloop = D;
+  p.norm_a = xsq; p.norm_b = xsq;
+  p.out = out; p.ldo = ldo; p.metric = metric; p.sym = 1; p.tile = tile;
+  return launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
+}
+
 int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
   PPS_ENFORCE(X && Z, "null pointer");
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");

@@ -268,6 +268,18 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
+  if (p.sym) {
+    // self-distance: square pipelined tiles only (the triangle is by tile)
+    const int v = p.tile >= GEMM_TILE_P_FIRST ? p.tile - GEMM_TILE_P_FIRST : GEMM_TILE_P16_FIRST -
+                                                                                 GEMM_TILE_P_FIRST;
+    const int vb = v % (GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST);
+    if (!(epi & EPI_DIST) || p.M != p.Ncol || !x3p_eligible(p, epi) || (vb != 0 && vb != 7)) {
+      set_error("symmetric distance: needs EPI_DIST, M == Ncol and a 128x128 pipelined tile "
+                "(29, 36, 38 or 45)");
+      return PPS_ERR_INVALID_ARG;
+    }
+    return launch_gemm_x3p(p, epi, batch, stream, v);
+  }
   if (p.a3 || (epi & EPI_F_PLANES)) {
     // bf16-plane activations exist only in the pipelined family
     if (!x3p_eligible(p, epi)) {

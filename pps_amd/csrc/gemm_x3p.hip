@@ -165,6 +165,9 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
   constexpr int TN = BN / WN / S;
   constexpr int NQ = S * S / 256;
   float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
+  const bool mirror = p.sym && m0 < n0;  // strictly-upper tile of a self-distance
+  const bool diag = p.sym && m0 == n0;   // diagonal tile: its own upper half, mirrored
+  float* __restrict__ outT = p.out + (int64_t)n0 * p.ldo + m0;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;
   const int nrem = p.Ncol - n0;
@@ -210,12 +213,28 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
           v[e] = d;
         }
         float* o = out + rr * ldo + c;
+        if (diag) {  // diagonal tile of a self-distance: upper half, mirrored
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int cc = c + e;
+            if (cc < nrem && rr <= cc) {
+              o[e] = v[e];
+              if (rr < cc) outT[cc * ldo + rr] = v[e];
+            }
+          }
+          continue;
+        }
         if (vec && c + 3 < nrem) {
           *reinterpret_cast<f32x4*>(o) = v;
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (c + e < nrem) o[e] = v[e];
+        }
+        if (mirror) {  // out[n0 + c + e][m0 + rr]: consecutive lanes, consecutive rows
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < nrem) outT[(c + e) * ldo + rr] = v[e];
         }
       }
     }
@@ -262,9 +281,25 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int r32 = lane & (S - 1);  // lane's row within an MFMA block
   const int h = lane / S;          // its K slot (S = 16: 0..3) / column half (S = 32)
 
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tile_m = bid / tiles_n;
-  const int tile_n = bid - tile_m * tiles_n;
+  const bool sym = (EPI & EPI_DIST) && p.sym;
+  int tile_m, tile_n;
+  if (sym) {
+    // self-distance: the grid enumerates only the upper-triangle tiles
+    // (row-major), so every XCD gets an equal, contiguous share of them
+    const int n = tiles_n;
+    const int k = xcd_remap(blockIdx.x, n * (n + 1) / 2);
+    const double b = 2.0 * n + 1.0;
+    int i = (int)((b - sqrt(b * b - 8.0 * k)) * 0.5);
+    auto row0 = [n](int r) { return r * n - r * (r - 1) / 2; };  // first index of row r
+    while (i > 0 && row0(i) > k) --i;
+    while (i + 1 < n && row0(i + 1) <= k) ++i;
+    tile_m = i;
+    tile_n = i + (k - row0(i));
+  } else {
+    const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    tile_m = bid / tiles_n;
+    tile_n = bid - tile_m * tiles_n;
+  }
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;
   const int batch = blockIdx.y / p.splitk;
@@ -556,9 +591,11 @@ template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3, int S>
 static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
+  // self-distance (square tiles, M == Ncol): upper-triangle tiles only
+  const int nblk = ((EPI & EPI_DIST) && p.sym) ? tiles_n * (tiles_n + 1) / 2 : tiles_m * tiles_n;
   hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS, A3, S>),
-                     dim3(tiles_m * tiles_n, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p,
-                     tiles_m, tiles_n);
+                     dim3(nblk, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p, tiles_m,
+                     tiles_n);
 }
 
 // NSF / NSP: LDS stages with f32 / bf16-plane A operands (NSP = 0: the tile

@@ -116,6 +116,10 @@ struct GemmParams {
   int relu;
   int metric;
   int zero_diag;
+  // EPI_DIST in the pipelined kernel, self-distance (A rows == B rows, square
+  // tiles): strictly-lower tiles exit, strictly-upper tiles also write the
+  // mirrored block out[c][r]
+  int sym;
   int tile;  // GemmTile; 0 = heuristic
   int splitk;           // >= 1; K slices enumerated with the batch on grid.y
   int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)

@@ -80,14 +80,22 @@ class GalleryIndex(object):
         return self.feats.shape
 
 
-def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes=None):
+SELF_TILES = (0, TILE_P_FIRST, TILE_P_FIRST + 7, TILE_P16_FIRST, TILE_P16_FIRST + 7)
+
+
+def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes=None,
+                 symmetric=None):
     """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244).
     g may be a GalleryIndex (then the x3 kernel runs on its prepared planes).
     q_planes (x3): also split the queries into bf16x3 planes first so the
     pipelined GEMM stages both operands by DMA (pps_distmat_x3p; pipelined
     tiles only).  Same bits either way; measured at the Market shape it is
     not faster (scripts/dist_probe.py: the split in the K loop is hidden),
-    so None = off."""
+    so None = off.
+    symmetric (x3): a self-distance (q and g the same rows, e.g.
+    compute_dist(g, g) of re-ranking) computed from the upper-triangle tiles
+    and mirrored (pps_distmat_x3_self, half the work); None = whenever q IS
+    g's data, D % 32 == 0 and the tile is a square one (SELF_TILES)."""
     math = 'x3' if isinstance(g, GalleryIndex) else (math or default_math())
     if q.dim() != 2 or len(g.shape) != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
@@ -101,6 +109,16 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
              _dev(out, 'out'), out.stride(0), int(tile), _stream())
         return out
     idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g)
+    if symmetric is None:
+        f = idx.feats
+        symmetric = (f.data_ptr() == q.data_ptr() and tuple(f.shape) == tuple(q.shape) and
+                     f.stride() == q.stride() and q.is_contiguous() and D % 32 == 0 and
+                     tile in SELF_TILES)
+    if symmetric:
+        call('pps_distmat_x3_self', _dev(q, 'x'), Q, D, _dev(idx.sqnorm, 'xsq'),
+             _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric], _dev(out, 'out'),
+             out.stride(0), int(tile), _stream())
+        return out
     qsq = row_sqnorm(q)
     if q_planes:
         q3 = split_bf16x3(q)

@@ -252,3 +252,35 @@ def test_distmat_query_planes_same_bits(Q, G, D):
         got = ops.compute_dist(q, idx, q_planes=True, tile=tile).cpu().numpy()
         np.testing.assert_array_equal(got, want, err_msg='tile %d' % tile)
     np.testing.assert_allclose(want, ev.compute_dist(qn, gn), rtol=0, atol=1e-4 * np.sqrt(D / 64))
+
+
+@pytest.mark.parametrize('N,D', [(1000, 3968), (301, 64), (129, 2048), (17, 32)])
+@pytest.mark.parametrize('metric', ['euclidean', 'cosine'])
+def test_self_distance_symmetric(N, D, metric):
+    """compute_dist(x, x) from the upper-triangle tiles + mirror: symmetric,
+    upper-triangle tiles bit-equal to the full product on the same tile, and
+    within the f32 tolerance of the NumPy formula everywhere."""
+    from oracle import evaluator as ev
+    from pps_amd import ops
+    rng = np.random.RandomState(N + D)
+    xn = rng.randn(N, D).astype(np.float32)
+    xn /= np.linalg.norm(xn, axis=1, keepdims=True)  # re-ID features are L2-normalised
+    x = _cuda(xn)
+    ref = ev.compute_dist(xn, xn, metric) if metric == 'euclidean' else None
+    for tile in ops.SELF_TILES:
+        d = ops.compute_dist(x, x, metric=metric, tile=tile).cpu().numpy()
+        full = ops.compute_dist(x, x, metric=metric, tile=tile or ops.TILE_P16_FIRST,
+                                symmetric=False).cpu().numpy()
+        np.testing.assert_array_equal(d, d.T, err_msg='tile %d' % tile)
+        iu = np.triu_indices(N)           # the upper triangle is the full product's
+        np.testing.assert_array_equal(d[iu], full[iu], err_msg='tile %d' % tile)
+        if ref is not None:
+            # off the diagonal within the f32 tolerance; ON it both sides take
+            # the sqrt of a cancelled |x|^2 + |x|^2 - 2 x.x, i.e. of f32
+            # rounding noise (~sqrt(D) * 2^-24 ~ 4e-6 for |x| = 1 -> ~2e-3),
+            # whose value depends on the summation order (NumPy: 0 .. 5e-4)
+            off = ~np.eye(N, dtype=bool)
+            np.testing.assert_allclose(d[off], ref[off], rtol=0, atol=1e-4)
+            assert np.abs(np.diag(d) - np.diag(ref)).max() < 5e-3
+        else:
+            np.testing.assert_allclose(d, full, rtol=0, atol=1e-5)
