@@ -26,6 +26,7 @@ LAYERS = {
     'res3c': (64, 48, 16, 128, 512, 1, 1, 0),
     'res4c': (64, 24, 8, 256, 1024, 1, 1, 0),
     'res2a': (64, 96, 32, 256, 64, 1, 1, 0),
+    'stemgemm': (64, 192, 64, 224, 64, 1, 1, 0),  # the stem as a plain K=224 GEMM
 }
 
 
