@@ -99,17 +99,21 @@ def retrieval_stage(rank, world, reps, tune=True):
         from pps_amd import ops
         qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
         best = None
-        for t in range(1, ops.num_tiles() + 1):
-            ops.compute_dist(qa, g_local, tile=t)
+        cands = [(t, False) for t in range(1, ops.num_tiles() + 1)]
+        if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
+            cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)]
+        for t, qp in cands:
+            ops.compute_dist(qa, g_local, tile=t, q_planes=qp)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.compute_dist(qa, g_local, tile=t)
+            ops.compute_dist(qa, g_local, tile=t, q_planes=qp)
             e1.record()
             e1.synchronize()
             ms = e0.elapsed_time(e1)
             if best is None or ms < best[1]:
-                best = (t, ms)
+                best = (t, ms, qp)
         pdist.HipBackend.distmat_tile = best[0]
+        pdist.HipBackend.distmat_qplanes = best[2]
         del qa
     # warm-up
     res = ev.run(q_local, g_local)
@@ -124,6 +128,7 @@ def retrieval_stage(rank, world, reps, tune=True):
         t_rank.append(res['t_rank_ms'])
         t_total.append(res['t_total_ms'])
     out = dict(distmat_tile=pdist.HipBackend.distmat_tile,
+               distmat_qplanes=pdist.HipBackend.distmat_qplanes,
                distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
                retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
                cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
@@ -249,6 +254,7 @@ def main():
         if '__planes__' in saved:
             m.set_planes(saved['__planes__'])
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
+        pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
     elif not args.no_autotune:
         m.autotune(xbuf)   # per-layer tile choice, outside the timed region
 
@@ -284,6 +290,7 @@ def main():
     if args.tiles_file and not tiles_saved and rank == 0:
         with open(args.tiles_file, 'w') as f:
             json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile'],
+                           __distmat_qplanes__=ret['distmat_qplanes'],
                            __planes__=m.planes()), f, indent=0)
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
@@ -321,7 +328,8 @@ def main():
             algorithmic_bytes_per_launch=dist_bytes,
             kernel='%s EPI_DIST, tile %d (+ split/norm of the gallery shard)' % (
                 'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
-                ret['distmat_tile'])),
+                ret['distmat_tile']) + (', queries as bf16x3 planes'
+                                        if ret['distmat_qplanes'] else '')),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(blobs)

@@ -297,8 +297,27 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     tile_n = i + (k - row0(i));
   } else {
     const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-    tile_m = bid / tiles_n;
-    tile_n = bid - tile_m * tiles_n;
+    if (EPI & EPI_DIST) {
+      // Grouped order: GM query panels sweep the gallery blocks together
+      // (XCD-contiguous after the remap), GM sized so the group's panels
+      // (~32 MB) stay in the Infinity Cache while every gallery block is
+      // streamed once per group.  Market: GM = 7 of 14 panels, memory-side
+      // traffic 5.6 -> 2.4 GB per launch and ~10 % faster than row-major
+      // (which re-streams the 379 MB gallery planes once per panel).
+      const int64_t panel = (int64_t)BM * p.Kloop * (A3 ? 6 : 4);
+      const int64_t want = ((int64_t)32 << 20) / (panel > 0 ? panel : 1);
+      const int GM = (int)(want < 1 ? 1 : (want < tiles_m ? want : tiles_m));
+      const int per = GM * tiles_n;
+      const int grp = bid / per;
+      const int first = grp * GM;
+      const int gm = tiles_m - first < GM ? tiles_m - first : GM;
+      const int r = bid - grp * per;
+      tile_n = r / gm;
+      tile_m = first + (r - tile_n * gm);
+    } else {
+      tile_m = bid / tiles_n;
+      tile_n = bid - tile_m * tiles_n;
+    }
   }
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;

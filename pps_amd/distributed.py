@@ -65,10 +65,12 @@ class HipBackend(object):
     """libpps_hip.so kernels (the product path)."""
     device = 'cuda'
     distmat_tile = 0   # GEMM tile for the distance matrix (0 = heuristic; bench tunes it)
+    distmat_qplanes = False  # queries pre-split into bf16x3 planes (ops.compute_dist)
 
     @classmethod
     def distmat(cls, q, g, metric):
-        return ops.compute_dist(q, g, metric=metric, tile=cls.distmat_tile)
+        return ops.compute_dist(q, g, metric=metric, tile=cls.distmat_tile,
+                                q_planes=cls.distmat_qplanes)
 
     @staticmethod
     def collect(dist, qid, qcam, gid, gcam, g_offset, pmax):
