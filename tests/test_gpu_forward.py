@@ -268,3 +268,38 @@ def test_fpn_variant_forward_vs_oracle():
     xin[..., :3] = x.transpose(0, 2, 3, 1)
     out = model.PPSModel(blobs, plan=plan).forward(_cuda(xin)).cpu().numpy()
     np.testing.assert_allclose(out, ref, rtol=0, atol=2e-5)
+
+
+def test_bench_configuration_vs_oracle():
+    """The configuration bench.py measures -- batch 64, the committed
+    autotune result (per-layer tiles from both rounding groups, bf16x3
+    activation-plane edges) -- against the CPU oracle on a few of the 64
+    images: forward -> normalised features."""
+    import json
+    import os
+    from oracle.forward import GraphForward
+    from oracle import preprocess as pre
+    from pps_amd import model, ops
+    tf = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      'profiles', 'r01', 'tiles_v9_final.json')
+    if not os.path.exists(tf):
+        pytest.skip('no committed tiles file')
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=0)
+    m = model.PPSModel(blobs, math='x3')
+    with open(tf) as f:
+        saved = json.load(f)
+    m.set_tiles(saved)
+    m.set_planes(saved.get('__planes__', []))
+    assert len(m.planes()) > 0
+    rng = np.random.RandomState(64)
+    imgs = rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)
+    x = ops.preprocess_bgr(torch.from_numpy(imgs).cuda(), pre.PIXEL_MEANS, (384, 128))
+    feat = m.forward(x).cpu().numpy()
+    pick = [0, 17, 63]
+    # the oracle forward on the kernel's own preprocessed input (preprocess
+    # parity is test_preprocess_vs_oracle's)
+    xin = x[pick, :, :, :3].cpu().numpy().transpose(0, 3, 1, 2)
+    ref = GraphForward(blobs)(np.ascontiguousarray(xin, np.float32)).numpy()
+    np.testing.assert_allclose(feat[pick], ref, rtol=0, atol=2e-5)
