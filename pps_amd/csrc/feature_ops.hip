@@ -2,6 +2,8 @@
 //   max pooling (stem pool1), part-power-set strip pooling + subset combine,
 //   row L2 normalisation, image preprocessing (mean-subtract + bicubic).
 // All NHWC float32, 16-B vectorised along channels where the layout allows.
+#include <algorithm>
+
 #include "pps_internal.hpp"
 
 namespace pps {
@@ -500,6 +502,103 @@ preprocess_bgr_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
   *reinterpret_cast<f32x4*>(y + ((int64_t)row * Wo + ox) * 4) = f32x4{acc[0], acc[1], acc[2], 0.f};
 }
 
+// Separable variant: block = (image n, band of kPrepRows output rows).  Pass
+// 1 filters the band's source rows horizontally into LDS (each source row
+// once, not once per output row that uses it), pass 2 filters vertically --
+// the same sums in the same order as the direct kernel above (row sums over
+// i, then acc over j).  A band whose source rows exceed the LDS cap (strong
+// downscaling) is computed directly.
+constexpr int kPrepRows = 16;
+__global__ void __launch_bounds__(256)
+preprocess_sep_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
+                      const int64_t* __restrict__ offsets, const int32_t* __restrict__ heights,
+                      const int32_t* __restrict__ widths, Means mean, int Ho, int Wo, int kcap,
+                      float* __restrict__ y) {
+  extern __shared__ float hrow[];  // [kcap][Wo][3]
+  const int nb = (Ho + kPrepRows - 1) / kPrepRows;
+  const int n = blockIdx.x / nb;
+  const int oy0 = (blockIdx.x - n * nb) * kPrepRows;
+  const int oy1 = min(Ho, oy0 + kPrepRows);
+  int Hi = Hi0, Wi = Wi0;
+  const uint8_t* img;
+  if (offsets) {
+    Hi = heights[n];
+    Wi = widths[n];
+    img = blob + offsets[n];
+  } else {
+    img = blob + (int64_t)n * Hi * Wi * 3;
+  }
+  const double sy = (double)Hi / (double)Ho, sx = (double)Wi / (double)Wo;
+  const int rb = Wi * 3;
+  auto src_y0 = [&](int oy) { return (int)floorf((float)((oy + 0.5) * sy - 0.5)); };
+  const int ys = min(max(src_y0(oy0) - 1, 0), Hi - 1);
+  const int ye = min(max(src_y0(oy1 - 1) + 2, 0), Hi - 1);
+  const int nr = ye - ys + 1;
+  const int nout = (oy1 - oy0) * Wo;
+  if (nr > kcap) {  // direct
+    for (int t = threadIdx.x; t < nout; t += blockDim.x) {
+      const int oy = oy0 + t / Wo, ox = t - (t / Wo) * Wo;
+      const float fy = (float)((oy + 0.5) * sy - 0.5);
+      const float fx = (float)((ox + 0.5) * sx - 0.5);
+      const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
+      float wx[4], wy[4];
+      cubic_coeffs(fx - x0, wx);
+      cubic_coeffs(fy - y0, wy);
+      float acc[3] = {0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t* rowp = img + (int64_t)min(max(y0 - 1 + j, 0), Hi - 1) * rb;
+        float rowv[3] = {0.f, 0.f, 0.f};
+        for (int i = 0; i < 4; ++i) {
+          const uint8_t* px = rowp + min(max(x0 - 1 + i, 0), Wi - 1) * 3;
+          for (int c = 0; c < 3; ++c) rowv[c] += wx[i] * ((float)px[c] - mean.m[c]);
+        }
+        for (int c = 0; c < 3; ++c) acc[c] += wy[j] * rowv[c];
+      }
+      *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oy) * Wo + ox) * 4) =
+          f32x4{acc[0], acc[1], acc[2], 0.f};
+    }
+    return;
+  }
+  // pass 1: horizontal filter of source rows ys..ye
+  for (int t = threadIdx.x; t < nr * Wo; t += blockDim.x) {
+    const int r = t / Wo, ox = t - r * Wo;
+    const float fx = (float)((ox + 0.5) * sx - 0.5);
+    const int x0 = (int)floorf(fx);
+    float wx[4];
+    cubic_coeffs(fx - x0, wx);
+    const uint8_t* rowp = img + (int64_t)(ys + r) * rb;
+    float rowv[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint8_t* px = rowp + min(max(x0 - 1 + i, 0), Wi - 1) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) rowv[c] += wx[i] * ((float)px[c] - mean.m[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) hrow[t * 3 + c] = rowv[c];
+  }
+  __syncthreads();
+  // pass 2: vertical filter
+  for (int t = threadIdx.x; t < nout; t += blockDim.x) {
+    const int oyl = t / Wo, ox = t - oyl * Wo;
+    const int oy = oy0 + oyl;
+    const float fy = (float)((oy + 0.5) * sy - 0.5);
+    const int y0 = (int)floorf(fy);
+    float wy[4];
+    cubic_coeffs(fy - y0, wy);
+    float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = min(max(y0 - 1 + j, 0), Hi - 1) - ys;
+      const float* h = hrow + (r * Wo + ox) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += wy[j] * h[c];
+    }
+    *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oy) * Wo + ox) * 4) =
+        f32x4{acc[0], acc[1], acc[2], 0.f};
+  }
+}
+
 int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* offsets,
                    const int32_t* heights, const int32_t* widths, const float* means,
                    int Ho, int Wo, float* y, hipStream_t st) {
@@ -510,9 +609,17 @@ int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* off
     set_error("preprocess: N * Ho must be < 2^31");
     return PPS_ERR_INVALID_ARG;
   }
-  // LDS staging needs the widest image's 4 rows in LDS: known for a dense
-  // batch; a ragged batch passes its maximum width as Wi (0 = unknown)
-  // (staging the 4 source rows in LDS measured 1.9x slower: byte taps hit L1)
+  // separable two-pass kernel when a band's horizontally filtered rows fit
+  // 48 KB of LDS (Wo <= 256 with the 16-row cap); the direct kernel otherwise
+  const int kcap = (int)std::min<int64_t>(kPrepRows, (48 * 1024) / ((int64_t)Wo * 12));
+  if (kcap >= 8) {
+    const int64_t nblk = (int64_t)N * ((Ho + kPrepRows - 1) / kPrepRows);
+    hipLaunchKernelGGL(preprocess_sep_kernel, dim3((unsigned)nblk), dim3(256),
+                       (size_t)kcap * Wo * 12, st, img, N, Hi, Wi, offsets, heights, widths, m,
+                       Ho, Wo, kcap, y);
+    PPS_CHECK_LAUNCH("preprocess_sep_kernel");
+    return PPS_OK;
+  }
   hipLaunchKernelGGL(preprocess_bgr_kernel, dim3((unsigned)(N * Ho), (Wo + 127) / 128),
                      dim3(128), 0, st, img, N, Hi, Wi, offsets, heights, widths, m, Ho, Wo, y);
   PPS_CHECK_LAUNCH("preprocess_bgr_kernel");
