@@ -301,8 +301,8 @@ __device__ inline void block_bitonic(unsigned long long* buf, int n2) {
 // index), so comparing packed values is the stable (distance, index) order.
 // An entry enters the LDS candidate buffer only if it beats the current
 // threshold = the k-th best packed value among the candidates kept so far;
-// when the buffer could overflow in the next chunk it is sorted and cut back
-// to its k best (rare after the first chunks: ~k*ln(G/k) insertions per row).
+// when the buffer could overflow in the next chunk it is cut back to its k
+// best (rare after the first chunks: ~k*ln(G/k) insertions per row).
 __global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
                             float* __restrict__ vals, int32_t* __restrict__ idx) {
   const int64_t q = blockIdx.x;
@@ -313,15 +313,79 @@ __global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t l
   if (threadIdx.x == 0) { s_n = 0; s_thr = ~0ull; }
   __syncthreads();
   const int64_t chunk = (int64_t)blockDim.x * kTopkUnroll;
-  auto cut = [&](int n) {  // sort the n candidates, keep the k best
-    int n2 = 1;
-    while (n2 < n) n2 <<= 1;
-    for (int i = n + threadIdx.x; i < n2; i += blockDim.x) cand[i] = ~0ull;
-    __syncthreads();
-    block_bitonic(cand, n2);
-    if (threadIdx.x == 0) {
-      s_n = n < k ? n : k;
-      s_thr = n >= k ? cand[k - 1] : ~0ull;
+  // cut(n, final): keep the k best of the n candidates.  The k-th best
+  // packed key T is found by an 8-pass radix select (8-bit digits from the
+  // top; packed keys are unique, so exactly k entries are <= T) and the k
+  // entries are compacted to the front -- a full bitonic sort of the
+  // buffer (78 LDS-bound stages for 4096 entries, shared by the CU's
+  // blocks) cost ~150 us per row block on short rows.  Only the final cut
+  // sorts, and only those k entries.
+  __shared__ unsigned s_hist[256];
+  __shared__ unsigned long long s_pref;
+  __shared__ int s_rank, s_cnt;
+  constexpr int kPerThr = kTopkBuf / kTopkThreads;
+  auto cut = [&](int n, bool final) {
+    int keep = n;
+    if (n > k) {
+      if (threadIdx.x == 0) { s_pref = 0ull; s_rank = k; }
+      for (int pass = 0; pass < 8; ++pass) {
+        const int shift = 56 - 8 * pass;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0u;
+        __syncthreads();
+        const unsigned long long pre = s_pref;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+          const unsigned long long v = cand[i];
+          if (pass == 0 || (v >> (shift + 8)) == pre)
+            atomicAdd(&s_hist[(unsigned)(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // one wave: the bin holding rank s_rank
+          const int l = threadIdx.x;
+          unsigned h[4], sum = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) { h[b] = s_hist[4 * l + b]; sum += h[b]; }
+          unsigned incl = sum;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const unsigned t = __shfl_up(incl, o);
+            if (l >= o) incl += t;
+          }
+          const unsigned r = (unsigned)s_rank;
+          const unsigned long long hit = __ballot(incl >= r);
+          const int hl = __ffsll((long long)hit) - 1;
+          if (l == hl) {
+            unsigned before = incl - sum;
+            int b = 0;
+            while (b < 3 && before + h[b] < r) before += h[b++];
+            s_pref = (pre << 8) | (unsigned long long)(4 * l + b);
+            s_rank = (int)(r - before);
+          }
+        }
+        __syncthreads();
+      }
+      const unsigned long long T = s_pref;  // the k-th best packed key
+      unsigned long long mine[kPerThr];
+#pragma unroll
+      for (int j = 0; j < kPerThr; ++j) {
+        const int i = threadIdx.x + j * kTopkThreads;
+        mine[j] = i < n ? cand[i] : ~0ull;
+      }
+      if (threadIdx.x == 0) s_cnt = 0;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kPerThr; ++j)
+        if (mine[j] <= T) cand[atomicAdd(&s_cnt, 1)] = mine[j];
+      __syncthreads();
+      keep = k;
+      if (threadIdx.x == 0) s_thr = T;
+    }
+    if (threadIdx.x == 0) s_n = keep;
+    if (final) {
+      int n2 = 1;
+      while (n2 < keep) n2 <<= 1;
+      for (int i = keep + threadIdx.x; i < n2; i += blockDim.x) cand[i] = ~0ull;
+      __syncthreads();
+      block_bitonic(cand, n2);
     }
     __syncthreads();
   };
@@ -347,7 +411,7 @@ __global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t l
     // s_n) can land before a slower wave has read it
     const int n_now = s_n;
     lds_barrier();
-    if (n_now + chunk > kTopkBuf) cut(n_now);
+    if (n_now + chunk > kTopkBuf) cut(n_now, false);
     const unsigned long long thr = s_thr;
     float dn[kTopkUnroll];
 #pragma unroll
@@ -371,7 +435,7 @@ __global__ void topk_kernel(const float* __restrict__ dist, int64_t G, int64_t l
     for (int u = 0; u < kTopkUnroll; ++u) d[u] = dn[u];
     lds_barrier();
   }
-  cut(s_n);
+  cut(s_n, true);
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const unsigned long long v = cand[i];
     vals[q * k + i] = key_float((uint32_t)(v >> 32));
