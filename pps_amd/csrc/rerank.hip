@@ -62,15 +62,30 @@ __global__ void rerank_rowmax_sq_kernel(const float* __restrict__ x, int64_t C, 
   if ((threadIdx.x & 63) == 0) atomicMax(out + r, __float_as_uint(m));
 }
 
-// OD[i][j] = M[j][i]^2 / colmax[i], via 32x32 LDS tiles (the transpose of :454)
-__global__ void rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
-                                       const float* __restrict__ gg, int64_t Q, int64_t G,
-                                       const float* __restrict__ colmax, float* __restrict__ od) {
-  __shared__ float tile[32][33];
+// OD[i][j] = M[j][i]^2 / colmax[i], via 64x64 LDS tiles (the transpose of
+// :454); a wave moves one 256-byte tile row per access
+__global__ void __launch_bounds__(256)
+rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
+                       const float* __restrict__ gg, int64_t Q, int64_t G,
+                       const float* __restrict__ colmax, float* __restrict__ od) {
+  __shared__ float tile[64][65];
   const int64_t N = Q + G;
-  const int64_t i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: ty 0..7
-  for (int k = ty; k < 32; k += 8) {  // read M[j0+k][i0+tx] (row j, col i)
+  const int64_t i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: ty 0..3
+  if (i0 + 64 <= Q && j0 >= Q) {
+    // query rows x gallery columns: M[j][i] = qg[i][j - Q], i.e. OD here is
+    // qg itself (squared, scaled) -- read it row-wise, no transpose (the
+    // generic path below would read qg down its columns, stride G)
+    for (int k = ty; k < 64; k += 4) {
+      const int64_t i = i0 + k, j = j0 + tx;
+      if (j < N) {
+        const float m = qg[i * G + (j - Q)];
+        od[i * N + j] = (m * m) / colmax[i];
+      }
+    }
+    return;
+  }
+  for (int k = ty; k < 64; k += 4) {  // read M[j0+k][i0+tx] (row j, col i)
     const int64_t r = j0 + k, c = i0 + tx;
     float v = 0.f;
     if (r < N && c < N) {
@@ -80,7 +95,7 @@ __global__ void rerank_build_od_kernel(const float* __restrict__ qg, const float
     tile[k][tx] = v;
   }
   __syncthreads();
-  for (int k = ty; k < 32; k += 8) {  // write OD[i0+k][j0+tx] = tile[tx][k] / colmax
+  for (int k = ty; k < 64; k += 4) {  // write OD[i0+k][j0+tx] = tile[tx][k] / colmax
     const int64_t i = i0 + k, j = j0 + tx;
     if (i < N && j < N) od[i * N + j] = tile[tx][k] / colmax[i];
   }
@@ -389,8 +404,8 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, G,
                      cm);       // columns c < Q: rows r >= Q (qg^T)
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
-  hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 31) / 32),
-                                                  (unsigned)((N + 31) / 32)),
+  hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 63) / 64),
+                                                  (unsigned)((N + 63) / 64)),
                      dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od);
   PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
   int rc = topk(od, N, N, N, K1, topv, rank, st);
