@@ -152,6 +152,19 @@ def _pmc_traffic(key, math, batch):
     return e.get('bytes_per_launch')
 
 
+def _pmc_mfma(math, batch):
+    """Conv stack's effective clock and MFMA-busy fraction from the committed
+    PMC pass (GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES), same math and batch."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            e = json.load(f).get('conv_mfma')
+    except (OSError, ValueError):
+        return None
+    if not e or e.get('math') != math or e.get('batch') != batch:
+        return None
+    return {k: e[k] for k in ('clock_GHz', 'mfma_busy_frac', 'mfma_busy_frac_at_2p4GHz')}
+
+
 def conv_roofline(m, x):
     """Per-launch HIP events over one forward (same stream as the kernels)."""
     timer = []
@@ -174,6 +187,7 @@ def conv_roofline(m, x):
     return dict(bound='mfma', achieved=round(achieved, 2), peak=round(peak, 1),
                 unit='TFLOP/s', frac=round(achieved / peak, 4),
                 traffic=_pmc_traffic('conv', m.math, x.shape[0]), kernel=kernel,
+                pmc_mfma=_pmc_mfma(m.math, x.shape[0]),
                 launches=n_launch, flops_per_forward=conv_flops,
                 algorithmic_bytes_per_launch=round(m.bytes_per_forward() / n_launch),
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2),

@@ -2,7 +2,8 @@
 # One GPU session that produces the round's measurement artefacts:
 #   1. bench (autotune; tiles saved)            -> gpurun_out/bench_tuned.log
 #   2. rocprofv3 --kernel-trace --stats (same tiles) -> gpurun_out/prof/
-#   3. PMC passes FETCH_SIZE / WRITE_SIZE (same tiles) -> gpurun_out/pmc_traffic.json
+#   3. PMC passes FETCH_SIZE / WRITE_SIZE / GRBM_GUI_ACTIVE+MFMA busy (same tiles)
+#      -> gpurun_out/pmc_traffic.json
 #   4. bench again (same tiles, traffic filled)  -> gpurun_out/bench_final.log
 # Each GPU step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -22,6 +23,7 @@ step pmc
 rm -rf $OUT/pmcb
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmcb/p1 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc1.log 2>&1 || { tail -5 $OUT/pmc1.log; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc2.log 2>&1 || { tail -5 $OUT/pmc2.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
 python scripts/pmc_traffic.py $OUT/pmcb $MATH 64 50 > $OUT/pmc_traffic.json || exit 1
 cat $OUT/pmc_traffic.json
 cp $OUT/pmc_traffic.json profiles/r01/pmc_traffic.json

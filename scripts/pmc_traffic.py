@@ -27,6 +27,17 @@ def load(path, counter):
     return [rows[k] for k in sorted(rows)]
 
 
+def load_all(path):
+    """[(kernel name, {counter: value}, duration ns)] in dispatch order."""
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        e = rows.setdefault(int(r['Dispatch_Id']),
+                            [r['Kernel_Name'], {},
+                             int(r['End_Timestamp']) - int(r['Start_Timestamp'])])
+        e[1][r['Counter_Name']] = float(r['Counter_Value'])
+    return [tuple(rows[k]) for k in sorted(rows)]
+
+
 def epi_of(name):
     args = name.split('<', 1)[1].split('>', 1)[0].split(',')
     return int(args[4])
@@ -54,6 +65,23 @@ def main():
                         bytes_per_launch=round((fb + wb) / n))
         if key == 'conv':
             out[key]['batch'] = batch
+    # optional third pass: GRBM_GUI_ACTIVE + SQ_VALU_MFMA_BUSY_CYCLES -> the
+    # conv stack's effective clock (GRBM_GUI_ACTIVE sums the 8 XCDs) and the
+    # fraction of SIMD cycles the MFMA pipe was busy (1024 SIMDs)
+    p3 = glob.glob(os.path.join(d, 'p3', '*counter_collection.csv'))
+    if p3:
+        rows = [(nm, c, dur) for nm, c, dur in load_all(p3[0])
+                if is_gemm(nm) and epi_of(nm) != 1 and 'GRBM_GUI_ACTIVE' in c][-nconv:]
+        if len(rows) == nconv:
+            dur = sum(r[2] for r in rows)
+            act = sum(r[1]['GRBM_GUI_ACTIVE'] for r in rows) / 8.0
+            busy = sum(r[1].get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) for r in rows)
+            out['conv_mfma'] = dict(
+                math=math, batch=batch, launches=nconv,
+                clock_GHz=round(act / dur, 3),
+                mfma_busy_frac=round(busy / (1024.0 * act), 4),
+                mfma_busy_frac_at_2p4GHz=round(busy / (1024.0 * dur * 2.4), 4),
+                source='rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (third pass)')
     print(json.dumps(out, indent=1))
 
 
