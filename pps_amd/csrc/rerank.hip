@@ -239,26 +239,42 @@ __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, i
       }
       __syncthreads();
     }
-  // segmented sums per column in row order t (key order), then / k2
+  // segmented sums per column in row order t (key order), then / k2.  Each
+  // thread owns a contiguous run of entries; a segment is summed left to
+  // right by the thread owning its first entry (the serial order), at the
+  // output slot given by a block scan of the segment starts.
+  __shared__ int s_scan[1024];
+  const int per = (n + nt - 1) / nt;
+  const int e0 = tid * per, e1 = min(n, e0 + per);
+  auto is_start = [&](int e) {
+    return e == 0 || (uint32_t)(key[e] >> 32) != (uint32_t)(key[e - 1] >> 32);
+  };
+  int cnt = 0;
+  for (int e = e0; e < e1; ++e) cnt += is_start(e);
+  s_scan[tid] = cnt;
+  __syncthreads();
   if (tid == 0) {
-    int u = 0;
-    int e = 0;
-    while (e < n) {
-      const uint32_t col = (uint32_t)(key[e] >> 32);
-      float s = val[key[e] & 0xffff];
-      int f = e + 1;
-      while (f < n && (uint32_t)(key[f] >> 32) == col) {
-        s += val[key[f] & 0xffff];
-        ++f;
-      }
-      if (u < qcap) {
-        q_idx[i * qcap + u] = (int32_t)col;
-        q_val[i * qcap + u] = s / (float)k2;
-      }
-      ++u;
-      e = f;
+    int run = 0;
+    for (int t = 0; t < nt; ++t) {
+      const int v = s_scan[t];
+      s_scan[t] = run;
+      run += v;
     }
-    q_cnt[i] = u;
+    q_cnt[i] = run;
+  }
+  __syncthreads();
+  int u = s_scan[tid];
+  for (int e = e0; e < e1; ++e) {
+    if (!is_start(e)) continue;
+    const uint32_t col = (uint32_t)(key[e] >> 32);
+    float sum = val[key[e] & 0xffff];
+    for (int f = e + 1; f < n && (uint32_t)(key[f] >> 32) == col; ++f)
+      sum += val[key[f] & 0xffff];
+    if (u < qcap) {
+      q_idx[i * qcap + u] = (int32_t)col;
+      q_val[i * qcap + u] = sum / (float)k2;
+    }
+    ++u;
   }
 }
 
