@@ -284,17 +284,38 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const bool sym = (EPI & EPI_DIST) && p.sym;
   int tile_m, tile_n;
   if (sym) {
-    // self-distance: the grid enumerates only the upper-triangle tiles
-    // (row-major), so every XCD gets an equal, contiguous share of them
+    // self-distance: the grid enumerates only the upper-triangle tiles, so
+    // every XCD gets an equal, contiguous share of them.  Grouped like the
+    // distance order below: GM row panels (~32 MB) sweep their columns
+    // together (column-major inside the group), so each column block is
+    // streamed once per group instead of once per row panel.
     const int n = tiles_n;
     const int k = xcd_remap(blockIdx.x, n * (n + 1) / 2);
-    const double b = 2.0 * n + 1.0;
-    int i = (int)((b - sqrt(b * b - 8.0 * k)) * 0.5);
-    auto row0 = [n](int r) { return r * n - r * (r - 1) / 2; };  // first index of row r
-    while (i > 0 && row0(i) > k) --i;
-    while (i + 1 < n && row0(i + 1) <= k) ++i;
-    tile_m = i;
-    tile_n = i + (k - row0(i));
+    const int64_t panel = (int64_t)BM * p.Kloop * (A3 ? 6 : 4);
+    const int64_t want = ((int64_t)32 << 20) / (panel > 0 ? panel : 1);
+    const int GM = (int)(want < 1 ? 1 : (want < n ? want : n));
+    int g0 = 0, base = 0;
+    for (;;) {  // find the group (at most n / GM + 1 steps)
+      const int gm = n - g0 < GM ? n - g0 : GM;
+      const int cnt = gm * (gm + 1) / 2 + gm * (n - g0 - gm);
+      if (k < base + cnt || g0 + gm >= n) break;
+      base += cnt;
+      g0 += gm;
+    }
+    const int gm = n - g0 < GM ? n - g0 : GM;
+    const int r = k - base;
+    const int t1 = gm * (gm + 1) / 2;  // the group's own triangle, column c has c+1 tiles
+    if (r < t1) {
+      int c = (int)((sqrt(8.0 * r + 1.0) - 1.0) * 0.5);
+      while (c > 0 && c * (c + 1) / 2 > r) --c;
+      while ((c + 1) * (c + 2) / 2 <= r) ++c;
+      tile_m = g0 + (r - c * (c + 1) / 2);
+      tile_n = g0 + c;
+    } else {
+      const int r2 = r - t1;
+      tile_n = g0 + gm + r2 / gm;
+      tile_m = g0 + r2 % gm;
+    }
   } else {
     const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
     if (EPI & EPI_DIST) {

@@ -254,7 +254,7 @@ def test_distmat_query_planes_same_bits(Q, G, D):
     np.testing.assert_allclose(want, ev.compute_dist(qn, gn), rtol=0, atol=1e-4 * np.sqrt(D / 64))
 
 
-@pytest.mark.parametrize('N,D', [(1000, 3968), (301, 64), (129, 2048), (17, 32)])
+@pytest.mark.parametrize('N,D', [(1000, 3968), (2500, 3968), (301, 64), (129, 2048), (17, 32)])
 @pytest.mark.parametrize('metric', ['euclidean', 'cosine'])
 def test_self_distance_symmetric(N, D, metric):
     """compute_dist(x, x) from the upper-triangle tiles + mirror: symmetric,
