@@ -267,6 +267,7 @@ def main():
         m.set_tiles(saved)
         if '__planes__' in saved:
             m.set_planes(saved['__planes__'])
+        m.set_splitks(saved.get('__splitk__', {}))
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
         pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
     elif not args.no_autotune:
@@ -305,7 +306,7 @@ def main():
         with open(args.tiles_file, 'w') as f:
             json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile'],
                            __distmat_qplanes__=ret['distmat_qplanes'],
-                           __planes__=m.planes()), f, indent=0)
+                           __planes__=m.planes(), __splitk__=m.splitks()), f, indent=0)
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
     dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
@@ -323,7 +324,7 @@ def main():
                                'batch %d/GPU, 384x128, 3368q x 15913g L2 distmat' % B,
                    'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': m.feat_dim,
                    'parallelism': 'dp%d' % world, 'hipgraph': graph is not None,
-                   'act_plane_edges': len(m.planes())},
+                   'act_plane_edges': len(m.planes()), 'splitk_layers': len(m.splitks())},
         'distmat_GBps': round(total_bytes / (dist_ms_max * 1e-3) / 1e9, 2),
         'distmat_ms': round(dist_ms_max, 3),
         'distmat_TFLOPs_per_gpu': round(dist_tflops, 2),

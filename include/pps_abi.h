@@ -247,6 +247,23 @@ int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane,
                           const float* shift, const float* residual, int relu,
                           float* y, uint16_t* y3, int64_t y_plane, int Ho,
                           int Wo, int ldy, int tile, void* stream);
+/* pps_conv2d_bn_act_x3p with split-K: the K = KH*KW*Cin reduction is cut
+ * into `splitk` slices (whole 32-wide chunks, Kpad % (32*splitk) == 0) that
+ * run as separate workgroups writing raw partial sums part
+ * [splitk][N*Ho*Wo][Cout] (caller-owned), then one pass sums them in slice
+ * order and applies scale/shift [+ residual] [ReLU] to y (f32) or y3
+ * (planes).  For layers whose output tiles alone under-fill the 256 CUs
+ * (res4 at batch 64: 12288 x 256).  A separate rounding group (the slices
+ * are summed at the end), same f32-level error. */
+int pps_conv2d_bn_act_x3p_splitk(const float* x, const uint16_t* x3, int64_t x_plane,
+                                 int N, int H, int W, int Cin, int ldx,
+                                 const uint16_t* w3, int Cout, int Kpad, int KH,
+                                 int KW, int stride, int pad, int dil,
+                                 const float* scale, const float* shift,
+                                 const float* residual, int relu, float* y,
+                                 uint16_t* y3, int64_t y_plane, int Ho, int Wo,
+                                 int ldy, int splitk, float* part, int tile,
+                                 void* stream);
 int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin,
                               int ldx, int KH, int KW, int stride, int pad,
                               const float* x2, int H2, int W2, int Cin2,

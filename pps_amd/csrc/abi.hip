@@ -43,6 +43,8 @@ int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int,
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
 int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
                             const float*, int, int, float*, hipStream_t);
+int splitk_conv_epilogue(const float*, int, int64_t, int, const float*, const float*,
+                         const float*, int, float*, uint16_t*, int64_t, hipStream_t);
 
 }  // namespace pps
 
@@ -297,7 +299,8 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       int pad, int dil, const float* scale, const float* shift,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
                       int tile, void* stream, const uint16_t* x_pl = nullptr,
-                      int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0) {
+                      int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0,
+                      int splitk = 1, float* part = nullptr) {
   PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
               "exactly one of x / x planes and one of y / y planes must be given");
   if (x_pl || y_pl) {
@@ -342,6 +345,28 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
     p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
   }
+  if (splitk > 1) {
+    // conv split-K: raw partial sums of K slices [splitk][M][Cout] on the
+    // pipelined kernel, then one pass that sums them in slice order and
+    // applies BN [+ residual] [ReLU] (f32 or bf16x3-plane output)
+    PPS_ENFORCE(x3 && part, "split-K needs the bf16x3 weights and a partials buffer");
+    PPS_ENFORCE(Cin % 32 == 0 && Kpad % (32 * splitk) == 0 && Kpad == KH * KW * Cin,
+                "split-K needs Cin % 32 == 0 and Kpad % (32 * splitk) == 0");
+    PPS_ENFORCE(ldy == Cout && Cout % 4 == 0 && aligned16(part), "split-K: dense output");
+    PPS_ENFORCE(tile == 0 || tile >= GEMM_TILE_P_FIRST, "split-K needs a pipelined tile");
+    const int64_t M = (int64_t)N * Ho * Wo;
+    p.splitk = splitk; p.ksplit_conv = 1;
+    p.Kloop = Kpad / splitk; p.kb_valid = p.Kloop;
+    p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
+    p.b_bytes = (uint32_t)(p.b_plane * 2);
+    p.out = part; p.out3 = nullptr; p.ldo = Cout; p.out_sstride = M * Cout;
+    p.residual = nullptr; p.relu = 0;
+    p.tile = tile ? tile : GEMM_TILE_P_FIRST + 8;
+    const int rc = launch_gemm_x3(p, EPI_CONV | EPI_F_RAW, 1, as_stream(stream));
+    if (rc != PPS_OK) return rc;
+    return splitk_conv_epilogue(part, splitk, M, Cout, scale, shift, residual, relu,
+                                y_pl ? nullptr : y, y_pl, y_plane, as_stream(stream));
+  }
   if (y_pl) { p.out = nullptr; p.out3 = y_pl; p.out_plane = y_plane; }
   if (x3) {
     p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
@@ -368,6 +393,19 @@ int pps_conv2d_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
                          int tile, void* stream) {
   return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
                    shift, residual, relu, y, Ho, Wo, ldy, tile, stream);
+}
+
+int pps_conv2d_bn_act_x3p_splitk(const float* x, const uint16_t* x3, int64_t x_plane, int N,
+                                 int H, int W, int Cin, int ldx, const uint16_t* w3, int Cout,
+                                 int Kpad, int KH, int KW, int stride, int pad, int dil,
+                                 const float* scale, const float* shift, const float* residual,
+                                 int relu, float* y, uint16_t* y3, int64_t y_plane, int Ho,
+                                 int Wo, int ldy, int splitk, float* part, int tile,
+                                 void* stream) {
+  PPS_ENFORCE(splitk >= 1 && splitk <= 16, "splitk must be in [1, 16]");
+  return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x3, x_plane, y3,
+                   y_plane, splitk, part);
 }
 
 int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N, int H,

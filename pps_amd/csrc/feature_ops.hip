@@ -5,6 +5,7 @@
 #include <algorithm>
 
 #include "pps_internal.hpp"
+#include "gemm_x3_common.hpp"
 
 namespace pps {
 
@@ -143,6 +144,61 @@ int part_power_set(const float* x, int N, int H, int W, int C, const int32_t* sp
   hipLaunchKernelGGL(part_power_set_v2_kernel, grid, block, 0, st, x, N, H, W, C, sp, S,
                      max_ave, out);
   PPS_CHECK_LAUNCH("part_power_set_v2_kernel");
+  return PPS_OK;
+}
+
+// ---- split-K conv epilogue ---------------------------------------------------
+// y = relu?(sum_s part[s] * scale + shift [+ residual]) over the S partial
+// slices in fixed order (deterministic), written as f32 or as bf16x3 planes
+// (y3 + k * plane: the exact split of the pipelined GEMM's EPI_F_PLANES).
+__global__ void splitk_conv_epilogue_kernel(const float* __restrict__ part, int S,
+                                            int64_t sstride, int64_t total4, int N4,
+                                            const float* __restrict__ scale,
+                                            const float* __restrict__ shift,
+                                            const float* __restrict__ res, int relu,
+                                            float* __restrict__ y, uint16_t* __restrict__ y3,
+                                            int64_t plane) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % N4);
+    f32x4 v = reinterpret_cast<const f32x4*>(part)[t];
+    for (int s = 1; s < S; ++s) {
+      const f32x4 w = reinterpret_cast<const f32x4*>(part + s * sstride)[t];
+      v += w;
+    }
+    const f32x4 sc = reinterpret_cast<const f32x4*>(scale)[c4];
+    const f32x4 sh = reinterpret_cast<const f32x4*>(shift)[c4];
+    const f32x4 rv = res ? reinterpret_cast<const f32x4*>(res)[t] : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = __builtin_fmaf(v[e], sc[e], sh[e]);
+      if (res) v[e] += rv[e];
+      if (relu) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (y3) {
+      unsigned h0, m0, l0, h1, m1, l1;
+      split2(v[0], v[1], h0, m0, l0);
+      split2(v[2], v[3], h1, m1, l1);
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      reinterpret_cast<u32x2_t*>(y3)[t] = (u32x2_t){h0, h1};
+      reinterpret_cast<u32x2_t*>(y3 + plane)[t] = (u32x2_t){m0, m1};
+      reinterpret_cast<u32x2_t*>(y3 + 2 * plane)[t] = (u32x2_t){l0, l1};
+    } else {
+      reinterpret_cast<f32x4*>(y)[t] = v;
+    }
+  }
+}
+
+int splitk_conv_epilogue(const float* part, int S, int64_t M, int N, const float* scale,
+                         const float* shift, const float* res, int relu, float* y,
+                         uint16_t* y3, int64_t plane, hipStream_t st) {
+  const int64_t total4 = M * N / 4;
+  if (total4 == 0) return PPS_OK;
+  const int64_t want = (total4 + 255) / 256;
+  hipLaunchKernelGGL(splitk_conv_epilogue_kernel, dim3((unsigned)(want < 16384 ? want : 16384)),
+                     dim3(256), 0, st, part, S, M * N, total4, N / 4, scale, shift, res, relu,
+                     y, y3, plane);
+  PPS_CHECK_LAUNCH("splitk_conv_epilogue_kernel");
   return PPS_OK;
 }
 

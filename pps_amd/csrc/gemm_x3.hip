@@ -268,6 +268,11 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
+  if (p.ksplit_conv && (p.tile < GEMM_TILE_P_FIRST || !x3p_eligible(p, epi))) {
+    set_error("conv split-K runs on the pipelined tiles only (tile >= " +
+              std::to_string((int)GEMM_TILE_P_FIRST) + ", Cin % 32 == 0)");
+    return PPS_ERR_INVALID_ARG;
+  }
   if (p.sym) {
     // self-distance: square pipelined tiles only (the triangle is by tile)
     const int v = p.tile >= GEMM_TILE_P_FIRST ? p.tile - GEMM_TILE_P_FIRST : GEMM_TILE_P16_FIRST -

@@ -345,6 +345,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const int batch = blockIdx.y / p.splitk;
   const int kslice = blockIdx.y - batch * p.splitk;
   const int64_t kofs0 = (int64_t)kslice * p.Kloop;
+  const int64_t aofs0 = p.ksplit_conv ? 0 : kofs0;  // conv split: start tap instead
 
   // ---- A pieces: piece q = wave*AI + i covers tile rows 8q..8q+7; lane l
   // takes row 8q + (l >> 3) and fills physical chunk l & 7 with logical
@@ -353,12 +354,12 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // l & 3 holding logical chunk (l & 3) ^ ((row >> 2) & 3) (8 bf16)
   rsrc_t ra, ra1, ra2;
   if (A3) {
-    const uint16_t* a3 = p.a3 + batch * p.a_bstride + kofs0;
+    const uint16_t* a3 = p.a3 + batch * p.a_bstride + aofs0;
     ra = make_rsrc(a3, p.a_bytes);
     ra1 = make_rsrc(a3 + p.a_plane, p.a_bytes);
     ra2 = make_rsrc(a3 + 2 * p.a_plane, p.a_bytes);
   } else {
-    ra = make_rsrc(p.a + batch * p.a_bstride + kofs0, p.a_bytes);
+    ra = make_rsrc(p.a + batch * p.a_bstride + aofs0, p.a_bytes);
     ra1 = ra;
     ra2 = DUAL ? make_rsrc(p.a2, p.a2_bytes) : ra;
   }
@@ -415,6 +416,13 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   int tc = 0, tt = 0, tkw = 0, toff = 0;
   const int step_w = p.dil * p.lda;
   const int step_h = p.dil * p.lda * (p.W - p.KW);
+  if (p.ksplit_conv && kslice) {  // this slice starts at tap t0, channel c0
+    const int k0 = (int)kofs0;
+    tt = k0 / p.Cin;
+    tc = k0 - tt * p.Cin;
+    tkw = tt % p.KW;
+    toff = (tt / p.KW) * p.dil * p.lda * p.W + tkw * step_w;
+  }
   const int nch1 = DUAL ? p.Kloop1 / BK : (1 << 30);
   int kiss = 0;  // next chunk to request
   int siss = 0;  // its LDS stage
@@ -652,6 +660,8 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
     switch (epi) {
       case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSP, EPI_DIST, true, S>(p, batch, stream); break;
       case C: launch_one_p<BM, BN, WM, WN, NSP, C, true, S>(p, batch, stream); break;
+      case C | EPI_F_RAW:
+        launch_one_p<BM, BN, WM, WN, NSP, C | EPI_F_RAW, true, S>(p, batch, stream); break;
       case C | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RL, true, S>(p, batch, stream); break;
       case C | RS | RL: launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL, true, S>(p, batch, stream); break;
       case C | PL: launch_one_p<BM, BN, WM, WN, NSP, C | PL, true, S>(p, batch, stream); break;

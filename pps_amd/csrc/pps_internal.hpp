@@ -120,6 +120,11 @@ struct GemmParams {
   // tiles): strictly-lower tiles exit, strictly-upper tiles also write the
   // mirrored block out[c][r]
   int sym;
+  // split-K of an implicit-GEMM conv (pipelined kernel, EPI_F_RAW partials):
+  // slice s covers K elements [s*Kloop, (s+1)*Kloop) of the full im2col K
+  // (tap t0 = k0 / Cin, channel k0 % Cin); the A pointer is NOT offset (the
+  // plain-GEMM split-K of the heads offsets it instead)
+  int ksplit_conv;
   int tile;  // GemmTile; 0 = heuristic
   int splitk;           // >= 1; K slices enumerated with the batch on grid.y
   int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)

@@ -260,6 +260,9 @@ def pack_conv_weight(w, cin_pad=None):
 # ---------------------------------------------------------------------------
 # Device model
 # ---------------------------------------------------------------------------
+MAX_SPLITK = 4  # conv split-K factors autotune tries (2..MAX_SPLITK)
+
+
 class PPSModel(object):
     """Device-resident PPS extractor.  forward(x_nhwc4) -> [N, 3968] features.
 
@@ -461,6 +464,13 @@ class PPSModel(object):
         self._bufs = {k: (ops.act_planes(v, self.device) if k in planes else
                           torch.empty(v, dtype=torch.float32, device=self.device))
                       for k, v in shapes.items() if k != 'data'}
+        # split-K partial sums (x3): room for MAX_SPLITK slices of the largest
+        # conv output, shared by the layers that use split-K
+        if self.math == 'x3':
+            big = max((np.prod(shapes[L['output']]) for L in self.layers if L['op'] == 'conv'),
+                      default=0)
+            self._part = torch.empty((int(MAX_SPLITK * big),), dtype=torch.float32,
+                                     device=self.device)
         self._batch = (N, H, W)
 
     def buffers(self):
@@ -473,15 +483,17 @@ class PPSModel(object):
         """Algorithmic HBM bytes of the GEMM launches of one forward."""
         return sum(L['bytes'] for L in self.layers if L['op'] in kinds)
 
-    def _run(self, L, bufs, out=None, tile=None):
+    def _run(self, L, bufs, out=None, tile=None, splitk=None):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
-        if op == 'conv' and (L.get('planes_in') or L.get('planes_out')):
-            tile = tile if tile >= ops.TILE_P_FIRST else 0  # planes: pipelined tiles only
+        sk = L.get('splitk', 1) if splitk is None else splitk
+        if op == 'conv' and (L.get('planes_in') or L.get('planes_out') or sk > 1):
+            tile = tile if tile >= ops.TILE_P_FIRST else 0  # pipelined tiles only
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
                                   L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
-                                  res, L['relu'], bufs[L['output']], tile=tile)
+                                  res, L['relu'], bufs[L['output']], tile=tile, splitk=sk,
+                                  part=self._part if sk > 1 else None)
         elif op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
@@ -531,14 +543,19 @@ class PPSModel(object):
                 timer.append((L.get('name', L['output']), L['op'], L['flops'], ev0, ev1))
         return bufs[self.plan.output]
 
-    def autotune(self, x, reps=3, tiles=None, finalists=4, final_reps=10, planes=True):
+    def autotune(self, x, reps=3, tiles=None, finalists=4, final_reps=10, planes=True,
+                 splitk=False):
         """Pick the fastest GEMM tile per conv layer by timing every candidate
         on this device (the cudnn_exhaustive_search analogue of the
         reference's DetectionModelHelper, detector.py:58): a screening pass
         over all tiles, then the `finalists` best re-timed with `final_reps`
         launches each.  Then (x3 with act_planes) each plane-eligible edge,
         in forward order, is switched to bf16x3 planes and kept if its two
-        layers, re-tuned, get > 2 % faster.  Results do not depend on the
+        layers, re-tuned, get > 2 % faster; last (x3, splitk=True) each conv
+        tries split-K 2..MAX_SPLITK on the pipelined tiles, kept if > 2 %
+        faster -- off by default: at batch 64 it wins 7-8 % on isolated res5
+        layers (scripts/splitk_probe.py) but never inside the forward, where
+        the extra partial-sum pass eats the gain.  Results do not depend on the
         tile or the plane choice (same per-element accumulation order)."""
         self.forward(x)
         torch.cuda.synchronize()
@@ -590,7 +607,50 @@ class PPSModel(object):
                 else:
                     self._set_edge(P, C, False)
                     P['tile'], C['tile'] = saved
+        if self.math == 'x3' and splitk:
+            # split-K (conv_bn_act_x3p_splitk) where it beats the one-pass
+            # kernel by > 2 % -- the res5 3x3/1x1 layers at batch 64
+            ptiles = [t for t in cands if t >= ops.TILE_P_FIRST]
+
+            def time_split(L, t, sk, n):
+                bufs = dict(self._bufs)
+                bufs['data'] = x
+                for _ in range(2):
+                    self._run(L, bufs, tile=t, splitk=sk)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(n):
+                    self._run(L, bufs, tile=t, splitk=sk)
+                e1.record()
+                e1.synchronize()
+                return e0.elapsed_time(e1) / n
+
+            for L in self.layers:
+                if L['op'] != 'conv' or L['cin_eff'] % 32 or L['kpad'] != L['k'] ** 2 * L['cin_eff']:
+                    continue
+                opts = [(t, sk) for sk in range(2, MAX_SPLITK + 1) if L['kpad'] % (32 * sk) == 0
+                        for t in ptiles]
+                if not opts:
+                    continue
+                times = {o: time_split(L, o[0], o[1], reps) for o in opts}
+                best = sorted(times, key=times.get)[:finalists]
+                final = {o: time_split(L, o[0], o[1], final_reps) for o in best}
+                o = min(final, key=final.get)
+                if final[o] < 0.98 * cost[id(L)]:
+                    L['tile'], L['splitk'] = o
+                    cost[id(L)] = final[o]
+                    report[L['name']] = (L['tile'], times)
         return report
+
+    def splitks(self):
+        """{layer name: split-K factor} of the conv layers that use split-K."""
+        return {L['name']: int(L['splitk']) for L in self.layers if L.get('splitk', 1) > 1}
+
+    def set_splitks(self, sks):
+        for L in self.layers:
+            if L['op'] == 'conv':
+                L['splitk'] = int(sks.get(L['name'], 1))
 
     def tiles(self):
         """{layer name: tile id} of the GEMM layers (0 = heuristic)."""

@@ -288,7 +288,7 @@ def _is_planes(t):
 
 
 def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, residual, relu,
-                      y, tile=0):
+                      y, tile=0, splitk=1, part=None):
     """conv2d_bn_act on the pipelined bf16x3 GEMM where the input and/or the
     output are bf16x3 activation planes (act_planes) instead of f32 NHWC:
     x / y may each be either.  Same bits as the f32-activation call."""
@@ -312,6 +312,16 @@ def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, resid
         yp, y3, ypl = 0, _dev(y, 'y planes', torch.int16), y[0].numel()
     else:
         yp, y3, ypl = _dev(y, 'y'), 0, 0
+    if splitk > 1:
+        M = N * Ho * Wo
+        if part is None or part.numel() < splitk * M * Cout:
+            raise RuntimeError('split-K needs a partials buffer of >= %d floats'
+                               % (splitk * M * Cout))
+        call('pps_conv2d_bn_act_x3p_splitk', xp, x3, xpl, N, H, W, cin, ldx,
+             _dev(w3, 'w', torch.int16), Cout, kpad, k, k, stride, pad, dil,
+             _dev(scale, 'scale'), _dev(shift, 'shift'), rp, int(bool(relu)), yp, y3, ypl, Ho,
+             Wo, Cout, int(splitk), _dev(part, 'part'), int(tile), _stream())
+        return y
     call('pps_conv2d_bn_act_x3p', xp, x3, xpl, N, H, W, cin, ldx, _dev(w3, 'w', torch.int16),
          Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp,
          int(bool(relu)), yp, y3, ypl, Ho, Wo, Cout, int(tile), _stream())

@@ -24,6 +24,7 @@ def main():
             saved = json.load(f)
         m.set_tiles(saved)
         m.set_planes(saved.get('__planes__', m.planes()))
+        m.set_splitks(saved.get('__splitk__', {}))
     elif not os.environ.get('NO_AUTOTUNE'):
         rep = m.autotune(x)
         for k, (t, ts) in rep.items():
@@ -51,6 +52,8 @@ def main():
         if L.get('planes_in') or L.get('planes_out'):
             op += '/p' + ('i' if L.get('planes_in') else '') + ('o' if L.get('planes_out') else '')
         op += ' t%d' % L.get('tile', 0) if op != 'pps' and op != 'maxpool' else ''
+        if L.get('splitk', 1) > 1:
+            op += 's%d' % L['splitk']
         rows.append((name, op, shp, ms, f / (ms * 1e-3) / 1e12 if f else 0))
     for r in rows:
         print('%-22s %-15s %-26s %8.3f ms %7.1f TF' % r)

@@ -292,6 +292,7 @@ def test_bench_configuration_vs_oracle():
         saved = json.load(f)
     m.set_tiles(saved)
     m.set_planes(saved.get('__planes__', []))
+    m.set_splitks(saved.get('__splitk__', {}))
     assert len(m.planes()) > 0
     rng = np.random.RandomState(64)
     imgs = rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)

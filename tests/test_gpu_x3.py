@@ -284,3 +284,57 @@ def test_self_distance_symmetric(N, D, metric):
             assert np.abs(np.diag(d) - np.diag(ref)).max() < 5e-3
         else:
             np.testing.assert_allclose(d, full, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 24, 8, 256, 256, 3, 1, 1),     # res4 branch2b
+    (2, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
+    (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+])
+@pytest.mark.parametrize('splitk', [2, 3, 4])
+@pytest.mark.parametrize('mode', ['f32', 'planes_in', 'planes_out', 'residual'])
+def test_conv_x3_splitk(N, H, W, Cin, Cout, k, s, p, splitk, mode):
+    """Conv split-K (raw slice partials + one summing BN/residual/ReLU pass):
+    within the f32-level bound of the fp64 reference, like the one-pass
+    kernel, for f32 / plane inputs and outputs and with a residual."""
+    from pps_amd import model, ops
+    Kpad = k * k * Cin
+    if Kpad % (32 * splitk):
+        pytest.skip('K does not split into whole 32-wide chunks')
+    rng = np.random.RandomState(Cin + Cout + splitk)
+    xn = rng.randn(N, H, W, Cin).astype(np.float32)
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, Cout).astype(np.float32)
+    sh = (rng.randn(Cout) * 0.1).astype(np.float32)
+    ref = F.conv2d(torch.from_numpy(xn.transpose(0, 3, 1, 2)).double(),
+                   torch.from_numpy(w).double(), stride=s, padding=p)
+    ref = ref * torch.from_numpy(sc).double()[None, :, None, None] + \
+        torch.from_numpy(sh).double()[None, :, None, None]
+    ref = ref.numpy().transpose(0, 2, 3, 1)
+    res = None
+    if mode == 'residual':
+        rn = rng.randn(*ref.shape).astype(np.float32)
+        ref = ref + rn
+        res = _cuda(rn)
+    ref = np.maximum(ref, 0)
+    wp, kpad = model.pack_conv_weight(w)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    x = _cuda(xn)
+    xin = _planes_of(x) if mode == 'planes_in' else x
+    y1 = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, s, p, 1, _cuda(sc), _cuda(sh), res, True, y1,
+                          tile=ops.TILE_P_FIRST)
+    part = torch.empty(splitk * y1.numel(), device='cuda')
+    for tile in (ops.TILE_P_FIRST, ops.TILE_P_FIRST + 8, ops.TILE_P16_FIRST + 7):
+        if mode == 'planes_out':
+            yp = ops.act_planes(ref.shape, 'cuda')
+            ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, s, p, 1, _cuda(sc), _cuda(sh), res,
+                                  True, yp, tile=tile, splitk=splitk, part=part)
+            y = yp.view(torch.bfloat16).double().sum(0).float()
+        else:
+            y = torch.full(ref.shape, float('nan'), device='cuda')
+            ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, s, p, 1, _cuda(sc), _cuda(sh), res,
+                                  True, y, tile=tile, splitk=splitk, part=part)
+        e_split = _rel_err(y.cpu().numpy(), ref)
+        e_one = _rel_err(y1.cpu().numpy(), ref)
+        assert e_split <= X3_VS_F32 * e_one + ERR_FLOOR, (tile, e_split, e_one)
