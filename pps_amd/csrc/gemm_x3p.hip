@@ -72,6 +72,11 @@ __device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f
   return c;
 }
 
+// grouped tile order of the distance GEMMs: MB of query panels per group
+#ifndef X3P_GM_MB
+#define X3P_GM_MB 32
+#endif
+
 template <int S> struct AccT { typedef f32x16 type; };
 template <> struct AccT<16> { typedef f32x4 type; };
 
@@ -292,7 +297,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     const int n = tiles_n;
     const int k = xcd_remap(blockIdx.x, n * (n + 1) / 2);
     const int64_t panel = (int64_t)BM * p.Kloop * (A3 ? 6 : 4);
-    const int64_t want = ((int64_t)32 << 20) / (panel > 0 ? panel : 1);
+    const int64_t want = ((int64_t)X3P_GM_MB << 20) / (panel > 0 ? panel : 1);
     const int GM = (int)(want < 1 ? 1 : (want < n ? want : n));
     int g0 = 0, base = 0;
     for (;;) {  // find the group (at most n / GM + 1 steps)
@@ -326,7 +331,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       // traffic 5.6 -> 2.4 GB per launch and ~10 % faster than row-major
       // (which re-streams the 379 MB gallery planes once per panel).
       const int64_t panel = (int64_t)BM * p.Kloop * (A3 ? 6 : 4);
-      const int64_t want = ((int64_t)32 << 20) / (panel > 0 ? panel : 1);
+      const int64_t want = ((int64_t)X3P_GM_MB << 20) / (panel > 0 ? panel : 1);
       const int GM = (int)(want < 1 ? 1 : (want < tiles_m ? want : tiles_m));
       const int per = GM * tiles_n;
       const int grp = bid / per;

@@ -464,13 +464,7 @@ class PPSModel(object):
         self._bufs = {k: (ops.act_planes(v, self.device) if k in planes else
                           torch.empty(v, dtype=torch.float32, device=self.device))
                       for k, v in shapes.items() if k != 'data'}
-        # split-K partial sums (x3): room for MAX_SPLITK slices of the largest
-        # conv output, shared by the layers that use split-K
-        if self.math == 'x3':
-            big = max((np.prod(shapes[L['output']]) for L in self.layers if L['op'] == 'conv'),
-                      default=0)
-            self._part = torch.empty((int(MAX_SPLITK * big),), dtype=torch.float32,
-                                     device=self.device)
+        self._part = None  # split-K partial sums, grown on first use (_part_for)
         self._batch = (N, H, W)
 
     def buffers(self):
@@ -493,7 +487,8 @@ class PPSModel(object):
             ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
                                   L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                                   res, L['relu'], bufs[L['output']], tile=tile, splitk=sk,
-                                  part=self._part if sk > 1 else None)
+                                  part=self._part_for(sk * np.prod(self._shapes[L['output']]))
+                                  if sk > 1 else None)
         elif op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
@@ -642,6 +637,13 @@ class PPSModel(object):
                     cost[id(L)] = final[o]
                     report[L['name']] = (L['tile'], times)
         return report
+
+    def _part_for(self, n):
+        """Split-K partials buffer of >= n floats, shared by the layers (grown
+        outside graph capture: autotune / the first eager forward)."""
+        if self._part is None or self._part.numel() < n:
+            self._part = torch.empty((int(n),), dtype=torch.float32, device=self.device)
+        return self._part
 
     def splitks(self):
         """{layer name: split-K factor} of the conv layers that use split-K."""
