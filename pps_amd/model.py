@@ -650,9 +650,17 @@ class PPSModel(object):
         return {L['name']: int(L['splitk']) for L in self.layers if L.get('splitk', 1) > 1}
 
     def set_splitks(self, sks):
+        """Apply a splitks() mapping; a factor must cut K into whole 32-wide
+        chunks of a Cin % 32 == 0 conv (bf16x3 math)."""
         for L in self.layers:
-            if L['op'] == 'conv':
-                L['splitk'] = int(sks.get(L['name'], 1))
+            if L['op'] != 'conv':
+                continue
+            sk = int(sks.get(L['name'], 1))
+            if sk > 1 and (self.math != 'x3' or L['cin_eff'] % 32 or sk > MAX_SPLITK or
+                           L['kpad'] != L['k'] ** 2 * L['cin_eff'] or L['kpad'] % (32 * sk)):
+                raise ValueError('split-K %d not possible for %s (K = %d)'
+                                 % (sk, L['name'], L['kpad']))
+            L['splitk'] = sk
 
     def tiles(self):
         """{layer name: tile id} of the GEMM layers (0 = heuristic)."""

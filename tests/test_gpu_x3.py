@@ -338,3 +338,37 @@ def test_conv_x3_splitk(N, H, W, Cin, Cout, k, s, p, splitk, mode):
         e_split = _rel_err(y.cpu().numpy(), ref)
         e_one = _rel_err(y1.cpu().numpy(), ref)
         assert e_split <= X3_VS_F32 * e_one + ERR_FLOOR, (tile, e_split, e_one)
+
+
+def test_forward_splitk_layers():
+    """The model with split-K on the res5 convs (and plane edges) gives the
+    one-pass features within the f32 forward tolerance."""
+    from pps_amd import config, model
+    cfg = config.cfg
+    cfg.MODEL.NUM_CLASSES = 752
+    cfg.MODEL.USE_BN = True
+    cfg.RESNETS.RES5_STRIDE = 1
+    cfg.REID.SCALE = (128, 384)
+    cfg.REID.BPM_STRIP_NUM = 5
+    cfg.REID.BPM_DIM = 128
+    cfg.REID.NORMALIZE_FEATURE = True
+    cfg.REID.MAX_AVE_FEATURE = True
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=2)
+    rng = np.random.RandomState(2)
+    x = np.zeros((4, 384, 128, 4), np.float32)
+    x[..., :3] = rng.randn(4, 384, 128, 3) * 50
+    xd = _cuda(x)
+    m = model.PPSModel(blobs, math='x3')
+    base = m.forward(xd).cpu().numpy()
+    sks = {}
+    for i, L in enumerate(m.layers):
+        if L['op'] == 'conv' and L['name'].startswith('res5'):
+            sk = 2 + (i % 3)
+            sks[L['name']] = sk if L['kpad'] % (32 * sk) == 0 else 2
+    with pytest.raises(ValueError):
+        m.set_splitks({'res5_1_branch2c': 3})  # K = 512: not whole 32-wide chunks
+    m.set_splitks(sks)
+    assert m.splitks() == sks
+    got = m.forward(xd).cpu().numpy()
+    np.testing.assert_allclose(got, base, rtol=0, atol=2e-5)
