@@ -20,6 +20,12 @@
 // * K chunk 32 and Cin % 32 == 0, so a chunk never straddles two im2col taps:
 //   the tap tracker is wave-uniform (scalar) and each lane keeps only a row
 //   base and a 64-bit tap-validity mask per DMA piece.
+//
+// Extensions on the same main loop: bf16x3 activation planes as A (A3) and
+// as output (EPI_F_PLANES); 16x16x32 MFMA blocks (S = 16, their own rounding
+// group); conv split-K (slices starting mid-im2col, raw partials); for the
+// distance epilogue a grouped tile order (GM query panels sweep the gallery
+// together) and the symmetric self-distance (upper-triangle tiles + mirror).
 #include "gemm_x3_common.hpp"
 
 namespace pps {
