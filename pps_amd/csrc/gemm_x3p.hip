@@ -166,6 +166,72 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   }
 }
 
+// The same conv epilogue staged through LDS: the waves park their
+// accumulators as a [BM][BN+4] f32 tile, then the workgroup walks it row by
+// row, so scale/shift, the residual and the output move as whole contiguous
+// rows (16 B per lane, consecutive lanes consecutive columns) instead of the
+// accumulator layout's 32-64 B row pieces.  Same per-element arithmetic in
+// the same order as conv_epilogue_t (identical bits).
+template <int BM, int BN>
+constexpr int lds_epi_bytes() { return BM * (BN + 4) * 4; }
+
+template <int EPI, int BM, int BN, int WM, int WN, int S>
+__device__ inline void conv_epilogue_lds(const GemmParams& p,
+                                         typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                         unsigned char* lds, int batch, int kslice, int m0,
+                                         int n0, int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
+  constexpr int LD = BN + 4;
+  constexpr int NT = 64 * WM * WN;
+  constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
+  constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
+  constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
+  float* t = reinterpret_cast<float*>(lds);
+  __syncthreads();  // every wave is done reading the last stage
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * (BM / WM) + i * S + r32;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cb = wn * (BN / WN) + j * S + 4 * h;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
+  float* __restrict__ out = p.out + obase;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0, nrem = p.Ncol - n0;
+  const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0;
+  const float* sh = p.shift + batch * p.ss_bstride + n0;
+  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+  const int ldr = (int)p.ldr;
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+    const int row = idx / C4, col = 4 * (idx - row * C4);
+    if (row >= mrem || col >= nrem) continue;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
+    const f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
+    const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + col);
+    f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_RES) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = __builtin_fmaf(a[e], s4[e], t4[e]);
+      if (HAS_RES) v[e] += rv[e];
+      if (RELU) v[e] = fmaxf(v[e], 0.f);
+    }
+    *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+  }
+}
+
 // Distance epilogue on transposed accumulators: same formulas as
 // dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
 template <int BM, int BN, int WM, int WN, int S = 32>
@@ -283,7 +349,19 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   static_assert(NLOAD * (NS - 2) <= 63, "vmcnt range");
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
 
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[NS * STAGE];
+  // conv epilogue through LDS where the [BM][BN+4] tile fits the 160 KB:
+  // 5-12 % faster on the epilogue-bound branch2c layers (residual + output
+  // streams) for the 128-row tiles; the 8-wave 192x128 tile is faster
+  // without it (scripts/gemm_probe.py --residual)
+#ifndef X3P_LDSEPI
+#define X3P_LDSEPI 1
+#endif
+  constexpr bool LDSEPI = X3P_LDSEPI && !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
+                          lds_epi_bytes<BM, BN>() <= 160 * 1024 &&
+                          !(BM == 192 && BN == 128 && NW == 8);
+  constexpr int LDS_BYTES =
+      (LDSEPI && lds_epi_bytes<BM, BN>() > NS * STAGE) ? lds_epi_bytes<BM, BN>() : NS * STAGE;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -640,8 +718,10 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
 
-  if (EPI & EPI_DIST)
+  if constexpr ((EPI & EPI_DIST) != 0)
     dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
+  else if constexpr (LDSEPI)
+    conv_epilogue_lds<EPI, BM, BN, WM, WN, S>(p, acc, lds, batch, kslice, m0, n0, wm, wn, r32, h);
   else
     conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
 }
