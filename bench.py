@@ -74,20 +74,26 @@ def synth_features(n, ids, gen, noise=4.0, n_ids=750):
     return (x / x.norm(dim=1, keepdim=True)).contiguous()
 
 
-def retrieval_stage(rank, world, reps, tune=True):
-    """Distance matrix + mAP/CMC at Market sizes.  Gallery sharded over ranks,
-    queries all-gathered.  Returns timings (ms) and scores."""
+def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
+                    n_distractors=2793, n_ids=750):
+    """Distance matrix + mAP/CMC (default: Market sizes; scripts/
+    bench_retrieval_sharded.py passes the CUHK03 / Duke splits).  Gallery
+    sharded over ranks, queries all-gathered.  Returns timings
+    (ms) and scores."""
     from pps_amd import distributed as pdist
+    Q_MARKET, G_MARKET = nq, ng   # local names: the sizes of this run
     rng = np.random.RandomState(0)
-    qid = rng.randint(1, 751, Q_MARKET)
-    gid = np.concatenate([rng.randint(1, 751, G_MARKET - 2793), np.zeros(2793, int)])
+    qid = rng.randint(1, n_ids + 1, Q_MARKET)
+    gid = np.concatenate([rng.randint(1, n_ids + 1, G_MARKET - n_distractors),
+                          np.zeros(n_distractors, int)])
     qcam = rng.randint(1, 7, Q_MARKET)
     gcam = rng.randint(1, 7, G_MARKET)
     gen = torch.Generator(device='cuda')
     gen.manual_seed(0)
     # same global features on every rank (seeded), each rank keeps its shards
     allf = synth_features(Q_MARKET + G_MARKET,
-                          torch.from_numpy(np.concatenate([qid, gid])).cuda(), gen)
+                          torch.from_numpy(np.concatenate([qid, gid])).cuda(), gen,
+                          n_ids=n_ids)
     qsl = pdist.shard_range(Q_MARKET, rank, world)
     gsl = pdist.shard_range(G_MARKET, rank, world)
     q_local = allf[qsl[0]:qsl[1]].contiguous()
