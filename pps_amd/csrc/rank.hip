@@ -16,8 +16,14 @@ constexpr int kPosCap = 2048;  // max merged positives per query in LDS
 
 // ---- 1) collect positives ------------------------------------------------------
 // One block per query; wave w scans its own contiguous quarter of the gallery
-// twice (count, then write at its offset), compacting with ballots -- no block
-// barrier inside the scan.  The list keeps ascending gallery order.
+// (count, then write at its offset), compacting with ballots -- no block
+// barrier inside the scan.  The list keeps ascending gallery order.  The id /
+// cam arrays are L2-resident, so the scan is bound by load latency: each
+// thread issues kCpU groups' loads before testing any, and the first pass
+// keeps its 64-entry ballot masks in LDS (up to kMaskCap groups per wave) so
+// the writing pass re-reads ids only beyond that.
+constexpr int kCpU = 4;
+constexpr int kMaskCap = 256;
 __global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t G,
                                          int64_t ldd, const int32_t* __restrict__ qid,
                                          const int32_t* __restrict__ qcam,
@@ -33,15 +39,36 @@ __global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int W = kEvalThreads / 64;
   __shared__ int wtot[W];
+  __shared__ unsigned long long masks[W][kMaskCap];
   const int64_t chunk = ((G + W - 1) / W + 63) / 64 * 64;
   const int64_t beg = wave * chunk;
   const int64_t end = beg + chunk < G ? beg + chunk : G;
   const unsigned long long below = (1ull << lane) - 1ull;
+  // buffer loads: entries at or past G read 0 without a branch (masked below)
+  const rsrc_t rid = make_rsrc(gid, (uint32_t)(G * 4));
+  const rsrc_t rcam = make_rsrc(gcam, (uint32_t)(G * 4));
+  auto group_flags = [&](int64_t t0, bool* f) {
+    int a[kCpU], c[kCpU];
+#pragma unroll
+    for (int u = 0; u < kCpU; ++u) {
+      const int off = (int)((t0 + 64 * u + lane) * 4);
+      a[u] = __builtin_amdgcn_raw_buffer_load_b32(rid, off, 0, 0);
+      c[u] = __builtin_amdgcn_raw_buffer_load_b32(rcam, off, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kCpU; ++u)
+      f[u] = (t0 + 64 * u + lane < end) && a[u] == qi && c[u] != qc;
+  };
   int cnt = 0;
-  for (int64_t t0 = beg; t0 < end; t0 += 64) {
-    const int64_t i = t0 + lane;
-    const bool flag = i < end && gid[i] == qi && gcam[i] != qc;
-    cnt += __popcll(__ballot(flag));
+  for (int64_t t0 = beg, g = 0; t0 < end; t0 += 64 * kCpU, g += kCpU) {
+    bool f[kCpU];
+    group_flags(t0, f);
+#pragma unroll
+    for (int u = 0; u < kCpU; ++u) {
+      const unsigned long long bal = __ballot(f[u]);
+      if (g + u < kMaskCap && lane == 0) masks[wave][g + u] = bal;
+      cnt += __popcll(bal);
+    }
   }
   if (lane == 0) wtot[wave] = cnt;
   __syncthreads();
@@ -52,16 +79,28 @@ __global__ void collect_positives_kernel(const float* __restrict__ dist, int64_t
     total += wtot[w];
   }
   if (slot < Pmax && cnt > 0) {
-    for (int64_t t0 = beg; t0 < end; t0 += 64) {
-      const int64_t i = t0 + lane;
-      const bool flag = i < end && gid[i] == qi && gcam[i] != qc;
-      const unsigned long long bal = __ballot(flag);
-      const int s = slot + __popcll(bal & below);
-      if (flag && s < Pmax) {
-        pos_d[q * Pmax + s] = row[i];
-        pos_idx[q * Pmax + s] = (int32_t)(g_offset + i);
+    for (int64_t t0 = beg, g = 0; t0 < end && slot < Pmax; t0 += 64 * kCpU, g += kCpU) {
+      unsigned long long bal[kCpU];
+      if (g + kCpU <= kMaskCap) {
+#pragma unroll
+        for (int u = 0; u < kCpU; ++u) bal[u] = masks[wave][g + u];
+      } else {
+        bool f[kCpU];
+        group_flags(t0, f);
+#pragma unroll
+        for (int u = 0; u < kCpU; ++u) bal[u] = __ballot(f[u]);
       }
-      slot += __popcll(bal);
+#pragma unroll
+      for (int u = 0; u < kCpU; ++u) {
+        const int64_t i = t0 + 64 * u + lane;
+        const bool flag = (bal[u] >> lane) & 1ull;
+        const int s = slot + __popcll(bal[u] & below);
+        if (flag && s < Pmax) {
+          pos_d[q * Pmax + s] = row[i];
+          pos_idx[q * Pmax + s] = (int32_t)(g_offset + i);
+        }
+        slot += __popcll(bal[u]);
+      }
     }
   }
   if (threadIdx.x == 0) pos_cnt[q] = total;
@@ -100,11 +139,15 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
   const int64_t q = blockIdx.x;
   const int Ptot = R * Pmax;
   const int qi = qid[q], qc = qcam[q];
-  __shared__ float ud[kPosCap];
-  __shared__ int ui[kPosCap];
-  __shared__ float sd[kPosCap];
-  __shared__ int si[kPosCap];
-  __shared__ int hs[kPosCap];
+  // positive lists in dynamic LDS sized to R*Pmax (<= kPosCap): tens of
+  // entries on real splits, so several blocks share a CU and keep enough
+  // row loads in flight (a fixed 40 KB allowed three)
+  extern __shared__ int dyn_lds[];
+  float* ud = reinterpret_cast<float*>(dyn_lds);
+  int* ui = dyn_lds + Ptot;
+  float* sd = reinterpret_cast<float*>(dyn_lds + 2 * Ptot);
+  int* si = dyn_lds + 3 * Ptot;
+  int* hs = dyn_lds + 4 * Ptot;
   __shared__ int offs[65];
   __shared__ int red[kEvalThreads / 64];
   // merged list layout: list r occupies [offs[r], offs[r+1])
@@ -163,22 +206,38 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
       if (lo < P) atomicAdd(&hs[lo], 1);
       nbefore += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
     };
-    constexpr int U = 4;  // independent row loads in flight per thread
+    // The row is streamed as 16-byte vectors: a scalar head up to the first
+    // 16-byte boundary (rows of odd length start unaligned), U float4 loads
+    // in flight per thread, a scalar tail.  visit() only accumulates
+    // order-free counts, so the visiting order does not matter.
+    const int64_t head0 = (int64_t)(((16 - ((uintptr_t)row & 15)) & 15) >> 2);
+    const int64_t head = head0 < G ? head0 : G;
+    const int64_t nb = (G - head) >> 2;
+    if (threadIdx.x < head) visit(threadIdx.x, row[threadIdx.x]);
+    const float4* body = reinterpret_cast<const float4*>(row + head);
+    constexpr int U = 4;
     const int64_t step = (int64_t)blockDim.x * U;
-    // buffer loads (tail reads zero without a branch; visit() skips it)
-    const rsrc_t rrow = make_rsrc(row, (uint32_t)(G * 4));
-    for (int64_t i0 = threadIdx.x; i0 < G; i0 += step) {
-      float d[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        d[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                             rrow, (int)((i0 + (int64_t)u * blockDim.x) * 4), 0, 0));
+    for (int64_t j0 = threadIdx.x; j0 < nb; j0 += step) {
+      float4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t i = i0 + (int64_t)u * blockDim.x;
-        if (i < G) visit(i, d[u]);
+        const int64_t j = j0 + (int64_t)u * blockDim.x;
+        v[u] = j < nb ? body[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = j0 + (int64_t)u * blockDim.x;
+        if (j < nb) {
+          const int64_t i = head + 4 * j;
+          visit(i, v[u].x);
+          visit(i + 1, v[u].y);
+          visit(i + 2, v[u].z);
+          visit(i + 3, v[u].w);
+        }
       }
     }
+    const int64_t t = head + 4 * nb + threadIdx.x;
+    if (t < G) visit(t, row[t]);
   }
   for (int o = 32; o > 0; o >>= 1) nbefore += __shfl_xor(nbefore, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nbefore;
@@ -198,7 +257,9 @@ int rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int3
                 int32_t* sorted_idx, int32_t* pos_total, int32_t* hist, int32_t* before,
                 hipStream_t st) {
   if (Q <= 0) return PPS_OK;
-  hipLaunchKernelGGL(rank_counts_kernel, dim3((unsigned)Q), dim3(kEvalThreads), 0, st,
+  if ((int64_t)R * Pmax > kPosCap) return PPS_ERR_CAPACITY;  // abi.hip reports it
+  const size_t lds = (size_t)5 * R * Pmax * sizeof(int);
+  hipLaunchKernelGGL(rank_counts_kernel, dim3((unsigned)Q), dim3(kEvalThreads), lds, st,
                      dist, Q, G, ldd, qid, qcam, gid, gcam, g_offset, R, Pmax, pos_d,
                      pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, hist, before);
   PPS_CHECK_LAUNCH("rank_counts_kernel");
