@@ -79,6 +79,12 @@ int pps_distmat(const float* q, int64_t Q, int64_t ldq,
  * split and normed once, then scored against any number of query batches). */
 int pps_row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out,
                    void* stream);
+/* Both in one read of x (a gallery index or a query batch): out3 =
+ * pps_split_bf16x3 planes [3][rows][D] (row stride D, plane stride rows*D),
+ * sqnorm = pps_row_sqnorm; bit-identical to the two calls.  D % 4 == 0,
+ * ld % 4 == 0, x 16-byte and out3 8-byte aligned. */
+int pps_split_bf16x3_sqnorm(const float* x, int64_t rows, int D, int64_t ld,
+                            uint16_t* out3, float* sqnorm, void* stream);
 int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
                    int metric, float* out, int64_t ldo, int tile, void* stream);

@@ -24,6 +24,7 @@ SIGNATURES = {
                     c_i64, c_int, c_ptr],
     'pps_pairwise_distance': [c_ptr, c_int, c_int, c_ptr, c_ptr],
     'pps_row_sqnorm': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr],
+    'pps_split_bf16x3_sqnorm': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr, c_ptr],
     'pps_distmat_x3': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
                        c_ptr, c_i64, c_int, c_ptr],
     'pps_distmat_x3p': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,

@@ -106,6 +106,15 @@ int pps_row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out,
   return row_sqnorm(x, rows, D, ld, out, as_stream(stream));
 }
 
+int pps_split_bf16x3_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3,
+                            float* sqnorm, void* stream) {
+  PPS_ENFORCE(x && out3 && sqnorm, "null pointer");
+  PPS_ENFORCE(rows >= 0 && D > 0 && D % 4 == 0 && ld >= D && ld % 4 == 0, "bad shape");
+  PPS_ENFORCE(aligned16(x), "x must be 16-byte aligned");
+  PPS_ENFORCE(((uintptr_t)out3 & 7) == 0, "out3 must be 8-byte aligned");
+  return split_sqnorm(x, rows, D, ld, out3, sqnorm, as_stream(stream));
+}
+
 int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
                    int metric, float* out, int64_t ldo, int tile, void* stream) {

@@ -358,6 +358,31 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t n, int 
   }
 }
 
+// Eight elements per thread: two 16-byte loads, three 16-byte plane stores
+// (the scalar kernel's 2-byte stores ran the gallery split at ~4 TB/s).
+// Needs n % 8 == 0 and 16-byte aligned x / out; same bits as the scalar one.
+__global__ void split_bf16x3_v8_kernel(const float* __restrict__ x, int64_t n, int nbatch,
+                                       unsigned short* __restrict__ out) {
+  const int64_t n8 = n >> 3;
+  const int64_t total = n8 * nbatch;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / n8, i = (e - b * n8) << 3;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(x + (e << 3));
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(x + (e << 3) + 4);
+    u32x4 hi, mid, lo;
+    unsigned a, m, l;
+    split2(v0[0], v0[1], a, m, l); hi[0] = a; mid[0] = m; lo[0] = l;
+    split2(v0[2], v0[3], a, m, l); hi[1] = a; mid[1] = m; lo[1] = l;
+    split2(v1[0], v1[1], a, m, l); hi[2] = a; mid[2] = m; lo[2] = l;
+    split2(v1[2], v1[3], a, m, l); hi[3] = a; mid[3] = m; lo[3] = l;
+    unsigned short* o = out + b * 3 * n + i;
+    *reinterpret_cast<u32x4*>(o) = hi;
+    *reinterpret_cast<u32x4*>(o + n) = mid;
+    *reinterpret_cast<u32x4*>(o + 2 * n) = lo;
+  }
+}
+
 // ---- squared row norms: one wave per row, fixed lane order + xor tree -----
 __global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
                                   float* __restrict__ out) {
@@ -378,6 +403,49 @@ __global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int
   if (lane == 0) out[row] = s;
 }
 
+// ---- gallery / query index in one pass: bf16x3 planes [3][rows][D] and
+// squared row norms, reading x once.  The norm uses row_sqnorm_kernel's lane
+// order and xor tree, the split is elementwise: bits equal to the two
+// separate kernels.
+__global__ void split_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
+                                    unsigned short* __restrict__ out3,
+                                    float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* r = x + row * ld;
+  const int64_t plane = rows * (int64_t)D;
+  unsigned short* o = out3 + row * (int64_t)D;
+  float s = 0.f;
+  for (int k = lane * 4; k < D; k += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
+    s = __builtin_fmaf(v[0], v[0], s);
+    s = __builtin_fmaf(v[1], v[1], s);
+    s = __builtin_fmaf(v[2], v[2], s);
+    s = __builtin_fmaf(v[3], v[3], s);
+    u32x2 hi, mid, lo;
+    unsigned a, m, l;
+    split2(v[0], v[1], a, m, l); hi[0] = a; mid[0] = m; lo[0] = l;
+    split2(v[2], v[3], a, m, l); hi[1] = a; mid[1] = m; lo[1] = l;
+    *reinterpret_cast<u32x2*>(o + k) = hi;
+    *reinterpret_cast<u32x2*>(o + plane + k) = mid;
+    *reinterpret_cast<u32x2*>(o + 2 * plane + k) = lo;
+  }
+#pragma unroll
+  for (int o2 = 32; o2 >= 1; o2 >>= 1) s += __shfl_xor(s, o2);
+  if (lane == 0) out[row] = s;
+}
+
+int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,
+                 hipStream_t stream) {
+  if (rows <= 0) return PPS_OK;
+  const int64_t blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(split_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, rows,
+                     D, ld, reinterpret_cast<unsigned short*>(out3), out);
+  PPS_CHECK_LAUNCH("split_sqnorm_kernel");
+  return PPS_OK;
+}
+
 int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream) {
   if (rows <= 0) return PPS_OK;
   const int64_t blocks = (rows + 3) / 4;
@@ -389,6 +457,14 @@ int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipS
 
 int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream) {
   const int threads = 256;
+  if (n % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    const int64_t blocks = (n / 8 * nbatch + threads - 1) / threads;
+    hipLaunchKernelGGL(split_bf16x3_v8_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
+                       dim3(threads), 0, stream, x, n, nbatch,
+                       reinterpret_cast<unsigned short*>(out));
+    PPS_CHECK_LAUNCH("split_bf16x3_v8_kernel");
+    return PPS_OK;
+  }
   const int64_t blocks = (n * nbatch + threads - 1) / threads;
   hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
                      dim3(threads), 0, stream, x, n, nbatch,

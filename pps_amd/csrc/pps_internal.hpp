@@ -152,6 +152,8 @@ bool x3p_eligible(const GemmParams& p, int epi);
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant);
 int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream);
 int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream);
+int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,
+                 hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
 
 }  // namespace pps

@@ -63,6 +63,17 @@ def row_sqnorm(x):
     return out
 
 
+def split_sqnorm(x):
+    """(split_bf16x3(x), row_sqnorm(x)) of a [R, D] tensor from one read of x
+    (pps_split_bf16x3_sqnorm; same bits as the two calls).  Planes [3, R, D]."""
+    R, D = x.shape
+    planes = torch.empty((3, R, D), dtype=torch.int16, device=x.device)
+    sq = torch.empty((R,), dtype=torch.float32, device=x.device)
+    call('pps_split_bf16x3_sqnorm', _dev(x, 'x'), R, D, x.stride(0),
+         _dev(planes, 'out3', torch.int16), _dev(sq, 'sqnorm'), _stream())
+    return planes, sq
+
+
 class GalleryIndex(object):
     """A gallery prepared once for the bf16x3 distance GEMM: features split
     into three bf16 planes + squared norms; score any number of query
@@ -72,8 +83,11 @@ class GalleryIndex(object):
         if g.dim() != 2:
             raise RuntimeError('gallery must be [G, D], got %s' % (tuple(g.shape),))
         self.feats = g
-        self.planes = split_bf16x3(g)
-        self.sqnorm = row_sqnorm(g)
+        if g.is_contiguous() and g.shape[1] % 4 == 0:
+            self.planes, self.sqnorm = split_sqnorm(g)
+        else:
+            self.planes = split_bf16x3(g)
+            self.sqnorm = row_sqnorm(g)
 
     @property
     def shape(self):
@@ -119,13 +133,13 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
              _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric], _dev(out, 'out'),
              out.stride(0), int(tile), _stream())
         return out
-    qsq = row_sqnorm(q)
     if q_planes:
-        q3 = split_bf16x3(q)
+        q3, qsq = split_sqnorm(q) if q.is_contiguous() else (split_bf16x3(q), row_sqnorm(q))
         call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
              _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
              METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
         return out
+    qsq = row_sqnorm(q)
     call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
          METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())

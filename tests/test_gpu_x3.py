@@ -42,6 +42,28 @@ def test_split_bf16x3_exact():
     assert hb.shape == (3, 3, 64, 64)
     np.testing.assert_array_equal(hb.view(torch.bfloat16).double().sum(1).cpu().numpy(),
                                   x[:12288].reshape(3, 64, 64))
+    # 8-wide vector kernel (n % 8 == 0, 16-byte aligned) == scalar kernel
+    # (same data at a 4-byte offset, which forces the scalar path)
+    xd = _cuda(np.concatenate([[0.0], x[:12288]]).astype(np.float32))
+    p_scalar = ops.split_bf16x3(xd[1:])
+    p_vector = ops.split_bf16x3(xd[1:].clone())
+    assert xd[1:].data_ptr() % 16 != 0 and p_vector.shape == (3, 12288)
+    assert torch.equal(p_scalar, p_vector)
+
+
+@pytest.mark.parametrize('R,D', [(1, 4), (7, 132), (33, 2048), (130, 3968)])
+def test_split_sqnorm_fused_equals_separate(R, D):
+    """pps_split_bf16x3_sqnorm (gallery index / query planes in one read)
+    gives the bits of pps_split_bf16x3 + pps_row_sqnorm."""
+    from pps_amd import ops
+    rng = np.random.RandomState(R + D)
+    x = _cuda(rng.randn(R, D).astype(np.float32))
+    planes, sq = ops.split_sqnorm(x)
+    assert planes.shape == (3, R, D)
+    assert torch.equal(planes, ops.split_bf16x3(x))
+    assert torch.equal(sq, ops.row_sqnorm(x))
+    idx = ops.GalleryIndex(x)
+    assert torch.equal(idx.planes, planes) and torch.equal(idx.sqnorm, sq)
 
 
 @pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
