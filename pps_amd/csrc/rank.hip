@@ -192,8 +192,8 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
   int nbefore = 0;
   if (P > 0) {
     // Entries farther than the farthest positive change neither the histogram
-    // (their bin would be P) nor the first-match count, so the common path
-    // reads only the distance; ids/cams are fetched for the few closer ones.
+    // (their bin would be P) nor the first-match count: only the closer ones
+    // (a few % of a row) are searched against the positives.
     const float dmax = sd[P - 1];
     auto visit = [&](int64_t i, float d) {
       if (d > dmax) return;
@@ -215,24 +215,48 @@ __global__ void rank_counts_kernel(const float* __restrict__ dist, int64_t Q, in
     const int64_t nb = (G - head) >> 2;
     if (threadIdx.x < head) visit(threadIdx.x, row[threadIdx.x]);
     const float4* body = reinterpret_cast<const float4*>(row + head);
+    // ids / cams of the same entries are fetched together with the distances
+    // (buffer loads: L2-resident arrays, past-the-end reads return 0): with
+    // 64 lanes nearly every element slot of a wave has an entry closer than
+    // the farthest positive, and a dependent id fetch per slot made the scan
+    // latency-bound (242 -> 115 -> this)
+    const rsrc_t rid = make_rsrc(gid, (uint32_t)(G * 4));
+    const rsrc_t rcam = make_rsrc(gcam, (uint32_t)(G * 4));
+    auto binned = [&](int64_t i, float d, int id, int cam) {
+      if (d > dmax || (id == qi && cam == qc)) return;
+      int lo = 0, hi = P;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sd[mid] < d) lo = mid + 1; else hi = mid;
+      }
+      if (lo < P) atomicAdd(&hs[lo], 1);
+      nbefore += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
+    };
     constexpr int U = 4;
     const int64_t step = (int64_t)blockDim.x * U;
     for (int64_t j0 = threadIdx.x; j0 < nb; j0 += step) {
       float4 v[U];
+      int id[U][4], cam[U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t j = j0 + (int64_t)u * blockDim.x;
         v[u] = j < nb ? body[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int off = (int)((head + 4 * j) * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          id[u][e] = __builtin_amdgcn_raw_buffer_load_b32(rid, off + 4 * e, 0, 0);
+          cam[u][e] = __builtin_amdgcn_raw_buffer_load_b32(rcam, off + 4 * e, 0, 0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t j = j0 + (int64_t)u * blockDim.x;
         if (j < nb) {
           const int64_t i = head + 4 * j;
-          visit(i, v[u].x);
-          visit(i + 1, v[u].y);
-          visit(i + 2, v[u].z);
-          visit(i + 3, v[u].w);
+          binned(i, v[u].x, id[u][0], cam[u][0]);
+          binned(i + 1, v[u].y, id[u][1], cam[u][1]);
+          binned(i + 2, v[u].z, id[u][2], cam[u][2]);
+          binned(i + 3, v[u].w, id[u][3], cam[u][3]);
         }
       }
     }
