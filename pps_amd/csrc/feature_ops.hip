@@ -13,20 +13,23 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---- MaxPool k x k / s, pad p (ResNet.py:255) --------------------------------
 // One thread per (n, oh, ow, 4 channels).  Padding never wins (Caffe2 / cuDNN
-// max pooling ignores padded taps).
+// max pooling ignores padded taps).  Index type IDX: 32-bit unsigned when the
+// element count allows it (the stem's 3.1M threads), so the index split is not
+// three 64-bit divisions per thread.
+template <typename IDX>
 __global__ void maxpool_nhwc_kernel(const float* __restrict__ x, int N, int H, int W,
                                     int C, int k, int s, int pad,
                                     float* __restrict__ y, int Ho, int Wo) {
-  const int C4 = C >> 2;
-  const int64_t total = (int64_t)N * Ho * Wo * C4;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  const IDX C4 = (IDX)(C >> 2);
+  const IDX total = (IDX)N * (IDX)Ho * (IDX)Wo * C4;
+  for (IDX t = (IDX)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (IDX)gridDim.x * blockDim.x) {
     const int c4 = (int)(t % C4);
-    int64_t r = t / C4;
-    const int ow = (int)(r % Wo);
-    r /= Wo;
-    const int oh = (int)(r % Ho);
-    const int n = (int)(r / Ho);
+    IDX r = t / C4;
+    const int ow = (int)(r % (IDX)Wo);
+    r /= (IDX)Wo;
+    const int oh = (int)(r % (IDX)Ho);
+    const int n = (int)(r / (IDX)Ho);
     f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     const int h0 = oh * s - pad, w0 = ow * s - pad;
     for (int kh = 0; kh < k; ++kh) {
@@ -52,10 +55,16 @@ int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int
   const int64_t total = (int64_t)N * Ho * Wo * (C / 4);
   const int block = 256;
   const int64_t want = (total + block - 1) / block;
-  const int grid = (int)(want < 8192 ? want : 8192);
-  if (grid == 0) return PPS_OK;
-  hipLaunchKernelGGL(maxpool_nhwc_kernel, dim3(grid), dim3(block), 0, st, x, N, H, W, C,
-                     k, stride, pad, y, Ho, Wo);
+  if (want == 0) return PPS_OK;
+  if (total < (int64_t)1 << 31) {
+    // one thread per output vector (no grid-stride loop)
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<uint32_t>, dim3((unsigned)want), dim3(block), 0, st,
+                       x, N, H, W, C, k, stride, pad, y, Ho, Wo);
+  } else {
+    const int grid = (int)(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<int64_t>, dim3(grid), dim3(block), 0, st, x, N, H,
+                       W, C, k, stride, pad, y, Ho, Wo);
+  }
   PPS_CHECK_LAUNCH("maxpool_nhwc_kernel");
   return PPS_OK;
 }
