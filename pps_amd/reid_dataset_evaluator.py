@@ -53,6 +53,9 @@ def compute_dist(array1, array2, type='euclidean'):
     return d.cpu().numpy() if as_numpy else d
 
 
+_PMAX_GUESS = 64
+
+
 def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams):
     """Per-query (ap float64, valid int32, first_rank int32) on the device."""
     d = _to_dev(distmat)
@@ -60,9 +63,15 @@ def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams):
     gid = _to_dev(gallery_ids, torch.int32)
     qc = _to_dev(query_cams, torch.int32)
     gc = _to_dev(gallery_cams, torch.int32)
-    pmax = max(1, ops.max_positives(np.asarray(query_ids), np.asarray(query_cams),
-                                    np.asarray(gallery_ids), np.asarray(gallery_cams)))
+    # positive-list capacity: a guess, re-collected at the exact size when a
+    # query has more (pos_cnt is exact either way, pps_abi.h) -- one small
+    # device->host read instead of a host pass over the metadata
+    pmax = _PMAX_GUESS
     pos_d, pos_idx, pos_cnt = ops.collect_positives(d, qid, qc, gid, gc, 0, pmax)
+    need = int(pos_cnt.max().item()) if pos_cnt.numel() else 0
+    if need > pmax:
+        pmax = need
+        pos_d, pos_idx, pos_cnt = ops.collect_positives(d, qid, qc, gid, gc, 0, pmax)
     sd, _, ptot, hist, before = ops.rank_counts(d, qid, qc, gid, gc, 0, pos_d[None],
                                                 pos_idx[None], pos_cnt[None])
     return ops.ap_finalize(sd, ptot, hist, before)

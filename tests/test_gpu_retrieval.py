@@ -126,6 +126,29 @@ def test_rank_eval_edge_cases():
             assert f[i] == -1
 
 
+def test_rank_eval_more_positives_than_first_guess():
+    """A query with more true matches than rank_eval's first positive-list
+    capacity (64) is re-collected at the exact size: same AP / first match."""
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(5)
+    Q, G = 4, 700
+    dist = rng.rand(Q, G).astype(np.float32)
+    qid = np.array([1, 2, 3, 4])
+    qcam = np.array([1, 1, 2, 2])
+    gid = rng.randint(2, 9, size=G)
+    gid[:300] = 1                          # query 0: ~250 positives + junk
+    gcam = rng.randint(1, 7, size=G)
+    ap, valid, first = gev.rank_eval(dist, qid, gid, qcam, gcam)
+    ref_ap, ref_valid = ev.mean_ap(dist, qid, gid, qcam, gcam, average=False)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
+    np.testing.assert_allclose(ap.cpu().numpy(), ref_ap, atol=1e-12)
+    ret, _ = ev.cmc(dist, qid, gid, qcam, gcam, topk=G, first_match_break=True,
+                    average=False)
+    f = first.cpu().numpy()
+    for i in range(Q):
+        assert (ret[i].argmax() == f[i]) if ref_valid[i] else (f[i] == -1)
+
+
 def test_rank_eval_exact_ties_stable_order():
     """Tied distances: CMC uses the stable (distance, index) order."""
     from pps_amd import reid_dataset_evaluator as gev
