@@ -161,6 +161,18 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
 int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k,
              float* vals, int32_t* idx, void* stream);
 
+/* Global rank list of a gallery-sharded search (per-shard
+ * stable top-k, all-gather of Q*k*8 B, k-way merge).  vals / idx are R lists
+ * [R][Q][k_in] as pps_topk writes them (ascending, ties by index; LOCAL
+ * indices, idx < 0 marks a pad entry), list r's global offset
+ * list_offsets[r] (HOST array); out_vals / out_idx [Q][k_out] = the stable
+ * (distance, global index) top-k_out of the union, padded with (+inf, -1)
+ * when it holds fewer entries.  Equals pps_topk over the concatenated
+ * shards.  R <= 64, R * k_in <= 8192. */
+int pps_topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int k_in,
+                   const int64_t* list_offsets, int k_out, float* out_vals,
+                   int32_t* out_idx, void* stream);
+
 /* k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519): out [Q][G] =
  * re_ranking(q_g, q_q, g_g, k1, k2, lambda) with the reference's float32
  * operand order for V, V_qe and the Jaccard sums; ties in the initial rank use

@@ -133,6 +133,22 @@ def cmc(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk=100,
     return ret, is_valid
 
 
+def first_match_rank(distmat, query_ids, gallery_ids, query_cams, gallery_cams):
+    """Per query, the CMC index `k - j` at which reid_dataset_evaluator.py
+    :340-355 (first_match_break=True) books its hit: the number of valid
+    entries ranked before the first true match in the stable argsort order;
+    -1 for queries without a valid match (:336-338).  Not capped at topk."""
+    distmat = np.asarray(distmat)
+    order = np.argsort(distmat, axis=1, kind='stable')
+    out = np.full(distmat.shape[0], -1, np.int64)
+    for i in range(distmat.shape[0]):
+        valid = _valid_mask(gallery_ids, gallery_cams, query_ids[i], query_cams[i], order[i])
+        hits = np.nonzero(gallery_ids[order[i]][valid] == query_ids[i])[0]
+        if len(hits):
+            out[i] = hits[0]
+    return out
+
+
 def re_ranking(q_g_dist, q_q_dist, g_g_dist, k1=20, k2=6, lambda_value=0.3):
     """k-reciprocal re-ranking, reid_dataset_evaluator.py:442-519 (Zhong et
     al., CVPR'17), restated with the same float32 intermediates."""
@@ -206,9 +222,13 @@ def evaluate_arrays(feat, ids, cams, marks, rerank=False, verbose=False):
         keys = np.array(list(groups.keys()))
         mq_g = compute_dist(mf, feat[g])
         mq_mAP, mq_cmc = score(mq_g, keys[:, 0], ids[g], keys[:, 1], cams[g])
-    if rerank:
+    if rerank:                                                        # :161-207
         qq = compute_dist(feat[q], feat[q])
         gg = compute_dist(feat[g], feat[g])
         rr = re_ranking(qg, qq, gg)
         mAP, cmc_s = score(rr, ids[q], ids[g], cams[q], cams[g])
+        if mq.any():                                                  # :185-206
+            mqmq = compute_dist(mf, mf)
+            rr_mq = re_ranking(mq_g, mqmq, gg)
+            mq_mAP, mq_cmc = score(rr_mq, keys[:, 0], ids[g], keys[:, 1], cams[g])
     return mAP, cmc_s, mq_mAP, mq_cmc

@@ -11,6 +11,22 @@ import torch
 from oracle import evaluator as ev
 
 
+def merge_topk(vals, idx, offsets, k):
+    """Stable (distance, global index) top-k of R per-shard lists [R, Q, k_in]
+    with local indices (idx < 0 = pad): the semantics of pps_topk_merge."""
+    R, Q, kin = vals.shape
+    out_v = np.full((Q, k), np.inf, np.float32)
+    out_i = np.full((Q, k), -1, np.int32)
+    gidx = idx.astype(np.int64) + np.asarray(offsets, np.int64)[:, None, None]
+    for q in range(Q):
+        ok = idx[:, q, :] >= 0
+        v, g = vals[:, q, :][ok], gidx[:, q, :][ok]
+        o = np.lexsort((g, v))[:k]
+        out_v[q, :len(o)] = v[o]
+        out_i[q, :len(o)] = g[o]
+    return out_v, out_i
+
+
 class CpuBackend(object):
     device = 'cpu'
 
@@ -64,6 +80,39 @@ class CpuBackend(object):
             before[q] = np.sum((dv < df) | ((dv == df) & (gidx[valid] < idf)))
         return (torch.from_numpy(sd), torch.from_numpy(si), torch.from_numpy(total),
                 torch.from_numpy(hist), torch.from_numpy(before))
+
+    @staticmethod
+    def topk(dist, k):
+        d = dist.numpy()
+        order = np.argsort(d, axis=1, kind='stable')[:, :k]
+        return (torch.from_numpy(np.take_along_axis(d, order, axis=1).astype(np.float32)),
+                torch.from_numpy(order.astype(np.int32)))
+
+    @staticmethod
+    def topk_merge(vals, idx, offsets, k):
+        return tuple(torch.from_numpy(a) for a in
+                     merge_topk(vals.numpy(), idx.numpy(), offsets, k))
+
+    @staticmethod
+    def group_mean(x, groups):
+        xn = x.numpy()
+        return torch.from_numpy(np.stack([xn[g].mean(axis=0) for g in groups])
+                                .astype(np.float32))
+
+    @staticmethod
+    def self_dist(x, metric):
+        return CpuBackend.distmat(x, x, metric)
+
+    @staticmethod
+    def re_ranking(q_g, q_q, g_g):
+        return torch.from_numpy(ev.re_ranking(q_g.numpy(), q_q.numpy(), g_g.numpy()))
+
+    @staticmethod
+    def rank_eval(dist, qid, gid, qcam, gcam):
+        d = dist.numpy() if isinstance(dist, torch.Tensor) else np.asarray(dist)
+        ap, valid = ev.mean_ap(d, qid, gid, qcam, gcam, average=False)
+        first = ev.first_match_rank(d, qid, gid, qcam, gcam)
+        return ap, valid.astype(np.int32), first
 
     @staticmethod
     def finalize(sorted_d, pos_total, hist, before):

@@ -39,6 +39,7 @@ SIGNATURES = {
     'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                         c_ptr],
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_topk_merge': [c_ptr, c_ptr, c_int, c_i64, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr],
     'pps_conv2d_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                           c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
                           c_ptr, c_int, c_int, c_int, c_int, c_ptr],

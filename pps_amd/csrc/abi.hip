@@ -58,7 +58,7 @@ const char* pps_last_error(void) { return g_last_error.c_str(); }
 
 const char* pps_registered_ops(void) {
   return "PairWiseDistance;Conv+SpatialBN+Sum+Relu;MaxPool;PartPowerSet;Normalize;"
-         "ComputeDist;RankCounts;TopK;PrepImForBlob";
+         "ComputeDist;RankCounts;TopK;TopKMerge;PrepImForBlob";
 }
 
 int pps_gemm_num_tiles(void) { return GEMM_NUM_TILES - 1; }
@@ -276,6 +276,25 @@ int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float*
   PPS_ENFORCE(G >= k && ldd >= G, "need G >= k");
   PPS_ENFORCE(G < (1ll << 31), "G must fit int32");
   return topk(dist, Q, G, ldd, k, vals, idx, as_stream(stream));
+}
+
+int pps_topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int k_in,
+                   const int64_t* list_offsets, int k_out, float* out_vals,
+                   int32_t* out_idx, void* stream) {
+  PPS_ENFORCE(vals && idx && list_offsets && out_vals && out_idx, "null pointer");
+  PPS_ENFORCE(R >= 1 && R <= kMergeMaxLists,
+              "R must be in [1, " + std::to_string(kMergeMaxLists) + "]");
+  PPS_ENFORCE(Q >= 0 && k_in >= 1 && k_out >= 1, "bad shape");
+  PPS_ENFORCE((int64_t)R * k_in <= 8192,
+              "R * k_in must be <= 8192 (LDS), got " + std::to_string((int64_t)R * k_in));
+  MergeOffsets offs{};
+  for (int r = 0; r < R; ++r) {
+    PPS_ENFORCE(list_offsets[r] >= 0 && list_offsets[r] + k_in <= (int64_t)INT32_MAX,
+                "list offset out of the int32 index range");
+    offs.off[r] = list_offsets[r];
+  }
+  return topk_merge(vals, idx, R, Q, k_in, offs, k_out, out_vals, out_idx,
+                    as_stream(stream));
 }
 
 int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {

@@ -70,8 +70,8 @@ int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int
 }
 
 // ---- Part power set (bpm_heads.py:18-55, pps_heads.py:38-80) ---------------
-// Thread per (n, c): strip-wise global average and max over the strip's
-// rows x W, then every non-empty subset i (bit j <=> strip j):
+// Per (n, c): strip-wise global average and max over the strip's rows x W,
+// then every non-empty subset i (bit j <=> strip j):
 //   max_ave: out = Mean(ave_j, j in i) + Max(max_j, j in i)
 //   else   : out = Max(ave_j, j in i)
 // Mean follows Caffe2's Mean op: sum in input order, then * (1/n).
@@ -79,55 +79,6 @@ constexpr int kMaxStrips = 10;
 struct Splits {
   int h[kMaxStrips];
 };
-
-__global__ void part_power_set_kernel(const float* __restrict__ x, int N, int H, int W,
-                                      int C, Splits sp, int S, int max_ave,
-                                      float* __restrict__ out) {
-  const int n = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float ave[kMaxStrips], mx[kMaxStrips];
-  const float* base = x + (int64_t)n * H * W * C + c;
-  int row = 0;
-#pragma unroll
-  for (int j = 0; j < kMaxStrips; ++j) {
-    if (j >= S) break;
-    float sum = 0.f, m = -INFINITY;
-    for (int hh = 0; hh < sp.h[j]; ++hh, ++row) {
-      for (int ww = 0; ww < W; ++ww) {
-        const float v = base[((int64_t)row * W + ww) * C];
-        sum += v;
-        m = fmaxf(m, v);
-      }
-    }
-    ave[j] = sum / (float)(sp.h[j] * W);
-    mx[j] = m;
-  }
-  const int nsub = (1 << S) - 1;
-  for (int i = 1; i <= nsub; ++i) {
-    float v;
-    if (max_ave) {
-      float s = 0.f, m = -INFINITY;
-      int cnt = 0;
-      bool first = true;
-      for (int j = 0; j < S; ++j) {
-        if (i & (1 << j)) {
-          s = first ? ave[j] : s + ave[j];
-          first = false;
-          m = fmaxf(m, mx[j]);
-          ++cnt;
-        }
-      }
-      v = s * (1.f / (float)cnt) + m;
-    } else {
-      float m = -INFINITY;
-      for (int j = 0; j < S; ++j)
-        if (i & (1 << j)) m = fmaxf(m, ave[j]);
-      v = m;
-    }
-    out[((int64_t)(i - 1) * N + n) * C + c] = v;
-  }
-}
 
 constexpr int kPpsC_fwd = 64;
 __global__ void part_power_set_v2_kernel(const float* __restrict__ x, int N, int H, int W,

@@ -156,4 +156,13 @@ int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3
                  hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
 
+// ---- retrieval (rank.hip) ---------------------------------------------------
+constexpr int kMergeMaxLists = 64;
+struct MergeOffsets {  // kernel-argument copy of the per-list global offsets
+  int64_t off[kMergeMaxLists];
+};
+int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
+               const MergeOffsets& offs, int kout, float* out_vals, int32_t* out_idx,
+               hipStream_t st);
+
 }  // namespace pps

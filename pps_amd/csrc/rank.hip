@@ -537,4 +537,79 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
   return PPS_OK;
 }
 
+// ---- k-way merge of per-shard top-k lists ------------------------
+// R gallery shards each hold a stable ascending top-k_in list per query
+// (local indices; list r's global offset off[r]).  The global stable top-k_out
+// is their merge by the packed (order-preserving key << 32 | global index)
+// value.  Packed values are unique (global indices are), so an entry's output
+// position is exactly its position in its own list plus, for every other list,
+// the number of that list's entries below it (a binary search in LDS): every
+// entry is placed independently, no sort and no serial merge.  Pad entries
+// (index < 0, e.g. shards shorter than k_in) pack to ~0 and are never placed;
+// output positions past the number of real entries get (+inf, -1).
+constexpr int kMergeThreads = 256;
+
+__global__ void topk_merge_kernel(const float* __restrict__ vals,
+                                  const int32_t* __restrict__ idx, int R, int64_t Q,
+                                  int kin, MergeOffsets offs, int kout,
+                                  float* __restrict__ out_vals,
+                                  int32_t* __restrict__ out_idx) {
+  const int64_t q = blockIdx.x;
+  extern __shared__ unsigned long long mkeys[];
+  __shared__ int s_real;
+  const int n = R * kin;
+  if (threadIdx.x == 0) s_real = 0;
+  __syncthreads();
+  int real = 0;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const int r = t / kin, p = t - r * kin;
+    const int64_t src = ((int64_t)r * Q + q) * kin + p;
+    const int32_t li = idx[src];
+    unsigned long long key = ~0ull;
+    if (li >= 0) {
+      key = ((unsigned long long)float_key(vals[src]) << 32) |
+            (uint32_t)(offs.off[r] + li);
+      ++real;
+    }
+    mkeys[t] = key;
+  }
+  atomicAdd(&s_real, real);
+  __syncthreads();
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const unsigned long long key = mkeys[t];
+    if (key == ~0ull) continue;
+    const int r = t / kin;
+    int pos = t - r * kin;
+    for (int o = 0; o < R && pos < kout; ++o) {
+      if (o == r) continue;
+      const unsigned long long* L = mkeys + o * kin;
+      int lo = 0, hi = kin;  // lower_bound: entries of list o below key
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (L[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      pos += lo;
+    }
+    if (pos < kout) {
+      out_vals[q * kout + pos] = key_float((uint32_t)(key >> 32));
+      out_idx[q * kout + pos] = (int32_t)(key & 0xffffffffu);
+    }
+  }
+  for (int p = s_real + threadIdx.x; p < kout; p += blockDim.x) {
+    out_vals[q * kout + p] = INFINITY;
+    out_idx[q * kout + p] = -1;
+  }
+}
+
+int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
+               const MergeOffsets& offs, int kout, float* out_vals, int32_t* out_idx,
+               hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  const size_t lds = (size_t)R * kin * sizeof(unsigned long long);
+  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)Q), dim3(kMergeThreads), lds, st,
+                     vals, idx, R, Q, kin, offs, kout, out_vals, out_idx);
+  PPS_CHECK_LAUNCH("topk_merge_kernel");
+  return PPS_OK;
+}
+
 }  // namespace pps

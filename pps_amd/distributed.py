@@ -1,30 +1,47 @@
-"""Multi-GPU retrieval: gallery-sharded distance + rank evaluation.
+"""Multi-GPU retrieval: gallery-sharded distance, rank list and evaluation.
 
 SURVEY §8(e).  The reference tests on several GPUs by spawning one process per
 GPU over contiguous image ranges and exchanging pickle files
 (detectron/utils/subprocess.py:39-103, np.array_split :53); its parent then
-vstacks all features and evaluates on one host.  Here each rank keeps its
-gallery shard resident in HBM:
+vstacks all features and evaluates on one host
+(detectron/core/test_engine.py:184-229, reid_dataset_evaluator.py:29-209).
+Here each rank keeps its gallery shard resident in HBM:
 
   1. all-gather the query embeddings (RCCL over xGMI; Market 53.5 MB total),
-  2. distance block [Q, G_r] on the local shard (HIP FP32 MFMA),
-  3. each rank lists its shard's true matches per query; all-gather the
-     lists ([R, Q, Pmax] distances + global gallery indices, kilobytes),
+  2. distance block [Q, G_r] on the local shard (HIP MFMA GEMM),
+  3. each rank lists its shard's true matches per query (capacity: a guess,
+     one all-reduce(MAX) of the true counts, re-collected only if a shard
+     overflowed); all-gather of the lists ([R, Q, Pmax], kilobytes),
   4. each rank bins its shard against the merged, sorted positives
      (additive counts), all-reduce(SUM) of the counts,
   5. AP / first-match rank per query from the summed counts.
 
-Only the all-gathers and one all-reduce cross ranks: there is no ring
-all-reduce of big tensors anywhere on this path.
+Rank list (the reference's np.argsort(distmat, axis=1), :319,:420): each
+rank takes the stable top-k of its block, the lists are all-gathered
+(Q·k·8 B per shard) and merged on the device by (distance, global index)
+(pps_topk_merge): equal to the top-k of the unsharded matrix.
+
+Multi-query (:131-159): the mq image features are all-gathered in global
+order and pooled per (id, cam) on every rank (bit-identical to the one-GPU
+pooling), then scored like single queries.  Re-ranking (:161-207) needs the
+whole (Q+G)^2 neighbour structure: it is gathered to rank 0 (replica work
+would only repeat it), whose scores are broadcast.
+
+Only all-gathers, one MAX and two SUM all-reduces of small count arrays and
+one broadcast of scalars cross ranks: no ring all-reduce of big tensors.
 
 The per-stage kernels come from a backend object so the collective logic can
 be exercised with world_size > 1 on CPU (gloo) in tests; the product backend
 is HipBackend (libpps_hip.so).
 """
+from collections import OrderedDict
+
 import numpy as np
 import torch
 
 from . import ops
+
+PMAX_GUESS = 64
 
 
 def shard_range(n, rank, world):
@@ -37,6 +54,11 @@ def shard_range(n, rank, world):
 def barrier(world):
     if world > 1:
         torch.distributed.barrier()
+
+
+def _coll_device(x):
+    """Collectives run on the tensors' device for nccl (RCCL), host for gloo."""
+    return x.device if torch.distributed.get_backend() == 'nccl' else torch.device('cpu')
 
 
 def max_over_ranks(x, world):
@@ -53,12 +75,21 @@ def all_gather_rows(x, sizes):
     world = len(sizes)
     if world == 1:
         return x
-    mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    mx = max(max(sizes), 1)
+    dev = _coll_device(x)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
     pad[:x.shape[0]] = x
     bufs = [torch.empty_like(pad) for _ in range(world)]
     torch.distributed.all_gather(bufs, pad)
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).contiguous()
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(x.device).contiguous()
+
+
+def broadcast_object(obj, world, src=0):
+    if world == 1:
+        return obj
+    box = [obj]
+    torch.distributed.broadcast_object_list(box, src=src)
+    return box[0]
 
 
 class HipBackend(object):
@@ -85,6 +116,31 @@ class HipBackend(object):
     def finalize(sorted_d, pos_total, hist, before):
         return ops.ap_finalize(sorted_d, pos_total, hist, before)
 
+    @staticmethod
+    def topk(dist, k):
+        return ops.topk(dist, k)
+
+    @staticmethod
+    def topk_merge(vals, idx, offsets, k):
+        return ops.topk_merge(vals, idx, offsets, k)
+
+    @staticmethod
+    def group_mean(x, groups):
+        return ops.group_mean(x, groups)
+
+    @staticmethod
+    def self_dist(x, metric):
+        return ops.compute_dist(x, x, metric=metric)
+
+    @staticmethod
+    def re_ranking(q_g, q_q, g_g):
+        return ops.re_ranking(q_g, q_q, g_g)
+
+    @staticmethod
+    def rank_eval(dist, qid, gid, qcam, gcam):
+        from .reid_dataset_evaluator import rank_eval
+        return rank_eval(dist, qid, gid, qcam, gcam)
+
 
 class ShardedEvaluator(object):
     """Market protocol (separate_camera_set=False, single_gallery_shot=False,
@@ -102,9 +158,7 @@ class ShardedEvaluator(object):
         self.g_ranges = [shard_range(self.G, r, world) for r in range(world)]
         g0, g1 = self.g_ranges[rank]
         self.g_offset = g0
-        # Pmax: max true matches per query inside any one shard (host metadata)
-        self.pmax = max(1, max(ops.max_positives(qid, qcam, gid[a:b], gcam[a:b])
-                               for a, b in self.g_ranges))
+        self.pmax = PMAX_GUESS
         dev = self.backend.device
         i32 = torch.int32
         self.qid = torch.from_numpy(qid.astype(np.int32)).to(dev)
@@ -113,40 +167,69 @@ class ShardedEvaluator(object):
         self.gcam = torch.from_numpy(gcam[g0:g1].astype(np.int32)).to(dev)
         assert self.qid.dtype == i32
 
-    def run(self, q_local, g_local, timed=False):
+    def _all_reduce(self, t, op=None):
+        """In-place all-reduce of a backend tensor (host-staged for gloo)."""
+        if self.world == 1:
+            return t
+        op = op if op is not None else torch.distributed.ReduceOp.SUM
+        dev = _coll_device(t)
+        s = t if t.device == dev else t.to(dev)
+        torch.distributed.all_reduce(s, op=op)
+        if s is not t:
+            t.copy_(s)
+        return t
+
+    def _collect(self, dist):
+        """Positive lists of this shard at a capacity every shard fits: one
+        all-reduce(MAX) of the largest true count; a shard re-collects only
+        when the guess was too small (pos_cnt is exact either way)."""
+        be = self.backend
+        pos = be.collect(dist, self.qid, self.qcam, self.gid, self.gcam, self.g_offset,
+                         self.pmax)
+        cnt = pos[2]
+        need = cnt.max().reshape(1).to(torch.int64) if cnt.numel() else \
+            torch.zeros(1, dtype=torch.int64, device=cnt.device)
+        need = int(self._all_reduce(need, torch.distributed.ReduceOp.MAX
+                                    if self.world > 1 else None).item())
+        if need > self.pmax:
+            self.pmax = need
+            pos = be.collect(dist, self.qid, self.qcam, self.gid, self.gcam,
+                             self.g_offset, self.pmax)
+        return pos
+
+    def _gather_lists(self, *ts):
+        if self.world == 1:
+            return [t[None] for t in ts]
+        return [all_gather_rows(t[None], [1] * self.world) for t in ts]
+
+    def run(self, q_local, g_local, timed=False, dist=None):
         be = self.backend
         use_ev = timed and be.device == 'cuda'
         if use_ev:
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             evs[0].record()
-        q_all = all_gather_rows(q_local, self.q_sizes)
-        if use_ev:
+        if dist is None:
+            q_all = all_gather_rows(q_local, self.q_sizes)
+            if use_ev:
+                evs[1].record()
+            dist = be.distmat(q_all, g_local, self.metric)
+        elif use_ev:
             evs[1].record()
-        dist = be.distmat(q_all, g_local, self.metric)
         if use_ev:
             evs[2].record()
-        pos_d, pos_idx, pos_cnt = be.collect(dist, self.qid, self.qcam, self.gid, self.gcam,
-                                             self.g_offset, self.pmax)
-        if self.world > 1:
-            pos_d = all_gather_rows(pos_d[None], [1] * self.world)
-            pos_idx = all_gather_rows(pos_idx[None], [1] * self.world)
-            pos_cnt = all_gather_rows(pos_cnt[None], [1] * self.world)
-        else:
-            pos_d, pos_idx, pos_cnt = pos_d[None], pos_idx[None], pos_cnt[None]
+        pos_d, pos_idx, pos_cnt = self._collect(dist)
+        pos_d, pos_idx, pos_cnt = self._gather_lists(pos_d, pos_idx, pos_cnt)
         sorted_d, _, pos_total, hist, before = be.counts(
             dist, self.qid, self.qcam, self.gid, self.gcam, self.g_offset, pos_d, pos_idx,
             pos_cnt)
-        if self.world > 1:
-            torch.distributed.all_reduce(hist)
-            torch.distributed.all_reduce(before)
+        self._all_reduce(hist)
+        self._all_reduce(before)
         ap, valid, first = be.finalize(sorted_d, pos_total, hist, before)
         if use_ev:
             evs[3].record()
         ap = ap.cpu().numpy()
         valid = valid.cpu().numpy().astype(bool)
         first = first.cpu().numpy()
-        if np.any(pos_cnt.cpu().numpy() > self.pmax):
-            raise RuntimeError('positive list overflow: Pmax=%d too small' % self.pmax)
         nvalid = int(valid.sum())
         mAP = float(ap.sum()) / nvalid if nvalid else float('nan')
         hits = np.zeros(self.topk)
@@ -159,3 +242,104 @@ class ShardedEvaluator(object):
             res['t_rank_ms'] = evs[2].elapsed_time(evs[3])
             res['t_total_ms'] = evs[0].elapsed_time(evs[3])
         return res
+
+    def rank_list(self, q_local=None, g_local=None, k=100, dist=None):
+        """Global stable top-k rank list [Q, k] (distances, global gallery
+        indices) on every rank: local top-k, all-gather, k-way merge."""
+        be = self.backend
+        if dist is None:
+            q_all = all_gather_rows(q_local, self.q_sizes)
+            dist = be.distmat(q_all, g_local, self.metric)
+        kin = min(k, dist.shape[1])
+        if kin > 0:
+            vals, idx = be.topk(dist, kin)
+        else:
+            vals = torch.zeros((self.Q, 1), dtype=torch.float32, device=dist.device)
+            idx = torch.full((self.Q, 1), -1, dtype=torch.int32, device=dist.device)
+        if kin < k and kin > 0:   # short shard: pad its list to k entries
+            pv = torch.full((self.Q, k), float('inf'), dtype=torch.float32, device=dist.device)
+            pi = torch.full((self.Q, k), -1, dtype=torch.int32, device=dist.device)
+            pv[:, :kin] = vals
+            pi[:, :kin] = idx
+            vals, idx = pv, pi
+        elif kin == 0:
+            vals = torch.full((self.Q, k), float('inf'), dtype=torch.float32,
+                              device=dist.device)
+            idx = torch.full((self.Q, k), -1, dtype=torch.int32, device=dist.device)
+        vals, idx = self._gather_lists(vals.contiguous(), idx.contiguous())
+        offsets = [a for a, _ in self.g_ranges]
+        return be.topk_merge(vals.contiguous(), idx.contiguous(), offsets, k)
+
+
+def _score(ap, valid, first, topk=10):
+    ap, valid, first = (np.asarray(t.cpu().numpy() if isinstance(t, torch.Tensor) else t)
+                        for t in (ap, valid, first))
+    valid = valid.astype(bool)
+    nvalid = int(valid.sum())
+    mAP = float(ap.sum()) / nvalid if nvalid else float('nan')
+    hits = np.zeros(topk)
+    fr = first[valid]
+    np.add.at(hits, fr[(fr >= 0) & (fr < topk)], 1)
+    return mAP, np.cumsum(hits) / max(nvalid, 1)
+
+
+def mq_groups(mq_ids, mq_cams):
+    """Per-(id, cam) member lists in first-appearance order
+    (reid_dataset_evaluator.py:136-140) -> (keys [n, 2], groups)."""
+    groups = OrderedDict()
+    for k, key in enumerate(zip(np.asarray(mq_ids).tolist(), np.asarray(mq_cams).tolist())):
+        groups.setdefault(key, []).append(k)
+    keys = np.array(list(groups.keys()), dtype=np.int64).reshape(-1, 2)
+    return keys, list(groups.values())
+
+
+def evaluate_sharded(q_local, g_local, mq_local, ids, cams, marks, rank, world,
+                     backend=None, metric='euclidean', rerank=False, verbose=False):
+    """The reference's evaluate() (reid_dataset_evaluator.py:29-209) over
+    features sharded across ranks: q_local / g_local / mq_local are this
+    rank's contiguous shards (shard_range) of the query (mark 0), gallery
+    (mark 1) and multi-query (mark 2) features in dataset order; ids / cams /
+    marks cover the whole dataset.  Returns (mAP, cmc, mq_mAP, mq_cmc) on
+    every rank, equal to the one-process evaluate."""
+    be = backend or HipBackend
+    ids, cams, marks = np.asarray(ids), np.asarray(cams), np.asarray(marks)
+    q, g, mq = marks == 0, marks == 1, marks == 2
+    ev = ShardedEvaluator(ids[q], cams[q], ids[g], cams[g], rank, world, backend=be,
+                          metric=metric)
+    q_all = all_gather_rows(q_local, ev.q_sizes)
+    q_g = be.distmat(q_all, g_local, metric)
+    res = ev.run(None, g_local, dist=q_g)
+    mAP, cmc = res['mAP'], res['cmc']
+    mq_mAP = mq_cmc = None
+    if mq.any():
+        n_mq = int(mq.sum())
+        mq_sizes = [b - a for a, b in (shard_range(n_mq, r, world) for r in range(world))]
+        mq_all = all_gather_rows(mq_local, mq_sizes)
+        keys, groups = mq_groups(ids[mq], cams[mq])
+        pooled = be.group_mean(mq_all, groups)
+        ev_mq = ShardedEvaluator(keys[:, 0], keys[:, 1], ids[g], cams[g], rank, world,
+                                 backend=be, metric=metric)
+        mq_g = be.distmat(pooled, g_local, metric)
+        r = ev_mq.run(None, g_local, dist=mq_g)
+        mq_mAP, mq_cmc = r['mAP'], r['cmc']
+    if rerank:
+        # the whole (Q+G)^2 neighbour structure: gathered to rank 0
+        g_sizes = [b - a for a, b in ev.g_ranges]
+        g_all = all_gather_rows(g_local, g_sizes)
+        scores = None
+        if rank == 0:
+            qg_full = be.distmat(q_all, g_all, metric)
+            g_g = be.self_dist(g_all, metric)
+            rr = be.re_ranking(qg_full, be.self_dist(q_all, metric), g_g)
+            s_sq = _score(*be.rank_eval(rr, ids[q], ids[g], cams[q], cams[g]))
+            s_mq = None
+            if mq.any():
+                mqg_full = be.distmat(pooled, g_all, metric)
+                rr_mq = be.re_ranking(mqg_full, be.self_dist(pooled, metric), g_g)
+                s_mq = _score(*be.rank_eval(rr_mq, keys[:, 0], ids[g], keys[:, 1], cams[g]))
+            scores = (s_sq, s_mq)
+        s_sq, s_mq = broadcast_object(scores, world)
+        mAP, cmc = s_sq
+        if s_mq is not None:
+            mq_mAP, mq_cmc = s_mq
+    return mAP, cmc, mq_mAP, mq_cmc

@@ -43,6 +43,27 @@ def _dev(t, name, dtype=torch.float32):
     return t.data_ptr()
 
 
+def _dev_rows(t, name, dtype=torch.float32):
+    """A 2-D device matrix whose rows may be padded (stride(1) == 1,
+    stride(0) >= columns): distance matrices are passed with their row
+    stride (ld*) so a [Q, G] view of a wider buffer needs no copy."""
+    if not isinstance(t, torch.Tensor) or t.dim() != 2:
+        raise RuntimeError('%s must be a 2-D torch.Tensor' % name)
+    if not t.is_cuda:
+        raise RuntimeError('%s must be a device (HIP) tensor; the product path has no '
+                           'CPU implementation' % name)
+    if t.dtype != dtype:
+        raise RuntimeError('%s must be %s, got %s' % (name, dtype, t.dtype))
+    if t.shape[0] > 1 and (t.stride(1) != 1 or t.stride(0) < t.shape[1]):
+        raise RuntimeError('%s must have unit column stride and row stride >= columns'
+                           % name)
+    return t.data_ptr()
+
+
+def _ld(t):
+    return t.stride(0) if t.shape[0] > 1 else t.shape[1]
+
+
 # ---------------------------------------------------------------------------
 # Retrieval
 # ---------------------------------------------------------------------------
@@ -118,9 +139,11 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     G = g.shape[0]
     if out is None:
         out = torch.empty((Q, G), dtype=torch.float32, device=q.device)
+    if tuple(out.shape) != (Q, G):
+        raise RuntimeError('out must be [%d, %d], got %s' % (Q, G, tuple(out.shape)))
     if math == 'f32':
         call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
-             _dev(out, 'out'), out.stride(0), int(tile), _stream())
+             _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
     idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g)
     if symmetric is None:
@@ -130,19 +153,19 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
                      tile in SELF_TILES)
     if symmetric:
         call('pps_distmat_x3_self', _dev(q, 'x'), Q, D, _dev(idx.sqnorm, 'xsq'),
-             _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric], _dev(out, 'out'),
-             out.stride(0), int(tile), _stream())
+             _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric],
+             _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
     if q_planes:
         q3, qsq = split_sqnorm(q) if q.is_contiguous() else (split_bf16x3(q), row_sqnorm(q))
         call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
              _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
-             METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
+             METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
     qsq = row_sqnorm(q)
     call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
-         METRICS[metric], _dev(out, 'out'), out.stride(0), int(tile), _stream())
+         METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
     return out
 
 
@@ -161,9 +184,26 @@ def topk(dist, k):
     Q, G = dist.shape
     vals = torch.empty((Q, k), dtype=torch.float32, device=dist.device)
     idx = torch.empty((Q, k), dtype=torch.int32, device=dist.device)
-    call('pps_topk', _dev(dist, 'dist'), Q, G, dist.stride(0), k, vals.data_ptr(),
+    call('pps_topk', _dev_rows(dist, 'dist'), Q, G, _ld(dist), k, vals.data_ptr(),
          idx.data_ptr(), _stream())
     return vals, idx
+
+
+def topk_merge(vals, idx, offsets, k):
+    """Merge R per-shard stable top-k lists vals/idx [R, Q, k_in] (local
+    indices; list r starts at global index offsets[r]) into the global stable
+    top-k [Q, k] (pps_topk_merge; (+inf, -1) past the available entries)."""
+    R, Q, kin = vals.shape
+    offs = np.ascontiguousarray(np.asarray(offsets, np.int64).reshape(-1))
+    if offs.shape[0] != R:
+        raise RuntimeError('need one offset per list: %d lists, %d offsets'
+                           % (R, offs.shape[0]))
+    out_v = torch.empty((Q, k), dtype=torch.float32, device=vals.device)
+    out_i = torch.empty((Q, k), dtype=torch.int32, device=vals.device)
+    call('pps_topk_merge', _dev(vals, 'vals'), _dev(idx, 'idx', torch.int32), R, Q, kin,
+         offs.ctypes.data_as(_lib.ctypes.c_void_p), k, out_v.data_ptr(), out_i.data_ptr(),
+         _stream())
+    return out_v, out_i
 
 
 def collect_positives(dist, qid, qcam, gid, gcam, g_offset, Pmax):
@@ -171,7 +211,7 @@ def collect_positives(dist, qid, qcam, gid, gcam, g_offset, Pmax):
     pos_d = torch.empty((Q, Pmax), dtype=torch.float32, device=dist.device)
     pos_idx = torch.empty((Q, Pmax), dtype=torch.int32, device=dist.device)
     pos_cnt = torch.empty((Q,), dtype=torch.int32, device=dist.device)
-    call('pps_collect_positives', _dev(dist, 'dist'), Q, G, dist.stride(0),
+    call('pps_collect_positives', _dev_rows(dist, 'dist'), Q, G, _ld(dist),
          _dev(qid, 'qid', torch.int32), _dev(qcam, 'qcam', torch.int32),
          _dev(gid, 'gid', torch.int32), _dev(gcam, 'gcam', torch.int32), int(g_offset),
          Pmax, pos_d.data_ptr(), pos_idx.data_ptr(), pos_cnt.data_ptr(), _stream())
@@ -192,7 +232,7 @@ def rank_counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt,
         hist = torch.zeros((Q, Ptot), dtype=torch.int32, device=dev)
     if before is None:
         before = torch.zeros((Q,), dtype=torch.int32, device=dev)
-    call('pps_rank_counts', _dev(dist, 'dist'), Q, G, dist.stride(0),
+    call('pps_rank_counts', _dev_rows(dist, 'dist'), Q, G, _ld(dist),
          _dev(qid, 'qid', torch.int32), _dev(qcam, 'qcam', torch.int32),
          _dev(gid, 'gid', torch.int32), _dev(gcam, 'gcam', torch.int32), int(g_offset),
          R, Pmax, _dev(pos_d, 'pos_d'), _dev(pos_idx, 'pos_idx', torch.int32),

@@ -112,7 +112,11 @@ class BatchFeeder(object):
             hs = dmeta[1].to(torch.int32).contiguous()
             ws = dmeta[2].to(torch.int32).contiguous()
             x = ops.preprocess_bgr_ragged(dblob, offs, hs, ws, self.means, (self.H, self.W))
+            # both staged buffers were allocated on copy_stream and are read
+            # on this stream: keep the allocator from recycling either block
+            # for the next batch's copy before the kernel above has run
             dblob.record_stream(torch.cuda.current_stream())
+            dmeta.record_stream(torch.cuda.current_stream())
             yield s, x
 
 
@@ -143,7 +147,8 @@ def test_net(weights_file, dataset_name, proposal_file, output_dir, ind_range=No
              gpu_id=0, model=None, trusted=False):
     """test_engine.py:259-370: features of every image in the (range of the)
     dataset, [N, 3968] float32 on the host; also written to output_dir as
-    features.npy (the reference's features.pkl held {'all_feats', 'cfg'})."""
+    features.pkl (feature_range_<s>_<e>.pkl for a range) = {'all_feats',
+    'cfg'} like the reference's save_object (:356-368)."""
     roidb, dataset, start, end, total = get_roidb_and_dataset(dataset_name, ind_range)
     if model is None:
         model = initialize_model_from_cfg(weights_file, gpu_id, trusted=trusted)
@@ -154,9 +159,42 @@ def test_net(weights_file, dataset_name, proposal_file, output_dir, ind_range=No
     logger.info('im_detect: %d images in %.2fs (%.1f img/s)', len(paths),
                 time.time() - t0, len(paths) / max(time.time() - t0, 1e-9))
     all_feats = feats.cpu().numpy()
-    name = 'features.npy' if ind_range is None else 'feature_range_%s_%s.npy' % (start, end)
-    np.save(os.path.join(output_dir, name), all_feats)
+    name = 'features.pkl' if ind_range is None else 'feature_range_%s_%s.pkl' % (start, end)
+    save_object(dict(all_feats=all_feats, cfg=cfg_yaml()), os.path.join(output_dir, name))
+    logger.info('Wrote features to: %s', os.path.abspath(os.path.join(output_dir, name)))
     return all_feats
+
+
+def cfg_yaml():
+    """envu.yaml_dump(cfg) (utils/env.py): the config as a YAML string."""
+    import yaml
+
+    def plain(x):
+        if isinstance(x, dict):
+            return {k: plain(v) for k, v in x.items()}
+        if isinstance(x, (list, tuple)):
+            return [plain(v) for v in x]
+        if isinstance(x, np.ndarray):
+            return x.tolist()
+        return x
+    return yaml.safe_dump(plain(cfg))
+
+
+def save_object(obj, file_name, pickle_format=2):
+    """utils/io.py:39-60 save_object: pickle protocol 2 (readable by the
+    reference's Python 2 tools), written to a temporary name on the same
+    filesystem and renamed into place."""
+    import pickle
+    import uuid
+    file_name = os.path.abspath(file_name)
+    tmp = file_name + '.tmp.' + uuid.uuid4().hex
+    try:
+        with open(tmp, 'wb') as f:
+            pickle.dump(obj, f, pickle_format)
+        os.rename(tmp, file_name)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
 
 
 def _split_qg(roidb):
@@ -167,31 +205,53 @@ def _split_qg(roidb):
     return ids, cams, marks
 
 
-def multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir, trusted=False):
-    """One process per GPU (already launched by torch.distributed.run).
-    Queries and gallery are split separately into contiguous shards; every
-    rank extracts its shards, then the gallery-sharded evaluator runs
-    (SURVEY §8(e)).  Returns (results dict on every rank)."""
+def multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir, trusted=False,
+                                  model=None):
+    """test_engine.py:184-229 with one process per GPU (already launched by
+    torch.distributed.run) instead of subprocesses + pickle files.  Queries,
+    gallery and multi-queries are split separately into contiguous shards
+    (np.array_split, subprocess.py:53); every rank extracts its shards, the
+    features are written once as features.npy (the reference's multi-GPU
+    output, :216-227) and the gallery-sharded evaluator computes the same
+    (mAP, cmc, mq_mAP, mq_cmc) as the one-GPU evaluate(),
+    including multi-query pooling and REID.RERANK (gathered to rank 0).
+    Returns the results dict on every rank."""
     rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
     local = int(os.environ.get('LOCAL_RANK', rank))
     roidb, dataset, _, _, _ = get_roidb_and_dataset(dataset_name, None)
     ids, cams, marks = _split_qg(roidb)
-    model = initialize_model_from_cfg(weights_file, local, trusted=trusted)
-    q_idx, g_idx = np.nonzero(marks == 0)[0], np.nonzero(marks == 1)[0]
-    qa, qb = pdist.shard_range(len(q_idx), rank, world)
-    ga, gb = pdist.shard_range(len(g_idx), rank, world)
+    if model is None:
+        model = initialize_model_from_cfg(weights_file, local, trusted=trusted)
     paths = [e['image'] for e in roidb]
-    qp = [paths[i] for i in q_idx[qa:qb]]
-    gp = [paths[i] for i in g_idx[ga:gb]]
-    qf = extract_features(model, lambda i: _decode_bgr(qp[i]), len(qp))
-    gf = extract_features(model, lambda i: _decode_bgr(gp[i]), len(gp))
-    ev = pdist.ShardedEvaluator(ids[q_idx], cams[q_idx], ids[g_idx], cams[g_idx], rank,
-                                world)
-    res = ev.run(qf, gf)
+    shards, rows_of = [], []
+    for m in (0, 1, 2):
+        rows = np.nonzero(marks == m)[0]
+        a, b = pdist.shard_range(len(rows), rank, world)
+        sp = [paths[i] for i in rows[a:b]]
+        shards.append(extract_features(model, lambda i, sp=sp: _decode_bgr(sp[i]), len(sp)))
+        rows_of.append(rows)
+    # features in dataset order, written by rank 0 (test_engine.py:216-227)
+    full = torch.empty((len(paths), model.feat_dim), dtype=torch.float32, device='cuda')
+    for m in (0, 1, 2):
+        n = len(rows_of[m])
+        if n == 0:
+            continue
+        sizes = [b - a for a, b in (pdist.shard_range(n, r, world) for r in range(world))]
+        allm = pdist.all_gather_rows(shards[m], sizes)
+        full[torch.from_numpy(rows_of[m]).cuda()] = allm
+    if rank == 0:
+        np.save(os.path.join(output_dir, 'features.npy'), full.cpu().numpy())
+    del full
+    s = pdist.evaluate_sharded(shards[0], shards[1], shards[2], ids, cams, marks, rank,
+                               world, metric=cfg.REID.get('DISTANCE', 'euclidean'),
+                               rerank=bool(cfg.REID.RERANK))
     if rank == 0:
         print('{:<30}'.format('Single Query:'), end='')
-        rde.print_scores(res['mAP'], res['cmc'])
-    return _reid_results(dataset.name, (res['mAP'], res['cmc'], None, None))
+        rde.print_scores(s[0], s[1])
+        if s[2] is not None:
+            print('{:<30}'.format('Multi Query:'), end='')
+            rde.print_scores(s[2], s[3])
+    return _reid_results(dataset.name, s)
 
 
 def _reid_results(name, s):

@@ -6,6 +6,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from _parity import check_rank_metrics, tie_eps
 
 pytestmark = pytest.mark.gpu
 
@@ -49,8 +50,14 @@ def test_run_inference_end_to_end(tmp_path):
     blobs = model.synthetic_weights(plan, seed=1)
     weights.save_npz(os.path.join(tmp, 'w.npz'), blobs)
     res = test_engine.run_inference(os.path.join(tmp, 'w.npz'))
-    feats = np.load(os.path.join(test_engine.get_output_dir(cfg.TEST.DATASETS[0]),
-                                 'features.npy'))
+    # features.pkl = {'all_feats', 'cfg'} (test_engine.py:356-368); written
+    # by this test's own run, so unpickling it is safe
+    import pickle
+    with open(os.path.join(test_engine.get_output_dir(cfg.TEST.DATASETS[0]),
+                           'features.pkl'), 'rb') as f:
+        saved = pickle.load(f)
+    assert set(saved) == {'all_feats', 'cfg'} and 'REID' in saved['cfg']
+    feats = saved['all_feats']
     # oracle pipeline on identical decoded pixels
     ims = [test_engine._decode_bgr(os.path.join(tmp, n)) for n in names]
     x = pre.im_list_to_blob([pre.prep_im_for_blob(im) for im in ims])
@@ -58,16 +65,27 @@ def test_run_inference_end_to_end(tmp_path):
     np.testing.assert_allclose(feats, ref, rtol=0, atol=1e-4)
     ids = np.array([int(n[:8]) for n in names])
     cams = np.array([int(n[9:13]) for n in names])
-    # ranking parity on the same features (the oracle ranks with NumPy fp32
-    # distances; a rank can only flip where two distances are within ~1e-6)
-    mAP, cmc, _, _ = ev.evaluate_arrays(feats, ids, cams, marks)
-    r = list(res.values())[0]['ReID']
     q, g = marks == 0, marks == 1
-    d = ev.compute_dist(feats[q], feats[g])
-    gaps = np.diff(np.sort(d, axis=1), axis=1)
-    tol = 1e-9 if gaps.min() > 1e-5 else 0.05
-    assert abs(r['mAP'] - mAP) < tol
-    assert abs(r['CMC1'] - cmc[0]) < max(tol, 1e-9)
-    # and the end-to-end features agree with the oracle pipeline's
-    mAP_ref, _, _, _ = ev.evaluate_arrays(ref, ids, cams, marks)
-    assert abs(mAP_ref - mAP) < 0.02
+    r = list(res.values())[0]['ReID']
+    # the reported scores are the GPU ranking of the GPU features' distances
+    from pps_amd import ops
+    from pps_amd import reid_dataset_evaluator as gev
+    ft = torch.from_numpy(feats).cuda()
+    d_gpu = ops.compute_dist(ft[torch.from_numpy(np.nonzero(q)[0]).cuda()].contiguous(),
+                             ft[torch.from_numpy(np.nonzero(g)[0]).cuda()].contiguous())
+    ap, valid, first = gev.rank_eval(d_gpu, ids[q], ids[g], cams[q], cams[g])
+    mAP_gpu, cmc_gpu = gev.scores_from_ranks(ap, valid, first)
+    assert r['mAP'] == mAP_gpu and r['CMC1'] == cmc_gpu[0]
+    # vs the all-CPU oracle pipeline (oracle features -> oracle distances ->
+    # oracle mean_ap / cmc): exact outside near-ties, which are counted
+    d_ref = ev.compute_dist(ref[q], ref[g])
+    eps = tie_eps(d_gpu.cpu().numpy(), d_ref)
+    out = check_rank_metrics(ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy(),
+                             d_ref, ids[q], ids[g], cams[q], cams[g], eps)
+    print('end to end vs oracle pipeline: %s' % out)
+    mAP_ref, cmc_ref, _, _ = ev.evaluate_arrays(ref, ids, cams, marks)
+    assert abs(out['mAP_ref'] - mAP_ref) <= 1e-12
+    if out['ap_affected'] == 0:
+        assert abs(r['mAP'] - mAP_ref) <= 1e-12
+    if out['first_affected'] == 0:
+        assert abs(r['CMC1'] - cmc_ref[0]) <= 1e-12

@@ -1,19 +1,26 @@
 """Market-1501-scale retrieval parity (BASELINE configs[1] sizes: Q=3368,
-G=15913, D=3968) on synthetic features of the SURVEY §8(d) distribution.
+G=15913, D=3968) on synthetic features of the SURVEY §8(d) distribution,
+held to the north_star bar ("bit-exact on rank indices and within 1e-4 on
+distances; mAP/Rank-1 equal to the CPU reference"):
 
 * distances: GPU (x3 and exact-f32 kernels) vs the oracle's NumPy
-  restatement of compute_dist, within 1e-4 (north_star);
-* ranking: the oracle's stable-argsort mean_ap / cmc on the GPU's own
-  distances vs the GPU count-based kernels -- AP per query within 1e-12 and
-  CMC exact (identical inputs, so the rank of every positive must agree);
-* end to end: mAP / CMC@1 of the GPU path vs the all-CPU oracle path; these
-  can differ only through near-tied distances whose fp32 rounding differs
-  (|Δd| < 1e-5), which moves a positive by a rank: mAP within 1e-4, CMC@k
-  within 2 queries.
+  restatement of compute_dist (reid_dataset_evaluator.py:244-272), <= 1e-4;
+* rank indices: the GPU's stable top-10 / top-100 (pps_topk on the GPU
+  distances) vs the stable argsort of the oracle's distances
+  (:319,:420) position by position -- a position may differ only where the
+  two entries are a near-tie (oracle gap <= 2 x the measured distance error);
+  the number of such positions is printed;
+* mAP / CMC: the GPU count kernels on the GPU's distances vs the oracle's
+  mean_ap / cmc on the oracle's distances -- AP and first-match rank equal
+  for every query outside the near-tie set, mAP / CMC equal when that set is
+  empty (tests/_parity.py);
+* ranking alone: the oracle on the GPU's own distances vs the GPU kernels,
+  exact (identical inputs).
 """
 import numpy as np
 import pytest
 import torch
+from _parity import check_rank_metrics, check_topk, tie_eps
 
 from oracle import evaluator as ev
 
@@ -34,7 +41,9 @@ def market():
     f /= np.linalg.norm(f, axis=1, keepdims=True)
     f = f.astype(np.float32)
     ref = ev.compute_dist(f[:Q], f[Q:])
-    return dict(qf=f[:Q], gf=f[Q:], qid=qid, gid=gid, qcam=qcam, gcam=gcam, ref=ref)
+    order = np.argsort(ref, axis=1, kind='stable')[:, :100]
+    return dict(qf=f[:Q], gf=f[Q:], qid=qid, gid=gid, qcam=qcam, gcam=gcam, ref=ref,
+                order=order)
 
 
 @pytest.mark.parametrize('math', ['x3', 'f32'])
@@ -47,20 +56,21 @@ def test_market_scale_parity(market, math):
     dn = d.cpu().numpy()
     err = np.abs(dn - m['ref']).max()
     assert err < 1e-4, err
-    # ranking on identical distances: exact
+    eps = tie_eps(dn, m['ref'])
+    # rank indices: GPU stable top-k vs the oracle's stable argsort
+    for k in (10, 100):
+        _, idx = ops.topk(d, k)
+        flips = check_topk(idx.cpu().numpy(), m['ref'], k, eps, m['order'][:, :k])
+        print('%s top-%d: %d of %d positions differ (all near-ties, eps %.3g)'
+              % (math, k, flips, Q * k, eps))
+    # mAP / CMC: GPU on GPU distances vs oracle on oracle distances
     ap, valid, first = gev.rank_eval(d, m['qid'], m['gid'], m['qcam'], m['gcam'])
-    ap, valid, first = ap.cpu().numpy(), valid.cpu().numpy().astype(bool), first.cpu().numpy()
-    ap_o, valid_o = ev.mean_ap(dn, m['qid'], m['gid'], m['qcam'], m['gcam'], average=False)
-    np.testing.assert_array_equal(valid, valid_o.astype(bool))
-    np.testing.assert_allclose(ap[valid], ap_o[valid_o.astype(bool)], rtol=0, atol=1e-12)
-    cmc_o = ev.cmc(dn, m['qid'], m['gid'], m['qcam'], m['gcam'], topk=10,
-                   first_match_break=True)
-    mAP, cmc = gev.scores_from_ranks(ap, valid, first, topk=10)
-    np.testing.assert_allclose(cmc, cmc_o, rtol=0, atol=1e-12)
-    # end to end against the all-CPU path
-    mAP_ref = ev.mean_ap(m['ref'], m['qid'], m['gid'], m['qcam'], m['gcam'])
-    cmc_ref = ev.cmc(m['ref'], m['qid'], m['gid'], m['qcam'], m['gcam'], topk=10,
-                     first_match_break=True)
-    assert abs(mAP - mAP_ref) < 1e-4, (mAP, mAP_ref)
-    assert np.abs(cmc - cmc_ref).max() <= 2.0 / valid.sum(), (cmc, cmc_ref)
-    assert 0.5 < mAP < 0.9   # non-trivial regime (~0.69)
+    ap, valid, first = ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy()
+    r = check_rank_metrics(ap, valid, first, m['ref'], m['qid'], m['gid'], m['qcam'],
+                           m['gcam'], eps)
+    print('%s end to end: %s' % (math, r))
+    assert 0.5 < r['mAP'] < 0.9   # non-trivial regime (~0.69)
+    # ranking alone on identical distances: exact
+    r2 = check_rank_metrics(ap, valid, first, dn, m['qid'], m['gid'], m['qcam'], m['gcam'],
+                            0.0)
+    assert r2['ap_differs'] == 0 and r2['first_differs'] == 0, r2
