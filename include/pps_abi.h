@@ -327,6 +327,27 @@ int pps_l2_normalize(const float* x, int64_t N, int D, float* y,
 int pps_group_mean(const float* x, int D, const int32_t* offsets,
                    const int32_t* members, int ngroups, float* out, void* stream);
 
+/* ---- unfused Caffe2 operators (op-by-op net execution) --------------------
+ * The product forward runs the recorded test net compiled into fused GEMM
+ * epilogues; these stand-alone forms back the operator registry's eager
+ * mode (pps_amd/net.py) for the remaining op names of the graph.
+ * pps_spatial_bn: Caffe2 SpatialBN, is_test (detector.py:419-447,
+ *   ResNet.py:252-253): y = (x - rm[c]) * (s[c] / sqrt(riv[c] + eps)) + b[c]
+ *   (+ ReLU if relu) over NHWC [M][C].
+ * pps_eltwise: n-ary elementwise over n floats, inputs = HOST array of k
+ *   device pointers (k <= 32): op 0 = Sum / Add (input order), 1 = Max,
+ *   2 = Mean (Sum * (1/k), pps_heads.py:58-68), 3 = Relu (k = 1).
+ * pps_global_pool: AveragePool / MaxPool with global_pooling
+ *   (bpm_heads.py:50-53): x image n at x + n*n_stride holds H*W*C values
+ *   (a Split strip is such a view); mode 0 = mean, 1 = max; y [N][C]. */
+int pps_spatial_bn(const float* x, int64_t M, int C, const float* s, const float* b,
+                   const float* rm, const float* riv, float eps, int relu, float* y,
+                   void* stream);
+int pps_eltwise(const float* const* inputs, int k, int64_t n, int op, float* y,
+                void* stream);
+int pps_global_pool(const float* x, int N, int H, int W, int C, int64_t n_stride,
+                    int mode, float* y, void* stream);
+
 /* Image preprocessing (utils/blob.py:97-117 prep_im_for_blob,
  * :65-94 im_list_to_blob): uint8 BGR HWC images [N][Hi][Wi][3] (device) ->
  * subtract pixel means (HOST float[3]) -> bicubic resize (a = -0.75,

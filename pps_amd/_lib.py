@@ -79,6 +79,10 @@ SIGNATURES = {
                            c_ptr],
     'pps_l2_normalize': [c_ptr, c_i64, c_int, c_ptr, c_ptr],
     'pps_group_mean': [c_ptr, c_int, c_ptr, c_ptr, c_int, c_ptr, c_ptr],
+    'pps_spatial_bn': [c_ptr, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_int,
+                       c_ptr, c_ptr],
+    'pps_eltwise': [c_ptr, c_int, c_i64, c_int, c_ptr, c_ptr],
+    'pps_global_pool': [c_ptr, c_int, c_int, c_int, c_int, c_i64, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr': [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr_ragged': [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int,
                                   c_ptr, c_ptr],

@@ -57,8 +57,12 @@ int pps_abi_version(void) { return 1; }
 const char* pps_last_error(void) { return g_last_error.c_str(); }
 
 const char* pps_registered_ops(void) {
-  return "PairWiseDistance;Conv+SpatialBN+Sum+Relu;MaxPool;PartPowerSet;Normalize;"
-         "ComputeDist;RankCounts;TopK;TopKMerge;PrepImForBlob";
+  // the reference's Caffe2 op names of the test net (pps_amd/net.py OPS) and
+  // the fused / retrieval entry points the product path runs
+  return "Conv;SpatialBN;Relu;Sum;Add;Max;Mean;MaxPool;AveragePool;Split;FC;Concat;"
+         "Reshape;Normalize;PairWiseDistance;"
+         "Conv+SpatialBN+Sum+Relu;PartPowerSet;ComputeDist;RankCounts;TopK;TopKMerge;"
+         "ReRanking;PrepImForBlob";
 }
 
 int pps_gemm_num_tiles(void) { return GEMM_NUM_TILES - 1; }

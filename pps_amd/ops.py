@@ -456,6 +456,51 @@ def group_mean(x, groups):
     return out
 
 
+ELTWISE = {'Sum': 0, 'Add': 0, 'Max': 1, 'Mean': 2, 'Relu': 3}
+
+
+def spatial_bn(x, s, b, rm, riv, eps=1e-5, relu=False, y=None):
+    """Caffe2 SpatialBN (is_test) over the last (channel) axis of an NHWC /
+    [M, C] tensor (pps_spatial_bn)."""
+    C = x.shape[-1]
+    if y is None:
+        y = torch.empty_like(x)
+    call('pps_spatial_bn', _dev(x, 'x'), x.numel() // C, C, _dev(s, 's'), _dev(b, 'b'),
+         _dev(rm, 'rm'), _dev(riv, 'riv'), float(eps), int(bool(relu)), _dev(y, 'y'),
+         _stream())
+    return y
+
+
+def eltwise(op, xs, y=None):
+    """Sum / Add / Max / Mean / Relu of same-shape tensors (pps_eltwise)."""
+    xs = list(xs)
+    for t in xs[1:]:
+        if tuple(t.shape) != tuple(xs[0].shape):
+            raise RuntimeError('%s: input shapes differ: %s vs %s'
+                               % (op, tuple(xs[0].shape), tuple(t.shape)))
+    if y is None:
+        y = torch.empty_like(xs[0])
+    ptrs = (_lib.ctypes.c_void_p * len(xs))(*[_dev(t, 'input %d' % i) for i, t in enumerate(xs)])
+    call('pps_eltwise', ptrs, len(xs), xs[0].numel(), ELTWISE[op], _dev(y, 'y'), _stream())
+    return y
+
+
+def global_pool(x, mode, y=None):
+    """AveragePool (mode 'ave') / MaxPool ('max') with global_pooling over an
+    NHWC tensor -> [N, C].  x may be an H-slice view of a taller NHWC tensor
+    (a Split strip): per-image blocks contiguous, image stride x.stride(0)."""
+    N, H, W, C = x.shape
+    if x.stride(3) != 1 or x.stride(2) != C or x.stride(1) != W * C:
+        raise RuntimeError('global_pool needs per-image contiguous NHWC blocks')
+    if y is None:
+        y = torch.empty((N, C), dtype=torch.float32, device=x.device)
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise RuntimeError('x must be a float32 device tensor')
+    call('pps_global_pool', x.data_ptr(), N, H, W, C, x.stride(0) if N > 1 else H * W * C,
+         0 if mode == 'ave' else 1, _dev(y, 'y'), _stream())
+    return y
+
+
 def l2_normalize(x, y=None):
     N, D = x.shape
     if y is None:
@@ -478,32 +523,13 @@ def preprocess_bgr(img_u8, pixel_means, out_hw, y=None):
 
 
 # ---------------------------------------------------------------------------
-# Operator registry (reference Caffe2 op names)
+# Operator registry (reference Caffe2 op names): pps_amd/net.py
 # ---------------------------------------------------------------------------
-def _op_pairwise_distance(inputs, **args):
-    (X,) = inputs
-    return [pairwise_distance(X)]
-
-
-def _op_normalize(inputs, axis=1, **args):
-    (X,) = inputs
-    if axis != 1 or X.dim() != 2:
-        raise RuntimeError('Normalize: only axis=1 on 2-D input is built')
-    return [l2_normalize(X)]
-
-
-OPS = {
-    'PairWiseDistance': _op_pairwise_distance,
-    'Normalize': _op_normalize,
-}
-
-
 def run_op(name, inputs, **args):
-    """Look up an operator by its reference (Caffe2) name and run it."""
-    if name not in OPS:
-        raise RuntimeError('Operator %s is not registered in pps_amd (have: %s)'
-                           % (name, ', '.join(sorted(OPS))))
-    return OPS[name](inputs, **args)
+    """Look up an operator by its reference (Caffe2) name and run it
+    (the registry is net.OPS: every op name of the reference's test net)."""
+    from .net import run_op as _run
+    return _run(name, inputs, **args)
 
 
 def preprocess_bgr_ragged(blob_u8, offsets, heights, widths, pixel_means, out_hw, y=None):

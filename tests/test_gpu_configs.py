@@ -196,7 +196,7 @@ def test_duke_rerank_vs_oracle_500x3000():
     qcam = rng.randint(1, 9, Q)
     gcam = rng.randint(1, 9, G)
     cent = rng.randn(200, D).astype(np.float32)
-    f = cent[np.concatenate([qid, gid])] + 1.5 * rng.randn(Q + G, D).astype(np.float32)
+    f = cent[np.concatenate([qid, gid])] + 2.5 * rng.randn(Q + G, D).astype(np.float32)
     f = (f / np.linalg.norm(f, axis=1, keepdims=True)).astype(np.float32)
     qg = ev.compute_dist(f[:Q], f[Q:])
     qq = ev.compute_dist(f[:Q], f[:Q])
@@ -210,7 +210,8 @@ def test_duke_rerank_vs_oracle_500x3000():
     ap, valid, first = gev.rank_eval(rr, qid, gid, qcam, gcam)
     r = check_rank_metrics(ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy(), ref,
                            qid, gid, qcam, gcam, tie_eps(rrn, ref))
-    print('Duke 500x3000 re-ranking: max|err| %.3g, %s' % (err, r))
+    print("Duke 500x3000 re-ranking: max|err| %.3g, %s" % (err, r))
+    assert 0.3 < r["mAP"] < 0.8   # non-trivial regime (plain mAP ~0.28, re-ranked ~0.50)
 
 
 def test_duke_full_size_cosine_rerank_properties():

@@ -88,3 +88,52 @@ def test_fpn_variant_plan_is_reference_subset():
     assert dead and all(k.startswith('fpn_inner_res4') or k.startswith('fpn_inner_res3') or
                         k.startswith('fpn_inner_res2') for k in dead), sorted(dead)[:5]
     assert mine['pps0_conv_w'] == (128, 256, 1, 1)
+
+
+def _compiled_vs_built(graph_file, overrides=()):
+    from pps_amd import config, model, net
+    _market()
+    if overrides:
+        config.merge_cfg_from_list(list(overrides))
+    with open(os.path.join(GOLDEN, graph_file)) as f:
+        g = json.load(f)
+    return net.compile_graph(g), model.build_plan(), g
+
+
+def test_compiled_graph_equals_build_plan():
+    """net.compile_graph fuses the recorded reference op list (Conv+BN(+Sum)
+    +Relu, projection shortcut, Split/pools/Mean/Max/Add, heads + Concat +
+    Reshape + Normalize) into exactly the plan model.build_plan() builds:
+    same layers in the same order, same parameters, same output."""
+    cp, bp, g = _compiled_vs_built('pps_graph_market1501.json')
+    assert cp.layers == bp.layers
+    assert cp.params == bp.params and cp.output == bp.output == g['output']
+    assert cp.feat_dim == bp.feat_dim == 3968
+
+
+def test_compiled_fpn_graph_drops_dead_levels():
+    """FPN variant: liveness removes the top-down levels and FC logits the
+    reference computes at test without reading (pps_heads.py:88-96)."""
+    from pps_amd import net
+    cp, bp, g = _compiled_vs_built('pps_graph_market1501_fpn.json',
+                                   ['FPN.FPN_ON', 'True', 'MODEL.CONV_BODY',
+                                    'FPN_reid.add_fpn_ResNet50_conv5_body'])
+    assert cp.layers == bp.layers and cp.params == bp.params
+    live = net.live_ops(g)
+    assert not any(o['type'] == 'FC' for o in live)
+    assert len(live) < len(g['ops'])
+
+
+def test_registry_covers_every_reference_op_name():
+    from pps_amd import _lib, net
+    names = set()
+    for f in ('pps_graph_market1501.json', 'pps_graph_market1501_fpn.json'):
+        with open(os.path.join(GOLDEN, f)) as fh:
+            names |= {o['type'] for o in net.live_ops(json.load(fh))}
+    names |= {'FC', 'PairWiseDistance'}
+    assert names <= set(net.OPS), sorted(names - set(net.OPS))
+    exported = set(_lib.lib().pps_registered_ops().decode().split(';'))
+    assert set(net.OPS) <= exported
+    import pytest
+    with pytest.raises(RuntimeError, match='not registered'):
+        net.run_op('BatchHard', [])
