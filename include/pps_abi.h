@@ -139,7 +139,9 @@ int pps_collect_positives(const float* dist, int64_t Q, int64_t G,
  *    sorted positives: hist[q][p] += 1 where p = first positive with
  *    d_p >= d_i, and before[q] counts entries ordered before the first
  *    positive.  hist / before are ADDITIVE over gallery shards (sum with an
- *    all-reduce), and must be zeroed by the caller. */
+ *    all-reduce), and must be zeroed by the caller.  Capacity: R*Pmax <=
+ *    2048 (LDS), else PPS_ERR_CAPACITY -- the streaming entry points below
+ *    have no such limit and are what the Python evaluator uses. */
 int pps_rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                     const int32_t* qid, const int32_t* qcam,
                     const int32_t* gid, const int32_t* gcam, int64_t g_offset,
@@ -154,6 +156,41 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
                     const int32_t* pos_total, const int32_t* hist,
                     const int32_t* before, double* ap, int32_t* valid,
                     int32_t* first_rank, void* stream);
+
+/* Streaming evaluation (the product path): the same counts as 1)-2) from a
+ * per-identity gallery index, with one pure stream over the distance row.
+ *
+ * a) pps_collect_matches: members = the shard's LOCAL gallery indices sorted
+ *    by (id, index) (a CSR over identities, built once per gallery from the
+ *    ids); query q's identity occupies members[q_beg[q], q_end[q]).  Lists
+ *    its positives (other camera) as pps_collect_positives does, and its junk
+ *    entries (same id, same camera, reid_dataset_evaluator.py:427-428) as
+ *    junk_d / junk_idx [Q][Jmax] with exact counts junk_cnt -- O(matches)
+ *    per query instead of a scan of G ids.
+ * b) pps_rank_prepare: merge R shards' lists [R][Q][Pmax] and sort by
+ *    (distance, global index) -> sorted_d / sorted_idx [Q][R*Pmax] (padding
+ *    +inf / -1), pos_total [Q].  R*Pmax <= 8192.
+ * c) pps_rank_count_stream: for this shard's rows, hist[q][p] += #entries
+ *    with p = first positive d_p >= d, before[q] += #entries ordered before
+ *    the first positive, over all entries of the row minus this shard's junk
+ *    entries -- the same additive counts as pps_rank_counts (caller zeroes
+ *    hist / before; sum over shards), then pps_ap_finalize.  Rows are read
+ *    as 16-byte vectors when 16-byte aligned (ldd % 4 == 0).  No capacity
+ *    limit on Ptot (long positive lists are searched in L2). */
+int pps_collect_matches(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                        const int32_t* qcam, const int32_t* gcam, const int32_t* members,
+                        const int32_t* q_beg, const int32_t* q_end, int64_t g_offset,
+                        int Pmax, float* pos_d, int32_t* pos_idx, int32_t* pos_cnt, int Jmax,
+                        float* junk_d, int32_t* junk_idx, int32_t* junk_cnt, void* stream);
+int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
+                     const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
+                     int32_t* pos_total, void* stream);
+int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                          int64_t g_offset, int Ptot, const float* sorted_d,
+                          const int32_t* sorted_idx, const int32_t* pos_total, int Jmax,
+                          const float* junk_d, const int32_t* junk_idx,
+                          const int32_t* junk_cnt, int32_t* hist, int32_t* before,
+                          void* stream);
 
 /* Stable per-row top-k (k <= 1024) of a distance matrix, ascending, ties by
  * gallery index.  Replaces the `np.argsort(distmat, axis=1)[:, :k]` rank

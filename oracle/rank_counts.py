@@ -35,7 +35,22 @@ class CpuBackend(object):
         return torch.from_numpy(ev.compute_dist(q.numpy(), g.numpy(), metric))
 
     @staticmethod
-    def collect(dist, qid, qcam, gid, gcam, g_offset, pmax):
+    def prepare(ev):
+        return None
+
+    @staticmethod
+    def collect(dist, ev, state, pmax):
+        pos = CpuBackend.collect_positives(dist, ev.qid, ev.qcam, ev.gid, ev.gcam, ev.g_offset,
+                                           pmax)
+        return pos + (None,)
+
+    @staticmethod
+    def counts(dist, ev, state, pos_d, pos_idx, pos_cnt, local):
+        return CpuBackend.rank_counts(dist, ev.qid, ev.qcam, ev.gid, ev.gcam, ev.g_offset,
+                                      pos_d, pos_idx, pos_cnt)
+
+    @staticmethod
+    def collect_positives(dist, qid, qcam, gid, gcam, g_offset, pmax):
         d, qi, qc, gi, gc = (t.numpy() for t in (dist, qid, qcam, gid, gcam))
         Q = d.shape[0]
         pos_d = np.zeros((Q, pmax), np.float32)
@@ -50,7 +65,7 @@ class CpuBackend(object):
         return torch.from_numpy(pos_d), torch.from_numpy(pos_idx), torch.from_numpy(cnt)
 
     @staticmethod
-    def counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt):
+    def rank_counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt):
         d, qi, qc, gi, gc = (t.numpy() for t in (dist, qid, qcam, gid, gcam))
         pd, px, pc = pos_d.numpy(), pos_idx.numpy(), pos_cnt.numpy()
         R, Q, pmax = pd.shape

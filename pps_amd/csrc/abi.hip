@@ -38,6 +38,14 @@ int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const i
 int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
                 const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+int collect_matches(const float*, int64_t, int64_t, const int32_t*, const int32_t*,
+                    const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
+                    int32_t*, int32_t*, int, float*, int32_t*, int32_t*, hipStream_t);
+int rank_prepare(int, int64_t, int, const float*, const int32_t*, const int32_t*, float*,
+                 int32_t*, int32_t*, hipStream_t);
+int rank_count_stream(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
+                      const int32_t*, const int32_t*, int, const float*, const int32_t*,
+                      const int32_t*, int32_t*, int32_t*, hipStream_t);
 int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int, double,
            void*, size_t, float*, hipStream_t);
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
@@ -261,6 +269,52 @@ int pps_rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd,
   return rank_counts(dist, Q, G, ldd, qid, qcam, gid, gcam, g_offset, R, Pmax, pos_d,
                      pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, hist, before,
                      as_stream(stream));
+}
+
+int pps_collect_matches(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                        const int32_t* qcam, const int32_t* gcam, const int32_t* members,
+                        const int32_t* q_beg, const int32_t* q_end, int64_t g_offset,
+                        int Pmax, float* pos_d, int32_t* pos_idx, int32_t* pos_cnt, int Jmax,
+                        float* junk_d, int32_t* junk_idx, int32_t* junk_cnt, void* stream) {
+  PPS_ENFORCE(dist && qcam && gcam && members && q_beg && q_end && pos_d && pos_idx &&
+                  pos_cnt && junk_d && junk_idx && junk_cnt,
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Pmax > 0 && Jmax > 0, "bad shape");
+  PPS_ENFORCE(G < (1ll << 31) && g_offset + G < (1ll << 31), "gallery indices must fit int32");
+  return collect_matches(dist, Q, ldd, qcam, gcam, members, q_beg, q_end, g_offset, Pmax,
+                         pos_d, pos_idx, pos_cnt, Jmax, junk_d, junk_idx, junk_cnt,
+                         as_stream(stream));
+}
+
+int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
+                     const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
+                     int32_t* pos_total, void* stream) {
+  PPS_ENFORCE(pos_d && pos_idx && pos_cnt && sorted_d && sorted_idx && pos_total,
+              "null pointer");
+  PPS_ENFORCE(R >= 1 && R <= kMergeMaxLists, "R must be in [1, 64]");
+  PPS_ENFORCE(Q >= 0 && Pmax > 0, "bad shape");
+  if ((int64_t)R * Pmax > 8192) {
+    set_error("merged positive capacity R*Pmax=" + std::to_string((int64_t)R * Pmax) +
+              " exceeds 8192 (LDS of the merge sort)");
+    return PPS_ERR_CAPACITY;
+  }
+  return rank_prepare(R, Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total,
+                      as_stream(stream));
+}
+
+int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
+                          int64_t g_offset, int Ptot, const float* sorted_d,
+                          const int32_t* sorted_idx, const int32_t* pos_total, int Jmax,
+                          const float* junk_d, const int32_t* junk_idx,
+                          const int32_t* junk_cnt, int32_t* hist, int32_t* before,
+                          void* stream) {
+  PPS_ENFORCE(dist && sorted_d && sorted_idx && pos_total && junk_d && junk_idx && junk_cnt &&
+                  hist && before,
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Ptot > 0 && Jmax > 0, "bad shape");
+  PPS_ENFORCE((G + 4095) / 4096 <= 65535, "G too large for the chunk grid");
+  return rank_count_stream(dist, Q, G, ldd, g_offset, Ptot, sorted_d, sorted_idx, pos_total,
+                           Jmax, junk_d, junk_idx, junk_cnt, hist, before, as_stream(stream));
 }
 
 int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* pos_total,

@@ -290,6 +290,283 @@ int rank_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, const int3
   return PPS_OK;
 }
 
+// ---- streaming evaluation from a per-identity gallery index ---------------------
+// The product path (v2).  A CSR index of the gallery (host-built once from the
+// ids: `members` = local gallery indices sorted by (id, index); the query's
+// identity occupies members[q_beg[q], q_end[q])) lets every query list its
+// true matches directly -- tens of gathers instead of a scan of all G ids and
+// cams -- split into positives (other camera) and junk (same camera,
+// reid_dataset_evaluator.py:427-428).  The counting pass then needs no ids at
+// all: it bins EVERY entry of the distance row against the sorted positives
+// and afterwards takes the junk entries (known, few) back out, so the row is
+// one pure 16-byte-vector stream of distances.
+//
+// a) collect_matches: one wave per query.
+constexpr int kMatchWaves = 4;
+__global__ void __launch_bounds__(64 * kMatchWaves)
+collect_matches_kernel(const float* __restrict__ dist, int64_t Q, int64_t ldd,
+                       const int32_t* __restrict__ qcam, const int32_t* __restrict__ gcam,
+                       const int32_t* __restrict__ members,
+                       const int32_t* __restrict__ q_beg, const int32_t* __restrict__ q_end,
+                       int64_t g_offset, int Pmax, float* __restrict__ pos_d,
+                       int32_t* __restrict__ pos_idx, int32_t* __restrict__ pos_cnt, int Jmax,
+                       float* __restrict__ junk_d, int32_t* __restrict__ junk_idx,
+                       int32_t* __restrict__ junk_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * kMatchWaves + (threadIdx.x >> 6);
+  if (q >= Q) return;
+  const int beg = q_beg[q], end = q_end[q], qc = qcam[q];
+  const float* row = dist + q * ldd;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int np = 0, nj = 0;
+  for (int m0 = beg; m0 < end; m0 += 64) {
+    const int m = m0 + lane;
+    const bool in = m < end;
+    const int idx = in ? members[m] : 0;
+    const bool pos = in && gcam[idx] != qc;
+    const bool junk = in && !pos;
+    const float d = in ? row[idx] : 0.f;
+    const unsigned long long bp = __ballot(pos), bj = __ballot(junk);
+    const int sp = np + __popcll(bp & below), sj = nj + __popcll(bj & below);
+    if (pos && sp < Pmax) {
+      pos_d[q * Pmax + sp] = d;
+      pos_idx[q * Pmax + sp] = (int32_t)(g_offset + idx);
+    }
+    if (junk && sj < Jmax) {
+      junk_d[q * Jmax + sj] = d;
+      junk_idx[q * Jmax + sj] = (int32_t)(g_offset + idx);
+    }
+    np += __popcll(bp);
+    nj += __popcll(bj);
+  }
+  if (lane == 0) {
+    pos_cnt[q] = np;
+    junk_cnt[q] = nj;
+  }
+}
+
+int collect_matches(const float* dist, int64_t Q, int64_t ldd, const int32_t* qcam,
+                    const int32_t* gcam, const int32_t* members, const int32_t* q_beg,
+                    const int32_t* q_end, int64_t g_offset, int Pmax, float* pos_d,
+                    int32_t* pos_idx, int32_t* pos_cnt, int Jmax, float* junk_d,
+                    int32_t* junk_idx, int32_t* junk_cnt, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  const unsigned grid = (unsigned)((Q + kMatchWaves - 1) / kMatchWaves);
+  hipLaunchKernelGGL(collect_matches_kernel, dim3(grid), dim3(64 * kMatchWaves), 0, st, dist,
+                     Q, ldd, qcam, gcam, members, q_beg, q_end, g_offset, Pmax, pos_d, pos_idx,
+                     pos_cnt, Jmax, junk_d, junk_idx, junk_cnt);
+  PPS_CHECK_LAUNCH("collect_matches_kernel");
+  return PPS_OK;
+}
+
+// b) rank_prepare: merge the R shards' positive lists of a query and sort
+// them by (distance, global index) -- rank by counting in LDS (one block per
+// query; tens of entries on real splits).
+__global__ void rank_prepare_kernel(int R, int64_t Q, int Pmax, const float* __restrict__ pos_d,
+                                    const int32_t* __restrict__ pos_idx,
+                                    const int32_t* __restrict__ pos_cnt,
+                                    float* __restrict__ sorted_d,
+                                    int32_t* __restrict__ sorted_idx,
+                                    int32_t* __restrict__ pos_total) {
+  const int64_t q = blockIdx.x;
+  const int Ptot = R * Pmax;
+  extern __shared__ int plds[];
+  float* ud = reinterpret_cast<float*>(plds);
+  int* ui = plds + Ptot;
+  __shared__ int offs[kMergeMaxLists + 1];
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int r = 0; r < R; ++r) {
+      offs[r] = o;
+      const int c = pos_cnt[(int64_t)r * Q + q];
+      o += c < Pmax ? c : Pmax;
+    }
+    offs[R] = o;
+  }
+  __syncthreads();
+  const int P = offs[R];
+  for (int r = 0; r < R; ++r) {
+    const int n = offs[r + 1] - offs[r];
+    for (int p = threadIdx.x; p < n; p += blockDim.x) {
+      ud[offs[r] + p] = pos_d[((int64_t)r * Q + q) * Pmax + p];
+      ui[offs[r] + p] = pos_idx[((int64_t)r * Q + q) * Pmax + p];
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const float d = ud[p];
+    const int ix = ui[p];
+    int rk = 0;
+    for (int o = 0; o < P; ++o) rk += key_less(ud[o], ui[o], d, ix) ? 1 : 0;
+    sorted_d[q * Ptot + rk] = d;
+    sorted_idx[q * Ptot + rk] = ix;
+  }
+  for (int p = P + threadIdx.x; p < Ptot; p += blockDim.x) {
+    sorted_d[q * Ptot + p] = INFINITY;
+    sorted_idx[q * Ptot + p] = -1;
+  }
+  if (threadIdx.x == 0) pos_total[q] = P;
+}
+
+int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
+                 const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
+                 int32_t* pos_total, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  const size_t lds = (size_t)2 * R * Pmax * sizeof(int);
+  hipLaunchKernelGGL(rank_prepare_kernel, dim3((unsigned)Q), dim3(kEvalThreads), lds, st, R,
+                     Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total);
+  PPS_CHECK_LAUNCH("rank_prepare_kernel");
+  return PPS_OK;
+}
+
+// c) rank_count_stream: grid (query, row chunk).  Each block streams its chunk
+// of the row as 16-byte vectors (kStreamU in flight per thread), bins the
+// entries closer than the farthest positive against the sorted positives
+// (binary search, LDS histogram), counts the entries ordered before the
+// first positive, takes this shard's junk entries back out (chunk 0), and
+// adds its counts to hist / before with one global atomic per non-empty bin.
+// KLDS = false: positive lists too long for LDS are searched in global memory
+// (L2) and binned with global atomics -- no capacity limit.
+constexpr int kStreamThreads = 256;
+constexpr int kStreamU = 4;                                  // float4 per thread in flight
+constexpr int kStreamChunk = kStreamThreads * kStreamU * 4;  // 4096 entries per block
+constexpr int kStreamLdsCap = 6144;                          // positives held in LDS
+
+template <bool KLDS>
+__global__ void __launch_bounds__(kStreamThreads)
+rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
+                         int64_t g_offset, int Ptot, const float* __restrict__ sorted_d,
+                         const int32_t* __restrict__ sorted_idx,
+                         const int32_t* __restrict__ pos_total, int Jmax,
+                         const float* __restrict__ junk_d,
+                         const int32_t* __restrict__ junk_idx,
+                         const int32_t* __restrict__ junk_cnt, int32_t* __restrict__ hist,
+                         int32_t* __restrict__ before) {
+  const int64_t q = blockIdx.x;
+  const int P = pos_total[q];
+  if (P == 0) return;
+  extern __shared__ int slds[];
+  const float* gsd = sorted_d + q * Ptot;
+  int32_t* ghist = hist + q * Ptot;
+  float* sd = reinterpret_cast<float*>(slds);
+  int* hs = slds + (KLDS ? P : 0);
+  __shared__ int red[kStreamThreads / 64];
+  if (KLDS) {
+    for (int p = threadIdx.x; p < P; p += kStreamThreads) {
+      sd[p] = gsd[p];
+      hs[p] = 0;
+    }
+    __syncthreads();
+  }
+  const float* S = KLDS ? sd : gsd;
+  const float dmax = S[P - 1], df = S[0];
+  const int64_t idf = sorted_idx[q * Ptot];
+  auto bin = [&](float d) {
+    int lo = 0, hi = P;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (S[mid] < d) lo = mid + 1; else hi = mid;
+    }
+    return lo;  // < P because d <= dmax
+  };
+  auto add = [&](int b, int v) {
+    if (KLDS) atomicAdd(&hs[b], v); else atomicAdd(&ghist[b], v);
+  };
+  int nb = 0;
+  auto visit = [&](int64_t i, float d) {
+    if (d <= dmax) {
+      add(bin(d), 1);
+      nb += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
+    }
+  };
+  const int64_t c0 = (int64_t)blockIdx.y * kStreamChunk;
+  const int64_t c1 = c0 + kStreamChunk < G ? c0 + kStreamChunk : G;
+  const float* row = dist + q * ldd;
+  if (((reinterpret_cast<uintptr_t>(row) & 15) == 0)) {
+    // 16-byte rows: the chunk [c0, c1) starts on a vector boundary
+    const f32x4* v4 = reinterpret_cast<const f32x4*>(row + c0);
+    const int nv = (int)((c1 - c0) >> 2);
+    f32x4 v[kStreamU];
+#pragma unroll
+    for (int u = 0; u < kStreamU; ++u) {
+      const int j = threadIdx.x + u * kStreamThreads;
+      // streamed once: non-temporal, so the row does not evict useful L2 lines
+      v[u] = j < nv ? __builtin_nontemporal_load(v4 + j) : f32x4{INFINITY, INFINITY, INFINITY,
+                                                                  INFINITY};
+    }
+#pragma unroll
+    for (int u = 0; u < kStreamU; ++u) {
+      const int64_t i = c0 + 4 * (int64_t)(threadIdx.x + u * kStreamThreads);
+      visit(i, v[u].x);
+      visit(i + 1, v[u].y);
+      visit(i + 2, v[u].z);
+      visit(i + 3, v[u].w);
+    }
+    const int64_t t = c0 + 4 * (int64_t)nv + threadIdx.x;
+    if (t < c1) visit(t, row[t]);
+  } else {
+    float v[4 * kStreamU];
+#pragma unroll
+    for (int u = 0; u < 4 * kStreamU; ++u) {
+      const int64_t i = c0 + threadIdx.x + (int64_t)u * kStreamThreads;
+      v[u] = i < c1 ? row[i] : INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 4 * kStreamU; ++u)
+      visit(c0 + threadIdx.x + (int64_t)u * kStreamThreads, v[u]);
+  }
+  if (blockIdx.y == 0) {  // junk entries of this shard were binned above: take them out
+    const int nj = junk_cnt[q] < Jmax ? junk_cnt[q] : Jmax;
+    for (int j = threadIdx.x; j < nj; j += kStreamThreads) {
+      const float d = junk_d[q * Jmax + j];
+      if (d <= dmax) {
+        add(bin(d), -1);
+        nb -= (d < df || (d == df && (int64_t)junk_idx[q * Jmax + j] < idf)) ? 1 : 0;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nb;
+  __syncthreads();
+  if (KLDS) {
+    for (int p = threadIdx.x; p < P; p += kStreamThreads)
+      if (hs[p]) atomicAdd(&ghist[p], hs[p]);
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < kStreamThreads / 64; ++w) s += red[w];
+    if (s) atomicAdd(&before[q], s);
+  }
+}
+
+int rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd, int64_t g_offset,
+                      int Ptot, const float* sorted_d, const int32_t* sorted_idx,
+                      const int32_t* pos_total, int Jmax, const float* junk_d,
+                      const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
+                      int32_t* before, hipStream_t st) {
+  if (Q <= 0 || G <= 0) return PPS_OK;
+  const int64_t nchunk = (G + kStreamChunk - 1) / kStreamChunk;
+  for (int64_t q0 = 0; q0 < Q; q0 += 65535) {  // grid.x limit
+    const int64_t qn = Q - q0 < 65535 ? Q - q0 : 65535;
+    const dim3 grid((unsigned)qn, (unsigned)nchunk);
+    const float* d = dist + q0 * ldd;
+    if (Ptot <= kStreamLdsCap) {
+      hipLaunchKernelGGL(rank_count_stream_kernel<true>, grid, dim3(kStreamThreads),
+                         (size_t)2 * Ptot * sizeof(int), st, d, G, ldd, g_offset, Ptot,
+                         sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot, pos_total + q0, Jmax,
+                         junk_d + q0 * Jmax, junk_idx + q0 * Jmax, junk_cnt + q0,
+                         hist + q0 * Ptot, before + q0);
+    } else {
+      hipLaunchKernelGGL(rank_count_stream_kernel<false>, grid, dim3(kStreamThreads), 0, st, d,
+                         G, ldd, g_offset, Ptot, sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot,
+                         pos_total + q0, Jmax, junk_d + q0 * Jmax, junk_idx + q0 * Jmax,
+                         junk_cnt + q0, hist + q0 * Ptot, before + q0);
+    }
+    PPS_CHECK_LAUNCH("rank_count_stream_kernel");
+  }
+  return PPS_OK;
+}
+
 // ---- 3) AP / first-match finalisation -----------------------------------------
 // One wave per query.  le[p] = prefix sum of hist (valid entries with
 // d <= d_p); pos_le[p] = #positives with d <= d_p (upper bound, so tied

@@ -9,10 +9,12 @@ Here each rank keeps its gallery shard resident in HBM:
 
   1. all-gather the query embeddings (RCCL over xGMI; Market 53.5 MB total),
   2. distance block [Q, G_r] on the local shard (HIP MFMA GEMM),
-  3. each rank lists its shard's true matches per query (capacity: a guess,
-     one all-reduce(MAX) of the true counts, re-collected only if a shard
-     overflowed); all-gather of the lists ([R, Q, Pmax], kilobytes),
-  4. each rank bins its shard against the merged, sorted positives
+  3. each rank lists its shard's true matches per query from a per-identity
+     index of its shard (capacity = the most same-id entries of any query in
+     any shard, exact from the ids every rank holds); all-gather of the
+     positive lists ([R, Q, Pmax], kilobytes),
+  4. each rank streams its block once, binning every entry against the
+     merged, sorted positives and taking its own junk entries back out
      (additive counts), all-reduce(SUM) of the counts,
   5. AP / first-match rank per query from the summed counts.
 
@@ -27,8 +29,8 @@ pooling), then scored like single queries.  Re-ranking (:161-207) needs the
 whole (Q+G)^2 neighbour structure: it is gathered to rank 0 (replica work
 would only repeat it), whose scores are broadcast.
 
-Only all-gathers, one MAX and two SUM all-reduces of small count arrays and
-one broadcast of scalars cross ranks: no ring all-reduce of big tensors.
+Only all-gathers, two SUM all-reduces of small count arrays and one
+broadcast of scalars cross ranks: no ring all-reduce of big tensors.
 
 The per-stage kernels come from a backend object so the collective logic can
 be exercised with world_size > 1 on CPU (gloo) in tests; the product backend
@@ -41,14 +43,25 @@ import torch
 
 from . import ops
 
-PMAX_GUESS = 64
-
 
 def shard_range(n, rank, world):
     """Contiguous, balanced split (np.array_split semantics, subprocess.py:53)."""
     base, rem = divmod(n, world)
     start = rank * base + min(rank, rem)
     return start, start + base + (1 if rank < rem else 0)
+
+
+def max_same_id(qid, gid):
+    """The most gallery entries sharing any query's id (>= 1): an exact bound
+    on a query's positive and junk lists in that gallery (shard)."""
+    qid, gid = np.asarray(qid), np.asarray(gid)
+    if len(qid) == 0 or len(gid) == 0:
+        return 1
+    ids, cnt = np.unique(gid, return_counts=True)
+    pos = np.searchsorted(ids, qid)
+    pos = np.minimum(pos, len(ids) - 1)
+    per_q = np.where(ids[pos] == qid, cnt[pos], 0)
+    return max(1, int(per_q.max()))
 
 
 def barrier(world):
@@ -104,13 +117,22 @@ class HipBackend(object):
                                 q_planes=cls.distmat_qplanes)
 
     @staticmethod
-    def collect(dist, qid, qcam, gid, gcam, g_offset, pmax):
-        return ops.collect_positives(dist, qid, qcam, gid, gcam, g_offset, pmax)
+    def prepare(ev):
+        """Per-identity index of this rank's gallery shard (host ids, once)."""
+        return ops.MatchIndex(ev.qid_np, ev.qcam_np, ev.gid_np, ev.gcam_np)
 
     @staticmethod
-    def counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx, pos_cnt):
-        return ops.rank_counts(dist, qid, qcam, gid, gcam, g_offset, pos_d, pos_idx,
-                               pos_cnt)
+    def collect(dist, ev, state, pmax):
+        """This shard's positive lists [Q, pmax] (+ its junk lists, kept local)."""
+        pos_d, pos_idx, pos_cnt, junk = ops.collect_matches(dist, state, ev.g_offset, pmax)
+        return pos_d, pos_idx, pos_cnt, junk
+
+    @staticmethod
+    def counts(dist, ev, state, pos_d, pos_idx, pos_cnt, local):
+        """Merged + sorted positives of all shards, this shard's additive counts."""
+        sd, si, tot = ops.rank_prepare(pos_d, pos_idx, pos_cnt)
+        hist, before = ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, local)
+        return sd, si, tot, hist, before
 
     @staticmethod
     def finalize(sorted_d, pos_total, hist, before):
@@ -158,7 +180,12 @@ class ShardedEvaluator(object):
         self.g_ranges = [shard_range(self.G, r, world) for r in range(world)]
         g0, g1 = self.g_ranges[rank]
         self.g_offset = g0
-        self.pmax = PMAX_GUESS
+        # list capacity: the most same-id entries any query has in any shard
+        # -- exact, from the ids every rank holds (no collective, no overflow)
+        self.pmax = max(max_same_id(qid, gid[a:b]) for a, b in self.g_ranges)
+        self.qid_np, self.qcam_np = qid, qcam
+        self.gid_np, self.gcam_np = gid[g0:g1], gcam[g0:g1]
+        self._state = None
         dev = self.backend.device
         i32 = torch.int32
         self.qid = torch.from_numpy(qid.astype(np.int32)).to(dev)
@@ -178,24 +205,6 @@ class ShardedEvaluator(object):
         if s is not t:
             t.copy_(s)
         return t
-
-    def _collect(self, dist):
-        """Positive lists of this shard at a capacity every shard fits: one
-        all-reduce(MAX) of the largest true count; a shard re-collects only
-        when the guess was too small (pos_cnt is exact either way)."""
-        be = self.backend
-        pos = be.collect(dist, self.qid, self.qcam, self.gid, self.gcam, self.g_offset,
-                         self.pmax)
-        cnt = pos[2]
-        need = cnt.max().reshape(1).to(torch.int64) if cnt.numel() else \
-            torch.zeros(1, dtype=torch.int64, device=cnt.device)
-        need = int(self._all_reduce(need, torch.distributed.ReduceOp.MAX
-                                    if self.world > 1 else None).item())
-        if need > self.pmax:
-            self.pmax = need
-            pos = be.collect(dist, self.qid, self.qcam, self.gid, self.gcam,
-                             self.g_offset, self.pmax)
-        return pos
 
     def _gather_lists(self, *ts):
         if self.world == 1:
@@ -217,11 +226,12 @@ class ShardedEvaluator(object):
             evs[1].record()
         if use_ev:
             evs[2].record()
-        pos_d, pos_idx, pos_cnt = self._collect(dist)
+        if self._state is None:
+            self._state = be.prepare(self)
+        pos_d, pos_idx, pos_cnt, local = be.collect(dist, self, self._state, self.pmax)
         pos_d, pos_idx, pos_cnt = self._gather_lists(pos_d, pos_idx, pos_cnt)
         sorted_d, _, pos_total, hist, before = be.counts(
-            dist, self.qid, self.qcam, self.gid, self.gcam, self.g_offset, pos_d, pos_idx,
-            pos_cnt)
+            dist, self, self._state, pos_d, pos_idx, pos_cnt, local)
         self._all_reduce(hist)
         self._all_reduce(before)
         ap, valid, first = be.finalize(sorted_d, pos_total, hist, before)

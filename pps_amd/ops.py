@@ -206,6 +206,87 @@ def topk_merge(vals, idx, offsets, k):
     return out_v, out_i
 
 
+class MatchIndex(object):
+    """Per-identity index of a gallery (shard) for one query set, built once
+    from the ids (host metadata, O(G log G)): members = local gallery indices
+    sorted by (id, index); query q's identity occupies
+    members[q_beg[q]:q_end[q]].  `capacity` = the most same-id entries any
+    query has = an exact bound for its positive and junk lists."""
+
+    def __init__(self, qid, qcam, gid, gcam, device='cuda'):
+        qid, qcam = np.asarray(qid).astype(np.int64), np.asarray(qcam)
+        gid, gcam = np.asarray(gid).astype(np.int64), np.asarray(gcam)
+        order = np.lexsort((np.arange(len(gid)), gid))
+        sid = gid[order]
+        beg = np.searchsorted(sid, qid, 'left')
+        end = np.searchsorted(sid, qid, 'right')
+        self.capacity = max(1, int((end - beg).max()) if len(qid) else 1)
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32)).to(device)
+        self.members, self.q_beg, self.q_end = i32(order), i32(beg), i32(end)
+        self.qcam, self.gcam = i32(qcam), i32(gcam)
+        self.Q, self.G = len(qid), len(gid)
+
+
+def collect_matches(dist, index, g_offset=0, pmax=None):
+    """(pos_d, pos_idx, pos_cnt, junk_d, junk_idx, junk_cnt) of every query
+    from the MatchIndex (pps_collect_matches)."""
+    Q, G = dist.shape
+    if (Q, G) != (index.Q, index.G):
+        raise RuntimeError('distance matrix %s does not match the index (%d, %d)'
+                           % (tuple(dist.shape), index.Q, index.G))
+    pmax = pmax or index.capacity
+    jmax = index.capacity
+    dev = dist.device
+    pos_d = torch.empty((Q, pmax), dtype=torch.float32, device=dev)
+    pos_idx = torch.empty((Q, pmax), dtype=torch.int32, device=dev)
+    pos_cnt = torch.empty((Q,), dtype=torch.int32, device=dev)
+    junk_d = torch.empty((Q, jmax), dtype=torch.float32, device=dev)
+    junk_idx = torch.empty((Q, jmax), dtype=torch.int32, device=dev)
+    junk_cnt = torch.empty((Q,), dtype=torch.int32, device=dev)
+    call('pps_collect_matches', _dev_rows(dist, 'dist'), Q, G, _ld(dist),
+         _dev(index.qcam, 'qcam', torch.int32), _dev(index.gcam, 'gcam', torch.int32),
+         _dev(index.members, 'members', torch.int32), _dev(index.q_beg, 'q_beg', torch.int32),
+         _dev(index.q_end, 'q_end', torch.int32), int(g_offset), pmax, pos_d.data_ptr(),
+         pos_idx.data_ptr(), pos_cnt.data_ptr(), jmax, junk_d.data_ptr(), junk_idx.data_ptr(),
+         junk_cnt.data_ptr(), _stream())
+    return pos_d, pos_idx, pos_cnt, (junk_d, junk_idx, junk_cnt)
+
+
+def rank_prepare(pos_d, pos_idx, pos_cnt):
+    """Merge [R, Q, Pmax] positive lists, sorted -> (sorted_d, sorted_idx,
+    pos_total) (pps_rank_prepare)."""
+    R, Q, Pmax = pos_d.shape
+    dev = pos_d.device
+    sd = torch.empty((Q, R * Pmax), dtype=torch.float32, device=dev)
+    si = torch.empty((Q, R * Pmax), dtype=torch.int32, device=dev)
+    tot = torch.empty((Q,), dtype=torch.int32, device=dev)
+    call('pps_rank_prepare', R, Q, Pmax, _dev(pos_d, 'pos_d'), _dev(pos_idx, 'pos_idx',
+                                                                   torch.int32),
+         _dev(pos_cnt, 'pos_cnt', torch.int32), sd.data_ptr(), si.data_ptr(), tot.data_ptr(),
+         _stream())
+    return sd, si, tot
+
+
+def rank_count_stream(dist, g_offset, sorted_d, sorted_idx, pos_total, junk, hist=None,
+                      before=None):
+    """Additive (hist, before) counts of this shard's rows
+    (pps_rank_count_stream); hist/before accumulate when given."""
+    Q, G = dist.shape
+    Ptot = sorted_d.shape[1]
+    junk_d, junk_idx, junk_cnt = junk
+    dev = dist.device
+    if hist is None:
+        hist = torch.zeros((Q, Ptot), dtype=torch.int32, device=dev)
+    if before is None:
+        before = torch.zeros((Q,), dtype=torch.int32, device=dev)
+    call('pps_rank_count_stream', _dev_rows(dist, 'dist'), Q, G, _ld(dist), int(g_offset),
+         Ptot, _dev(sorted_d, 'sorted_d'), _dev(sorted_idx, 'sorted_idx', torch.int32),
+         _dev(pos_total, 'pos_total', torch.int32), junk_d.shape[1], _dev(junk_d, 'junk_d'),
+         _dev(junk_idx, 'junk_idx', torch.int32), _dev(junk_cnt, 'junk_cnt', torch.int32),
+         _dev(hist, 'hist', torch.int32), _dev(before, 'before', torch.int32), _stream())
+    return hist, before
+
+
 def collect_positives(dist, qid, qcam, gid, gcam, g_offset, Pmax):
     Q, G = dist.shape
     pos_d = torch.empty((Q, Pmax), dtype=torch.float32, device=dist.device)

@@ -53,27 +53,25 @@ def compute_dist(array1, array2, type='euclidean'):
     return d.cpu().numpy() if as_numpy else d
 
 
-_PMAX_GUESS = 64
+def _host_ids(x):
+    return x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
 
 
-def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams):
-    """Per-query (ap float64, valid int32, first_rank int32) on the device."""
-    d = _to_dev(distmat)
-    qid = _to_dev(query_ids, torch.int32)
-    gid = _to_dev(gallery_ids, torch.int32)
-    qc = _to_dev(query_cams, torch.int32)
-    gc = _to_dev(gallery_cams, torch.int32)
-    # positive-list capacity: a guess, re-collected at the exact size when a
-    # query has more (pos_cnt is exact either way, pps_abi.h) -- one small
-    # device->host read instead of a host pass over the metadata
-    pmax = _PMAX_GUESS
-    pos_d, pos_idx, pos_cnt = ops.collect_positives(d, qid, qc, gid, gc, 0, pmax)
-    need = int(pos_cnt.max().item()) if pos_cnt.numel() else 0
-    if need > pmax:
-        pmax = need
-        pos_d, pos_idx, pos_cnt = ops.collect_positives(d, qid, qc, gid, gc, 0, pmax)
-    sd, _, ptot, hist, before = ops.rank_counts(d, qid, qc, gid, gc, 0, pos_d[None],
-                                                pos_idx[None], pos_cnt[None])
+def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams, index=None):
+    """Per-query (ap float64, valid int32, first_rank int32) on the device:
+    true matches listed from a per-identity gallery index (ops.MatchIndex,
+    built from the ids unless given), then one streaming count pass over the
+    distance rows (pps_collect_matches / pps_rank_prepare /
+    pps_rank_count_stream / pps_ap_finalize)."""
+    d = distmat if isinstance(distmat, torch.Tensor) and distmat.is_cuda and \
+        distmat.dtype == torch.float32 and distmat.dim() == 2 and \
+        (distmat.shape[0] < 2 or distmat.stride(1) == 1) else _to_dev(distmat)
+    if index is None:
+        index = ops.MatchIndex(_host_ids(query_ids), _host_ids(query_cams),
+                               _host_ids(gallery_ids), _host_ids(gallery_cams), d.device)
+    pos_d, pos_idx, pos_cnt, junk = ops.collect_matches(d, index)
+    sd, si, ptot = ops.rank_prepare(pos_d[None], pos_idx[None], pos_cnt[None])
+    hist, before = ops.rank_count_stream(d, 0, sd, si, ptot, junk)
     return ops.ap_finalize(sd, ptot, hist, before)
 
 

@@ -261,3 +261,42 @@ def test_multi_query_pooling_vs_oracle():
     ref = ev.evaluate_arrays(x, ids, cams, marks)
     assert abs(res[0] - ref[0]) < 1e-9 and abs(res[2] - ref[2]) < 1e-9
     np.testing.assert_allclose(res[3], ref[3], atol=1e-12)
+
+
+def test_rank_eval_long_positive_lists_and_unaligned_rows():
+    """The streaming count pass with a positive list too long for LDS (the
+    global-memory path: 7000 matches) and rows that are not 16-byte aligned
+    (odd G: the scalar path), plus junk entries removed after the stream."""
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(8)
+    Q, G = 6, 20001
+    dist = rng.rand(Q, G).astype(np.float32)
+    dist[:, ::97] = 0.5                                   # ties
+    qid = np.array([1, 2, 3, 1, 5, 9])
+    qcam = np.array([1, 2, 1, 3, 1, 1])
+    gid = rng.randint(2, 50, size=G)
+    gid[:7500] = 1
+    gcam = rng.randint(1, 7, size=G)
+    ap, valid, first = gev.rank_eval(dist, qid, gid, qcam, gcam)
+    ref_ap, ref_valid = ev.mean_ap(dist, qid, gid, qcam, gcam, average=False)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
+    np.testing.assert_allclose(ap.cpu().numpy(), ref_ap, rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(first.cpu().numpy(),
+                                  ev.first_match_rank(dist, qid, gid, qcam, gcam))
+
+
+def test_rank_eval_padded_rows_view(golden):
+    """A [Q, G] view of a wider, 16-byte-padded buffer (row stride > G): the
+    same per-query results as the dense matrix."""
+    from pps_amd import reid_dataset_evaluator as gev
+    g = golden('market_small')
+    d = g['dist']
+    Q, G = d.shape
+    buf = torch.full((Q, G + 3), float('nan'), device='cuda')
+    buf[:, :G] = _cuda(d)
+    view = buf[:, :G]
+    a1 = [t.cpu().numpy() for t in gev.rank_eval(view, g['qid'], g['gid'], g['qcam'], g['gcam'])]
+    a2 = [t.cpu().numpy() for t in gev.rank_eval(d, g['qid'], g['gid'], g['qcam'], g['gcam'])]
+    for x, y in zip(a1, a2):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_allclose(a1[0], g['aps'], rtol=0, atol=1e-12)
