@@ -31,7 +31,7 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA
 PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # bf16 MFMA = 16x the f32 rate (~2.5 PF)
 # bf16x3 path: every f32 product costs 6 bf16 MFMA terms -> its own MFMA roof
 PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
-TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r01', 'pmc_traffic.json')
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r02', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -109,10 +109,10 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
             cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)]
         for t, qp in cands:
-            ops.compute_dist(qa, g_local, tile=t, q_planes=qp)
+            ops.compute_dist(qa, g_local, tile=t, q_planes=qp, pad_rows=True)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.compute_dist(qa, g_local, tile=t, q_planes=qp)
+            ops.compute_dist(qa, g_local, tile=t, q_planes=qp, pad_rows=True)
             e1.record()
             e1.synchronize()
             ms = e0.elapsed_time(e1)
@@ -128,18 +128,50 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
     for _ in range(reps):
         pdist.barrier(world)
         torch.cuda.synchronize()
-        res = ev.run(q_local, g_local, timed=True)
+        res = ev.run(q_local, g_local, timed=True, keep_dist=True)
         torch.cuda.synchronize()
         t_dist.append(res['t_distmat_ms'])
         t_rank.append(res['t_rank_ms'])
         t_total.append(res['t_total_ms'])
-    out = dict(distmat_tile=pdist.HipBackend.distmat_tile,
+    rank_roof = rank_roofline(ev, res['dist'])
+    del res['dist']
+    out = dict(rank_roofline=rank_roof, distmat_tile=pdist.HipBackend.distmat_tile,
                distmat_qplanes=pdist.HipBackend.distmat_qplanes,
                distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
                retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
                cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
                cmc10=float(res['cmc'][9]), G_local=gsl[1] - gsl[0])
     return out
+
+
+def rank_roofline(ev, dist, reps=20):
+    """The rank stage's dominant kernel, rank_count_stream (one pure stream
+    over the [Q, G_r] distance block), timed with HIP events on the stream it
+    runs on: algorithmic bytes = Q * G_r * 4 (every distance read once; the
+    sorted positive lists and counts are kilobytes) per launch."""
+    from pps_amd import ops
+    from pps_amd import distributed as pdist
+    state = ev._state or pdist.HipBackend.prepare(ev)
+    pd_, pi_, pc_, junk = ops.collect_matches(dist, state, ev.g_offset, ev.pmax)
+    sd, si, tot = ops.rank_prepare(pd_[None], pi_[None], pc_[None])
+    hist, before = ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, junk)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, junk, hist, before)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    Q, G = dist.shape
+    byt = Q * G * 4
+    return dict(bound='hbm', achieved=round(byt / (us * 1e-6) / 1e9, 1), peak=PEAK_HBM_GBPS,
+                unit='GB/s', frac=round(byt / (us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4),
+                traffic=_pmc_traffic('rank', ops.default_math(), None),
+                kernel='rank_count_stream_kernel (one 16-byte stream per row chunk, '
+                       'binary search + LDS histogram against the sorted positives)',
+                avg_launch_us=round(us, 2), algorithmic_bytes_per_launch=byt,
+                rows=Q, cols=G, row_stride=dist.stride(0))
 
 
 def _pmc_traffic(key, math, batch):
@@ -153,7 +185,8 @@ def _pmc_traffic(key, math, batch):
     except (OSError, ValueError):
         return None
     e = t.get(key)
-    if not e or e.get('math') != math or e.get('batch', batch) != batch:
+    if not e or (e.get('math', math) != math) or \
+            (batch is not None and e.get('batch', batch) != batch):
         return None
     return e.get('bytes_per_launch')
 
@@ -172,14 +205,33 @@ def _pmc_mfma(math, batch):
 
 
 def conv_roofline(m, x):
-    """Per-launch HIP events over one forward (same stream as the kernels)."""
+    """Per-launch durations of the GEMM launches of one forward, timed on
+    the kernels' stream by HIP events recorded INSIDE a captured hipGraph
+    (external event nodes) and read after a replay -- the launches exactly
+    as the timed graph runs them, without eager launch gaps.  Falls back to
+    eager per-launch events if event capture is unavailable."""
     timer = []
-    torch.cuda.synchronize()
-    m.forward(x, timer=timer)
-    torch.cuda.synchronize()
-    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in ('conv', 'conv_dual', 'heads'))
-    conv_flops = sum(f for _, op, f, _, _ in timer if op in ('conv', 'conv_dual', 'heads'))
-    n_launch = sum(1 for _, op, _, _, _ in timer if op in ('conv', 'conv_dual', 'heads'))
+    method = 'hipGraph replay, event nodes between launches'
+    try:
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            m.forward(x, timer=timer, timer_external=True)
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        [e0.elapsed_time(e1) for _, _, _, e0, e1 in timer]   # probe once
+    except Exception as exc:  # noqa: BLE001 -- report, then time eagerly
+        method = 'eager launches, events between launches (%s)' % type(exc).__name__
+        timer = []
+        torch.cuda.synchronize()
+        m.forward(x, timer=timer)
+        torch.cuda.synchronize()
+    gemm = ('conv', 'conv_dual', 'heads')
+    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in gemm)
+    conv_flops = sum(f for _, op, f, _, _ in timer if op in gemm)
+    n_launch = sum(1 for _, op, _, _, _ in timer if op in gemm)
+    all_ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in timer)
     per = {}
     for name, op, f, e0, e1 in timer:
         per[name] = (op, f, e0.elapsed_time(e1))
@@ -197,36 +249,78 @@ def conv_roofline(m, x):
                 launches=n_launch, flops_per_forward=conv_flops,
                 algorithmic_bytes_per_launch=round(m.bytes_per_forward() / n_launch),
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2),
+                forward_kernels_ms=round(all_ms, 3), timing=method,
                 frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
 
 
-def cpu_baseline(blobs, dist_sample=True):
-    """Oracle (CPU restatement) timed on this host's cores: bounded sample."""
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or 'unknown'
+
+
+def cpu_baseline(blobs, n_img=8, n_q=400, runs=3):
+    """SURVEY §8(d) "How the CPU path is timed": the build's CPU restatement
+    of the reference path (oracle/: the recorded reference graph in torch CPU
+    fp32, the NumPy evaluator) per stage, median of `runs` after one warm-up,
+    on this host's cores.  Workload = BASELINE configs[1] sizes: the forward
+    on n_img images 384x128; the Market-size distance matrix (3368 x 15913,
+    D=3968, SURVEY §8(d) feature recipe) in full; argsort / mAP / CMC on the
+    first n_q query rows of that matrix against the whole gallery, scaled by
+    3368 / n_q (per-query work is independent of the other queries)."""
     from oracle import evaluator as ev
     from oracle.forward import GraphForward
     threads = torch.get_num_threads()
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
     fw = GraphForward(blobs)
     rng = np.random.RandomState(0)
-    n_img = 4
     x = (rng.randn(n_img, 3, 384, 128) * 50).astype(np.float32)
-    fw(x[:1])  # warm-up
-    t0 = time.time()
-    fw(x)
-    fwd_s = time.time() - t0
-    out = dict(value=round(n_img / fwd_s, 3), unit='images/s', cores=threads, kind='port',
-               sample='%d images 384x128 through oracle/forward.py (recorded reference '
-                      'graph, torch CPU fp32, %d threads)' % (n_img, threads))
-    if dist_sample:
-        qs, gs = 1024, 4096
-        q = rng.randn(qs, D_FEAT).astype(np.float32)
-        g = rng.randn(gs, D_FEAT).astype(np.float32)
-        t0 = time.time()
-        ev.compute_dist(q, g)
-        ds = time.time() - t0
-        byt = (qs + gs) * D_FEAT * 4 + qs * gs * 4
-        out['distmat_GBps'] = round(byt / ds / 1e9, 3)
-        out['distmat_sample'] = '%dx%d D=%d NumPy fp32 (reference formula)' % (qs, gs, D_FEAT)
-    return out
+    fwd_s = med(lambda: fw(x))
+    # Market-size features, SURVEY §8(d) recipe (750 centroids + 4.0 noise, L2 norm)
+    Q, G = Q_MARKET, G_MARKET
+    qid = rng.randint(1, 751, Q)
+    gid = np.concatenate([rng.randint(1, 751, G - 2793), np.zeros(2793, int)])
+    qcam, gcam = rng.randint(1, 7, Q), rng.randint(1, 7, G)
+    cent = rng.randn(751, D_FEAT).astype(np.float32)
+    f = cent[np.concatenate([qid, gid])]
+    f += (4.0 * rng.randn(*f.shape)).astype(np.float32)
+    f /= np.linalg.norm(f, axis=1, keepdims=True)
+    qf, gf = f[:Q], f[Q:]
+    box = {}
+    dist_s = med(lambda: box.__setitem__('d', ev.compute_dist(qf, gf)))
+    d = box['d'][:n_q]
+    scale = Q / float(n_q)
+    argsort_s = med(lambda: np.argsort(d, axis=1)) * scale
+    map_s = med(lambda: ev.mean_ap(d, qid[:n_q], gid, qcam[:n_q], gcam)) * scale
+    cmc_s = med(lambda: ev.cmc(d, qid[:n_q], gid, qcam[:n_q], gcam, topk=10,
+                               first_match_break=True)) * scale
+    byt = (Q + G) * D_FEAT * 4 + Q * G * 4
+    return dict(value=round(n_img / fwd_s, 3), unit='images/s', cores=threads, kind='port',
+                sample='forward: %d images 384x128 through oracle/forward.py (the recorded '
+                       'reference graph, torch CPU fp32); retrieval: Market 3368 x 15913 x '
+                       '3968 distance in full, argsort / mAP / CMC on %d query rows scaled x%.2f; '
+                       'median of %d after 1 warm-up' % (n_img, n_q, scale, runs),
+                cpu_model=_cpu_model(), cpu_count=os.cpu_count(),
+                stages=dict(forward_img_s=round(n_img / fwd_s, 3),
+                            distmat_s=round(dist_s, 3), distmat_GBps=round(byt / dist_s / 1e9, 3),
+                            argsort_s=round(argsort_s, 3), mAP_s=round(map_s, 3),
+                            cmc_s=round(cmc_s, 3),
+                            retrieval_total_s=round(dist_s + argsort_s + map_s + cmc_s, 3)))
 
 
 def main():
@@ -338,6 +432,7 @@ def main():
         'retrieval_ms': round(ret['retrieval_ms'], 3),
         'mAP_synthetic': round(ret['mAP'], 6), 'cmc1_synthetic': round(ret['cmc1'], 6),
         'roofline': roof,
+        'roofline_rank': ret['rank_roofline'],
         'roofline_distmat': dict(
             bound='mfma', achieved=round(dist_tflops, 2),
             peak=round(PEAK_X3_TFLOPS if dist_math == 'x3' else PEAK_FP32_MFMA_TFLOPS, 1),

@@ -114,7 +114,7 @@ class HipBackend(object):
     @classmethod
     def distmat(cls, q, g, metric):
         return ops.compute_dist(q, g, metric=metric, tile=cls.distmat_tile,
-                                q_planes=cls.distmat_qplanes)
+                                q_planes=cls.distmat_qplanes, pad_rows=True)
 
     @staticmethod
     def prepare(ev):
@@ -156,7 +156,7 @@ class HipBackend(object):
 
     @staticmethod
     def re_ranking(q_g, q_q, g_g):
-        return ops.re_ranking(q_g, q_q, g_g)
+        return ops.re_ranking(q_g.contiguous(), q_q.contiguous(), g_g.contiguous())
 
     @staticmethod
     def rank_eval(dist, qid, gid, qcam, gcam):
@@ -211,7 +211,7 @@ class ShardedEvaluator(object):
             return [t[None] for t in ts]
         return [all_gather_rows(t[None], [1] * self.world) for t in ts]
 
-    def run(self, q_local, g_local, timed=False, dist=None):
+    def run(self, q_local, g_local, timed=False, dist=None, keep_dist=False):
         be = self.backend
         use_ev = timed and be.device == 'cuda'
         if use_ev:
@@ -247,6 +247,8 @@ class ShardedEvaluator(object):
         np.add.at(hits, fr[fr < self.topk], 1)
         cmc = np.cumsum(hits) / max(nvalid, 1)
         res = dict(mAP=mAP, cmc=cmc, ap=ap, valid=valid, first_rank=first)
+        if keep_dist:
+            res['dist'] = dist
         if use_ev:
             res['t_distmat_ms'] = evs[1].elapsed_time(evs[2])
             res['t_rank_ms'] = evs[2].elapsed_time(evs[3])

@@ -517,9 +517,11 @@ class PPSModel(object):
             ops.l2_normalize(bufs[L['input']], y)
             bufs[L['output']] = y
 
-    def forward(self, x, out=None, timer=None):
+    def forward(self, x, out=None, timer=None, timer_external=False):
         """Run the plan.  `timer`, if a list, receives (layer, op, flops,
-        start_event, end_event) per layer, recorded on the current stream."""
+        start_event, end_event) per layer, recorded on the current stream
+        (timer_external: events that may be recorded inside a hipGraph
+        capture, so a graph replay times each launch)."""
         assert x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
         assert x.shape[3] == 4, 'input must be NHWC with 4 channels (see preprocess)'
         N, H, W, _ = x.shape
@@ -529,8 +531,8 @@ class PPSModel(object):
         bufs['data'] = x
         for L in self.layers:
             if timer is not None:
-                ev0 = torch.cuda.Event(enable_timing=True)
-                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0 = torch.cuda.Event(enable_timing=True, external=timer_external)
+                ev1 = torch.cuda.Event(enable_timing=True, external=timer_external)
                 ev0.record()
             self._run(L, bufs, out)
             if timer is not None:

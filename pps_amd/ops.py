@@ -118,8 +118,16 @@ class GalleryIndex(object):
 SELF_TILES = (0, TILE_P_FIRST, TILE_P_FIRST + 7, TILE_P16_FIRST, TILE_P16_FIRST + 7)
 
 
+def dist_buffer(Q, G, device):
+    """[Q, G] float32 view of a buffer whose rows are padded to a multiple of
+    4 floats: every row starts 16-byte aligned, so the distance epilogue
+    stores whole 16-byte vectors and the rank kernels stream 16-byte loads."""
+    ld = (G + 3) // 4 * 4
+    return torch.empty((Q, ld), dtype=torch.float32, device=device)[:, :G]
+
+
 def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes=None,
-                 symmetric=None):
+                 symmetric=None, pad_rows=False):
     """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244).
     g may be a GalleryIndex (then the x3 kernel runs on its prepared planes).
     q_planes (x3): also split the queries into bf16x3 planes first so the
@@ -127,6 +135,8 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     tiles only).  Same bits either way; measured at the Market shape it is
     not faster (scripts/dist_probe.py: the split in the K loop is hidden),
     so None = off.
+    pad_rows: return a [Q, G] view of a buffer with 16-byte-aligned rows
+    (dist_buffer) instead of a dense matrix.
     symmetric (x3): a self-distance (q and g the same rows, e.g.
     compute_dist(g, g) of re-ranking) computed from the upper-triangle tiles
     and mirrored (pps_distmat_x3_self, half the work); None = whenever q IS
@@ -138,7 +148,8 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     Q, D = q.shape
     G = g.shape[0]
     if out is None:
-        out = torch.empty((Q, G), dtype=torch.float32, device=q.device)
+        out = dist_buffer(Q, G, q.device) if pad_rows else \
+            torch.empty((Q, G), dtype=torch.float32, device=q.device)
     if tuple(out.shape) != (Q, G):
         raise RuntimeError('out must be [%d, %d], got %s' % (Q, G, tuple(out.shape)))
     if math == 'f32':

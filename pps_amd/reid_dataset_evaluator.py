@@ -171,7 +171,7 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
     with measure_time('Computing distance...', verbose):
         if verbose:
             print('Array size: ', tuple(qf.shape), tuple(gf.shape))
-        q_g = ops.compute_dist(qf, gf, metric=metric)
+        q_g = ops.compute_dist(qf, gf, metric=metric, pad_rows=True)
     with measure_time('Computing scores...', verbose):
         mAP, cmc_scores = compute_score(q_g, ids[q_inds], ids[g_inds], cams[q_inds],
                                         cams[g_inds])
@@ -188,7 +188,7 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         pooled = ops.group_mean(feat, [mq_rows[v] for v in groups.values()])
         keys = np.array(list(groups.keys()))
         with measure_time('Multi Query, Computing distance...', verbose):
-            mq_g = ops.compute_dist(pooled, gf, metric=metric)
+            mq_g = ops.compute_dist(pooled, gf, metric=metric, pad_rows=True)
         with measure_time('Multi Query, Computing scores...', verbose):
             mq_mAP, mq_cmc = compute_score(mq_g, keys[:, 0], ids[g_inds], keys[:, 1],
                                            cams[g_inds])
@@ -201,7 +201,7 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         with measure_time('Re-ranking distance...', verbose):
             q_q = ops.compute_dist(qf, qf, metric=metric)
             g_g = ops.compute_dist(gf, gf, metric=metric)
-            rr = ops.re_ranking(q_g, q_q, g_g)
+            rr = ops.re_ranking(q_g.contiguous(), q_q, g_g)
         with measure_time('Computing scores for re-ranked distance...', verbose):
             mAP, cmc_scores = compute_score(rr, ids[q_inds], ids[g_inds], cams[q_inds],
                                             cams[g_inds])
@@ -211,7 +211,7 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         if mq_inds.any():
             with measure_time('Multi Query, Re-ranking distance...', verbose):
                 mq_mq = ops.compute_dist(pooled, pooled, metric=metric)
-                rr_mq = ops.re_ranking(mq_g, mq_mq, g_g)
+                rr_mq = ops.re_ranking(mq_g.contiguous(), mq_mq, g_g)
             with measure_time('Multi Query, Computing scores for re-ranked distance...',
                               verbose):
                 mq_mAP, mq_cmc = compute_score(rr_mq, keys[:, 0], ids[g_inds], keys[:, 1],
