@@ -153,13 +153,13 @@ def rank_roofline(ev, dist, reps=20):
     from pps_amd import distributed as pdist
     state = ev._state or pdist.HipBackend.prepare(ev)
     pd_, pi_, pc_, junk = ops.collect_matches(dist, state, ev.g_offset, ev.pmax)
-    sd, si, tot = ops.rank_prepare(pd_[None], pi_[None], pc_[None])
-    hist, before = ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, junk)
+    sp = ops.rank_prepare(pd_[None], pi_[None], pc_[None])
+    hist, before = ops.rank_count_stream(dist, ev.g_offset, sp, junk)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, junk, hist, before)
+        ops.rank_count_stream(dist, ev.g_offset, sp, junk, hist, before)
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps

@@ -169,7 +169,9 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
  *    per query instead of a scan of G ids.
  * b) pps_rank_prepare: merge R shards' lists [R][Q][Pmax] and sort by
  *    (distance, global index) -> sorted_d / sorted_idx [Q][R*Pmax] (padding
- *    +inf / -1), pos_total [Q].  R*Pmax <= 8192.
+ *    +inf / -1), pos_total [Q], and the query's bin-lookup cells
+ *    [Q][pps_rank_cells()] (int32, 16-byte aligned) that c) reads.
+ *    R*Pmax <= 8192.
  * c) pps_rank_count_stream: for this shard's rows, hist[q][p] += #entries
  *    with p = first positive d_p >= d, before[q] += #entries ordered before
  *    the first positive, over all entries of the row minus this shard's junk
@@ -182,15 +184,16 @@ int pps_collect_matches(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                         const int32_t* q_beg, const int32_t* q_end, int64_t g_offset,
                         int Pmax, float* pos_d, int32_t* pos_idx, int32_t* pos_cnt, int Jmax,
                         float* junk_d, int32_t* junk_idx, int32_t* junk_cnt, void* stream);
+int pps_rank_cells(void);
 int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
                      const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
-                     int32_t* pos_total, void* stream);
+                     int32_t* pos_total, int32_t* cells, void* stream);
 int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                           int64_t g_offset, int Ptot, const float* sorted_d,
-                          const int32_t* sorted_idx, const int32_t* pos_total, int Jmax,
-                          const float* junk_d, const int32_t* junk_idx,
-                          const int32_t* junk_cnt, int32_t* hist, int32_t* before,
-                          void* stream);
+                          const int32_t* sorted_idx, const int32_t* pos_total,
+                          const int32_t* cells, int Jmax, const float* junk_d,
+                          const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
+                          int32_t* before, void* stream);
 
 /* Stable per-row top-k (k <= 1024) of a distance matrix, ascending, ties by
  * gallery index.  Replaces the `np.argsort(distmat, axis=1)[:, :k]` rank

@@ -39,9 +39,10 @@ SIGNATURES = {
     'pps_collect_matches': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                             c_i64, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                             c_ptr],
-    'pps_rank_prepare': [c_int, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_rank_prepare': [c_int, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                         c_ptr],
     'pps_rank_count_stream': [c_ptr, c_i64, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr,
-                              c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+                              c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                         c_ptr],
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
@@ -96,6 +97,7 @@ SIGNATURES = {
 EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
     'pps_gemm_num_tiles': ([], ctypes.c_int),
+    'pps_rank_cells': ([], ctypes.c_int),
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),

@@ -42,10 +42,10 @@ int collect_matches(const float*, int64_t, int64_t, const int32_t*, const int32_
                     const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
                     int32_t*, int32_t*, int, float*, int32_t*, int32_t*, hipStream_t);
 int rank_prepare(int, int64_t, int, const float*, const int32_t*, const int32_t*, float*,
-                 int32_t*, int32_t*, hipStream_t);
+                 int32_t*, int32_t*, int32_t*, hipStream_t);
 int rank_count_stream(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
-                      const int32_t*, const int32_t*, int, const float*, const int32_t*,
-                      const int32_t*, int32_t*, int32_t*, hipStream_t);
+                      const int32_t*, const int32_t*, const int32_t*, int, const float*,
+                      const int32_t*, const int32_t*, int32_t*, int32_t*, hipStream_t);
 int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int, double,
            void*, size_t, float*, hipStream_t);
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
@@ -286,11 +286,14 @@ int pps_collect_matches(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                          as_stream(stream));
 }
 
+int pps_rank_cells(void) { return 1024; }
+
 int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
                      const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
-                     int32_t* pos_total, void* stream) {
-  PPS_ENFORCE(pos_d && pos_idx && pos_cnt && sorted_d && sorted_idx && pos_total,
+                     int32_t* pos_total, int32_t* cells, void* stream) {
+  PPS_ENFORCE(pos_d && pos_idx && pos_cnt && sorted_d && sorted_idx && pos_total && cells,
               "null pointer");
+  PPS_ENFORCE(((uintptr_t)cells & 15) == 0, "cells must be 16-byte aligned");
   PPS_ENFORCE(R >= 1 && R <= kMergeMaxLists, "R must be in [1, 64]");
   PPS_ENFORCE(Q >= 0 && Pmax > 0, "bad shape");
   if ((int64_t)R * Pmax > 8192) {
@@ -299,22 +302,24 @@ int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32
     return PPS_ERR_CAPACITY;
   }
   return rank_prepare(R, Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total,
-                      as_stream(stream));
+                      cells, as_stream(stream));
 }
 
 int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                           int64_t g_offset, int Ptot, const float* sorted_d,
-                          const int32_t* sorted_idx, const int32_t* pos_total, int Jmax,
-                          const float* junk_d, const int32_t* junk_idx,
-                          const int32_t* junk_cnt, int32_t* hist, int32_t* before,
-                          void* stream) {
-  PPS_ENFORCE(dist && sorted_d && sorted_idx && pos_total && junk_d && junk_idx && junk_cnt &&
-                  hist && before,
+                          const int32_t* sorted_idx, const int32_t* pos_total,
+                          const int32_t* cells, int Jmax, const float* junk_d,
+                          const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
+                          int32_t* before, void* stream) {
+  PPS_ENFORCE(dist && sorted_d && sorted_idx && pos_total && cells && junk_d && junk_idx &&
+                  junk_cnt && hist && before,
               "null pointer");
+  PPS_ENFORCE(((uintptr_t)cells & 15) == 0, "cells must be 16-byte aligned");
   PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Ptot > 0 && Jmax > 0, "bad shape");
-  PPS_ENFORCE((G + 4095) / 4096 <= 65535, "G too large for the chunk grid");
+  PPS_ENFORCE(G / 1024 < 65535, "G too large for the chunk grid");
   return rank_count_stream(dist, Q, G, ldd, g_offset, Ptot, sorted_d, sorted_idx, pos_total,
-                           Jmax, junk_d, junk_idx, junk_cnt, hist, before, as_stream(stream));
+                           cells, Jmax, junk_d, junk_idx, junk_cnt, hist, before,
+                           as_stream(stream));
 }
 
 int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* pos_total,

@@ -359,20 +359,39 @@ int collect_matches(const float* dist, int64_t Q, int64_t ldd, const int32_t* qc
   return PPS_OK;
 }
 
+// Bin-lookup cells of a query (used by c)): (df, dmax] of its sorted positives
+// cut into kStreamCells equal cells by a monotone map; cells[c] = the number
+// of positives whose cell is below c, | kCellDirty if a positive lies in c.
+constexpr int kStreamCells = 1024;
+constexpr int kCellDirty = 1 << 30;
+__device__ inline float cell_scale(float df, float dmax) {
+  const float span = dmax - df;
+  const float inv = span > 0.f ? (float)kStreamCells / span : 0.f;
+  return isfinite(inv) ? inv : 0.f;  // a denormal span: one cell
+}
+__device__ inline int cell_of(float d, float df, float inv) {
+  const float t = (d - df) * inv;
+  const int c = t < (float)(kStreamCells - 1) ? (int)t : kStreamCells - 1;
+  return c > 0 ? c : 0;
+}
+
 // b) rank_prepare: merge the R shards' positive lists of a query and sort
 // them by (distance, global index) -- rank by counting in LDS (one block per
-// query; tens of entries on real splits).
+// query; tens of entries on real splits) -- and build its bin-lookup cells.
 __global__ void rank_prepare_kernel(int R, int64_t Q, int Pmax, const float* __restrict__ pos_d,
                                     const int32_t* __restrict__ pos_idx,
                                     const int32_t* __restrict__ pos_cnt,
                                     float* __restrict__ sorted_d,
                                     int32_t* __restrict__ sorted_idx,
-                                    int32_t* __restrict__ pos_total) {
+                                    int32_t* __restrict__ pos_total,
+                                    int32_t* __restrict__ cells) {
   const int64_t q = blockIdx.x;
   const int Ptot = R * Pmax;
   extern __shared__ int plds[];
   float* ud = reinterpret_cast<float*>(plds);
   int* ui = plds + Ptot;
+  float* sd = reinterpret_cast<float*>(plds + 2 * Ptot);
+  int* ct = plds + 3 * Ptot;
   __shared__ int offs[kMergeMaxLists + 1];
   if (threadIdx.x == 0) {
     int o = 0;
@@ -400,21 +419,35 @@ __global__ void rank_prepare_kernel(int R, int64_t Q, int Pmax, const float* __r
     for (int o = 0; o < P; ++o) rk += key_less(ud[o], ui[o], d, ix) ? 1 : 0;
     sorted_d[q * Ptot + rk] = d;
     sorted_idx[q * Ptot + rk] = ix;
+    sd[rk] = d;
   }
   for (int p = P + threadIdx.x; p < Ptot; p += blockDim.x) {
     sorted_d[q * Ptot + p] = INFINITY;
     sorted_idx[q * Ptot + p] = -1;
   }
   if (threadIdx.x == 0) pos_total[q] = P;
+  if (P == 0) return;  // uniform: the count pass skips this query
+  __syncthreads();
+  const float df = sd[0], inv = cell_scale(df, sd[P - 1]);
+  for (int p = threadIdx.x; p < P; p += blockDim.x) ct[p] = cell_of(sd[p], df, inv);
+  __syncthreads();
+  for (int c = threadIdx.x; c < kStreamCells; c += blockDim.x) {
+    int lo = 0, hi = P;  // first positive whose cell is >= c (ct is non-decreasing)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ct[mid] < c) lo = mid + 1; else hi = mid;
+    }
+    cells[q * kStreamCells + c] = lo | ((lo < P && ct[lo] == c) ? kCellDirty : 0);
+  }
 }
 
 int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
                  const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
-                 int32_t* pos_total, hipStream_t st) {
+                 int32_t* pos_total, int32_t* cells, hipStream_t st) {
   if (Q <= 0) return PPS_OK;
-  const size_t lds = (size_t)2 * R * Pmax * sizeof(int);
+  const size_t lds = (size_t)4 * R * Pmax * sizeof(int);
   hipLaunchKernelGGL(rank_prepare_kernel, dim3((unsigned)Q), dim3(kEvalThreads), lds, st, R,
-                     Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total);
+                     Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, cells);
   PPS_CHECK_LAUNCH("rank_prepare_kernel");
   return PPS_OK;
 }
@@ -427,8 +460,15 @@ int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* 
 // adds its counts to hist / before with one global atomic per non-empty bin.
 // KLDS = false: positive lists too long for LDS are searched in global memory
 // (L2) and binned with global atomics -- no capacity limit.
+#ifndef RANK_STREAM_VARIANT
+#define RANK_STREAM_VARIANT 0  // probes only (scripts/rank_probe.py): 1 = stream + compare,
+                               // 2 = + binary search, no histogram atomics
+#endif
+#ifndef RANK_STREAM_U
+#define RANK_STREAM_U 8
+#endif
 constexpr int kStreamThreads = 256;
-constexpr int kStreamU = 4;                                  // float4 per thread in flight
+constexpr int kStreamU = RANK_STREAM_U;                      // float4 per thread in flight
 constexpr int kStreamChunk = kStreamThreads * kStreamU * 4;  // 4096 entries per block
 constexpr int kStreamLdsCap = 6144;                          // positives held in LDS
 
@@ -437,7 +477,8 @@ __global__ void __launch_bounds__(kStreamThreads)
 rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
                          int64_t g_offset, int Ptot, const float* __restrict__ sorted_d,
                          const int32_t* __restrict__ sorted_idx,
-                         const int32_t* __restrict__ pos_total, int Jmax,
+                         const int32_t* __restrict__ pos_total,
+                         const int32_t* __restrict__ cells, int Jmax,
                          const float* __restrict__ junk_d,
                          const int32_t* __restrict__ junk_idx,
                          const int32_t* __restrict__ junk_cnt, int32_t* __restrict__ hist,
@@ -448,26 +489,41 @@ rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
   extern __shared__ int slds[];
   const float* gsd = sorted_d + q * Ptot;
   int32_t* ghist = hist + q * Ptot;
+  const int Pa = (P + 3) & ~3;  // keeps the cell arrays 16-byte aligned
   float* sd = reinterpret_cast<float*>(slds);
-  int* hs = slds + (KLDS ? P : 0);
+  int* hs = slds + (KLDS ? Pa : 0);
+  int* cs = slds + (KLDS ? 2 * Pa : 0);  // bin-lookup cells (rank_prepare)
+  int* cc = cs + kStreamCells;          // per-cell entry counts (clean cells)
   __shared__ int red[kStreamThreads / 64];
+  const float df = gsd[0], dmax = gsd[P - 1];
+  // Binning without a per-entry binary search: a "clean" cell holds no
+  // positive, so every entry in it has bin cs[c] exactly and only bumps the
+  // cell's counter cc[c] (1024 addresses: a wave's LDS atomics rarely collide;
+  // with one counter per positive they serialised).  A cell holding
+  // positives finishes the lower_bound with a short forward scan from cs[c].
+  // The clean-cell counts are folded into the positives' bins once per block.
+  const float inv = cell_scale(df, dmax);
   if (KLDS) {
     for (int p = threadIdx.x; p < P; p += kStreamThreads) {
       sd[p] = gsd[p];
       hs[p] = 0;
     }
+    const int4* gc = reinterpret_cast<const int4*>(cells + q * kStreamCells);
+    for (int c = threadIdx.x; c < kStreamCells / 4; c += kStreamThreads) {
+      reinterpret_cast<int4*>(cs)[c] = gc[c];
+      reinterpret_cast<int4*>(cc)[c] = make_int4(0, 0, 0, 0);
+    }
     __syncthreads();
   }
   const float* S = KLDS ? sd : gsd;
-  const float dmax = S[P - 1], df = S[0];
   const int64_t idf = sorted_idx[q * Ptot];
-  auto bin = [&](float d) {
+  auto bin = [&](float d) {  // lower_bound(S, d) for d <= dmax: < P
     int lo = 0, hi = P;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (S[mid] < d) lo = mid + 1; else hi = mid;
     }
-    return lo;  // < P because d <= dmax
+    return lo;
   };
   auto add = [&](int b, int v) {
     if (KLDS) atomicAdd(&hs[b], v); else atomicAdd(&ghist[b], v);
@@ -475,8 +531,28 @@ rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
   int nb = 0;
   auto visit = [&](int64_t i, float d) {
     if (d <= dmax) {
-      add(bin(d), 1);
-      nb += (d < df || (d == df && g_offset + i < idf)) ? 1 : 0;
+#if RANK_STREAM_VARIANT == 1
+      nb += 1;
+#elif RANK_STREAM_VARIANT == 2
+      nb += bin(d);
+#else
+      if (d <= df) {  // bin 0; the only entries that can precede the first positive
+        add(0, 1);
+        nb += (d < df || g_offset + i < idf) ? 1 : 0;
+      } else if (KLDS) {
+        const int c = cell_of(d, df, inv);
+        const int e = cs[c];
+        if (e & kCellDirty) {
+          int b = e & (kCellDirty - 1);
+          while (S[b] < d) ++b;
+          atomicAdd(&hs[b], 1);
+        } else {
+          atomicAdd(&cc[c], 1);
+        }
+      } else {
+        add(bin(d), 1);
+      }
+#endif
     }
   };
   const int64_t c0 = (int64_t)blockIdx.y * kStreamChunk;
@@ -529,6 +605,9 @@ rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nb;
   __syncthreads();
   if (KLDS) {
+    for (int c = threadIdx.x; c < kStreamCells; c += kStreamThreads)
+      if (cc[c]) atomicAdd(&hs[cs[c] & (kCellDirty - 1)], cc[c]);
+    __syncthreads();
     for (int p = threadIdx.x; p < P; p += kStreamThreads)
       if (hs[p]) atomicAdd(&ghist[p], hs[p]);
   }
@@ -541,7 +620,7 @@ rank_count_stream_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd,
 
 int rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd, int64_t g_offset,
                       int Ptot, const float* sorted_d, const int32_t* sorted_idx,
-                      const int32_t* pos_total, int Jmax, const float* junk_d,
+                      const int32_t* pos_total, const int32_t* cells, int Jmax, const float* junk_d,
                       const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
                       int32_t* before, hipStream_t st) {
   if (Q <= 0 || G <= 0) return PPS_OK;
@@ -552,14 +631,16 @@ int rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd, int6
     const float* d = dist + q0 * ldd;
     if (Ptot <= kStreamLdsCap) {
       hipLaunchKernelGGL(rank_count_stream_kernel<true>, grid, dim3(kStreamThreads),
-                         (size_t)2 * Ptot * sizeof(int), st, d, G, ldd, g_offset, Ptot,
-                         sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot, pos_total + q0, Jmax,
-                         junk_d + q0 * Jmax, junk_idx + q0 * Jmax, junk_cnt + q0,
+                         (size_t)(2 * ((Ptot + 3) & ~3) + 2 * kStreamCells) * sizeof(int), st,
+                         d, G, ldd,
+                         g_offset, Ptot,
+                         sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot, pos_total + q0,
+                         cells + q0 * kStreamCells, Jmax, junk_d + q0 * Jmax, junk_idx + q0 * Jmax, junk_cnt + q0,
                          hist + q0 * Ptot, before + q0);
     } else {
       hipLaunchKernelGGL(rank_count_stream_kernel<false>, grid, dim3(kStreamThreads), 0, st, d,
                          G, ldd, g_offset, Ptot, sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot,
-                         pos_total + q0, Jmax, junk_d + q0 * Jmax, junk_idx + q0 * Jmax,
+                         pos_total + q0, cells + q0 * kStreamCells, Jmax, junk_d + q0 * Jmax, junk_idx + q0 * Jmax,
                          junk_cnt + q0, hist + q0 * Ptot, before + q0);
     }
     PPS_CHECK_LAUNCH("rank_count_stream_kernel");

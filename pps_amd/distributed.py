@@ -130,9 +130,9 @@ class HipBackend(object):
     @staticmethod
     def counts(dist, ev, state, pos_d, pos_idx, pos_cnt, local):
         """Merged + sorted positives of all shards, this shard's additive counts."""
-        sd, si, tot = ops.rank_prepare(pos_d, pos_idx, pos_cnt)
-        hist, before = ops.rank_count_stream(dist, ev.g_offset, sd, si, tot, local)
-        return sd, si, tot, hist, before
+        sp = ops.rank_prepare(pos_d, pos_idx, pos_cnt)
+        hist, before = ops.rank_count_stream(dist, ev.g_offset, sp, local)
+        return sp.sorted_d, sp.sorted_idx, sp.pos_total, hist, before
 
     @staticmethod
     def finalize(sorted_d, pos_total, hist, before):

@@ -263,26 +263,40 @@ def collect_matches(dist, index, g_offset=0, pmax=None):
     return pos_d, pos_idx, pos_cnt, (junk_d, junk_idx, junk_cnt)
 
 
+class SortedPositives(object):
+    """Merged, sorted positive lists of a query set (pps_rank_prepare):
+    sorted_d / sorted_idx [Q, Ptot], pos_total [Q], bin-lookup cells."""
+
+    def __init__(self, sorted_d, sorted_idx, pos_total, cells):
+        self.sorted_d, self.sorted_idx, self.pos_total = sorted_d, sorted_idx, pos_total
+        self.cells = cells
+
+    def __iter__(self):   # (sorted_d, sorted_idx, pos_total), as the old triple
+        return iter((self.sorted_d, self.sorted_idx, self.pos_total))
+
+
 def rank_prepare(pos_d, pos_idx, pos_cnt):
-    """Merge [R, Q, Pmax] positive lists, sorted -> (sorted_d, sorted_idx,
-    pos_total) (pps_rank_prepare)."""
+    """Merge [R, Q, Pmax] positive lists, sorted -> SortedPositives
+    (pps_rank_prepare)."""
     R, Q, Pmax = pos_d.shape
     dev = pos_d.device
     sd = torch.empty((Q, R * Pmax), dtype=torch.float32, device=dev)
     si = torch.empty((Q, R * Pmax), dtype=torch.int32, device=dev)
     tot = torch.empty((Q,), dtype=torch.int32, device=dev)
+    cells = torch.empty((Q, _lib.lib().pps_rank_cells()), dtype=torch.int32, device=dev)
     call('pps_rank_prepare', R, Q, Pmax, _dev(pos_d, 'pos_d'), _dev(pos_idx, 'pos_idx',
                                                                    torch.int32),
          _dev(pos_cnt, 'pos_cnt', torch.int32), sd.data_ptr(), si.data_ptr(), tot.data_ptr(),
-         _stream())
-    return sd, si, tot
+         cells.data_ptr(), _stream())
+    return SortedPositives(sd, si, tot, cells)
 
 
-def rank_count_stream(dist, g_offset, sorted_d, sorted_idx, pos_total, junk, hist=None,
-                      before=None):
-    """Additive (hist, before) counts of this shard's rows
-    (pps_rank_count_stream); hist/before accumulate when given."""
+def rank_count_stream(dist, g_offset, sp, junk, hist=None, before=None):
+    """Additive (hist, before) counts of this shard's rows against the
+    SortedPositives sp (pps_rank_count_stream); hist/before accumulate when
+    given."""
     Q, G = dist.shape
+    sorted_d, sorted_idx, pos_total = sp.sorted_d, sp.sorted_idx, sp.pos_total
     Ptot = sorted_d.shape[1]
     junk_d, junk_idx, junk_cnt = junk
     dev = dist.device
@@ -292,7 +306,8 @@ def rank_count_stream(dist, g_offset, sorted_d, sorted_idx, pos_total, junk, his
         before = torch.zeros((Q,), dtype=torch.int32, device=dev)
     call('pps_rank_count_stream', _dev_rows(dist, 'dist'), Q, G, _ld(dist), int(g_offset),
          Ptot, _dev(sorted_d, 'sorted_d'), _dev(sorted_idx, 'sorted_idx', torch.int32),
-         _dev(pos_total, 'pos_total', torch.int32), junk_d.shape[1], _dev(junk_d, 'junk_d'),
+         _dev(pos_total, 'pos_total', torch.int32), _dev(sp.cells, 'cells', torch.int32),
+         junk_d.shape[1], _dev(junk_d, 'junk_d'),
          _dev(junk_idx, 'junk_idx', torch.int32), _dev(junk_cnt, 'junk_cnt', torch.int32),
          _dev(hist, 'hist', torch.int32), _dev(before, 'before', torch.int32), _stream())
     return hist, before

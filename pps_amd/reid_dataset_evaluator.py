@@ -70,9 +70,9 @@ def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams, index=N
         index = ops.MatchIndex(_host_ids(query_ids), _host_ids(query_cams),
                                _host_ids(gallery_ids), _host_ids(gallery_cams), d.device)
     pos_d, pos_idx, pos_cnt, junk = ops.collect_matches(d, index)
-    sd, si, ptot = ops.rank_prepare(pos_d[None], pos_idx[None], pos_cnt[None])
-    hist, before = ops.rank_count_stream(d, 0, sd, si, ptot, junk)
-    return ops.ap_finalize(sd, ptot, hist, before)
+    sp = ops.rank_prepare(pos_d[None], pos_idx[None], pos_cnt[None])
+    hist, before = ops.rank_count_stream(d, 0, sp, junk)
+    return ops.ap_finalize(sp.sorted_d, sp.pos_total, hist, before)
 
 
 def _np(x):
