@@ -232,6 +232,76 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
   }
 }
 
+// The distance epilogue staged through LDS (not for self-distance tiles,
+// which also write their mirror): the dot products are parked as a
+// [BM][BN+4] f32 tile and the workgroup then writes whole output rows, 16 B
+// per lane with consecutive lanes on consecutive columns, so each store
+// instruction covers full 64-256 B row segments instead of 16-B pieces of 16-32
+// rows (PMC: the direct epilogue wrote 1.56x the matrix).  Same per-element
+// formulas as dist_epilogue_t (identical bits).
+template <int BM, int BN, int WM, int WN, int S>
+__device__ inline void dist_epilogue_lds(const GemmParams& p,
+                                         typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                         unsigned char* lds, int m0, int n0, int wm, int wn,
+                                         int r32, int h) {
+  constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
+  constexpr int LD = BN + 4;
+  constexpr int NT = 64 * WM * WN;
+  float* t = reinterpret_cast<float*>(lds);
+  __syncthreads();  // every wave is done reading the last stage
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * (BM / WM) + i * S + r32;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cb = wn * (BN / WN) + j * S + 4 * h;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
+      }
+    }
+  }
+  __syncthreads();
+  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0, nrem = p.Ncol - n0;
+  const bool vec = (p.ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+    const int row = idx / C4, col = 4 * (idx - row * C4);
+    if (row >= mrem || col >= nrem) continue;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
+    const float qn = p.norm_a[m0 + row];
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gn = col + e < nrem ? p.norm_b[n0 + col + e] : 0.f;
+      const float dot = a[e];
+      float d;
+      if (p.metric == PPS_METRIC_COSINE) {
+        const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
+        d = 1.f - dot / den;
+      } else {
+        d = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
+        if (p.metric == PPS_METRIC_EUCLIDEAN) d = sqrtf(d);
+      }
+      if (p.zero_diag && m0 + row == n0 + col + e) d = 0.f;
+      v[e] = d;
+    }
+    float* o = out + row * ldo + col;
+    if (vec && col + 3 < nrem) {
+      *reinterpret_cast<f32x4*>(o) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < nrem) o[e] = v[e];
+    }
+  }
+}
+
 // Distance epilogue on transposed accumulators: same formulas as
 // dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
 template <int BM, int BN, int WM, int WN, int S = 32>
@@ -359,6 +429,11 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool LDSEPI = X3P_LDSEPI && !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
                           lds_epi_bytes<BM, BN>() <= 160 * 1024 &&
                           !(BM == 192 && BN == 128 && NW == 8);
+#ifndef X3P_DISTLDS
+#define X3P_DISTLDS 1
+#endif
+  constexpr bool DISTLDS = X3P_DISTLDS && (EPI & EPI_DIST) != 0 &&
+                           lds_epi_bytes<BM, BN>() <= NS * STAGE;
   constexpr int LDS_BYTES =
       (LDSEPI && lds_epi_bytes<BM, BN>() > NS * STAGE) ? lds_epi_bytes<BM, BN>() : NS * STAGE;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
@@ -718,7 +793,12 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
 
-  if constexpr ((EPI & EPI_DIST) != 0)
+  if constexpr (DISTLDS) {
+    if (p.sym)
+      dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
+    else
+      dist_epilogue_lds<BM, BN, WM, WN, S>(p, acc, lds, m0, n0, wm, wn, r32, h);
+  } else if constexpr ((EPI & EPI_DIST) != 0)
     dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
   else if constexpr (LDSEPI)
     conv_epilogue_lds<EPI, BM, BN, WM, WN, S>(p, acc, lds, batch, kslice, m0, n0, wm, wn, r32, h);

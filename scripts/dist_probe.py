@@ -15,7 +15,8 @@ def main():
     q = torch.nn.functional.normalize(torch.randn(Q, D, device='cuda'), dim=1)
     g = torch.nn.functional.normalize(torch.randn(G, D, device='cuda'), dim=1)
     idx = ops.GalleryIndex(g)
-    out = torch.empty(Q, G, device='cuda')
+    out = ops.dist_buffer(Q, G, 'cuda') if os.environ.get('PAD', '1') == '1' else \
+        torch.empty(Q, G, device='cuda')
     flops = 2.0 * Q * G * D
     for tile in range(ops.TILE_P_FIRST, ops.num_tiles() + 1):
         row = []
