@@ -1,4 +1,4 @@
-# Build libpps_hip.so (gfx950) and the oracle's C restatement.
+# Build libpps_hip.so (gfx950): the HIP kernels + the C ABI (include/pps_abi.h).
 # `python -c "import __graft_entry__ as g; g.build()"` drives the same recipe.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950

@@ -227,7 +227,7 @@ def conv_roofline(m, x):
         torch.cuda.synchronize()
         m.forward(x, timer=timer)
         torch.cuda.synchronize()
-    gemm = ('conv', 'conv_dual', 'heads')
+    from pps_amd.model import GEMM_OPS as gemm
     conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in gemm)
     conv_flops = sum(f for _, op, f, _, _ in timer if op in gemm)
     n_launch = sum(1 for _, op, _, _, _ in timer if op in gemm)

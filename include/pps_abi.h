@@ -340,6 +340,18 @@ int pps_splitk_bn_act_normalize(const float* part, int splitk, int M, int N,
                                 const float* scale, const float* shift, int relu,
                                 int normalize, float* y, void* stream);
 
+/* Fused ResNet stem (ResNet.py:246-256 basic_bn_stem): conv1 7x7/2 pad 3
+ * (3 -> 64 channels) + test-mode BN (scale/shift) + ReLU + MaxPool 3x3/2 pad
+ * 1 in one kernel, the conv output kept on chip.  x NHWC4 [N][H][128][4]
+ * (BGR + zero, as pps_preprocess_bgr writes it); w3 = pps_split_bf16x3 of
+ * the [64][pps_stem_k()] weight (K index (kh*3 + c)*8 + kw, kw = 7 and the
+ * tail zero); y NHWC [N][Hp][32][64].  f32 products as six bf16 MFMA terms
+ * (the "x3" arithmetic).  W must be 128. */
+int pps_stem_k(void);
+int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w3,
+                          const float* scale, const float* shift, float* y, int Hp, int Wp,
+                          void* stream);
+
 /* MaxPool kernel k, stride s, pad p (padding never wins), NHWC
  * (ResNet.py:255 `pool1`). */
 int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k,

@@ -80,6 +80,8 @@ SIGNATURES = {
                                     c_ptr, c_ptr],
     'pps_re_ranking': [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int, ctypes.c_double,
                        c_ptr, c_i64, c_ptr, c_ptr],
+    'pps_stem_conv_pool_x3': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
+                              c_int, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
                       c_int, c_int, c_ptr],
     'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,
@@ -98,6 +100,7 @@ EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
     'pps_gemm_num_tiles': ([], ctypes.c_int),
     'pps_rank_cells': ([], ctypes.c_int),
+    'pps_stem_k': ([], ctypes.c_int),
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),

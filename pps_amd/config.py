@@ -14,38 +14,36 @@ import yaml
 
 
 class AttrDict(dict):
-    """detectron/utils/collections.py AttrDict: attribute access + immutability."""
-
-    IMMUTABLE = '__immutable__'
+    """Nested config node: keys readable and writable as attributes, and a
+    recursive freeze (the behaviour of the reference's AttrDict,
+    detectron/utils/collections.py:24-60, that detectron/core/config.py
+    relies on: cfg.A.B access, cfg.immutable(True) after
+    assert_and_infer_cfg so later writes raise AttributeError)."""
 
     def __init__(self, *args, **kwargs):
-        super(AttrDict, self).__init__(*args, **kwargs)
-        self.__dict__[AttrDict.IMMUTABLE] = False
+        dict.__init__(self, *args, **kwargs)
+        object.__setattr__(self, '_frozen', False)
 
-    def __getattr__(self, name):
-        if name in self.__dict__:
-            return self.__dict__[name]
-        if name in self:
-            return self[name]
-        raise AttributeError(name)
+    def __getattr__(self, key):
+        try:
+            return self[key]
+        except KeyError:
+            raise AttributeError(key)
 
-    def __setattr__(self, name, value):
-        if self.__dict__[AttrDict.IMMUTABLE]:
-            raise AttributeError('Attempted to set "{}" to "{}", but AttrDict is '
-                                 'immutable'.format(name, value))
-        if name in self.__dict__:
-            self.__dict__[name] = value
-        else:
-            self[name] = value
+    def __setattr__(self, key, value):
+        if object.__getattribute__(self, '_frozen'):
+            raise AttributeError('config is frozen: cannot set %s = %r' % (key, value))
+        self[key] = value
 
-    def immutable(self, is_immutable):
-        self.__dict__[AttrDict.IMMUTABLE] = is_immutable
-        for v in self.values():
-            if isinstance(v, AttrDict):
-                v.immutable(is_immutable)
+    def immutable(self, frozen):
+        """Freeze (True) or thaw (False) this node and every node below it."""
+        object.__setattr__(self, '_frozen', bool(frozen))
+        for child in self.values():
+            if isinstance(child, AttrDict):
+                child.immutable(frozen)
 
     def is_immutable(self):
-        return self.__dict__[AttrDict.IMMUTABLE]
+        return object.__getattribute__(self, '_frozen')
 
 
 def _defaults():

@@ -244,6 +244,19 @@ def fold_bn(blobs, bn, conv_bias=None):
     return scale.astype(np.float32), shift.astype(np.float32)
 
 
+def pack_stem_weight(w):
+    """conv1 [64][3][7][7] -> the fused stem's [64][176] layout: K index
+    (kh * 3 + c) * 8 + kw, kw = 7 and the last 8 columns zero (stem.hip)."""
+    cout, cin, kh_, kw_ = w.shape
+    assert (cin, kh_, kw_) == (3, 7, 7), w.shape
+    out = np.zeros((cout, ops.stem_k()), np.float32)
+    for kh in range(7):
+        for c in range(3):
+            g = kh * 3 + c
+            out[:, g * 8:g * 8 + 7] = w[:, c, kh, :]
+    return out
+
+
 def pack_conv_weight(w, cin_pad=None):
     """[Cout][Cin][KH][KW] -> [Cout][Kpad], K ordered (kh, kw, cin), Kpad % 16."""
     cout, cin, kh, kw = w.shape
@@ -261,6 +274,7 @@ def pack_conv_weight(w, cin_pad=None):
 # Device model
 # ---------------------------------------------------------------------------
 MAX_SPLITK = 4  # conv split-K factors autotune tries (2..MAX_SPLITK)
+GEMM_OPS = ('conv', 'conv_dual', 'heads', 'stem_pool')  # MFMA layers of a forward
 
 
 class PPSModel(object):
@@ -271,7 +285,7 @@ class PPSModel(object):
     """
 
     def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True, math=None,
-                 act_planes=None):
+                 act_planes=None, fused_stem=None):
         """math: 'x3' (default; f32 products on bf16 matrix cores, weights
         split once into three bf16 planes -- gemm_x3.hip) or 'f32' (exact
         f32 MFMA, gemm_f32.hip).  Env PPS_MATH overrides the default.
@@ -352,6 +366,11 @@ class PPSModel(object):
             for L in self.layers:
                 if L['op'] in ('conv', 'conv_dual', 'heads'):
                     L['w'] = ops.split_bf16x3(L['w'], batched=L['op'] == 'heads')
+        if fused_stem is None:
+            fused_stem = os.environ.get('PPS_FUSED_STEM', '1') != '0'
+        self.fused_stem = bool(fused_stem) and self.math == 'x3'
+        if self.fused_stem:
+            self._fuse_stem(blobs)
         if act_planes is None:
             act_planes = os.environ.get('PPS_ACT_PLANES', '1') != '0'
         self.act_planes = bool(act_planes) and self.math == 'x3'
@@ -361,6 +380,22 @@ class PPSModel(object):
                          if C['k'] > 1 and C['cin'] >= 256])
         self.feat_dim = self.plan.feat_dim
         self._batch = None
+
+    def _fuse_stem(self, blobs):
+        """Replace the stem conv + maxpool pair by one 'stem_pool' layer."""
+        for i, L in enumerate(self.layers[:-1]):
+            P = self.layers[i + 1]
+            if (L['op'] == 'conv' and L['input'] == 'data' and L['k'] == 7 and
+                    L['stride'] == 2 and L['pad'] == 3 and L['dil'] == 1 and L['cin'] == 3 and
+                    L['cout'] == 64 and L['relu'] and not L['residual'] and
+                    P['op'] == 'maxpool' and P['input'] == L['output'] and P['k'] == 3 and
+                    P['stride'] == 2 and P['pad'] == 1 and
+                    sum(1 for M in self.layers if M.get('input') == L['output']) == 1):
+                w = pack_stem_weight(blobs[L['name'] + '_w'])
+                F = dict(L, op='stem_pool', output=P['output'], conv_output=L['output'],
+                         w=ops.split_bf16x3(torch.from_numpy(w).to(self.device)))
+                self.layers[i:i + 2] = [F]
+                return
 
     def _plane_edges(self):
         """(producer, consumer) conv pairs whose tensor may travel as bf16x3
@@ -419,6 +454,11 @@ class PPSModel(object):
                 ho = (h + 2 * L['pad'] - L['k']) // L['stride'] + 1
                 wo = (w + 2 * L['pad'] - L['k']) // L['stride'] + 1
                 shapes[L['output']] = (n, ho, wo, c)
+            elif L['op'] == 'stem_pool':
+                n, h, w, _ = shapes[L['input']]
+                hc, wc = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+                L['conv_hw'] = (hc, wc)
+                shapes[L['output']] = (n, (hc - 1) // 2 + 1, (wc - 1) // 2 + 1, L['cout'])
             elif L['op'] == 'pps':
                 n, h, w, c = shapes[L['input']]
                 shapes[L['output']] = (len(L['prefixes']), n, c)
@@ -432,7 +472,10 @@ class PPSModel(object):
         # algorithmic FLOPs per launch (2*M*Cout*K with the TRUE Cin: the
         # stem's 4th packed channel is not counted) -- SURVEY §8(d)
         for L in self.layers:
-            if L['op'] in ('conv', 'conv_dual'):
+            if L['op'] == 'stem_pool':
+                hc, wc = L['conv_hw']
+                L['flops'] = 2.0 * N * hc * wc * L['cout'] * L['k'] * L['k'] * L['cin']
+            elif L['op'] in ('conv', 'conv_dual'):
                 n, ho, wo, co = shapes[L['output']]
                 L['flops'] = 2.0 * n * ho * wo * co * (L['k'] * L['k'] * L['cin'] +
                                                       L.get('shortcut_cin', 0))
@@ -444,7 +487,11 @@ class PPSModel(object):
         # written once (f32 activations; weights in the format the GEMM reads)
         wbytes = 6 if self.math == 'x3' else 4
         for L in self.layers:
-            if L['op'] in ('conv', 'conv_dual'):
+            if L['op'] == 'stem_pool':
+                L['bytes'] = float(4 * np.prod(shapes[L['input']]) +
+                                   4 * np.prod(shapes[L['output']]) +
+                                   wbytes * L['cout'] * ops.stem_k())
+            elif L['op'] in ('conv', 'conv_dual'):
                 n, ho, wo, co = shapes[L['output']]
                 b = 4 * np.prod(shapes[L['input']]) + 4 * n * ho * wo * co
                 b += wbytes * co * (L['k'] * L['k'] * L['cin'] + L.get('shortcut_cin', 0))
@@ -470,10 +517,10 @@ class PPSModel(object):
     def buffers(self):
         return self._bufs
 
-    def flops_per_forward(self, kinds=('conv', 'conv_dual', 'heads')):
+    def flops_per_forward(self, kinds=GEMM_OPS):
         return sum(L['flops'] for L in self.layers if L['op'] in kinds)
 
-    def bytes_per_forward(self, kinds=('conv', 'conv_dual', 'heads')):
+    def bytes_per_forward(self, kinds=GEMM_OPS):
         """Algorithmic HBM bytes of the GEMM launches of one forward."""
         return sum(L['bytes'] for L in self.layers if L['op'] in kinds)
 
@@ -502,6 +549,9 @@ class PPSModel(object):
         elif op == 'maxpool':
             ops.maxpool2d(bufs[L['input']], L['k'], L['stride'], L['pad'],
                           bufs[L['output']])
+        elif op == 'stem_pool':
+            ops.stem_conv_pool_x3(bufs[L['input']], L['w'], L['scale'], L['shift'],
+                                  bufs[L['output']])
         elif op == 'pps':
             ops.part_power_set(bufs[L['input']], L['split_arr'], L['max_ave'],
                                bufs[L['output']])
@@ -551,7 +601,7 @@ class PPSModel(object):
         layers, re-tuned, get > 2 % faster; last (x3, splitk=True) each conv
         tries split-K 2..MAX_SPLITK on the pipelined tiles, kept if > 2 %
         faster -- off by default: at batch 64 it wins 7-8 % on isolated res5
-        layers (scripts/splitk_probe.py) but never inside the forward, where
+        layers (scripts/probes/splitk_probe.py) but never inside the forward, where
         the extra partial-sum pass eats the gain.  Results do not depend on the
         tile or the plane choice (same per-element accumulation order)."""
         self.forward(x)

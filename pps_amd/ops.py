@@ -133,7 +133,7 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     q_planes (x3): also split the queries into bf16x3 planes first so the
     pipelined GEMM stages both operands by DMA (pps_distmat_x3p; pipelined
     tiles only).  Same bits either way; measured at the Market shape it is
-    not faster (scripts/dist_probe.py: the split in the K loop is hidden),
+    not faster (scripts/probes/dist_probe.py: the split in the K loop is hidden),
     so None = off.
     pad_rows: return a [Q, G] view of a buffer with 16-byte-aligned rows
     (dist_buffer) instead of a dense matrix.
@@ -528,6 +528,23 @@ def splitk_bn_act_normalize(part, scale, shift, relu, normalize, y):
     S, M, N = part.shape
     call('pps_splitk_bn_act_normalize', _dev(part, 'part'), S, M, N, _dev(scale, 'scale'),
          _dev(shift, 'shift'), int(bool(relu)), int(bool(normalize)), _dev(y, 'y'), _stream())
+    return y
+
+
+def stem_k():
+    return _lib.lib().pps_stem_k()
+
+
+def stem_conv_pool_x3(x, w3, scale, shift, y):
+    """Fused conv1 7x7/2 + BN + ReLU + maxpool 3x3/2 (pps_stem_conv_pool_x3):
+    x NHWC4 [N, H, 128, 4] -> y NHWC [N, Hp, 32, 64]; w3 = split_bf16x3 of
+    model.pack_stem_weight."""
+    N, H, W, C = x.shape
+    _, Hp, Wp, Co = y.shape
+    if C != 4 or Co != 64 or tuple(w3.shape) != (3, 64, stem_k()):
+        raise RuntimeError('stem: x must be NHWC4, y 64 channels, w3 [3, 64, %d]' % stem_k())
+    call('pps_stem_conv_pool_x3', _dev(x, 'x'), N, H, W, _dev(w3, 'w3', torch.int16),
+         _dev(scale, 'scale'), _dev(shift, 'shift'), _dev(y, 'y'), Hp, Wp, _stream())
     return y
 
 

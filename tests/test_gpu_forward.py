@@ -304,3 +304,50 @@ def test_bench_configuration_vs_oracle():
     xin = x[pick, :, :, :3].cpu().numpy().transpose(0, 3, 1, 2)
     ref = GraphForward(blobs)(np.ascontiguousarray(xin, np.float32)).numpy()
     np.testing.assert_allclose(feat[pick], ref, rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize('N,H', [(2, 384), (3, 100), (1, 30)])
+def test_fused_stem_vs_fp64(N, H):
+    """conv1 7x7/2 + BN + ReLU + maxpool 3x3/2 in one kernel (stem.hip) vs a
+    float64 reference (ResNet.py:246-256)."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(H + N)
+    x = (rng.randn(N, 3, H, 128) * 50).astype(np.float32)
+    w = (rng.randn(64, 3, 7, 7) / np.sqrt(147)).astype(np.float32)
+    scale = rng.uniform(0.5, 1.5, 64).astype(np.float32)
+    shift = (rng.randn(64) * 0.1).astype(np.float32)
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w).double(), stride=2,
+                   padding=3)
+    ref = ref * torch.from_numpy(scale).double()[None, :, None, None] + \
+        torch.from_numpy(shift).double()[None, :, None, None]
+    ref = F.max_pool2d(torch.clamp_min(ref, 0), 3, 2, 1).numpy().transpose(0, 2, 3, 1)
+    xin = np.zeros((N, H, 128, 4), np.float32)
+    xin[..., :3] = x.transpose(0, 2, 3, 1)
+    w3 = ops.split_bf16x3(_cuda(model.pack_stem_weight(w)))
+    y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+    ops.stem_conv_pool_x3(_cuda(xin), w3, _cuda(scale), _cuda(shift), y)
+    got = y.cpu().numpy()
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < 2e-6, err
+    with pytest.raises(RuntimeError, match='width'):
+        ops.stem_conv_pool_x3(_cuda(xin[:, :, :64]), w3, _cuda(scale), _cuda(shift), y)
+
+
+def test_fused_stem_model_matches_two_kernel_stem():
+    from pps_amd import model
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=4)
+    rng = np.random.RandomState(4)
+    xin = np.zeros((2, 384, 128, 4), np.float32)
+    xin[..., :3] = rng.randn(2, 384, 128, 3) * 50
+    a = model.PPSModel(blobs, fused_stem=True)
+    b = model.PPSModel(blobs, fused_stem=False)
+    assert any(L['op'] == 'stem_pool' for L in a.layers)
+    assert not any(L['op'] == 'stem_pool' for L in b.layers)
+    fa = a.forward(_cuda(xin)).cpu().numpy()
+    pa = a.buffers()['pool1'].cpu().numpy()
+    fb = b.forward(_cuda(xin)).cpu().numpy()
+    pb = b.buffers()['pool1'].cpu().numpy()
+    assert np.abs(pa - pb).max() / np.abs(pb).max() < 2e-6
+    np.testing.assert_allclose(fa, fb, rtol=0, atol=1e-5)
