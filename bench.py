@@ -222,7 +222,8 @@ def conv_roofline(m, x):
         torch.cuda.synchronize()
         [e0.elapsed_time(e1) for _, _, _, e0, e1 in timer]   # probe once
     except Exception as exc:  # noqa: BLE001 -- report, then time eagerly
-        method = 'eager launches, events between launches (%s)' % type(exc).__name__
+        method = 'eager launches, events between launches (graph event capture: %s: %s)' % (
+            type(exc).__name__, str(exc).splitlines()[0][:120] if str(exc) else '')
         timer = []
         torch.cuda.synchronize()
         m.forward(x, timer=timer)
@@ -233,8 +234,9 @@ def conv_roofline(m, x):
     n_launch = sum(1 for _, op, _, _, _ in timer if op in gemm)
     all_ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in timer)
     per = {}
-    for name, op, f, e0, e1 in timer:
-        per[name] = (op, f, e0.elapsed_time(e1))
+    for L, (name, op, f, e0, e1) in zip(m.layers, timer):
+        per[name] = dict(op=op, flops=f, ms=e0.elapsed_time(e1), bytes=L.get('bytes', 0.0),
+                         tile=int(L.get('tile', 0)), planes_out=bool(L.get('planes_out')))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if m.math == 'x3':
         peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv, f32 products as 6 '

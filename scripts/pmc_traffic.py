@@ -40,6 +40,8 @@ def load_all(path):
 
 
 def epi_of(name):
+    if '<' not in name:
+        return 0   # the fused stem: a conv epilogue
     args = name.split('<', 1)[1].split('>', 1)[0].split(',')
     return int(args[4])
 
@@ -51,8 +53,8 @@ def main():
     # the x3 path launches both the register-staged and the pipelined family
     knames = ('gemm_x3_kernel', 'gemm_x3p_kernel') if math == 'x3' else ('gemm_f32_kernel',)
 
-    def is_gemm(nm):
-        return any(k + '<' in nm for k in knames)
+    def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
+        return any(k + '<' in nm for k in knames) or 'stem_conv_pool_x3_kernel' in nm
     out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
                       'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
     for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):
