@@ -27,6 +27,12 @@
 
 namespace pps {
 
+#ifndef STEM_PAIR
+#define STEM_PAIR 0  // 1: two conv rows per MFMA pass (measured slower: 129 vs 122 us)
+#endif
+#ifndef STEM_VARIANT
+#define STEM_VARIANT 0  // probes only: 1 = no epilogue/pool, 2 = no MFMA, 3 = staging only
+#endif
 constexpr int kStemPR = 4;                    // pooled rows per workgroup
 constexpr int kStemCR = 2 * kStemPR + 1;      // conv rows per workgroup
 constexpr int kStemIR = 4 * kStemPR + 7;      // input rows staged in LDS
@@ -54,25 +60,35 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
   const int ph0 = (blockIdx.x - n * tiles_h) * kStemPR;
   const int r0 = 4 * ph0 - 5;  // input row of LDS row 0
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave (mb, nb): conv pixels 32*mb .. 32*mb + 31 (lane row r32 = pixel
+  // 32*mb + r32), channels 32*nb .. 32*nb + 31
   const int mb = wave & 1, nb = wave >> 1;
   const int r32 = lane & 31, h = lane >> 5;
 
   // ---- stage the input rows: f32 NHWC4 -> bf16x3 planes, channel-planar ----
+  // (4 staged columns per item: 4 pixel loads, one 8-byte LDS store per
+  // channel and plane)
   const float* xin = x + (int64_t)n * H * kStemW * 4;
-  for (int e = threadIdx.x; e < kStemIR * kStemCols; e += 256) {
-    const int rr = e / kStemCols, cc = e - rr * kStemCols;
-    const int gr = r0 + rr, gc = cc - 3;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (gr >= 0 && gr < H && gc >= 0 && gc < kStemW)
-      v = *reinterpret_cast<const f32x4*>(xin + ((int64_t)gr * kStemW + gc) * 4);
+  for (int e = threadIdx.x; e < kStemIR * (kStemCols / 4); e += 256) {
+    const int rr = e / (kStemCols / 4), c4 = 4 * (e - rr * (kStemCols / 4));
+    const int gr = r0 + rr;
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gc = c4 + u - 3;
+      v[u] = (gr >= 0 && gr < H && gc >= 0 && gc < kStemW)
+                 ? *reinterpret_cast<const f32x4*>(xin + ((int64_t)gr * kStemW + gc) * 4)
+                 : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      unsigned hi, mid, lo;
-      split2(v[c], 0.f, hi, mid, lo);
-      uint16_t* t = tile + c * 3 * kStemPlane + rr * kStemCols + cc;
-      t[0] = (uint16_t)hi;
-      t[kStemPlane] = (uint16_t)mid;
-      t[2 * kStemPlane] = (uint16_t)lo;
+      unsigned h01, m01, l01, h23, m23, l23;
+      split2(v[0][c], v[1][c], h01, m01, l01);
+      split2(v[2][c], v[3][c], h23, m23, l23);
+      u32x2* t = reinterpret_cast<u32x2*>(tile + c * 3 * kStemPlane + rr * kStemCols + c4);
+      t[0] = (u32x2){h01, h23};
+      t[kStemPlane / 4] = (u32x2){m01, m23};
+      t[kStemPlane / 2] = (u32x2){l01, l23};
     }
   }
   // ---- this lane's B fragments (weights) for all chunks -------------------
@@ -92,30 +108,56 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
   // pooling ownership: pooled column pw, channels cg .. cg+7
   const int pw = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
   f32x4 cur0 = {0.f, 0.f, 0.f, 0.f}, cur1 = cur0;
-  const int ow = 32 * mb + r32;
   float* yimg = y + (int64_t)n * Hp * kStemWp * kStemCout;
 
-  for (int i = 0; i < kStemCR; ++i) {
-    const int oh = 2 * ph0 - 1 + i;
-    const bool row_ok = oh >= 0 && oh < Hc;
-    if (row_ok) {
-      f32x16 acc = {};
+  // A fragment of conv row i, chunk k: staged columns 2*ow .. 2*ow + 7 of
+  // one (kh, c) row = four bf16 pairs at a 4-byte-aligned offset per plane
+  const int ow = 32 * mb + r32;
+  auto read_a = [&](int i, int k, bf16x8 (&a)[3]) {
+    int g = 2 * k + h;     // (kh, c) group of this lane's 8 K values
+    g = g < 21 ? g : 20;   // the pad group: any finite values (zero weights)
+    const int kh = g / 3, c = g - 3 * kh;
+    const uint16_t* src = tile + c * 3 * kStemPlane + (2 * i + kh) * kStemCols + 2 * ow;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      u32x4 u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        u[j] = *reinterpret_cast<const unsigned*>(src + p * kStemPlane + 2 * j);
+      a[p] = __builtin_bit_cast(bf16x8, u);
+    }
+  };
+
+  for (int i0 = 0; i0 < kStemCR; i0 += STEM_PAIR ? 2 : 1) {
+    // two conv rows per pass: two independent MFMA chains whose fragment
+    // reads overlap each other's MFMAs (rows past the image compute on the
+    // staged zeros and are discarded below)
+    const bool pair = STEM_PAIR && i0 + 1 < kStemCR;
+    f32x16 acc2[2] = {{}, {}};
+    if (STEM_VARIANT != 3) {
 #pragma unroll
       for (int k = 0; k < kStemChunks; ++k) {
-        int g = 2 * k + h;     // (kh, c) group of this lane's 8 K values
-        g = g < 21 ? g : 20;   // the pad group: any finite values (zero weights)
-        const int kh = g / 3, c = g - 3 * kh;
-        const uint16_t* src = tile + c * 3 * kStemPlane + (2 * i + kh) * kStemCols + 2 * ow;
-        bf16x8 a[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          u32x4 u;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            u[j] = *reinterpret_cast<const unsigned*>(src + p * kStemPlane + 2 * j);
-          a[p] = __builtin_bit_cast(bf16x8, u);
+        bf16x8 a0[3], a1[3];
+        read_a(i0, k, a0);
+        if (pair) read_a(i0 + 1, k, a1);
+        if (STEM_VARIANT != 2) {
+          acc2[0] = mfma_x3(a0, b[k], acc2[0]);
+          if (pair) acc2[1] = mfma_x3(a1, b[k], acc2[1]);
+        } else {
+          acc2[0][0] += (float)a0[0][0] + (float)a0[1][1] + (float)a0[2][2];
         }
-        acc = mfma_x3(a, b[k], acc);
+      }
+    }
+    for (int ii = 0; ii < (pair ? 2 : 1); ++ii) {
+    const int i = i0 + ii;
+    const f32x16 acc = acc2[ii];
+    const int oh = 2 * ph0 - 1 + i;
+    const bool row_ok = oh >= 0 && oh < Hc;
+    if (STEM_VARIANT == 3) continue;
+    if (row_ok) {
+      if (STEM_VARIANT == 1) {
+        if (acc[0] == 12345.f && acc[15] == 1.f) y[threadIdx.x] = acc[1];
+        continue;
       }
       // BN + ReLU into the row buffer: lane holds channel 32nb + r32 of 16 pixels
 #pragma unroll
@@ -167,6 +209,7 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
       }
     }
     __syncthreads();  // the row buffer is rewritten by the next conv row
+    }
   }
 }
 

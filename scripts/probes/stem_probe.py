@@ -15,7 +15,7 @@ plan = model.build_plan()
 blobs = model.synthetic_weights(plan, seed=0)
 x = torch.randn(64, 384, 128, 4, device='cuda') * 50
 x[..., 3] = 0
-for fused in (True, False):
+for fused in ((True, False) if not os.environ.get('FUSED_ONLY') else (True,)):
     m = model.PPSModel(blobs, fused_stem=fused)
     m.forward(x)
     if not fused:
