@@ -204,42 +204,43 @@ def _pmc_mfma(math, batch):
     return {k: e[k] for k in ('clock_GHz', 'mfma_busy_frac', 'mfma_busy_frac_at_2p4GHz')}
 
 
-def conv_roofline(m, x):
-    """Per-launch durations of the GEMM launches of one forward, timed on
-    the kernels' stream by HIP events recorded INSIDE a captured hipGraph
-    (external event nodes) and read after a replay -- the launches exactly
-    as the timed graph runs them, without eager launch gaps.  Falls back to
-    eager per-launch events if event capture is unavailable."""
+def conv_roofline(m, x, reps=20):
+    """Conv-stack roofline from the timed execution: the forward captured in
+    a hipGraph and replayed `reps` times between two HIP events gives the
+    forward's time as the timed step runs it; one eager pass with events
+    around every launch (on the kernels' stream) splits it by launch.  The
+    events add ~1-10 us per launch to the eager split, so the split is
+    rescaled to the graph-replay total (ROCm does not allow event nodes inside
+    a captured graph, which would time launches in the replay directly)."""
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.forward(x)
+    for _ in range(3):
+        g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    fwd_ms = e0.elapsed_time(e1) / reps
     timer = []
-    method = 'hipGraph replay, event nodes between launches'
-    try:
-        g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize()
-        with torch.cuda.graph(g):
-            m.forward(x, timer=timer, timer_external=True)
-        for _ in range(3):
-            g.replay()
-        torch.cuda.synchronize()
-        [e0.elapsed_time(e1) for _, _, _, e0, e1 in timer]   # probe once
-    except Exception as exc:  # noqa: BLE001 -- report, then time eagerly
-        method = 'eager launches, events between launches (graph event capture: %s: %s)' % (
-            type(exc).__name__, str(exc).splitlines()[0][:120] if str(exc) else '')
-        timer = []
-        torch.cuda.synchronize()
-        m.forward(x, timer=timer)
-        torch.cuda.synchronize()
+    m.forward(x, timer=timer)
+    torch.cuda.synchronize()
     from pps_amd.model import GEMM_OPS as gemm
-    conv_ms = sum(e0.elapsed_time(e1) for _, op, _, e0, e1 in timer if op in gemm)
+    eager = [e0.elapsed_time(e1) for _, _, _, e0, e1 in timer]
+    scale = fwd_ms / sum(eager)
+    conv_ms = scale * sum(t for (_, op, _, _, _), t in zip(timer, eager) if op in gemm)
     conv_flops = sum(f for _, op, f, _, _ in timer if op in gemm)
     n_launch = sum(1 for _, op, _, _, _ in timer if op in gemm)
-    all_ms = sum(e0.elapsed_time(e1) for _, _, _, e0, e1 in timer)
     per = {}
-    for L, (name, op, f, e0, e1) in zip(m.layers, timer):
-        per[name] = dict(op=op, flops=f, ms=e0.elapsed_time(e1), bytes=L.get('bytes', 0.0),
+    for L, (name, op, f, _, _), t in zip(m.layers, timer, eager):
+        per[name] = dict(op=op, flops=f, ms=t * scale, ms_eager=t, bytes=L.get('bytes', 0.0),
                          tile=int(L.get('tile', 0)), planes_out=bool(L.get('planes_out')))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if m.math == 'x3':
-        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv, f32 products as 6 '
+        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv + the fused stem_conv_pool_x3_kernel, f32 products as 6 '
                                         'bf16 MFMA terms (%d launches/forward)' % n_launch)
     else:
         peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '
@@ -251,7 +252,11 @@ def conv_roofline(m, x):
                 launches=n_launch, flops_per_forward=conv_flops,
                 algorithmic_bytes_per_launch=round(m.bytes_per_forward() / n_launch),
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2),
-                forward_kernels_ms=round(all_ms, 3), timing=method,
+                forward_graph_ms=round(fwd_ms, 3),
+                forward_eager_event_ms=round(sum(eager), 3),
+                timing='forward hipGraph replayed %d x between HIP events; per-launch split '
+                       'from one eager pass with events per launch, rescaled to the replay '
+                       'total' % reps,
                 frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
 
 
