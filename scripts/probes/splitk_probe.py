@@ -6,7 +6,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from pps_amd import model, ops  # noqa: E402
 
 LAYERS = {'res4b': (64, 24, 8, 256, 256, 3), 'res4a': (64, 24, 8, 1024, 256, 1),
