@@ -378,7 +378,9 @@ def main():
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
         pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
     elif not args.no_autotune:
-        m.autotune(xbuf)   # per-layer tile choice, outside the timed region
+        # per-layer tile choice, outside the timed region (PPS_AUTOTUNE_SPLITK=1:
+        # also try split-K per conv)
+        m.autotune(xbuf, splitk=os.environ.get('PPS_AUTOTUNE_SPLITK') == '1')
 
     for _ in range(max(1, args.warmup)):
         step()
