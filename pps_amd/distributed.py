@@ -64,8 +64,14 @@ def max_same_id(qid, gid):
     return max(1, int(per_q.max()))
 
 
+def _active(world):
+    """Collectives run whenever a process group exists, also at world size 1
+    (a one-rank RCCL communicator), and are skipped only without one."""
+    return world > 1 or (torch.distributed.is_available() and torch.distributed.is_initialized())
+
+
 def barrier(world):
-    if world > 1:
+    if _active(world):
         torch.distributed.barrier()
 
 
@@ -75,7 +81,7 @@ def _coll_device(x):
 
 
 def max_over_ranks(x, world):
-    if world == 1:
+    if not _active(world):
         return x
     dev = 'cuda' if torch.distributed.get_backend() == 'nccl' else 'cpu'
     t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
@@ -86,7 +92,7 @@ def max_over_ranks(x, world):
 def all_gather_rows(x, sizes):
     """Gather [n_r, ...] blocks of unequal n_r (known on every rank)."""
     world = len(sizes)
-    if world == 1:
+    if not _active(world):
         return x
     mx = max(max(sizes), 1)
     dev = _coll_device(x)
@@ -98,7 +104,7 @@ def all_gather_rows(x, sizes):
 
 
 def broadcast_object(obj, world, src=0):
-    if world == 1:
+    if not _active(world):
         return obj
     box = [obj]
     torch.distributed.broadcast_object_list(box, src=src)
@@ -196,7 +202,7 @@ class ShardedEvaluator(object):
 
     def _all_reduce(self, t, op=None):
         """In-place all-reduce of a backend tensor (host-staged for gloo)."""
-        if self.world == 1:
+        if not _active(self.world):
             return t
         op = op if op is not None else torch.distributed.ReduceOp.SUM
         dev = _coll_device(t)
@@ -207,7 +213,7 @@ class ShardedEvaluator(object):
         return t
 
     def _gather_lists(self, *ts):
-        if self.world == 1:
+        if not _active(self.world):
             return [t[None] for t in ts]
         return [all_gather_rows(t[None], [1] * self.world) for t in ts]
 

@@ -45,7 +45,7 @@ def _worker(rank, world, port, data, k, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('world', [1, 2, 3])
 def test_sharded_eval_matches_single_process(golden, world):
     from oracle import evaluator as ev
     g = golden('market_small')
@@ -84,10 +84,11 @@ def _eval_worker(rank, world, port, data, rerank, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('rerank', [False, True])
-def test_sharded_evaluate_multi_query_and_rerank(rerank):
+@pytest.mark.parametrize('rerank,world', [(False, 2), (True, 2), (True, 1)])
+def test_sharded_evaluate_multi_query_and_rerank(rerank, world):
     """evaluate() with marks 0/1/2 over 2 ranks == the oracle's one-process
-    evaluate_arrays (single query, multi-query pooling, re-ranking of both)."""
+    evaluate_arrays (single query, multi-query pooling, re-ranking of both).
+    World size 1 runs every collective on a one-rank group."""
     from oracle import evaluator as ev
     rng = np.random.RandomState(9)
     n = 240
@@ -96,7 +97,6 @@ def test_sharded_evaluate_multi_query_and_rerank(rerank):
     marks = rng.choice([0, 1, 1, 2], n)
     cent = rng.randn(16, 64).astype(np.float32)
     feat = (cent[ids] + 0.8 * rng.randn(n, 64)).astype(np.float32)
-    world = 2
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_eval_worker, args=(world, _free_port(), (feat, ids, cams, marks), rerank, out),
