@@ -348,6 +348,11 @@ int pps_splitk_bn_act_normalize(const float* part, int splitk, int M, int N,
  * tail zero); y NHWC [N][Hp][32][64].  f32 products as six bf16 MFMA terms
  * (the "x3" arithmetic).  W must be 128. */
 int pps_stem_k(void);
+/* Stem kernel choice (process-wide): 0 = ring-staged input rows, whole conv
+ * rows per wave, no LDS epilogue (default); 1 = whole input tile staged, LDS
+ * row-buffer epilogue.  Identical bits.  Returns the previous choice; other
+ * values only query. */
+int pps_stem_variant(int v);
 int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w3,
                           const float* scale, const float* shift, float* y, int Hp, int Wp,
                           void* stream);

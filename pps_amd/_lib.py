@@ -101,6 +101,7 @@ EXTRA = {
     'pps_gemm_num_tiles': ([], ctypes.c_int),
     'pps_rank_cells': ([], ctypes.c_int),
     'pps_stem_k': ([], ctypes.c_int),
+    'pps_stem_variant': ([ctypes.c_int], ctypes.c_int),
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),

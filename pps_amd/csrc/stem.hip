@@ -213,9 +213,261 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ring-staged variant (default): no LDS epilogue and one two-wave barrier per
+// conv row.  Workgroup = 2 waves = the two 32-channel halves of kRingPR
+// pooled rows of one image; each wave computes WHOLE conv rows (64 pixels =
+// two 32x32 MFMA blocks, same K order and term order as above -> identical
+// bits), so the horizontal 3-wide max needs only the partner lane (l ^ 32)
+// and the vertical one stays in registers.  The input rows live in a ring of
+// kRingSlots LDS rows: while conv row i is multiplied, the two input rows
+// conv row i + 1 first needs are fetched into registers, then split and
+// written into the slots conv row i - 1 released.  LDS layout
+// [channel][slot][plane][column] keeps the three planes of a row within the
+// ds_read2 offset range: one address per (chunk, lane) serves both pixel
+// blocks and all three planes.  24 KB of LDS and <= 256 VGPRs: four
+// workgroups (8 waves) per CU.
+#ifndef RING_ABL
+#define RING_ABL 0  // probes only, bit mask: 1 = no epilogue, 2 = no ring staging, 4 = no
+                    // barrier, 8 = no MFMA, 16 = no fragment reads in the K loop
+#endif
+constexpr int kRingPR = 6;                    // pooled rows per workgroup
+constexpr int kRingCR = 2 * kRingPR + 1;      // conv rows per workgroup
+constexpr int kRingSlots = 10;                // 7 read by row i + 1 in flight + 2 written
+constexpr int kRingRow = 3 * kStemCols;       // bf16 elements per (channel, slot): 3 planes
+
+#ifndef RING_STREAMS
+#define RING_STREAMS 2  // row streams per workgroup (2: 4-wave workgroups)
+#endif
+constexpr int kRingThreads = 128 * RING_STREAMS;
+#ifndef RING_CLK
+#define RING_CLK 0
+#endif
+
+__global__ void __launch_bounds__(kRingThreads, 2)
+stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
+                    const uint16_t* __restrict__ w3, const float* __restrict__ scale,
+                    const float* __restrict__ shift, float* __restrict__ y, int Hc, int Hp) {
+  __shared__ __attribute__((aligned(16))) uint16_t ring[RING_STREAMS * 3 * kRingSlots * kRingRow];
+  const int n = blockIdx.x / tiles_h;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nb = wid & 1;        // channel half
+  const int stream = wid >> 1;   // row stream: its own pooled rows and ring
+  uint16_t* tile = ring + stream * (3 * kRingSlots * kRingRow);
+  const int ph0 = (blockIdx.x - n * tiles_h) * (kRingPR * RING_STREAMS) + stream * kRingPR;
+  const int r0 = 4 * ph0 - 5;  // input row of ring row ri = 0
+  const int lane = threadIdx.x & 63;
+  const int r32 = lane & 31, h = lane >> 5;
+  const float* xin = x + (int64_t)n * H * kStemW * 4;
+
+  // staged columns 0, 1 and 132..135 (input columns -3, -2, 129..132) stay zero
+  for (int e = threadIdx.x; e < RING_STREAMS * 9 * kRingSlots; e += kRingThreads) {
+    uint16_t* row = ring + e * kStemCols;
+    *reinterpret_cast<unsigned*>(row) = 0u;
+    *reinterpret_cast<u32x2*>(row + kStemW + 4) = (u32x2){0u, 0u};
+  }
+  // staging of ring rows (ri, ri + 1): wave nb takes row ri + nb, lane l the
+  // staged columns 2l + 2, 2l + 3 (input columns 2l - 1, 2l); lane 63 also
+  // columns 130, 131 (input column 127 and the zero past the edge).  The
+  // loads are unconditional (clamped addresses); masks zero them on the put.
+  auto fetch = [&](int ri, f32x4& a, f32x4& b, f32x4& c, int& ok) {
+    const int gr = r0 + ri + nb;
+    const bool rok = gr >= 0 && gr < H;
+    const float* src = xin + (int64_t)(rok ? gr : 0) * kStemW * 4;
+    a = *reinterpret_cast<const f32x4*>(src + (lane > 0 ? 2 * lane - 1 : 0) * 4);
+    b = *reinterpret_cast<const f32x4*>(src + 2 * lane * 4);
+    // (a per-lane address: a uniform one becomes a scalar load, whose
+    // lgkmcnt would hold up the first LDS fragment wait)
+    c = *reinterpret_cast<const f32x4*>(src + (lane == 63 ? kStemW - 1 : 2 * lane) * 4);
+    ok = rok ? ((lane > 0 ? 1 : 0) | 2 | (lane == 63 ? 4 : 0)) : 0;
+  };
+  auto put = [&](int ri, const f32x4& a, const f32x4& b, const f32x4& c, int ok) {
+    const int slot = (ri + nb) % kRingSlots;
+    unsigned* t = reinterpret_cast<unsigned*>(tile + slot * kRingRow + 2 * lane + 2);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      unsigned hh, mm, ll;
+      split2((ok & 1) ? a[ch] : 0.f, (ok & 2) ? b[ch] : 0.f, hh, mm, ll);
+      unsigned* tc = t + ch * (kRingSlots * kRingRow / 2);
+      tc[0] = hh;
+      tc[kStemCols / 2] = mm;
+      tc[kStemCols] = ll;
+      if (lane == 63) {
+        split2((ok & 4) ? c[ch] : 0.f, 0.f, hh, mm, ll);
+        tc[1] = hh;
+        tc[kStemCols / 2 + 1] = mm;
+        tc[kStemCols + 1] = ll;
+      }
+    }
+  };
+  {
+    f32x4 a, b, c;
+    int ok;
+#pragma unroll 1
+    for (int ri = 0; ri < 8; ri += 2) {  // rows 0..7: conv rows 0 and 1
+      fetch(ri, a, b, c, ok);
+      put(ri, a, b, c, ok);
+    }
+  }
+  // this lane's B fragments (weights) for all chunks: channel 32 nb + r32
+  bf16x8 b[kStemChunks][3];
+  const int co = 32 * nb + r32;
+#pragma unroll
+  for (int k = 0; k < kStemChunks; ++k)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      b[k][p] = *reinterpret_cast<const bf16x8*>(w3 + ((int64_t)p * kStemCout + co) * kStemK +
+                                                  16 * k + 8 * h);
+  const float sc = scale[co], sh = shift[co];
+  __syncthreads();
+
+  float cur[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) cur[q] = 0.f;
+  float* yimg = y + (int64_t)n * Hp * kStemWp * kStemCout + co;
+#if RING_CLK
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+#pragma unroll 1
+  for (int i = 0; i < kRingCR; ++i) {
+    const int rnext = 2 * i + 8;  // ring rows conv row i + 1 (and i + 2) first need
+    f32x4 pa, pb, pc;
+    int pok;
+    if (!(RING_ABL & 2)) fetch(rnext, pa, pb, pc, pok);
+    // keep the loads here: the scheduler would otherwise sink them to their
+    // use after the MFMAs and expose their latency
+    __builtin_amdgcn_sched_barrier(0);
+    const int rs = (2 * i) % kRingSlots;  // slot of ring row 2 i (wave-uniform)
+    f32x16 acc0 = {}, acc1 = {};
+    // fragment reads one half-chunk ahead of the MFMAs: block 1 of chunk k
+    // is read under block 0's terms, block 0 of chunk k + 1 under block 1's
+    auto src_of = [&](int k) {
+      // (kh, c) group of this lane's 8 K values: g = 2k + h (pad group 21
+      // reads group 20, zero weights); both candidates are wave-uniform
+      const int g0 = 2 * k, g1 = 2 * k + 1 < 21 ? 2 * k + 1 : 20;
+      const int kh0 = g0 / 3, c0 = g0 - 3 * kh0, kh1 = g1 / 3, c1 = g1 - 3 * kh1;
+      int s0 = rs + kh0, s1 = rs + kh1;
+      s0 = s0 >= kRingSlots ? s0 - kRingSlots : s0;
+      s1 = s1 >= kRingSlots ? s1 - kRingSlots : s1;
+      const int o0 = (c0 * kRingSlots + s0) * kRingRow, o1 = (c1 * kRingSlots + s1) * kRingRow;
+      return tile + (h ? o1 : o0) + 2 * r32;
+    };
+    auto frag = [&](const uint16_t* src, int blk, bf16x8 (&a)[3]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        u32x4 u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          u[j] = *reinterpret_cast<const unsigned*>(src + p * kStemCols + 32 * 2 * blk + 2 * j);
+        a[p] = __builtin_bit_cast(bf16x8, u);
+      }
+    };
+    bf16x8 fa[3], fb[3];
+    frag(src_of(0), 0, fa);
+    if (RING_ABL & 16) frag(src_of(0), 1, fb);
+#pragma unroll
+    for (int k = 0; k < kStemChunks; ++k) {
+      // (sched_barrier: the scheduler would regroup the reads behind the
+      // MFMAs that free their registers, exposing the LDS latency)
+      if (!(RING_ABL & 16)) frag(src_of(k), 1, fb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (RING_ABL & 8) asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]));
+      else acc0 = mfma_x3(fa, b[k], acc0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < kStemChunks && !(RING_ABL & 16)) frag(src_of(k + 1), 0, fa);
+      __builtin_amdgcn_sched_barrier(0);
+      if (RING_ABL & 8) asm volatile("" ::"v"(fb[0]), "v"(fb[1]), "v"(fb[2]));
+      else acc1 = mfma_x3(fb, b[k], acc1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the loads' unused 4th lanes stay allocated until here, so no register
+    // reuse forces an early wait on them
+    if (!(RING_ABL & 2)) asm volatile("" ::"v"(pa), "v"(pb), "v"(pc));
+    // (unconditional, also past the last ring row: the ring invariant keeps
+    // those writes in free slots, and a conditional put lets the compiler
+    // sink the loads into its branch, behind the MFMAs)
+    if (!(RING_ABL & 2)) put(rnext, pa, pb, pc, pok);
+    if (RING_ABL & 1) {
+      asm volatile("" ::"v"(acc0), "v"(acc1));
+      if (!(RING_ABL & 4)) __syncthreads();
+      continue;
+    }
+
+    // BN + ReLU, horizontal 3-wide max: lane (r32, h) holds pixels
+    // 32 blk + 8 t + 4 h + e (r = 4 t + e); pooled column 16 blk + 4 t + 2 h
+    // takes the pixel before its run from the partner lane
+    const int oh = 2 * ph0 - 1 + i;
+    float hp[16];
+    if (oh >= 0 && oh < Hc) {
+      float v[2][16], pl[2][4];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        v[0][r] = fmaxf(__builtin_fmaf(acc0[r], sc, sh), 0.f);
+        v[1][r] = fmaxf(__builtin_fmaf(acc1[r], sc, sh), 0.f);
+      }
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) pl[blk][t] = __shfl_xor(v[blk][4 * t + 3], 32);
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float before = t > 0 ? pl[blk][t - 1] : (blk > 0 ? pl[0][3] : 0.f);
+          const float xb = h ? pl[blk][t] : before;
+          hp[8 * blk + 2 * t] = fmaxf(xb, fmaxf(v[blk][4 * t], v[blk][4 * t + 1]));
+          hp[8 * blk + 2 * t + 1] =
+              fmaxf(v[blk][4 * t + 1], fmaxf(v[blk][4 * t + 2], v[blk][4 * t + 3]));
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hp[q] = 0.f;  // padded / missing conv rows
+    }
+    // vertical: conv row i = 2j closes pooled row j - 1 and opens row j
+    if ((i & 1) == 0) {
+      if (i > 0) {
+        const int ph = ph0 + i / 2 - 1;
+        if (ph < Hp) {
+          float* o = yimg + (int64_t)ph * kStemWp * kStemCout;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int pw = 16 * (q >> 3) + 4 * ((q >> 1) & 3) + 2 * h + (q & 1);
+            o[pw * kStemCout] = fmaxf(cur[q], hp[q]);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cur[q] = hp[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cur[q] = fmaxf(cur[q], hp[q]);
+    }
+    if (!(RING_ABL & 4)) __syncthreads();  // ring rows written above are read by the next conv row
+  }
+#if RING_CLK  // diagnostic build: shader clocks and 100 MHz ticks of the loop -> y
+  const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    y[2 * blockIdx.x] = (float)(clk1 - clk0);
+    y[2 * blockIdx.x + 1] = (float)(rt1 - rt0);
+  }
+#endif
+}
+
+static int g_stem_variant = 0;  // 0: ring-staged, 1: whole-tile staged + LDS epilogue
+
 int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const float* scale,
                       const float* shift, float* y, int Hc, int Hp, hipStream_t st) {
   if (N <= 0) return PPS_OK;
+  if (g_stem_variant == 0) {
+    const int tiles_h = (Hp + kRingPR * RING_STREAMS - 1) / (kRingPR * RING_STREAMS);
+    hipLaunchKernelGGL(stem_ring_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(kRingThreads), 0,
+                       st, x,
+                       H, tiles_h, w3, scale, shift, y, Hc, Hp);
+    PPS_CHECK_LAUNCH("stem_ring_x3_kernel");
+    return PPS_OK;
+  }
   const int tiles_h = (Hp + kStemPR - 1) / kStemPR;
   hipLaunchKernelGGL(stem_conv_pool_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(256),
                      kStemLdsBytes, st, x, H, tiles_h, w3, scale, shift, y, Hc, Hp);
@@ -230,6 +482,12 @@ using namespace pps;
 extern "C" {
 
 int pps_stem_k(void) { return kStemK; }
+
+int pps_stem_variant(int v) {
+  const int old = g_stem_variant;
+  if (v == 0 || v == 1) g_stem_variant = v;
+  return old;
+}
 
 int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w3,
                           const float* scale, const float* shift, float* y, int Hp, int Wp,

@@ -535,6 +535,13 @@ def stem_k():
     return _lib.lib().pps_stem_k()
 
 
+def stem_variant(v=-1):
+    """Select the fused stem kernel (0: ring-staged, the default; 1: whole
+    tile staged with an LDS epilogue); returns the previous choice, v < 0
+    only queries.  Both give identical bits."""
+    return _lib.lib().pps_stem_variant(int(v))
+
+
 def stem_conv_pool_x3(x, w3, scale, shift, y):
     """Fused conv1 7x7/2 + BN + ReLU + maxpool 3x3/2 (pps_stem_conv_pool_x3):
     x NHWC4 [N, H, 128, 4] -> y NHWC [N, Hp, 32, 64]; w3 = split_bf16x3 of

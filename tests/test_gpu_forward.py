@@ -306,7 +306,7 @@ def test_bench_configuration_vs_oracle():
     np.testing.assert_allclose(feat[pick], ref, rtol=0, atol=2e-5)
 
 
-@pytest.mark.parametrize('N,H', [(2, 384), (3, 100), (1, 30)])
+@pytest.mark.parametrize('N,H', [(2, 384), (3, 100), (1, 30), (2, 7), (1, 390)])
 def test_fused_stem_vs_fp64(N, H):
     """conv1 7x7/2 + BN + ReLU + maxpool 3x3/2 in one kernel (stem.hip) vs a
     float64 reference (ResNet.py:246-256)."""
@@ -324,11 +324,20 @@ def test_fused_stem_vs_fp64(N, H):
     xin = np.zeros((N, H, 128, 4), np.float32)
     xin[..., :3] = x.transpose(0, 2, 3, 1)
     w3 = ops.split_bf16x3(_cuda(model.pack_stem_weight(w)))
-    y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
-    ops.stem_conv_pool_x3(_cuda(xin), w3, _cuda(scale), _cuda(shift), y)
-    got = y.cpu().numpy()
-    err = np.abs(got - ref).max() / np.abs(ref).max()
-    assert err < 2e-6, err
+    outs = []
+    for variant in (0, 1):   # ring-staged (default), whole-tile staged
+        old = ops.stem_variant(variant)
+        try:
+            y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+            ops.stem_conv_pool_x3(_cuda(xin), w3, _cuda(scale), _cuda(shift), y)
+        finally:
+            ops.stem_variant(old)
+        got = y.cpu().numpy()
+        err = np.abs(got - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (variant, err)
+        outs.append(got)
+    # same K order, chunks and term order: identical bits
+    np.testing.assert_array_equal(outs[0], outs[1])
     with pytest.raises(RuntimeError, match='width'):
         ops.stem_conv_pool_x3(_cuda(xin[:, :, :64]), w3, _cuda(scale), _cuda(shift), y)
 
