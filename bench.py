@@ -207,8 +207,9 @@ def _pmc_mfma(math, batch):
 def conv_roofline(m, x, reps=20):
     """Conv-stack roofline from the timed execution: the forward captured in
     a hipGraph and replayed `reps` times between two HIP events gives the
-    forward's time as the timed step runs it; one eager pass with events
-    around every launch (on the kernels' stream) splits it by launch.  The
+    forward's time as the timed step runs it; eager passes with events
+    around every launch (on the kernels' stream; median of five) split it by
+    launch.  The
     events add ~1-10 us per launch to the eager split, so the split is
     rescaled to the graph-replay total (ROCm does not allow event nodes inside
     a captured graph, which would time launches in the replay directly)."""
@@ -225,11 +226,14 @@ def conv_roofline(m, x, reps=20):
     e1.record()
     e1.synchronize()
     fwd_ms = e0.elapsed_time(e1) / reps
-    timer = []
-    m.forward(x, timer=timer)
-    torch.cuda.synchronize()
+    splits = []
+    for _ in range(5):   # per-launch medians of five eager passes
+        timer = []
+        m.forward(x, timer=timer)
+        torch.cuda.synchronize()
+        splits.append([a.elapsed_time(b) for _, _, _, a, b in timer])
     from pps_amd.model import GEMM_OPS as gemm
-    eager = [e0.elapsed_time(e1) for _, _, _, e0, e1 in timer]
+    eager = [float(v) for v in np.median(np.array(splits), axis=0)]
     scale = fwd_ms / sum(eager)
     conv_ms = scale * sum(t for (_, op, _, _, _), t in zip(timer, eager) if op in gemm)
     conv_flops = sum(f for _, op, f, _, _ in timer if op in gemm)
@@ -240,7 +244,7 @@ def conv_roofline(m, x, reps=20):
                          tile=int(L.get('tile', 0)), planes_out=bool(L.get('planes_out')))
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if m.math == 'x3':
-        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv + the fused stem_conv_pool_x3_kernel, f32 products as 6 '
+        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv + the fused stem (stem_ring_x3_kernel), f32 products as 6 '
                                         'bf16 MFMA terms (%d launches/forward)' % n_launch)
     else:
         peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '
@@ -255,7 +259,7 @@ def conv_roofline(m, x, reps=20):
                 forward_graph_ms=round(fwd_ms, 3),
                 forward_eager_event_ms=round(sum(eager), 3),
                 timing='forward hipGraph replayed %d x between HIP events; per-launch split '
-                       'from one eager pass with events per launch, rescaled to the replay '
+                       'from eager passes with events per launch (median of 5), rescaled to the replay '
                        'total' % reps,
                 frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
 

@@ -54,7 +54,7 @@ def main():
     knames = ('gemm_x3_kernel', 'gemm_x3p_kernel') if math == 'x3' else ('gemm_f32_kernel',)
 
     def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
-        return any(k + '<' in nm for k in knames) or 'stem_conv_pool_x3_kernel' in nm
+        return any(k + '<' in nm for k in knames) or ('stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)
     out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
                       'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
     for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):
