@@ -384,7 +384,10 @@ def main():
     elif not args.no_autotune:
         # per-layer tile choice, outside the timed region (PPS_AUTOTUNE_SPLITK=1:
         # also try split-K per conv)
-        m.autotune(xbuf, splitk=os.environ.get('PPS_AUTOTUNE_SPLITK') == '1')
+        # (PPS_AUTOTUNE_MAXTILE=n: candidates 1..n only, for A/B runs)
+        maxt = int(os.environ.get('PPS_AUTOTUNE_MAXTILE', '0'))
+        m.autotune(xbuf, splitk=os.environ.get('PPS_AUTOTUNE_SPLITK') == '1',
+                   tiles=list(range(1, maxt + 1)) if maxt else None)
 
     for _ in range(max(1, args.warmup)):
         step()

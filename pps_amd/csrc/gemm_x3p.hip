@@ -395,9 +395,19 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
 // S: MFMA block, 32 (v_mfma_f32_32x32x16_bf16, two 16-wide K groups per
 // chunk) or 16 (v_mfma_f32_16x16x32_bf16, one group per chunk; the wave's
 // column blocks are processed in two halves to keep the same pipeline).
+#ifndef X3P_CLK
+#define X3P_CLK 0  // diagnostic builds: per-workgroup shader clocks / 100 MHz ticks
+#endif
+#if X3P_CLK
+__device__ float g_x3p_clk[2 * 65536];
+#endif
+
 template <int BM, int BN, int WM, int WN, int EPI, int NS, bool A3, int S = 32>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
+#if X3P_CLK
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   constexpr int BK = 32;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / S;
@@ -792,6 +802,16 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     }
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
+#if X3P_CLK
+  {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    const int wg = blockIdx.x + gridDim.x * blockIdx.y;
+    if (threadIdx.x == 0 && wg < 65536) {
+      g_x3p_clk[2 * wg] = (float)(clk1 - clk0);
+      g_x3p_clk[2 * wg + 1] = (float)(rt1 - rt0);
+    }
+  }
+#endif
 
   if constexpr (DISTLDS) {
     if (p.sym)
@@ -923,8 +943,28 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;  // variants per block size
+  if (variant == GEMM_TILE_P16_192x128W42 - GEMM_TILE_P_FIRST) {
+    // f32 activations only (192 rows do not split into 8 waves x 16-row
+    // plane pieces): plane A takes the 8-wave 128x128 tile of the same family
+    if (p.a3) return launch_tile_p<128, 128, 4, 2, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<192, 128, 4, 2, 2, 0, 16>(p, epi, batch, stream);
+  }
+  if (variant == GEMM_TILE_P16_192x64W41 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<192, 64, 4, 1, 2, 2, 16>(p, epi, batch, stream);
+  if (variant == GEMM_TILE_P16_96x128W22 - GEMM_TILE_P_FIRST) {
+    if (p.a3) return launch_tile_p<128, 128, 2, 2, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<96, 128, 2, 2, 2, 0, 16>(p, epi, batch, stream);
+  }
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }
 
 }  // namespace pps
+
+#if X3P_CLK
+extern "C" int pps_debug_x3p_clocks(float* dst, int n) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(pps::g_x3p_clk), sizeof(float) * n) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

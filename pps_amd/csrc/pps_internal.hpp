@@ -79,7 +79,14 @@ enum GemmTile {
   // 36, 37: 128x128 and 192x128 with 8 waves
   // 38..46 (bf16x3 only): ids 29..37 on 16x16x32 MFMA blocks (own rounding)
   GEMM_TILE_P16_FIRST = 38,
-  GEMM_NUM_TILES = 47
+  // 47 (bf16x3 only, 16x16x32 rounding): 192x128 with 8 waves as 4 x 2 (48 x 64
+  // per wave) -- 256 tiles for the res5 layers' M = 12,288 x N = 512
+  GEMM_TILE_P16_192x128W42 = 47,
+  // 48, 49 (16x16x32): 192x64 (4 x 1 waves) and 96x128 (2 x 2 waves), 48 x 64
+  // per wave -- 256 tiles for M = 12,288 x N = 256 (res4 2a / 2b)
+  GEMM_TILE_P16_192x64W41 = 48,
+  GEMM_TILE_P16_96x128W22 = 49,
+  GEMM_NUM_TILES = 50
 };
 
 struct GemmParams {
