@@ -174,6 +174,9 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
 // the same order as conv_epilogue_t (identical bits).
 template <int BM, int BN>
 constexpr int lds_epi_bytes() { return BM * (BN + 4) * 4; }
+#ifndef X3P_RES_PREFETCH
+#define X3P_RES_PREFETCH 16  // residual vectors per thread requested early (0: off)
+#endif
 
 template <int EPI, int BM, int BN, int WM, int WN, int S>
 __device__ inline void conv_epilogue_lds(const GemmParams& p,
@@ -187,6 +190,30 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   float* t = reinterpret_cast<float*>(lds);
+  const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
+  float* __restrict__ out = p.out + obase;
+  const int ldo = (int)p.ldo;
+  const int mrem = p.M - m0, nrem = p.Ncol - n0;
+  const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0;
+  const float* sh = p.shift + batch * p.ss_bstride + n0;
+  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+  const int ldr = (int)p.ldr;
+  constexpr int C4 = BN / 4;
+  // the residual tile is requested before the accumulators are parked, so
+  // its HBM latency overlaps the LDS round trip (up to 8 vectors per thread)
+  constexpr int IT = (BM * C4) / NT;
+  constexpr bool PRE = HAS_RES && (BM * C4) % NT == 0 && IT <= X3P_RES_PREFETCH;
+  f32x4 rpre[PRE ? IT : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = it * NT + threadIdx.x;
+      const int row = idx / C4, col = 4 * (idx - row * C4);
+      rpre[it] = (row < mrem && col < nrem)
+                     ? *reinterpret_cast<const f32x4*>(res + row * ldr + col)
+                     : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  }
   __syncthreads();  // every wave is done reading the last stage
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -204,23 +231,12 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
     }
   }
   __syncthreads();
-  const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
-  float* __restrict__ out = p.out + obase;
-  const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0, nrem = p.Ncol - n0;
-  const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0;
-  const float* sh = p.shift + batch * p.ss_bstride + n0;
-  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
-  const int ldr = (int)p.ldr;
-  constexpr int C4 = BN / 4;
-  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+  auto finish = [&](int idx, const f32x4& rv) {
     const int row = idx / C4, col = 4 * (idx - row * C4);
-    if (row >= mrem || col >= nrem) continue;
+    if (row >= mrem || col >= nrem) return;
     const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
     const f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
     const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + col);
-    f32x4 rv = {0.f, 0.f, 0.f, 0.f};
-    if (HAS_RES) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
     f32x4 v;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -229,6 +245,19 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       if (RELU) v[e] = fmaxf(v[e], 0.f);
     }
     *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) finish(it * NT + threadIdx.x, rpre[it]);
+  } else {
+    for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+      f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+      if (HAS_RES) {
+        const int row = idx / C4, col = 4 * (idx - row * C4);
+        if (row < mrem && col < nrem) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
+      }
+      finish(idx, rv);
+    }
   }
 }
 
