@@ -386,8 +386,10 @@ def main():
         # also try split-K per conv)
         # (PPS_AUTOTUNE_MAXTILE=n: candidates 1..n only, for A/B runs)
         maxt = int(os.environ.get('PPS_AUTOTUNE_MAXTILE', '0'))
+        fin = int(os.environ.get('PPS_AUTOTUNE_FINALISTS', '4'))
         m.autotune(xbuf, splitk=os.environ.get('PPS_AUTOTUNE_SPLITK') == '1',
-                   tiles=list(range(1, maxt + 1)) if maxt else None)
+                   tiles=list(range(1, maxt + 1)) if maxt else None, finalists=fin,
+                   final_reps=int(os.environ.get('PPS_AUTOTUNE_FINAL_REPS', '10')))
 
     for _ in range(max(1, args.warmup)):
         step()
