@@ -357,6 +357,26 @@ int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w
                           const float* scale, const float* shift, float* y, int Hp, int Wp,
                           void* stream);
 
+/* The last res5 conv with the part pooling fused into its epilogue
+ * (ResNet.py:276-333 res5_2 branch2c + Sum + Relu feeding bpm_heads.py:18-55
+ * and pps_heads.py:38-80): conv + BN (scale/shift) + residual + ReLU on a
+ * pipelined bf16x3 tile whose rows are exactly one image (Ho*Wo rows, <= 128
+ * columns; pps_x3p_tile_shape tells a tile's rows/columns); every tile pools
+ * its image's S horizontal strips (heights `splits`, average and max) and
+ * writes the 2^S - 1 part subsets to pps_out [2^S - 1][N][Cout] with
+ * pps_part_power_set's arithmetic (same bits).  Exactly one of x (f32 NHWC)
+ * or x3 (bf16x3 activation planes, x_plane apart) is given; y (the conv
+ * output, NHWC) may be NULL and is then not written.  tile 0 = default. */
+int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N,
+                              int H, int W, int Cin, int ldx, const uint16_t* w3, int Cout,
+                              int Kpad, int KH, int KW, int stride, int pad, int dil,
+                              const float* scale, const float* shift, const float* residual,
+                              float* y, int Ho, int Wo, const int32_t* splits, int S,
+                              int max_ave, float* pps_out, int tile, void* stream);
+/* Rows and columns of the tile a pipelined GEMM id launches (0 if none);
+ * planes != 0: with bf16x3-plane activations. */
+int pps_x3p_tile_shape(int tile, int planes, int* rows, int* cols);
+
 /* MaxPool kernel k, stride s, pad p (padding never wins), NHWC
  * (ResNet.py:255 `pool1`). */
 int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k,

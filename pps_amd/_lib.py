@@ -66,6 +66,11 @@ SIGNATURES = {
                               c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr,
                               c_ptr, c_int, c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int,
                               c_ptr],
+    'pps_conv2d_bn_act_pps_x3p': [c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int,
+                                  c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_ptr, c_int,
+                                  c_int, c_ptr, c_int, c_ptr],
+    'pps_x3p_tile_shape': [c_int, c_int, c_ptr, c_ptr],
     'pps_conv2d_bn_act_x3p_splitk': [c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int,
                                      c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_i64, c_int,

@@ -510,6 +510,74 @@ int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane, i
                    y_plane);
 }
 
+int pps_x3p_tile_shape(int tile, int planes, int* rows, int* cols) {
+  PPS_ENFORCE(rows && cols, "null pointer");
+  *rows = x3p_tile_rows(tile, planes != 0);
+  *cols = x3p_tile_cols(tile, planes != 0);
+  return PPS_OK;
+}
+
+// The last res5 conv with the part pooling fused into its epilogue
+// (ResNet.py:276-333 res5_2 branch2c + Sum + Relu, then bpm_heads.py:18-55 /
+// pps_heads.py:38-80): conv + BN + residual + ReLU on a pipelined tile whose
+// rows are exactly one image (Ho * Wo); each tile pools its image's strips
+// and writes the 2^S - 1 part subsets into pps_out [2^S - 1][N][Cout] as
+// pps_part_power_set does (same bits).  y (the conv output) may be null: it
+// is then never written.
+int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N,
+                              int H, int W, int Cin, int ldx, const uint16_t* w3, int Cout,
+                              int Kpad, int KH, int KW, int stride, int pad, int dil,
+                              const float* scale, const float* shift, const float* residual,
+                              float* y, int Ho, int Wo, const int32_t* splits, int S,
+                              int max_ave, float* pps_out, int tile, void* stream) {
+  PPS_ENFORCE((x != nullptr) != (x3 != nullptr), "exactly one of x / x planes must be given");
+  PPS_ENFORCE(w3 && scale && shift && residual && pps_out && splits, "null pointer");
+  PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cout % 4 == 0, "bad shape");
+  PPS_ENFORCE(Cin % 32 == 0 && ldx % 8 == 0 && ldx >= Cin && Kpad == KH * KW * Cin,
+              "pipelined conv: Cin % 32 == 0, Kpad == KH*KW*Cin");
+  PPS_ENFORCE(KH * KW <= 64 && stride >= 1 && dil >= 1 && pad >= 0, "bad filter");
+  PPS_ENFORCE(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 &&
+                  Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
+              "output size does not match conv arithmetic");
+  PPS_ENFORCE(S >= 1 && S <= kPpsFuseMaxStrips, "1..10 strips");
+  int hsum = 0;
+  for (int j = 0; j < S; ++j) {
+    PPS_ENFORCE(splits[j] > 0, "strip heights must be positive");
+    hsum += splits[j];
+  }
+  PPS_ENFORCE(hsum == Ho, "strip heights must sum to the output height");
+  const bool pl = x3 != nullptr;
+  if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
+  PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= 128,
+              "the fused pooling needs a pipelined tile of exactly Ho*Wo = " +
+                  std::to_string(Ho * Wo) + " rows and <= 128 columns, tile " +
+                  std::to_string(tile) + " has " + std::to_string(x3p_tile_rows(tile, pl)));
+  PPS_ENFORCE((int64_t)N * H * W * ldx * (pl ? 2 : 4) < kMaxBufBytes, "input larger than 2 GiB");
+  PPS_ENFORCE((int64_t)(1 << S) * N * Cout < (1ll << 31), "part output too large");
+  PPS_ENFORCE(aligned16(pl ? (const void*)x3 : (const void*)x) && aligned16(w3) &&
+                  aligned16(scale) && aligned16(shift) && aligned16(residual) &&
+                  (!y || aligned16(y)),
+              "16-byte aligned pointers");
+  PPS_ENFORCE(!pl || x_plane >= (int64_t)N * H * W * ldx, "x plane stride too small");
+  GemmParams p{};
+  p.splitk = 1;
+  p.a = x; p.H = H; p.W = W; p.Cin = Cin; p.lda = ldx;
+  p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * (pl ? 2 : 4));
+  if (pl) { p.a = nullptr; p.a3 = x3; p.a_plane = x_plane; }
+  p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = dil;
+  p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
+  p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
+  p.b3 = w3; p.b_plane = (int64_t)Cout * Kpad; p.b_bytes = (uint32_t)(p.b_plane * 2);
+  p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = Cout;
+  p.out = y; p.ldo = Cout; p.relu = 1; p.tile = tile;
+  p.pps_out = pps_out; p.pps_S = S; p.pps_max_ave = max_ave ? 1 : 0; p.pps_nimg = N;
+  p.pps_write_y = y ? 1 : 0;
+  for (int j = 0; j < S; ++j) p.pps_h[j] = splits[j];
+  PPS_ENFORCE(x3p_eligible(p, EPI_CONV | EPI_F_RES | EPI_F_RELU), "shape not eligible for the pipelined GEMM");
+  return launch_gemm_x3p(p, EPI_CONV | EPI_F_RES | EPI_F_RELU | EPI_F_PPS, 1, as_stream(stream),
+                         tile - GEMM_TILE_P_FIRST);
+}
+
 static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                            int KH, int KW, int stride, int pad, const float* x2, int H2,
                            int W2, int Cin2, int ldx2, int stride2, const void* w, int x3,

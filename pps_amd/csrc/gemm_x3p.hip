@@ -174,6 +174,9 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
 // the same order as conv_epilogue_t (identical bits).
 template <int BM, int BN>
 constexpr int lds_epi_bytes() { return BM * (BN + 4) * 4; }
+#ifndef X3P_PPS_ABL
+#define X3P_PPS_ABL 0  // probes only: 1 = no strip pooling, 2 = no subsets, 3 = neither
+#endif
 #ifndef X3P_RES_PREFETCH
 #define X3P_RES_PREFETCH 16  // residual vectors per thread requested early (0: off)
 #endif
@@ -189,6 +192,7 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
+  constexpr bool PPS = (EPI & EPI_F_PPS) != 0;
   float* t = reinterpret_cast<float*>(lds);
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
   float* __restrict__ out = p.out + obase;
@@ -244,7 +248,12 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       if (HAS_RES) v[e] += rv[e];
       if (RELU) v[e] = fmaxf(v[e], 0.f);
     }
-    *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+    if (PPS) {  // the pooling below reads the tile back from LDS
+      *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
+      if (p.pps_write_y) *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+    } else {
+      *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+    }
   };
   if constexpr (PRE) {
 #pragma unroll
@@ -257,6 +266,117 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
         if (row < mrem && col < nrem) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
       }
       finish(idx, rv);
+    }
+  }
+  if constexpr (PPS) {
+    // The tile is one image (BM = Ho * Wo rows, row-major positions) x BN
+    // channels.  Per (strip, channel): sum and max over the strip's rows in
+    // row-major order, then the 2^S - 1 subsets -- the arithmetic of
+    // part_power_set_v3_kernel (feature_ops.hip), so the bits are the same.
+    __syncthreads();
+    float* s_ave = t + BM * LD;
+    float* s_max = s_ave + kPpsFuseMaxStrips * BN;
+    // (work split by whole waves: the strip / subset group is wave-uniform,
+    // so the strip table is read with scalar loads)
+    const int W = p.Wo, NS5 = p.pps_S;
+    constexpr int CB = BN / 64;  // 64-channel slices per tile
+    static_assert(BN % 64 == 0, "fused pooling: BN must be a multiple of 64");
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ln = threadIdx.x & 63;
+    for (int it = wv; it < ((X3P_PPS_ABL & 1) ? 0 : NS5 * CB); it += NT / 64) {
+      const int j = it / CB, c = (it - j * CB) * 64 + ln;
+      int r0 = 0;
+      for (int q = 0; q < j; ++q) r0 += p.pps_h[q];
+      const int cnt = p.pps_h[j] * W;
+      const float* colp = t + (r0 * W) * LD + c;
+      float sum = 0.f, mx = -INFINITY;
+#pragma unroll 16
+      for (int e = 0; e < cnt; ++e) {
+        const float v = colp[e * LD];
+        sum += v;
+        mx = fmaxf(mx, v);
+      }
+      s_ave[j * BN + c] = sum / (float)cnt;
+      s_max[j * BN + c] = mx;
+    }
+    __syncthreads();
+    // subsets.  S <= 5 (Market: 5 strips): one lane per channel builds all
+    // 2^S - 1 subsets in increasing order, each from the subset without its
+    // highest strip plus that strip -- the same ascending-order sum as the
+    // standalone kernel, one add and one max per subset.  Larger S: thread
+    // (channel, group of 8 subsets) with the standalone loop.
+    const int img = m0 / (p.Ho * p.Wo);
+    const int nsub = (1 << NS5) - 1;
+    float* po = p.pps_out + (int64_t)img * p.Ncol + n0;
+    const int64_t sub_stride = (int64_t)p.pps_nimg * p.Ncol;
+    if (NS5 <= 5) {
+      for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : CB); o += NT / 64) {
+        const int cc = o * 64 + ln;
+        if (cc >= nrem) continue;
+        float av[5], mv[5], ss[32], sm[32];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          av[q] = q < NS5 ? s_ave[q * BN + cc] : 0.f;
+          mv[q] = q < NS5 ? s_max[q * BN + cc] : 0.f;
+        }
+#pragma unroll
+        for (int i = 1; i < 32; ++i) {
+          const int top = 31 - __builtin_clz(i), rest = i & ~(1 << top);
+          ss[i] = rest ? ss[rest] + av[top] : av[top];
+          sm[i] = rest ? fmaxf(sm[rest], mv[top]) : mv[top];
+          if (i <= nsub) {
+            const float v = p.pps_max_ave
+                                ? ss[i] * (1.f / (float)__builtin_popcount(i)) + sm[i]
+                                : 0.f;
+            if (p.pps_max_ave) po[(int64_t)(i - 1) * sub_stride + cc] = v;
+          }
+        }
+        if (!p.pps_max_ave) {  // Max-only: the max of the strip averages
+          float mx[32];
+#pragma unroll
+          for (int i = 1; i < 32; ++i) {
+            const int top = 31 - __builtin_clz(i), rest = i & ~(1 << top);
+            mx[i] = rest ? fmaxf(mx[rest], av[top]) : av[top];
+            if (i <= nsub) po[(int64_t)(i - 1) * sub_stride + cc] = mx[i];
+          }
+        }
+      }
+    } else {
+      const int ngrp = (nsub + 7) / 8;
+      for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : ngrp * CB); o += NT / 64) {
+        const int g = o / CB, cc = (o - g * CB) * 64 + ln;
+        if (cc >= nrem) continue;
+        float av[kPpsFuseMaxStrips], mv[kPpsFuseMaxStrips];
+#pragma unroll
+        for (int q = 0; q < kPpsFuseMaxStrips; ++q) {
+          av[q] = q < NS5 ? s_ave[q * BN + cc] : 0.f;
+          mv[q] = q < NS5 ? s_max[q * BN + cc] : 0.f;
+        }
+        for (int i = 8 * g + 1; i <= 8 * g + 8 && i <= nsub; ++i) {
+          float v;
+          if (p.pps_max_ave) {
+            float sm = 0.f, mx = -INFINITY;
+            int k = 0;
+            bool first = true;
+#pragma unroll
+            for (int q = 0; q < kPpsFuseMaxStrips; ++q)
+              if (q < NS5 && (i & (1 << q))) {
+                sm = first ? av[q] : sm + av[q];
+                first = false;
+                mx = fmaxf(mx, mv[q]);
+                ++k;
+              }
+            v = sm * (1.f / (float)k) + mx;
+          } else {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int q = 0; q < kPpsFuseMaxStrips; ++q)
+              if (q < NS5 && (i & (1 << q))) mx = fmaxf(mx, av[q]);
+            v = mx;
+          }
+          po[(int64_t)(i - 1) * sub_stride + cc] = v;
+        }
+      }
     }
   }
 }
@@ -465,16 +585,23 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #ifndef X3P_LDSEPI
 #define X3P_LDSEPI 1
 #endif
-  constexpr bool LDSEPI = X3P_LDSEPI && !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
+  constexpr bool PPSEPI = (EPI & EPI_F_PPS) != 0;  // needs the LDS epilogue
+  constexpr int PPS_BYTES = PPSEPI ? 2 * kPpsFuseMaxStrips * BN * 4 : 0;
+  static_assert(!PPSEPI || lds_epi_bytes<BM, BN>() + PPS_BYTES <= 160 * 1024,
+                "part-power-set epilogue does not fit in LDS");
+  constexpr bool LDSEPI = (X3P_LDSEPI || PPSEPI) &&
+                          !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
                           lds_epi_bytes<BM, BN>() <= 160 * 1024 &&
-                          !(BM == 192 && BN == 128 && NW == 8);
+                          (PPSEPI || !(BM == 192 && BN == 128 && NW == 8));
 #ifndef X3P_DISTLDS
 #define X3P_DISTLDS 1
 #endif
   constexpr bool DISTLDS = X3P_DISTLDS && (EPI & EPI_DIST) != 0 &&
                            lds_epi_bytes<BM, BN>() <= NS * STAGE;
   constexpr int LDS_BYTES =
-      (LDSEPI && lds_epi_bytes<BM, BN>() > NS * STAGE) ? lds_epi_bytes<BM, BN>() : NS * STAGE;
+      (LDSEPI && lds_epi_bytes<BM, BN>() + PPS_BYTES > NS * STAGE)
+          ? lds_epi_bytes<BM, BN>() + PPS_BYTES
+          : NS * STAGE;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
   const int lane = threadIdx.x & 63;
@@ -876,7 +1003,30 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
       set_error("tile not built for bf16-plane activations");
       return PPS_ERR_INVALID_ARG;
     }
-  } else if (p.a3) {
+  }
+  if (epi & EPI_F_PPS) {
+    // the fused part-power-set epilogue: conv + BN + residual + ReLU, one
+    // image per 192-row tile (Market's 24 x 8 res5 output)
+    if constexpr (BM == 192 && BN <= 128) {
+      if (epi != (C | RS | RL | EPI_F_PPS)) {
+        set_error("part-power-set epilogue: conv + BN + residual + ReLU only");
+        return PPS_ERR_INVALID_ARG;
+      }
+      if (p.a3) {
+        if constexpr (NSP != 0) launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL | EPI_F_PPS, true, S>(p, batch, stream);
+        else { set_error("tile not built for bf16-plane activations"); return PPS_ERR_INVALID_ARG; }
+      } else {
+        launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | EPI_F_PPS, false, S>(p, batch, stream);
+      }
+      PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+      return PPS_OK;
+    } else {
+      set_error("part-power-set epilogue needs a 192-row tile with at most 128 columns");
+      return PPS_ERR_INVALID_ARG;
+    }
+  }
+  if constexpr (NSP != 0) {
+  if (p.a3) {
     switch (epi) {
       case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSP, EPI_DIST, true, S>(p, batch, stream); break;
       case C: launch_one_p<BM, BN, WM, WN, NSP, C, true, S>(p, batch, stream); break;
@@ -892,6 +1042,7 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
     }
     PPS_CHECK_LAUNCH("gemm_x3p_kernel");
     return PPS_OK;
+  }
   }
   switch (epi) {
     case EPI_DIST: launch_one_p<BM, BN, WM, WN, NSF, EPI_DIST, false, S>(p, batch, stream); break;
@@ -967,6 +1118,41 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
     default:
       set_error("unknown pipelined GEMM variant " + std::to_string(v));
       return PPS_ERR_INVALID_ARG;
+  }
+}
+
+// Rows (BM) of the tile a pipelined id launches (as launch_variant /
+// launch_gemm_x3p map it), 0 for a non-pipelined id.
+int x3p_tile_rows(int tile, bool a3) {
+  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
+  if (tile == GEMM_TILE_P16_192x128W42) return a3 ? 128 : 192;
+  if (tile == GEMM_TILE_P16_192x64W41) return 192;
+  if (tile == GEMM_TILE_P16_96x128W22) return a3 ? 128 : 96;
+  constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
+  const int v = (tile - GEMM_TILE_P_FIRST) % NV;
+  const bool s16 = tile >= GEMM_TILE_P16_FIRST;
+  switch (v) {
+    case 0: case 2: case 5: case 7: return 128;
+    case 1: case 3: return 192;
+    case 4: return 256;
+    case 6: return (a3 || s16) ? 128 : 192;
+    case 8: return a3 ? 128 : 192;
+    default: return 0;
+  }
+}
+
+// Columns (BN) of that tile.
+int x3p_tile_cols(int tile, bool a3) {
+  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
+  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22) return 128;
+  if (tile == GEMM_TILE_P16_192x64W41) return 64;
+  constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
+  const int v = (tile - GEMM_TILE_P_FIRST) % NV;
+  (void)a3;
+  switch (v) {
+    case 2: case 3: return 64;
+    case 5: case 6: return 256;
+    default: return 128;
   }
 }
 

@@ -54,7 +54,8 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 constexpr int64_t kMaxBufBytes = (int64_t)1 << 31;  // buffer-resource addressing limit
 enum Epi {
   EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16,
-  EPI_F_PLANES = 32  // gemm_x3p.hip: result written as three bf16 planes (out3)
+  EPI_F_PLANES = 32,  // gemm_x3p.hip: result written as three bf16 planes (out3)
+  EPI_F_PPS = 64      // gemm_x3p.hip: + strip pooling and part power set of each image
 };
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
@@ -151,12 +152,23 @@ struct GemmParams {
   int64_t a_plane;
   uint16_t* out3;
   int64_t out_plane;
+  // EPI_F_PPS (pipelined conv whose M tile is exactly one image, BM = Ho*Wo):
+  // the tile's BN + residual + ReLU output is pooled per horizontal strip
+  // (pps_h rows each, average and max) and combined into the 2^S - 1 part
+  // subsets, written to pps_out [2^S - 1][pps_nimg][Ncol] exactly as
+  // pps_part_power_set would; out is written only if pps_write_y
+  float* pps_out;
+  int pps_S, pps_max_ave, pps_nimg, pps_write_y;
+  int pps_h[10];
 };
+constexpr int kPpsFuseMaxStrips = 10;
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
 int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream);
 bool x3p_eligible(const GemmParams& p, int epi);
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant);
+int x3p_tile_rows(int tile, bool a3);  // rows (BM) of a pipelined tile id, 0 if none
+int x3p_tile_cols(int tile, bool a3);  // its columns (BN)
 int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream_t stream);
 int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream);
 int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,

@@ -274,7 +274,7 @@ def pack_conv_weight(w, cin_pad=None):
 # Device model
 # ---------------------------------------------------------------------------
 MAX_SPLITK = 4  # conv split-K factors autotune tries (2..MAX_SPLITK)
-GEMM_OPS = ('conv', 'conv_dual', 'heads', 'stem_pool')  # MFMA layers of a forward
+GEMM_OPS = ('conv', 'conv_dual', 'heads', 'stem_pool', 'conv_pps')  # MFMA layers of a forward
 
 
 class PPSModel(object):
@@ -285,7 +285,7 @@ class PPSModel(object):
     """
 
     def __init__(self, blobs, device='cuda', plan=None, fuse_shortcut=True, math=None,
-                 act_planes=None, fused_stem=None):
+                 act_planes=None, fused_stem=None, fused_pps=None):
         """math: 'x3' (default; f32 products on bf16 matrix cores, weights
         split once into three bf16 planes -- gemm_x3.hip) or 'f32' (exact
         f32 MFMA, gemm_f32.hip).  Env PPS_MATH overrides the default.
@@ -297,7 +297,13 @@ class PPSModel(object):
         skips the operand split at the price of 6 instead of 4 bytes per
         element.  Which edges use planes is a speed choice made per edge by
         autotune() (heuristic before that: the 3x3 convs with Cin >= 256);
-        the bits are the same either way."""
+        the bits are the same either way.
+
+        fused_stem / fused_pps (x3 only; default on, env PPS_FUSED_STEM=0 /
+        PPS_FUSED_PPS=0 disable): conv1 + BN + ReLU + pool1 as one kernel;
+        the last res5 conv with the part pooling in its epilogue (its 100 MB
+        output is then never written -- `res5_2_sum` is not in buffers()).
+        Both give the bits of the unfused pair on the same GEMM tile."""
         self.math = math or ops.default_math()
         if self.math not in ('x3', 'f32'):
             raise ValueError("math must be 'x3' or 'f32', got %r" % self.math)
@@ -371,6 +377,9 @@ class PPSModel(object):
         self.fused_stem = bool(fused_stem) and self.math == 'x3'
         if self.fused_stem:
             self._fuse_stem(blobs)
+        if fused_pps is None:
+            fused_pps = os.environ.get('PPS_FUSED_PPS', '1') != '0'
+        self.fused_pps = bool(fused_pps) and self.math == 'x3' and self._fuse_pps()
         if act_planes is None:
             act_planes = os.environ.get('PPS_ACT_PLANES', '1') != '0'
         self.act_planes = bool(act_planes) and self.math == 'x3'
@@ -397,6 +406,38 @@ class PPSModel(object):
                 self.layers[i:i + 2] = [F]
                 return
 
+    def _fuse_pps(self):
+        """Replace the last conv (+ residual + ReLU) and the part pooling that
+        is its only reader by one 'conv_pps' layer (pooling in the GEMM
+        epilogue).  Returns whether a pair was fused."""
+        for i, L in enumerate(self.layers[:-1]):
+            P = self.layers[i + 1]
+            if (L['op'] == 'conv' and L.get('residual') and L['relu'] and
+                    P['op'] == 'pps' and P['input'] == L['output'] and
+                    L['output'] != self.plan.output and L['cin_eff'] % 32 == 0 and
+                    L['kpad'] == L['k'] ** 2 * L['cin_eff'] and
+                    sum(1 for M in self.layers for key in ('input', 'input2', 'residual')
+                        if M.get(key) == L['output']) == 1):
+                F = dict(L, op='conv_pps', output=P['output'], conv_output=L['output'],
+                         split_arr=P['split_arr'], max_ave=P['max_ave'],
+                         prefixes=P['prefixes'], pps_name=P.get('name', P['output']))
+                self.layers[i:i + 2] = [F]
+                return True
+        return False
+
+    def pps_tiles(self, L):
+        """Tiles the fused conv + pooling can run on: pipelined, exactly one
+        image (Ho x Wo rows) per tile, <= 128 columns (empty: unfused fallback)."""
+        n, ho, wo, co = self._shapes[L['conv_output']]
+        planes = bool(L.get('planes_in'))
+        key = (ho * wo, planes)
+        cache = L.setdefault('_pps_tiles', {})
+        if key not in cache:
+            cache[key] = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)
+                          if ops.tile_shape(t, planes)[0] == ho * wo and
+                          0 < ops.tile_shape(t, planes)[1] <= 128]
+        return cache[key]
+
     def _plane_edges(self):
         """(producer, consumer) conv pairs whose tensor may travel as bf16x3
         planes: the producer's output has exactly one reader, a plain conv
@@ -412,7 +453,7 @@ class PPSModel(object):
             rs = readers.get(L['output'], [])
             if (L['op'] == 'conv' and L['cin_eff'] % 4 == 0 and L['cout'] % 4 == 0
                     and L['output'] != self.plan.output and len(rs) == 1
-                    and rs[0][0]['op'] == 'conv' and rs[0][1] == 'input'
+                    and rs[0][0]['op'] in ('conv', 'conv_pps') and rs[0][1] == 'input'
                     and rs[0][0]['cin_eff'] % 32 == 0):
                 edges.append((L, rs[0][0]))
         return edges
@@ -462,6 +503,12 @@ class PPSModel(object):
             elif L['op'] == 'pps':
                 n, h, w, c = shapes[L['input']]
                 shapes[L['output']] = (len(L['prefixes']), n, c)
+            elif L['op'] == 'conv_pps':
+                n, h, w, _ = shapes[L['input']]
+                ho = (h + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
+                wo = (w + 2 * L['pad'] - L['dil'] * (L['k'] - 1) - 1) // L['stride'] + 1
+                shapes[L['conv_output']] = (n, ho, wo, L['cout'])
+                shapes[L['output']] = (len(L['prefixes']), n, L['cout'])
             elif L['op'] == 'heads':
                 shapes[L['output']] = (N, len(L['prefixes']) * L['dim_inner'])
                 shapes[L['output'] + '_partials'] = (HEAD_SPLITK, N,
@@ -475,8 +522,8 @@ class PPSModel(object):
             if L['op'] == 'stem_pool':
                 hc, wc = L['conv_hw']
                 L['flops'] = 2.0 * N * hc * wc * L['cout'] * L['k'] * L['k'] * L['cin']
-            elif L['op'] in ('conv', 'conv_dual'):
-                n, ho, wo, co = shapes[L['output']]
+            elif L['op'] in ('conv', 'conv_dual', 'conv_pps'):
+                n, ho, wo, co = shapes[L.get('conv_output', L['output'])]
                 L['flops'] = 2.0 * n * ho * wo * co * (L['k'] * L['k'] * L['cin'] +
                                                       L.get('shortcut_cin', 0))
             elif L['op'] == 'heads':
@@ -499,6 +546,13 @@ class PPSModel(object):
                     b += 4 * n * ho * wo * co
                 if L['op'] == 'conv_dual':
                     b += 4 * np.prod(shapes[L['input2']])
+                L['bytes'] = float(b)
+            elif L['op'] == 'conv_pps':
+                # input + residual + weights read, the part subsets written (the
+                # conv output itself never leaves the chip)
+                n, ho, wo, co = shapes[L['conv_output']]
+                b = 4 * np.prod(shapes[L['input']]) + 4 * n * ho * wo * co
+                b += wbytes * co * L['k'] * L['k'] * L['cin'] + 4 * np.prod(shapes[L['output']])
                 L['bytes'] = float(b)
             elif L['op'] == 'heads':
                 nb = len(L['prefixes'])
@@ -555,6 +609,22 @@ class PPSModel(object):
         elif op == 'pps':
             ops.part_power_set(bufs[L['input']], L['split_arr'], L['max_ave'],
                                bufs[L['output']])
+        elif op == 'conv_pps':
+            res = bufs[L['residual']]
+            ok = self.pps_tiles(L)
+            if ok:
+                t = tile if tile in ok else ok[0]
+                ops.conv2d_bn_act_pps(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+                                      L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
+                                      res, L['split_arr'], L['max_ave'], bufs[L['output']],
+                                      y=None, tile=t)
+            else:   # no tile holds exactly one image: conv, then the pooling kernel
+                ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'],
+                                      L['k'], L['stride'], L['pad'], L['dil'], L['scale'],
+                                      L['shift'], res, True, bufs[L['conv_output']],
+                                      tile=tile if tile >= ops.TILE_P_FIRST else 0)
+                ops.part_power_set(bufs[L['conv_output']], L['split_arr'], L['max_ave'],
+                                   bufs[L['output']])
         elif op == 'heads':
             y = bufs[L['output']] if out is None or self.layers[-1] is not L else out
             part = bufs[L['output'] + '_partials']
@@ -626,6 +696,8 @@ class PPSModel(object):
             lc = cands
             if L.get('planes_in') or L.get('planes_out'):
                 lc = [t for t in cands if t >= ops.TILE_P_FIRST] or [0]
+            if L['op'] == 'conv_pps':
+                lc = [t for t in cands if t in self.pps_tiles(L)] or [0]
             times = {t: time_tile(L, t, reps) for t in lc}
             best = sorted(times, key=times.get)[:finalists]
             final = {t: time_tile(L, t, final_reps) for t in best}
@@ -637,7 +709,7 @@ class PPSModel(object):
             self.set_planes([])
         report, cost = {}, {}
         for L in self.layers:
-            if L['op'] not in ('conv', 'conv_dual', 'heads'):
+            if L['op'] not in ('conv', 'conv_dual', 'heads', 'conv_pps'):
                 continue
             cost[id(L)], times = tune(L)
             report[L.get('name', L['output'])] = (L['tile'], times)
@@ -717,7 +789,7 @@ class PPSModel(object):
     def tiles(self):
         """{layer name: tile id} of the GEMM layers (0 = heuristic)."""
         return {L.get('name', L['output']): int(L.get('tile', 0)) for L in self.layers
-                if L['op'] in ('conv', 'conv_dual', 'heads')}
+                if L['op'] in ('conv', 'conv_dual', 'heads', 'conv_pps')}
 
     def set_tiles(self, tiles):
         """Apply a tiles() mapping (e.g. a saved autotune result)."""

@@ -435,6 +435,44 @@ def conv2d_bn_act(x, cin, w, kpad, k, stride, pad, dil, scale, shift, residual, 
     return y
 
 
+def tile_shape(tile, planes=False):
+    """(rows, cols) of the tile a pipelined GEMM id launches ((0, 0) if none)."""
+    r, c = _lib.ctypes.c_int(0), _lib.ctypes.c_int(0)
+    call('pps_x3p_tile_shape', int(tile), int(bool(planes)), _lib.ctypes.addressof(r),
+         _lib.ctypes.addressof(c))
+    return r.value, c.value
+
+
+def conv2d_bn_act_pps(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, residual, split,
+                      max_ave, pps_out, y=None, tile=0):
+    """The last res5 conv (+ BN + residual + ReLU) with the part pooling fused
+    into its epilogue (pps_conv2d_bn_act_pps_x3p): pps_out [2^S-1, N, Cout]
+    gets what part_power_set would compute from the conv output; y (NHWC, or
+    None = not written) the conv output itself.  x: f32 NHWC or bf16x3
+    planes (act_planes)."""
+    xs = x.shape[1:] if _is_planes(x) else x.shape
+    N, H, W, ldx = xs
+    nsub, n2, Cout = pps_out.shape
+    split = np.ascontiguousarray(split, dtype=np.int32)
+    Ho = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    if nsub != (1 << len(split)) - 1 or n2 != N:
+        raise RuntimeError('pps_out must be [2^S - 1, N, Cout]')
+    if tuple(residual.shape) != (N, Ho, Wo, Cout) or (y is not None and
+                                                       tuple(y.shape) != (N, Ho, Wo, Cout)):
+        raise RuntimeError('residual / y must be [N, Ho, Wo, Cout]')
+    if _is_planes(x):
+        xp, x3, xpl = 0, _dev(x, 'x planes', torch.int16), x[0].numel()
+    else:
+        xp, x3, xpl = _dev(x, 'x'), 0, 0
+    call('pps_conv2d_bn_act_pps_x3p', xp, x3, xpl, N, H, W, cin, ldx,
+         _dev(w3, 'w3', torch.int16), Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'),
+         _dev(shift, 'shift'), _dev(residual, 'residual'), _dev(y, 'y') if y is not None else 0,
+         Ho, Wo, split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
+         _dev(pps_out, 'pps_out'), int(tile), _stream())
+    return pps_out
+
+
 def act_planes(shape, device):
     """Buffer for a bf16x3 activation tensor: int16 [3, N, H, W, C] holding
     hi, mid, lo planes with x = hi + mid + lo exactly (split as the x3 GEMMs

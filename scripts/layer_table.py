@@ -28,7 +28,7 @@ def main():
     layers = json.load(open(sys.argv[1]))
     d = sys.argv[2]
     gemm = [(k, v) for k, v in layers.items() if v['op'] in
-            ('conv', 'conv_dual', 'heads', 'stem_pool')]
+            ('conv', 'conv_dual', 'heads', 'stem_pool', 'conv_pps')]
     n = len(gemm)
     f = [v for nm, v in load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0],
                              'FETCH_SIZE') if is_mfma(nm)][-n:]

@@ -142,7 +142,9 @@ def test_full_forward_vs_oracle(math):
     x = (rng.randn(3, 3, 384, 128) * 50).astype(np.float32)
     ref, kept = GraphForward(blobs)(x, keep=('res2_2_sum', 'res3_3_sum', 'res4_5_sum',
                                              'res5_2_sum', 'reid_feature_concat'))
-    m = model.PPSModel(blobs, math=math)
+    # (fused_pps=False: the res5 output is materialised for the check below;
+    # the fused pooling is test_conv_pps_* / test_fused_pps_model_*)
+    m = model.PPSModel(blobs, math=math, fused_pps=False)
     xin = np.zeros((3, 384, 128, 4), np.float32)
     xin[..., :3] = x.transpose(0, 2, 3, 1)
     out = m.forward(_cuda(xin)).cpu().numpy()
@@ -360,3 +362,77 @@ def test_fused_stem_model_matches_two_kernel_stem():
     pb = b.buffers()['pool1'].cpu().numpy()
     assert np.abs(pa - pb).max() / np.abs(pb).max() < 2e-6
     np.testing.assert_allclose(fa, fb, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize('planes', [False, True])
+def test_conv_pps_matches_conv_then_pooling(planes):
+    """The last res5 conv with the part pooling in its epilogue
+    (pps_conv2d_bn_act_pps_x3p) == the same conv on the same tile followed by
+    pps_part_power_set, bit for bit, on every eligible tile (one image of
+    24 x 8 per 192-row tile); the conv output itself when requested."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(11)
+    N, H, W, Cin, Cout = 3, 24, 8, 512, 2048
+    x = _cuda((rng.randn(N, H, W, Cin)).astype(np.float32))
+    w = (rng.randn(Cout, Cin, 1, 1) / np.sqrt(Cin)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    sc = _cuda(rng.uniform(0.5, 1.5, Cout).astype(np.float32))
+    sh = _cuda((rng.randn(Cout) * 0.1).astype(np.float32))
+    res = _cuda(rng.randn(N, H, W, Cout).astype(np.float32))
+    split = [5, 5, 4, 5, 5]
+    xa = ops.split_bf16x3(x) if planes else x
+    tiles = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)
+             if ops.tile_shape(t, planes)[0] == H * W and ops.tile_shape(t, planes)[1] <= 128]
+    assert len(tiles) >= (4 if planes else 7), tiles
+    for tile in tiles:
+        y = torch.empty(N, H, W, Cout, device='cuda')
+        ops.conv2d_bn_act_x3p(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, True, y, tile=tile)
+        want = torch.empty(31, N, Cout, device='cuda')
+        ops.part_power_set(y, split, True, want)
+        got = torch.full((31, N, Cout), float('nan'), device='cuda')
+        y2 = torch.full((N, H, W, Cout), float('nan'), device='cuda')
+        ops.conv2d_bn_act_pps(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, split, True, got,
+                              y=y2, tile=tile)
+        np.testing.assert_array_equal(got.cpu().numpy(), want.cpu().numpy(), err_msg=str(tile))
+        np.testing.assert_array_equal(y2.cpu().numpy(), y.cpu().numpy(), err_msg=str(tile))
+        got2 = torch.full((31, N, Cout), float('nan'), device='cuda')
+        ops.conv2d_bn_act_pps(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, split, True, got2,
+                              tile=tile)   # conv output not written
+        np.testing.assert_array_equal(got2.cpu().numpy(), want.cpu().numpy())
+    # Max-only combination (MAX_AVE_FEATURE off)
+    ops.conv2d_bn_act_x3p(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, True, y, tile=tiles[0])
+    ops.part_power_set(y, split, False, want)
+    ops.conv2d_bn_act_pps(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, split, False, got,
+                          tile=tiles[0])
+    np.testing.assert_array_equal(got.cpu().numpy(), want.cpu().numpy())
+    bad = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1) if t not in tiles][0]
+    with pytest.raises(RuntimeError, match='rows'):
+        ops.conv2d_bn_act_pps(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, split, True, got,
+                              tile=bad)
+
+
+def test_fused_pps_model_matches_unfused():
+    """PPSModel with the pooling fused into the last conv == the unfused
+    model on the same tile for that conv: identical features."""
+    from pps_amd import model
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=5)
+    rng = np.random.RandomState(5)
+    xin = np.zeros((2, 384, 128, 4), np.float32)
+    xin[..., :3] = rng.randn(2, 384, 128, 3) * 50
+    a = model.PPSModel(blobs, fused_pps=True)
+    b = model.PPSModel(blobs, fused_pps=False)
+    assert any(L['op'] == 'conv_pps' for L in a.layers)
+    assert not any(L['op'] == 'conv_pps' for L in b.layers)
+    fa = a.forward(_cuda(xin)).cpu().numpy()
+    L = [L for L in a.layers if L['op'] == 'conv_pps'][0]
+    tiles = a.pps_tiles(L)
+    assert tiles
+    a.set_tiles({L['name']: tiles[0]})
+    b.set_tiles({L['name']: tiles[0]})
+    fa = a.forward(_cuda(xin)).cpu().numpy()
+    fb = b.forward(_cuda(xin)).cpu().numpy()
+    np.testing.assert_array_equal(fa, fb)
+    assert L['conv_output'] == 'res5_2_sum'
