@@ -283,7 +283,7 @@ def test_bench_configuration_vs_oracle():
     from oracle import preprocess as pre
     from pps_amd import model, ops
     tf = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                      'profiles', 'r02', 'tiles_v3.json')
+                      'profiles', 'r02', 'tiles_v4.json')
     if not os.path.exists(tf):
         pytest.skip('no committed tiles file')
     _market_cfg()
