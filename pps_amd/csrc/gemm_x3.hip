@@ -279,7 +279,7 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
                                                                                  GEMM_TILE_P_FIRST;
     const int vb = v % (GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST);
     if (!(epi & EPI_DIST) || p.M != p.Ncol || !x3p_eligible(p, epi) || (vb != 0 && vb != 7) ||
-        p.tile >= GEMM_NUM_TILES - 1) {
+        p.tile >= GEMM_TILE_P16_192x128W42) {  // ids 47+ are not square
       set_error("symmetric distance: needs EPI_DIST, M == Ncol and a 128x128 pipelined tile "
                 "(29, 36, 38 or 45)");
       return PPS_ERR_INVALID_ARG;
