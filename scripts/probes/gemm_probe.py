@@ -41,6 +41,8 @@ def main():
     ap.add_argument('--math', default='x3,f32')
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--residual', action='store_true', help='conv + BN + residual Sum + ReLU')
+    ap.add_argument('--planes', action='store_true',
+                    help='x3 only: input as bf16x3 activation planes (conv2d_bn_act_x3p)')
     a = ap.parse_args()
     from pps_amd import model, ops
     for name in a.layers.split(','):
@@ -55,18 +57,26 @@ def main():
         sh = torch.zeros(Cout, device='cuda')
         y = torch.empty(N, Ho, Wo, Cout, device='cuda')
         resid = torch.randn(N, Ho, Wo, Cout, device="cuda") if a.residual else None
+        if a.planes:
+            xp = ops.split_bf16x3(x.reshape(-1, Cin)).reshape(3, N, H, W, Cin)
         flops = 2.0 * N * Ho * Wo * Cout * k * k * Cin
         for math in a.math.split(','):
             wt = w3 if math == 'x3' else wf
             res = []
+            def launch(tile):
+                if a.planes:
+                    ops.conv2d_bn_act_x3p(xp, Cin, w3, kpad, k, s, p, 1, sc, sh, resid, True, y,
+                                          tile=tile)
+                else:
+                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y,
+                                      tile=tile)
             for tile in [int(t) for t in a.tiles.split(',')]:
-                ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y, tile=tile)
+                launch(tile)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
-                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y,
-                                      tile=tile)
+                    launch(tile)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps
