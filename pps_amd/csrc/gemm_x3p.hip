@@ -567,11 +567,19 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
   constexpr int STAGE = A_BYTES + 3 * B_PLANE;
   constexpr int AROWS = A3 ? 16 : 8;    // rows per A piece (1 KiB)
-  constexpr int AI = BM / AROWS / NW;   // A pieces per wave and chunk (per plane if A3)
-  constexpr int BPW = BN / 16 / NW;     // B pieces (16 rows each) per wave, plane and chunk
+  constexpr int NPA = BM / AROWS;       // A pieces per chunk (per plane if A3)
+  constexpr int NPB = BN / 16;          // B pieces (16 rows each) per plane and chunk
+  // Pieces per wave.  Even tiles give every wave the same count (piece
+  // q = wave * AI + i); otherwise the pieces go round-robin (q = i * NW +
+  // wave) and the last slots of some waves are empty -- allowed with two
+  // stages only, whose chunk wait is vmcnt(0) whatever a wave issued.
+  constexpr bool AEVEN = NPA % NW == 0;
+  constexpr bool BEVEN = NPB % NW == 0;
+  constexpr int AI = (NPA + NW - 1) / NW;
+  constexpr int BPW = (NPB + NW - 1) / NW;
   constexpr int NLOAD = (A3 ? 3 : 1) * AI + 3 * BPW;  // DMA instructions per wave and chunk
-  static_assert(AI * AROWS * NW == BM && BPW * 16 * NW == BN,
-                "tile does not split into DMA pieces");
+  static_assert(NPA * AROWS == BM && NPB * 16 == BN, "tile does not split into DMA pieces");
+  static_assert((AEVEN && BEVEN) || NS == 2, "uneven DMA pieces need two LDS stages");
   static_assert(!(A3 && (EPI & EPI_F_DUAL)), "fused shortcut reads f32 activations");
   static_assert(TM >= 1 && TN >= 1 && (BM / WM) % S == 0 && (BN / WN) % S == 0, "wave tile");
   static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
@@ -693,6 +701,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     ra1 = ra;
     ra2 = DUAL ? make_rsrc(p.a2, p.a2_bytes) : ra;
   }
+  // piece of slot i of this wave (>= NPA: an empty slot of an uneven tile)
+  auto apiece = [&](int i) { return AEVEN ? wave * AI + i : i * NW + wave; };
+  auto bpiece = [&](int j) { return BEVEN ? wave * BPW + j : j * NW + wave; };
   int abase[AI];
   uint64_t amask[AI];
   int abase2[AI];
@@ -701,7 +712,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     const int ntaps = p.KH * p.KW;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int rt = A3 ? (wave * AI + i) * 16 + (lane >> 2) : (wave * AI + i) * 8 + (lane >> 3);
+      const int rt = A3 ? apiece(i) * 16 + (lane >> 2) : apiece(i) * 8 + (lane >> 3);
       // first element (of the 32-wide K chunk) this lane fetches
       const int ce = A3 ? 8 * ((lane & 3) ^ ((rt >> 2) & 3)) : 4 * ((lane & 7) ^ ((rt >> 1) & 7));
       const int row = m0 + rt;
@@ -738,7 +749,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   int boff[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
-    const int col = n0 + (wave * BPW + j) * 16 + (lane >> 2);
+    const int col = n0 + bpiece(j) * 16 + (lane >> 2);
     boff[j] = col < p.Ncol ? (col * p.ldb + bcl * 8) * 2 : kOOB;
   }
 
@@ -762,19 +773,21 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const int kofs = (kiss - nch1) * BK * 4;
 #pragma unroll
       for (int i = 0; i < AI; ++i)
-        glds16(ra2, st + (wave * AI + i) * 1024, abase2[i] == kOOB ? kOOB : abase2[i] + kofs);
+        if (AEVEN || apiece(i) < NPA)
+          glds16(ra2, st + apiece(i) * 1024, abase2[i] == kOOB ? kOOB : abase2[i] + kofs);
     } else {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
+        if (!AEVEN && apiece(i) >= NPA) continue;  // wave-uniform: an empty slot
         const bool ok = tt < 64 && ((amask[i] >> tt) & 1ull);
         if (A3) {
           const int off = ok ? (abase[i] + toff + tc) * 2 : kOOB;
-          const unsigned char* d = st + (wave * AI + i) * 1024;
+          const unsigned char* d = st + apiece(i) * 1024;
           glds16(ra, d, off);
           glds16(ra1, d + A_PLANE, off);
           glds16(ra2, d + 2 * A_PLANE, off);
         } else {
-          glds16(ra, st + (wave * AI + i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
+          glds16(ra, st + apiece(i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
         }
       }
       tc += BK;
@@ -788,8 +801,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     const bool kok = kiss * BK + bcl * 8 < p.kb_valid;
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
+      if (!BEVEN && bpiece(j) >= NPB) continue;
       const int off = (kok && boff[j] != kOOB) ? boff[j] + kiss * BK * 2 : kOOB;
-      const unsigned char* d = st + A_BYTES + (wave * BPW + j) * 1024;
+      const unsigned char* d = st + A_BYTES + bpiece(j) * 1024;
       glds16(rb0, d, off);
       glds16(rb1, d + B_PLANE, off);
       glds16(rb2, d + 2 * B_PLANE, off);
@@ -1112,9 +1126,8 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
     // workgroup; 128x128 also two workgroups per CU): res3/res4 3x3 and
     // res4 2c run 6-10 % faster on them
     case 7: return launch_tile_p<128, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
-    case 8:  // plane A: 192 rows do not split into 8 waves x 16-row pieces
-      if (p.a3) return launch_tile_p<128, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
-      return launch_tile_p<192, 128, 2, 4, 2, 0, S>(p, epi, batch, stream);
+    case 8:  // plane A: 12 pieces of 16 rows over 8 waves (uneven, two stages)
+      return launch_tile_p<192, 128, 2, 4, 2, 2, S>(p, epi, batch, stream);
     default:
       set_error("unknown pipelined GEMM variant " + std::to_string(v));
       return PPS_ERR_INVALID_ARG;
@@ -1125,9 +1138,8 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 // launch_gemm_x3p map it), 0 for a non-pipelined id.
 int x3p_tile_rows(int tile, bool a3) {
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
-  if (tile == GEMM_TILE_P16_192x128W42) return a3 ? 128 : 192;
-  if (tile == GEMM_TILE_P16_192x64W41) return 192;
-  if (tile == GEMM_TILE_P16_96x128W22) return a3 ? 128 : 96;
+  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41) return 192;
+  if (tile == GEMM_TILE_P16_96x128W22 || tile == GEMM_TILE_P16_96x128W24) return 96;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
   const int v = (tile - GEMM_TILE_P_FIRST) % NV;
   const bool s16 = tile >= GEMM_TILE_P16_FIRST;
@@ -1136,7 +1148,7 @@ int x3p_tile_rows(int tile, bool a3) {
     case 1: case 3: return 192;
     case 4: return 256;
     case 6: return (a3 || s16) ? 128 : 192;
-    case 8: return a3 ? 128 : 192;
+    case 8: return 192;
     default: return 0;
   }
 }
@@ -1144,7 +1156,9 @@ int x3p_tile_rows(int tile, bool a3) {
 // Columns (BN) of that tile.
 int x3p_tile_cols(int tile, bool a3) {
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
-  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22) return 128;
+  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
+      tile == GEMM_TILE_P16_96x128W24)
+    return 128;
   if (tile == GEMM_TILE_P16_192x64W41) return 64;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
   const int v = (tile - GEMM_TILE_P_FIRST) % NV;
@@ -1158,18 +1172,18 @@ int x3p_tile_cols(int tile, bool a3) {
 
 int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream, int variant) {
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;  // variants per block size
-  if (variant == GEMM_TILE_P16_192x128W42 - GEMM_TILE_P_FIRST) {
-    // f32 activations only (192 rows do not split into 8 waves x 16-row
-    // plane pieces): plane A takes the 8-wave 128x128 tile of the same family
-    if (p.a3) return launch_tile_p<128, 128, 4, 2, 2, 2, 16>(p, epi, batch, stream);
-    return launch_tile_p<192, 128, 4, 2, 2, 0, 16>(p, epi, batch, stream);
-  }
+  // plane A on the 192-row 8-wave and 96-row tiles: 12 / 6 pieces of 16 rows
+  // spread unevenly over the waves (two stages)
+  if (variant == GEMM_TILE_P16_192x128W42 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<192, 128, 4, 2, 2, 2, 16>(p, epi, batch, stream);
   if (variant == GEMM_TILE_P16_192x64W41 - GEMM_TILE_P_FIRST)
     return launch_tile_p<192, 64, 4, 1, 2, 2, 16>(p, epi, batch, stream);
-  if (variant == GEMM_TILE_P16_96x128W22 - GEMM_TILE_P_FIRST) {
-    if (p.a3) return launch_tile_p<128, 128, 2, 2, 2, 2, 16>(p, epi, batch, stream);
-    return launch_tile_p<96, 128, 2, 2, 2, 0, 16>(p, epi, batch, stream);
-  }
+  if (variant == GEMM_TILE_P16_96x128W22 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<96, 128, 2, 2, 2, 2, 16>(p, epi, batch, stream);
+  // 96x128 with 8 waves as 2 x 4 (48 x 32 per wave): 256 tiles for
+  // M = 12,288 x N = 256 at two waves per SIMD
+  if (variant == GEMM_TILE_P16_96x128W24 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<96, 128, 2, 4, 2, 2, 16>(p, epi, batch, stream);
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }

@@ -87,7 +87,9 @@ enum GemmTile {
   // per wave -- 256 tiles for M = 12,288 x N = 256 (res4 2a / 2b)
   GEMM_TILE_P16_192x64W41 = 48,
   GEMM_TILE_P16_96x128W22 = 49,
-  GEMM_NUM_TILES = 50
+  // 50 (16x16x32): 96x128 with 8 waves as 2 x 4 (48 x 32 per wave)
+  GEMM_TILE_P16_96x128W24 = 50,
+  GEMM_NUM_TILES = 51
 };
 
 struct GemmParams {

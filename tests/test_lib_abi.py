@@ -53,21 +53,24 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 def test_pipelined_tile_shapes():
     """pps_x3p_tile_shape (host-only) mirrors the pipelined tile table
     (pps_internal.hpp): the ids the fused part pooling may use are exactly
-    the 192-row tiles with <= 128 columns, fewer with plane activations."""
+    the 192-row tiles with <= 128 columns, with f32 or plane activations."""
     from pps_amd import ops
     want = {29: (128, 128), 30: (192, 128), 31: (128, 64), 32: (192, 64), 33: (256, 128),
             34: (128, 256), 35: (192, 256), 36: (128, 128), 37: (192, 128), 38: (128, 128),
             39: (192, 128), 40: (128, 64), 41: (192, 64), 42: (256, 128), 43: (128, 256),
             44: (128, 256), 45: (128, 128), 46: (192, 128), 47: (192, 128), 48: (192, 64),
-            49: (96, 128)}
-    assert ops.num_tiles() == 49
+            49: (96, 128), 50: (96, 128)}
+    assert ops.num_tiles() == 50
     for t, shape in want.items():
         assert ops.tile_shape(t) == shape, t
-    assert ops.tile_shape(28) == (0, 0) and ops.tile_shape(50) == (0, 0)
-    # plane activations: 192-row 8-wave f32-only tiles fall back to 128 rows
-    assert ops.tile_shape(35, True) == (128, 256) and ops.tile_shape(37, True)[0] == 128
-    assert ops.tile_shape(47, True)[0] == 128 and ops.tile_shape(49, True)[0] == 128
+    assert ops.tile_shape(28) == (0, 0) and ops.tile_shape(51) == (0, 0)
+    # plane activations: only the 192x256 8-wave tile falls back (to 128 rows:
+    # two stages of it would not fit the LDS); the 192-row 8-wave and 96-row
+    # tiles take the planes natively (uneven DMA pieces per wave)
+    assert ops.tile_shape(35, True) == (128, 256) and ops.tile_shape(37, True)[0] == 192
+    assert ops.tile_shape(47, True)[0] == 192 and ops.tile_shape(49, True)[0] == 96
+    assert ops.tile_shape(50, True) == (96, 128)
     pps_f32 = [t for t in want if ops.tile_shape(t)[0] == 192 and ops.tile_shape(t)[1] <= 128]
     pps_pl = [t for t in want if ops.tile_shape(t, True)[0] == 192 and
               ops.tile_shape(t, True)[1] <= 128]
-    assert pps_f32 == [30, 32, 37, 39, 41, 46, 47, 48] and pps_pl == [30, 32, 39, 41, 48]
+    assert pps_f32 == [30, 32, 37, 39, 41, 46, 47, 48] and pps_pl == pps_f32
