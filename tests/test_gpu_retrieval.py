@@ -202,6 +202,28 @@ def test_topk_many_rows_odd_stride(k):
     np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, ref, axis=1))
 
 
+@pytest.mark.parametrize('G', [1, 3, 4, 4097, 8190, 16387, 19889])
+def test_topk_padded_rows_vector_path(G):
+    """16-byte rows (ops.dist_buffer pads the stride to 4 floats) take the
+    dwordx4 path with two chunks of lookahead; the < 4 entries past the last
+    full vector are taken by the scalar tail.  Stable order vs NumPy, with
+    ties and negative distances."""
+    from pps_amd import ops
+    rng = np.random.RandomState(G)
+    Q = 300
+    d = rng.randint(-50, 50, size=(Q, G)).astype(np.float32) / 8
+    d[:, -1] = -100.0  # the very last entry is every row's best
+    buf = ops.dist_buffer(Q, G, 'cuda')
+    assert buf.stride(0) % 4 == 0
+    buf.copy_(torch.from_numpy(d))
+    for k in (1, 21, 100):
+        kk = min(k, G)
+        vals, idx = ops.topk(buf, kk)
+        ref = np.argsort(d, axis=1, kind='stable')[:, :kk]
+        np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+        np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, ref, axis=1))
+
+
 def test_evaluate_vs_golden(golden):
     from pps_amd import reid_dataset_evaluator as gev
     from pps_amd.config import cfg
