@@ -886,7 +886,9 @@ topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
     // s_n) can land before a slower wave has read it
     const int n_now = s_n;
     lds_barrier();
-    if (n_now + chunk > kTopkBuf) cut(n_now, false);
+    // the first chunk enters unfiltered: cut it at once (a 2048-entry select
+    // instead of a 4096-entry one a chunk later) so the next chunks filter
+    if (n_now + chunk > kTopkBuf || (c0 == chunk && n_now > k)) cut(n_now, false);
     const unsigned long long thr = s_thr;
     float dn2[kTopkUnroll];
     load_chunk(c0 + (V4 ? 2 : 1) * chunk, dn2);
