@@ -1138,7 +1138,10 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 // launch_gemm_x3p map it), 0 for a non-pipelined id.
 int x3p_tile_rows(int tile, bool a3) {
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
-  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41) return 192;
+  if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41 ||
+      tile == GEMM_TILE_P16_192x128W42S3)
+    return 192;
+  if (tile == GEMM_TILE_P16_128x128W42S3) return 128;
   if (tile == GEMM_TILE_P16_96x128W22 || tile == GEMM_TILE_P16_96x128W24) return 96;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
   const int v = (tile - GEMM_TILE_P_FIRST) % NV;
@@ -1157,7 +1160,8 @@ int x3p_tile_rows(int tile, bool a3) {
 int x3p_tile_cols(int tile, bool a3) {
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
-      tile == GEMM_TILE_P16_96x128W24)
+      tile == GEMM_TILE_P16_96x128W24 || tile == GEMM_TILE_P16_128x128W42S3 ||
+      tile == GEMM_TILE_P16_192x128W42S3)
     return 128;
   if (tile == GEMM_TILE_P16_192x64W41) return 64;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
@@ -1184,6 +1188,14 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
   // M = 12,288 x N = 256 at two waves per SIMD
   if (variant == GEMM_TILE_P16_96x128W24 - GEMM_TILE_P_FIRST)
     return launch_tile_p<96, 128, 2, 4, 2, 2, 16>(p, epi, batch, stream);
+  // three LDS stages (two chunks in flight behind the one being consumed) on
+  // the 8-wave 128x128 / 192x128 tiles, for long-K GEMMs whose operands come
+  // from the Infinity Cache rather than L2 (distance matrix, res5);
+  // 192-row plane A keeps two stages (uneven pieces)
+  if (variant == GEMM_TILE_P16_128x128W42S3 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<128, 128, 4, 2, 3, 3, 16>(p, epi, batch, stream);
+  if (variant == GEMM_TILE_P16_192x128W42S3 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<192, 128, 4, 2, 3, 2, 16>(p, epi, batch, stream);
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }

@@ -89,7 +89,11 @@ enum GemmTile {
   GEMM_TILE_P16_96x128W22 = 49,
   // 50 (16x16x32): 96x128 with 8 waves as 2 x 4 (48 x 32 per wave)
   GEMM_TILE_P16_96x128W24 = 50,
-  GEMM_NUM_TILES = 51
+  // 51, 52 (16x16x32): 128x128 and 192x128 with 8 waves as 4 x 2 and three
+  // LDS stages (192x128 with plane activations: two)
+  GEMM_TILE_P16_128x128W42S3 = 51,
+  GEMM_TILE_P16_192x128W42S3 = 52,
+  GEMM_NUM_TILES = 53
 };
 
 struct GemmParams {
