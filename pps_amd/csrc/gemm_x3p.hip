@@ -579,7 +579,11 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int BPW = (NPB + NW - 1) / NW;
   constexpr int NLOAD = (A3 ? 3 : 1) * AI + 3 * BPW;  // DMA instructions per wave and chunk
   static_assert(NPA * AROWS == BM && NPB * 16 == BN, "tile does not split into DMA pieces");
-  static_assert((AEVEN && BEVEN) || NS == 2, "uneven DMA pieces need two LDS stages");
+  // Uneven tiles: only a wave's last slot can be empty (round-robin), so a
+  // wave issues NLOAD, NLOAD - (A3 ? 3 : 1) (A slot empty), NLOAD - 3 (B slot
+  // empty) or both fewer DMA instructions per chunk; the chunk wait counts
+  // its own (see chunk_barrier).
+  constexpr int LA = A3 ? 3 : 1;
   static_assert(!(A3 && (EPI & EPI_F_DUAL)), "fused shortcut reads f32 activations");
   static_assert(TM >= 1 && TN >= 1 && (BM / WM) % S == 0 && (BN / WN) % S == 0, "wave tile");
   static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
@@ -830,7 +834,16 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // the stage the next request overwrites (lgkmcnt(0) before it)
   auto chunk_barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait_vmcnt<NLOAD * (NS - 2)>();
+    if constexpr (NS == 2 || (AEVEN && BEVEN)) {
+      wait_vmcnt<NLOAD * (NS - 2)>();
+    } else {  // this wave's own count of younger DMA instructions
+      const bool ea = !AEVEN && apiece(AI - 1) >= NPA;  // wave-uniform
+      const bool eb = !BEVEN && bpiece(BPW - 1) >= NPB;
+      if (!ea && !eb) wait_vmcnt<NLOAD * (NS - 2)>();
+      else if (ea && !eb) wait_vmcnt<(NLOAD - LA) * (NS - 2)>();
+      else if (!ea && eb) wait_vmcnt<(NLOAD - 3) * (NS - 2)>();
+      else wait_vmcnt<(NLOAD - LA - 3) * (NS - 2)>();
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
@@ -1142,7 +1155,9 @@ int x3p_tile_rows(int tile, bool a3) {
       tile == GEMM_TILE_P16_192x128W42S3)
     return 192;
   if (tile == GEMM_TILE_P16_128x128W42S3) return 128;
-  if (tile == GEMM_TILE_P16_96x128W22 || tile == GEMM_TILE_P16_96x128W24) return 96;
+  if (tile == GEMM_TILE_P16_96x128W22 || tile == GEMM_TILE_P16_96x128W24 ||
+      tile == GEMM_TILE_P16_96x128W24S3)
+    return 96;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
   const int v = (tile - GEMM_TILE_P_FIRST) % NV;
   const bool s16 = tile >= GEMM_TILE_P16_FIRST;
@@ -1161,7 +1176,7 @@ int x3p_tile_cols(int tile, bool a3) {
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
       tile == GEMM_TILE_P16_96x128W24 || tile == GEMM_TILE_P16_128x128W42S3 ||
-      tile == GEMM_TILE_P16_192x128W42S3)
+      tile == GEMM_TILE_P16_192x128W42S3 || tile == GEMM_TILE_P16_96x128W24S3)
     return 128;
   if (tile == GEMM_TILE_P16_192x64W41) return 64;
   constexpr int NV = GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST;
@@ -1196,6 +1211,9 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
     return launch_tile_p<128, 128, 4, 2, 3, 3, 16>(p, epi, batch, stream);
   if (variant == GEMM_TILE_P16_192x128W42S3 - GEMM_TILE_P_FIRST)
     return launch_tile_p<192, 128, 4, 2, 3, 2, 16>(p, epi, batch, stream);
+  // 96x128 as 2 x 4 waves with three stages (uneven pieces, per-wave waits)
+  if (variant == GEMM_TILE_P16_96x128W24S3 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<96, 128, 2, 4, 3, 3, 16>(p, epi, batch, stream);
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }

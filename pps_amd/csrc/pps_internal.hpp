@@ -93,7 +93,9 @@ enum GemmTile {
   // LDS stages (192x128 with plane activations: two)
   GEMM_TILE_P16_128x128W42S3 = 51,
   GEMM_TILE_P16_192x128W42S3 = 52,
-  GEMM_NUM_TILES = 53
+  // 53 (16x16x32): 96x128 with 8 waves as 2 x 4 and three LDS stages
+  GEMM_TILE_P16_96x128W24S3 = 53,
+  GEMM_NUM_TILES = 54
 };
 
 struct GemmParams {
