@@ -38,18 +38,44 @@ Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--gpus', type=int, default=None,
+                   help='ranks (one per GPU); > 1 without WORLD_SIZE in the environment '
+                        'launches them (torch.distributed.run, before any GPU call)')
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--batch', type=int, default=64)
     p.add_argument('--no-graph', action='store_true', help='eager launches (no hipGraph)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-e2e', action='store_true',
+                   help='skip the end-to-end JPEG-files stage (e2e block of the line)')
+    p.add_argument('--e2e-images', type=int, default=Q_MARKET + G_MARKET)
     p.add_argument('--dist-reps', type=int, default=5)
     p.add_argument('--no-autotune', action='store_true')
+    p.add_argument('--dry-run', action='store_true',
+                   help='no GPU work: exercise the launch / rendezvous / reporting path only')
     p.add_argument('--tiles-file', default=None,
                    help='JSON {layer: tile}: reuse (if present) or save the autotune result, '
                         'so profiling passes run the same kernels as the timed run')
     return p.parse_args()
+
+
+def launch_ranks(n):
+    """`--gpus n` (n > 1) without a launcher: start n ranks of this script
+    with torch.distributed.run as a CHILD process (this process has touched
+    no GPU and is not replaced), wait, and return its exit code.  Rank 0
+    prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(n), '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+        'HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    return subprocess.call(cmd, env=env)
 
 
 def market_cfg():
@@ -209,19 +235,24 @@ def _pmc_mfma(math, batch):
     return {k: e[k] for k in ('clock_GHz', 'mfma_busy_frac', 'mfma_busy_frac_at_2p4GHz')}
 
 
-def conv_roofline(m, x, reps=20):
-    """Conv-stack roofline from the timed execution: the forward captured in
-    a hipGraph and replayed `reps` times between two HIP events gives the
-    forward's time as the timed step runs it; eager passes with events
-    around every launch (on the kernels' stream; median of five) split it by
-    launch.  The
-    events add ~1-10 us per launch to the eager split, so the split is
-    rescaled to the graph-replay total (ROCm does not allow event nodes inside
-    a captured graph, which would time launches in the replay directly)."""
+def conv_roofline(nm, x, reps=20):
+    """Conv-stack roofline from the timed execution, through the whole-network
+    C entry point: pps_forward captured in a hipGraph and replayed `reps`
+    times between two HIP events on the kernels' stream gives the forward's
+    time as the timed step runs it; eager passes of pps_forward_layers, one
+    layer each with an event between layers (median of five), split it by
+    launch.  The events add ~1-10 us per launch to the eager split, so the
+    split is rescaled to the graph-replay total (ROCm does not allow event
+    nodes inside a captured graph, which would time launches in the replay
+    directly)."""
+    N = int(x.shape[0])
+    layers = nm.layers(N)
+    out = torch.empty((N, nm.feat_dim), dtype=torch.float32, device='cuda')
+    nm.forward(x, out=out)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        m.forward(x)
+        nm.forward(x, out=out)
     for _ in range(3):
         g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -233,40 +264,125 @@ def conv_roofline(m, x, reps=20):
     fwd_ms = e0.elapsed_time(e1) / reps
     splits = []
     for _ in range(5):   # per-launch medians of five eager passes
-        timer = []
-        m.forward(x, timer=timer)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(layers) + 1)]
+        evs[0].record()
+        for i in range(len(layers)):
+            nm.forward_layers(x, i, i + 1, out=out)
+            evs[i + 1].record()
         torch.cuda.synchronize()
-        splits.append([a.elapsed_time(b) for _, _, _, a, b in timer])
-    from pps_amd.model import GEMM_OPS as gemm
+        splits.append([evs[i].elapsed_time(evs[i + 1]) for i in range(len(layers))])
     eager = [float(v) for v in np.median(np.array(splits), axis=0)]
     scale = fwd_ms / sum(eager)
-    conv_ms = scale * sum(t for (_, op, _, _, _), t in zip(timer, eager) if op in gemm)
-    conv_flops = sum(f for _, op, f, _, _ in timer if op in gemm)
-    n_launch = sum(1 for _, op, _, _, _ in timer if op in gemm)
-    per = {}
-    for L, (name, op, f, _, _), t in zip(m.layers, timer, eager):
-        per[name] = dict(op=op, flops=f, ms=t * scale, ms_eager=t, bytes=L.get('bytes', 0.0),
-                         tile=int(L.get('tile', 0)), planes_out=bool(L.get('planes_out')))
+    conv_ms = scale * sum(t for L, t in zip(layers, eager) if L['gemm'])
+    conv_flops = sum(L['flops'] for L in layers if L['gemm'])
+    conv_bytes = sum(L['bytes'] for L in layers if L['gemm'])
+    n_launch = sum(1 for L in layers if L['gemm'])
+    per = {L['name']: dict(op=L['op'], flops=L['flops'], ms=t * scale, ms_eager=t,
+                           bytes=L['bytes'], tile=L['tile'], planes_out=L['planes_out'])
+           for L, t in zip(layers, eager)}
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
-    if m.math == 'x3':
+    if nm.math == 'x3':
         peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv + the fused stem (stem_ring_x3_kernel), f32 products as 6 '
-                                        'bf16 MFMA terms (%d launches/forward)' % n_launch)
+                                        'bf16 MFMA terms (%d launches/forward, run by pps_forward)' % n_launch)
     else:
         peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '
-                                               '(%d launches/forward)' % n_launch)
+                                               '(%d launches/forward, run by pps_forward)' % n_launch)
     return dict(bound='mfma', achieved=round(achieved, 2), peak=round(peak, 1),
                 unit='TFLOP/s', frac=round(achieved / peak, 4),
-                traffic=_pmc_traffic('conv', m.math, x.shape[0]), kernel=kernel,
-                pmc_mfma=_pmc_mfma(m.math, x.shape[0]),
+                traffic=_pmc_traffic('conv', nm.math, N), kernel=kernel,
+                pmc_mfma=_pmc_mfma(nm.math, N),
                 launches=n_launch, flops_per_forward=conv_flops,
-                algorithmic_bytes_per_launch=round(m.bytes_per_forward() / n_launch),
+                algorithmic_bytes_per_launch=round(conv_bytes / n_launch),
                 avg_launch_us=round(conv_ms * 1e3 / n_launch, 2),
                 forward_graph_ms=round(fwd_ms, 3),
                 forward_eager_event_ms=round(sum(eager), 3),
-                timing='forward hipGraph replayed %d x between HIP events; per-launch split '
-                       'from eager passes with events per launch (median of 5), rescaled to the replay '
-                       'total' % reps,
+                timing='pps_forward hipGraph replayed %d x between HIP events; per-launch split '
+                       'from eager pps_forward_layers passes with events between layers (median '
+                       'of 5), rescaled to the replay total' % reps,
                 frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
+
+
+def usable_cores():
+    """(threads to use, sched_getaffinity count, cgroup CPU quota or None):
+    the CPUs this process may run on, capped by a cgroup v2 quota if one is
+    set (a GPU box's share of a larger host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, period = f.read().split()[:2]
+        if q != 'max':
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, aff, quota
+
+
+def e2e_stage(nm, rank, world, n_images, batch, threads):
+    """End-to-end images/s from image FILES (north_star "end-to-end
+    images/sec"; the reference's loop is detectron/core/test_engine.py:
+    282-315): Market-sized 128x64 JPEGs written to local disk, then the
+    product loop pps_amd.test_engine.extract_features -- PIL decode on
+    `threads` host threads, one pinned H2D copy per batch, the preprocessing
+    kernel and pps_forward on the GPU -- followed (one rank) by the
+    distance matrix + mAP/CMC of the first 3368 images as queries against
+    the rest.  Images are split over ranks; the rate is all images / the
+    slowest rank's time."""
+    import shutil
+    import tempfile
+    import concurrent.futures as cf
+    from PIL import Image
+    from pps_amd import distributed as pdist
+    from pps_amd import test_engine
+    a, b = pdist.shard_range(n_images, rank, world)
+    n = b - a
+    d = tempfile.mkdtemp(prefix='pps_e2e_', dir='/tmp')
+    try:
+        rng = np.random.RandomState(100 + rank)
+        base = rng.randint(0, 256, (64, 32, 16, 3)).astype(np.float32)
+
+        def write(i):   # smooth colour blobs + noise: JPEG-typical content
+            im = np.kron(base[i % 64], np.ones((4, 4, 1), np.float32))
+            im = im + np.random.RandomState(i).randint(-24, 24, im.shape)
+            p = os.path.join(d, '%08d.jpg' % i)
+            Image.fromarray(np.clip(im, 0, 255).astype(np.uint8)).save(p, quality=95)
+            return p
+        with cf.ThreadPoolExecutor(threads) as pool:
+            paths = list(pool.map(write, range(n)))
+        jpeg_bytes = sum(os.path.getsize(p) for p in paths)
+        feats = torch.empty((n, nm.feat_dim), dtype=torch.float32, device='cuda')
+        # warm: the decode pool, pinned allocations, the batch shapes
+        test_engine.extract_features(nm, lambda i: test_engine._decode_bgr(paths[i]),
+                                     min(n, 2 * batch), batch=batch, out=feats, workers=threads)
+        pdist.barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        test_engine.extract_features(nm, lambda i: test_engine._decode_bgr(paths[i]), n,
+                                     batch=batch, out=feats, workers=threads)
+        torch.cuda.synchronize()
+        t_ext = time.perf_counter() - t0
+        t_max = pdist.max_over_ranks(t_ext, world)
+        out = dict(images=n_images, decode_threads=threads, jpeg_MB=round(jpeg_bytes / 1e6, 2),
+                   extract_s=round(t_max, 4), images_per_s=round(n_images / t_max, 2),
+                   note='JPEG files on local disk -> PIL decode on host threads -> pinned H2D '
+                        '-> pps_preprocess_bgr_ragged -> pps_forward (test_engine.'
+                        'extract_features); rate = all images / slowest rank')
+        if world == 1 and n > Q_MARKET:
+            from pps_amd.distributed import ShardedEvaluator
+            rs = np.random.RandomState(0)
+            ids = rs.randint(1, 751, n)
+            cams = rs.randint(1, 7, n)
+            t1 = time.perf_counter()
+            ev = ShardedEvaluator(ids[:Q_MARKET], cams[:Q_MARKET], ids[Q_MARKET:],
+                                  cams[Q_MARKET:], 0, 1)
+            ev.run(feats[:Q_MARKET], feats[Q_MARKET:])
+            t_ret = time.perf_counter() - t1
+            out.update(retrieval_s=round(t_ret, 4), total_s=round(t_ext + t_ret, 4),
+                       total_images_per_s=round(n / (t_ext + t_ret), 2))
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def _cpu_model():
@@ -292,7 +408,8 @@ def cpu_baseline(blobs, n_img=8, n_q=400, runs=3):
     3368 / n_q (per-query work is independent of the other queries)."""
     from oracle import evaluator as ev
     from oracle.forward import GraphForward
-    threads = torch.get_num_threads()
+    threads, aff, quota = usable_cores()
+    torch.set_num_threads(threads)
 
     def med(fn):
         fn()
@@ -331,7 +448,8 @@ def cpu_baseline(blobs, n_img=8, n_q=400, runs=3):
                        'reference graph, torch CPU fp32); retrieval: Market 3368 x 15913 x '
                        '3968 distance in full, argsort / mAP / CMC on %d query rows scaled x%.2f; '
                        'median of %d after 1 warm-up' % (n_img, n_q, scale, runs),
-                cpu_model=_cpu_model(), cpu_count=os.cpu_count(),
+                cpu_model=_cpu_model(), cpu_count=os.cpu_count(), affinity_cpus=aff,
+                cgroup_cpu_quota=quota,
                 stages=dict(forward_img_s=round(n_img / fwd_s, 3),
                             distmat_s=round(dist_s, 3), distmat_GBps=round(byt / dist_s / 1e9, 3),
                             argsort_s=round(argsort_s, 3), mAP_s=round(map_s, 3),
@@ -339,11 +457,45 @@ def cpu_baseline(blobs, n_img=8, n_q=400, runs=3):
                             retrieval_total_s=round(dist_s + argsort_s + map_s + cmc_s, 3)))
 
 
+def dry_run(args, rank, world):
+    """--dry-run: the rendezvous, barrier, timing and reporting path of a
+    multi-rank run with no GPU work (gloo), so `--gpus N` is testable on CPU."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group('gloo')
+    pdist_barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    pdist_barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    pdist_barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({'metric': 'gallery images/sec + distmat GB/s; mAP/Rank-1 parity on '
+                          'Market-1501', 'value': None, 'unit': 'images/s', 'n_gpus': world,
+                          'steps': args.steps, 'warmup': args.warmup, 'dry_run': True,
+                          'ms_per_step': el * 1e3 / max(args.steps, 1)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    env_world = os.environ.get('WORLD_SIZE')
+    if args.gpus is not None and args.gpus > 1 and env_world is None:
+        # one process per GPU: this process only launches them (no GPU call yet)
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.dry_run:
+        return dry_run(args, rank, world)
     # PPS_DIST_BACKEND=gloo: rehearse the N>1 path with several ranks sharing
     # the devices there are (one-GPU box); the product path is nccl (= RCCL)
     backend = os.environ.get('PPS_DIST_BACKEND', 'nccl')
@@ -356,12 +508,14 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
-    from pps_amd import model, ops
+    from pps_amd import model, native
     from pps_amd import distributed as pdist
     cfg = market_cfg()
     plan = model.build_plan()
     blobs = model.synthetic_weights(plan, seed=0)
-    m = model.PPSModel(blobs)
+    # the product form: one handle behind the whole-network C ABI
+    # (pps_model_create / pps_forward_bgr), tuned by pps_model_autotune
+    nm = native.NativeModel(blobs)
     B = args.batch
     H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
     g = torch.Generator(device='cuda')
@@ -369,32 +523,24 @@ def main():
     imgs = torch.randint(0, 256, (B, 128, 64, 3), generator=g, device='cuda',
                          dtype=torch.int64).to(torch.uint8)
     xbuf = torch.empty((B, H, W, 4), dtype=torch.float32, device='cuda')
-    feat = torch.empty((B, m.feat_dim), dtype=torch.float32, device='cuda')
-    means = cfg.PIXEL_MEANS.ravel()
-
-    def step():
-        ops.preprocess_bgr(imgs, means, (H, W), xbuf)
-        m.forward(xbuf, out=feat)
-
-    ops.preprocess_bgr(imgs, means, (H, W), xbuf)
+    feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')
+    from pps_amd import ops
+    ops.preprocess_bgr(imgs, cfg.PIXEL_MEANS.ravel(), (H, W), xbuf)
     if args.tiles_file and os.path.exists(args.tiles_file):
         with open(args.tiles_file) as f:
             saved = json.load(f)
-        m.set_tiles(saved)
-        if '__planes__' in saved:
-            m.set_planes(saved['__planes__'])
-        m.set_splitks(saved.get('__splitk__', {}))
+        nm.apply_table(saved)
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
         pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
     elif not args.no_autotune:
-        # per-layer tile choice, outside the timed region (PPS_AUTOTUNE_SPLITK=1:
-        # also try split-K per conv)
-        # (PPS_AUTOTUNE_MAXTILE=n: candidates 1..n only, for A/B runs)
-        maxt = int(os.environ.get('PPS_AUTOTUNE_MAXTILE', '0'))
-        fin = int(os.environ.get('PPS_AUTOTUNE_FINALISTS', '4'))
-        m.autotune(xbuf, splitk=os.environ.get('PPS_AUTOTUNE_SPLITK') == '1',
-                   tiles=list(range(1, maxt + 1)) if maxt else None, finalists=fin,
-                   final_reps=int(os.environ.get('PPS_AUTOTUNE_FINAL_REPS', '10')))
+        # per-layer tile / plane choice on this device, outside the timed
+        # region (PPS_AUTOTUNE_SPLITK=1: also try conv split-K)
+        nm.autotune(xbuf, native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1'
+                    else 0)
+    nm.reserve(B)
+
+    def step():   # uint8 images -> preprocess -> forward, one C call
+        nm.forward_bgr(imgs, out=feat)
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -443,16 +589,20 @@ def main():
                 ms_per_step=round(el_h2d * 1e3 / args.steps, 3),
                 h2d_bytes_per_step=int(host.numel()),
                 note='uint8 BGR batch copied from pinned host memory before every step')
+    del graph
 
-    roof, per_layer = conv_roofline(m, xbuf)
+    roof, per_layer = conv_roofline(nm, xbuf)
     tiles_saved = bool(args.tiles_file and os.path.exists(args.tiles_file))
     ret = retrieval_stage(rank, world, args.dist_reps,
                           tune=not (args.no_autotune or tiles_saved))
     if args.tiles_file and not tiles_saved and rank == 0:
         with open(args.tiles_file, 'w') as f:
-            json.dump(dict(m.tiles(), __distmat__=ret['distmat_tile'],
+            json.dump(dict(nm.tiles(), __distmat__=ret['distmat_tile'],
                            __distmat_qplanes__=ret['distmat_qplanes'],
-                           __planes__=m.planes(), __splitk__=m.splitks()), f, indent=0)
+                           __planes__=nm.planes(), __splitk__=nm.splitks()), f, indent=0)
+    e2e = None
+    if not args.no_e2e:
+        e2e = e2e_stage(nm, rank, world, args.e2e_images, B, min(16, usable_cores()[0]))
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
     dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
@@ -468,13 +618,15 @@ def main():
         'data': 'synthetic (uint8 images, seeded weights of the PPS R-50 architecture)',
         'config': {'workload': 'Market-1501 ResNet-50 PPS (stride-1 res5, 31 part subsets), '
                                'batch %d/GPU, 384x128, 3368q x 15913g L2 distmat' % B,
-                   'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': m.feat_dim,
-                   'parallelism': 'dp%d' % world, 'hipgraph': graph is not None,
-                   'act_plane_edges': len(m.planes()), 'splitk_layers': len(m.splitks())},
+                   'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': nm.feat_dim,
+                   'parallelism': 'dp%d' % world, 'hipgraph': not args.no_graph,
+                   'entry_point': 'pps_forward_bgr (whole-network C ABI)',
+                   'act_plane_edges': len(nm.planes()), 'splitk_layers': len(nm.splitks())},
         'distmat_GBps': round(total_bytes / (dist_ms_max * 1e-3) / 1e9, 2),
         'distmat_ms': round(dist_ms_max, 3),
         'distmat_TFLOPs_per_gpu': round(dist_tflops, 2),
         'pcie_inclusive': pcie,
+        'e2e_from_jpeg': e2e,
         'rank_eval_ms': round(ret['rank_eval_ms'], 3),
         'retrieval_ms': round(ret['retrieval_ms'], 3),
         'mAP_synthetic': round(ret['mAP'], 6), 'cmc1_synthetic': round(ret['cmc1'], 6),

@@ -175,7 +175,10 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
  *    (distance, global index) -> sorted_d / sorted_idx [Q][R*Pmax] (padding
  *    +inf / -1), pos_total [Q], and the query's bin-lookup cells
  *    [Q][pps_rank_cells()] (int32, 16-byte aligned) that c) reads.
- *    R*Pmax <= 8192.
+ *    Capacity: R*Pmax <= 8192 merged positives per query (the merge sort
+ *    holds 16 B per positive in LDS: 128 KiB of gfx950's 160 KiB), else
+ *    PPS_ERR_CAPACITY -- i.e. one identity may have at most 8192 / R
+ *    same-id gallery entries per shard (Market: 72).
  * c) pps_rank_count_stream: for this shard's rows, hist[q][p] += #entries
  *    with p = first positive d_p >= d, before[q] += #entries ordered before
  *    the first positive, over all entries of the row minus this shard's junk
@@ -198,6 +201,27 @@ int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
                           const int32_t* cells, int Jmax, const float* junk_d,
                           const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
                           int32_t* before, void* stream);
+
+/* CMC beyond the Market protocol (reid_dataset_evaluator.py:283-363 `cmc`
+ * with its defaults first_match_break=False, topk=100, and with
+ * separate_camera_set=True).  pps_cmc_counts bins every valid entry of this
+ * shard's rows by the number of positives whose (distance, global index) key
+ * is below its own: hist[q][b] += 1 (b < pos_total[q]; caller zeroes hist,
+ * sums over shards).  Valid = not junk (junk lists of pps_collect_matches),
+ * or with qcam / gcam given (separate_camera_set; gcam = this shard's LOCAL
+ * cams) = not from the query's camera.  pps_cmc_finalize then writes the
+ * reference's per-query CMC row after its cumsum, ret [Q][topk] float64
+ * (the j-th positive at valid position k adds 1/P at k - j, or 1 once with
+ * first_match_break), and valid [Q].  Exact under the stable (distance,
+ * index) order. */
+int pps_cmc_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, int64_t g_offset,
+                   int Ptot, const float* sorted_d, const int32_t* sorted_idx,
+                   const int32_t* pos_total, const int32_t* qcam, const int32_t* gcam,
+                   int Jmax, const float* junk_d, const int32_t* junk_idx,
+                   const int32_t* junk_cnt, int32_t* hist, void* stream);
+int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_t* hist,
+                     int topk, int first_match_break, double* ret, int32_t* valid,
+                     void* stream);
 
 /* Stable per-row top-k (k <= 1024) of a distance matrix, ascending, ties by
  * gallery index.  Replaces the `np.argsort(distmat, axis=1)[:, :k]` rank
@@ -444,6 +468,110 @@ int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets
                               const int32_t* heights, const int32_t* widths,
                               const float* pixel_means, int Ho, int Wo, float* y,
                               void* stream);
+
+/* ---- whole network ---------------------------------------------------------
+ * The PPS test net as one handle (SURVEY §8(b) "pps_forward + model
+ * create/destroy from a weights blob map").  Replaces the reference's
+ * `workspace.RunNet(model.net.Proto().name)` of the test net, fed with the
+ * `data` blob and fetching `reid_feature_concat_norm`
+ * (detectron/core/test.py:155-165, test_engine.py:282-315), and the
+ * net build it runs (model_builder.py build_generic_reid_model: ResNet.py
+ * add_ResNet50_conv5_body, pps_heads.py add_pps_part_head, reid_heads.py
+ * add_reid_outputs).  The handle owns the packed / bf16x3-split weights, the
+ * activation buffers per batch size and the per-layer GEMM tile, activation-
+ * plane and split-K table; every launch of a forward is the op-level entry
+ * point above with the same arguments pps_amd/model.py uses, so both
+ * orchestrators give identical bits for the same table.
+ *
+ * Unlike the op-level entry points, the handle allocates device memory:
+ * pps_model_create (weights) and pps_model_reserve (activations for batch N,
+ * ~62 MB per image at 384x128).  pps_forward itself never allocates or
+ * synchronises once N is reserved, so it can be captured into a hipGraph.
+ * One forward at a time per handle (the activation buffers are shared); use
+ * one handle per concurrent stream. */
+#define PPS_MATH_X3 0   /* f32 products as six bf16 MFMA terms (default)   */
+#define PPS_MATH_F32 1  /* exact f32 MFMA (v_mfma_f32_32x32x2_f32)         */
+#define PPS_AUTOTUNE_NO_PLANES 1  /* keep the plane edges as they are     */
+#define PPS_AUTOTUNE_SPLITK 2     /* also try conv split-K 2..4           */
+
+typedef struct PpsBlob {     /* one Detectron blob, HOST float32 memory   */
+  const char* name;          /* e.g. "res2_0_branch2a_w", "pps01_bn_riv"  */
+  const float* data;
+  int ndim;
+  int64_t shape[4];
+} PpsBlob;
+
+typedef struct PpsModelConfig {  /* reference cfg keys (core/config.py)   */
+  int struct_size;               /* = sizeof(PpsModelConfig)               */
+  int height, width;             /* REID.SCALE[1], REID.SCALE[0]: 384, 128 */
+  int strip_num;                 /* REID.BPM_STRIP_NUM                     */
+  int bpm_dim;                   /* REID.BPM_DIM                           */
+  int num_groups, width_per_group, stride_1x1; /* RESNETS.*               */
+  int res5_stride, res5_dilation;
+  int fpn_on, fpn_dim;           /* FPN.FPN_ON, FPN.DIM                    */
+  int max_ave;                   /* REID.MAX_AVE_FEATURE                   */
+  int normalize;                 /* REID.NORMALIZE_FEATURE                 */
+  int math;                      /* PPS_MATH_*                             */
+  int fused_stem, fused_pps, act_planes;  /* x3 fusions (1 = on)          */
+  float pixel_means[3];          /* PIXEL_MEANS (BGR), pps_forward_bgr     */
+} PpsModelConfig;
+
+typedef struct PpsLayerInfo {
+  const char* name;   /* tuning key: conv name, or the output blob        */
+  const char* op;     /* conv, conv_dual, stem_pool, conv_pps, heads, ...  */
+  int tile, splitk, planes_in, planes_out;
+  int gemm;           /* an MFMA launch (counted in the conv roofline)     */
+  double flops;       /* algorithmic FLOP at batch N                       */
+  double bytes;       /* algorithmic HBM bytes at batch N                  */
+  int64_t out_shape[4];
+} PpsLayerInfo;
+
+typedef struct PpsModel PpsModel;
+
+/* The reference's PPS Market-1501 test configuration. */
+int pps_model_config_default(PpsModelConfig* cfg);
+/* Build the net from `nblobs` host blobs (every parameter of the test net;
+ * `<prefix>_conv_b` head biases optional), fold BN, pack and split the
+ * weights on the current device.  Synchronous. */
+int pps_model_create(const PpsBlob* blobs, int nblobs, const PpsModelConfig* cfg,
+                     PpsModel** model);
+int pps_model_destroy(PpsModel* model);
+int pps_model_feat_dim(const PpsModel* model);
+int pps_model_num_layers(const PpsModel* model);
+int pps_model_layer_info(const PpsModel* model, int layer, int N, PpsLayerInfo* info);
+/* Tuning table (results do not depend on it beyond the MFMA block group, see
+ * pps_gemm_num_tiles).  Autotune results of pps_model_autotune or of
+ * pps_amd/model.py (tiles JSON) are applied by name. */
+int pps_model_set_tile(PpsModel* model, const char* layer, int tile);
+int pps_model_set_splitk(PpsModel* model, const char* layer, int splitk);
+int pps_model_num_plane_edges(const PpsModel* model);
+int pps_model_plane_edge(const PpsModel* model, int edge, const char** producer,
+                         const char** consumer, int* on);
+int pps_model_set_planes(PpsModel* model, const char* producer, int on);
+/* Time every tile per layer on this device (then plane edges, optionally
+ * split-K) with x [N][H][W][4] as input; not capturable. */
+int pps_model_autotune(PpsModel* model, const float* x, int N, int flags, void* stream);
+/* Allocate (synchronously) the activation buffers for batch N. */
+int pps_model_reserve(PpsModel* model, int N);
+int pps_model_release(PpsModel* model, int N);   /* N <= 0: all */
+/* An intermediate tensor of the last forward at batch N (debug / parity):
+ * device pointer, planes flag (bf16x3 [3][...]) and its 4-D shape. */
+int pps_model_tensor(const PpsModel* model, int N, const char* blob, void** ptr,
+                     int* planes, int64_t* shape4);
+/* feat [N][feat_dim] = reid_feature_concat_norm of x NHWC4 [N][H][W][4]
+ * (pps_preprocess_bgr's layout: BGR minus PIXEL_MEANS, 4th channel 0). */
+int pps_forward(const PpsModel* model, const float* nhwc4, int N, float* feat,
+                void* stream);
+/* Layers [first, last) only (per-layer timing); the intermediates persist
+ * in the handle, the last layer writes feat. */
+int pps_forward_layers(const PpsModel* model, const float* nhwc4, int N, float* feat,
+                       int first, int last, void* stream);
+/* The reference's `data` blob as it is: NCHW [N][3][H][W] float32. */
+int pps_forward_nchw(const PpsModel* model, const float* nchw, int N, float* feat,
+                     void* stream);
+/* uint8 BGR images [N][Hi][Wi][3] (device) -> preprocess -> forward. */
+int pps_forward_bgr(const PpsModel* model, const uint8_t* img, int N, int Hi, int Wi,
+                    float* feat, void* stream);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,9 @@ SIGNATURES = {
     'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                         c_ptr],
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_cmc_counts': [c_ptr, c_i64, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
+                       c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_cmc_finalize': [c_i64, c_int, c_ptr, c_ptr, c_int, c_int, c_ptr, c_ptr, c_ptr],
     'pps_topk_merge': [c_ptr, c_ptr, c_int, c_i64, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr],
     'pps_conv2d_bn_act': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int,
                           c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int,
@@ -100,6 +103,23 @@ SIGNATURES = {
     'pps_preprocess_bgr': [c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr],
     'pps_preprocess_bgr_ragged': [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int,
                                   c_ptr, c_ptr],
+    # whole network (pps_amd/native.py); struct arguments by address
+    'pps_model_config_default': [c_ptr],
+    'pps_model_create': [c_ptr, c_int, c_ptr, c_ptr],
+    'pps_model_destroy': [c_ptr],
+    'pps_model_layer_info': [c_ptr, c_int, c_int, c_ptr],
+    'pps_model_set_tile': [c_ptr, ctypes.c_char_p, c_int],
+    'pps_model_set_splitk': [c_ptr, ctypes.c_char_p, c_int],
+    'pps_model_plane_edge': [c_ptr, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_model_set_planes': [c_ptr, ctypes.c_char_p, c_int],
+    'pps_model_autotune': [c_ptr, c_ptr, c_int, c_int, c_ptr],
+    'pps_model_reserve': [c_ptr, c_int],
+    'pps_model_release': [c_ptr, c_int],
+    'pps_model_tensor': [c_ptr, c_int, ctypes.c_char_p, c_ptr, c_ptr, c_ptr],
+    'pps_forward': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
+    'pps_forward_layers': [c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_ptr],
+    'pps_forward_nchw': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
+    'pps_forward_bgr': [c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr],
 }
 EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
@@ -110,6 +130,9 @@ EXTRA = {
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),
+    'pps_model_feat_dim': ([c_ptr], ctypes.c_int),
+    'pps_model_num_layers': ([c_ptr], ctypes.c_int),
+    'pps_model_num_plane_edges': ([c_ptr], ctypes.c_int),
 }
 
 METRICS = {'euclidean': 0, 'sqeuclidean': 1, 'cosine': 2}

@@ -38,6 +38,11 @@ int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const i
 int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
                 const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+int cmc_counts(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
+               const int32_t*, const int32_t*, const int32_t*, const int32_t*, int,
+               const float*, const int32_t*, const int32_t*, int32_t*, hipStream_t);
+int cmc_finalize(int64_t, int, const int32_t*, const int32_t*, int, int, double*, int32_t*,
+                 hipStream_t);
 int collect_matches(const float*, int64_t, int64_t, const int32_t*, const int32_t*,
                     const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
                     int32_t*, int32_t*, int, float*, int32_t*, int32_t*, hipStream_t);
@@ -69,7 +74,7 @@ const char* pps_registered_ops(void) {
   // the fused / retrieval entry points the product path runs
   return "Conv;SpatialBN;Relu;Sum;Add;Max;Mean;MaxPool;AveragePool;Split;FC;Concat;"
          "Reshape;Normalize;PairWiseDistance;"
-         "Conv+SpatialBN+Sum+Relu;PartPowerSet;ComputeDist;RankCounts;TopK;TopKMerge;"
+         "Conv+SpatialBN+Sum+Relu;PartPowerSet;ComputeDist;RankCounts;CMC;TopK;TopKMerge;"
          "ReRanking;PrepImForBlob";
 }
 
@@ -296,9 +301,9 @@ int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32
   PPS_ENFORCE(((uintptr_t)cells & 15) == 0, "cells must be 16-byte aligned");
   PPS_ENFORCE(R >= 1 && R <= kMergeMaxLists, "R must be in [1, 64]");
   PPS_ENFORCE(Q >= 0 && Pmax > 0, "bad shape");
-  if ((int64_t)R * Pmax > 8192) {
+  if ((int64_t)R * Pmax > kRankMergeCap) {
     set_error("merged positive capacity R*Pmax=" + std::to_string((int64_t)R * Pmax) +
-              " exceeds 8192 (LDS of the merge sort)");
+              " exceeds " + std::to_string(kRankMergeCap) + " (LDS of the merge sort)");
     return PPS_ERR_CAPACITY;
   }
   return rank_prepare(R, Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total,
@@ -316,7 +321,9 @@ int pps_rank_count_stream(const float* dist, int64_t Q, int64_t G, int64_t ldd,
               "null pointer");
   PPS_ENFORCE(((uintptr_t)cells & 15) == 0, "cells must be 16-byte aligned");
   PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Ptot > 0 && Jmax > 0, "bad shape");
-  PPS_ENFORCE(G / 1024 < 65535, "G too large for the chunk grid");
+  PPS_ENFORCE((G + kRankStreamChunk - 1) / kRankStreamChunk <= 65535,
+              "G too large for the chunk grid (65535 chunks of " +
+                  std::to_string(kRankStreamChunk) + ")");
   return rank_count_stream(dist, Q, G, ldd, g_offset, Ptot, sorted_d, sorted_idx, pos_total,
                            cells, Jmax, junk_d, junk_idx, junk_cnt, hist, before,
                            as_stream(stream));
@@ -330,6 +337,33 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* p
   PPS_ENFORCE(Q >= 0 && Ptot >= 0, "bad shape");
   return ap_finalize(Q, Ptot, sorted_d, pos_total, hist, before, ap, valid, first_rank,
                      as_stream(stream));
+}
+
+int pps_cmc_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, int64_t g_offset,
+                   int Ptot, const float* sorted_d, const int32_t* sorted_idx,
+                   const int32_t* pos_total, const int32_t* qcam, const int32_t* gcam, int Jmax,
+                   const float* junk_d, const int32_t* junk_idx, const int32_t* junk_cnt,
+                   int32_t* hist, void* stream) {
+  PPS_ENFORCE(dist && sorted_d && sorted_idx && pos_total && hist, "null pointer");
+  PPS_ENFORCE((qcam == nullptr) == (gcam == nullptr),
+              "qcam and gcam are given together (separate_camera_set) or not at all");
+  PPS_ENFORCE(gcam || (junk_d && junk_idx && junk_cnt && Jmax > 0),
+              "without separate_camera_set the junk lists are required");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && Ptot > 0, "bad shape");
+  PPS_ENFORCE(G < (1ll << 31) && g_offset + G < (1ll << 31), "gallery indices must fit int32");
+  PPS_ENFORCE((G + kRankStreamChunk - 1) / kRankStreamChunk <= 65535,
+              "G too large for the chunk grid");
+  return cmc_counts(dist, Q, G, ldd, g_offset, Ptot, sorted_d, sorted_idx, pos_total, qcam,
+                    gcam, Jmax, junk_d, junk_idx, junk_cnt, hist, as_stream(stream));
+}
+
+int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_t* hist,
+                     int topk, int first_match_break, double* ret, int32_t* valid,
+                     void* stream) {
+  PPS_ENFORCE(pos_total && hist && ret && valid, "null pointer");
+  PPS_ENFORCE(Q >= 0 && Ptot > 0 && topk >= 1, "bad shape");
+  return cmc_finalize(Q, Ptot, pos_total, hist, topk, first_match_break ? 1 : 0, ret, valid,
+                      as_stream(stream));
 }
 
 int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* vals,

@@ -1,0 +1,1233 @@
+// Whole-network entry points of libpps_hip.so (include/pps_abi.h, "feature
+// extractor as one call"): pps_model_create builds the PPS test net from a
+// Detectron weights blob map, owns its packed / bf16x3-split weights, the
+// activation buffers per batch size and the per-layer tile / plane / split-K
+// table; pps_forward enqueues the whole forward on one stream.
+//
+// The plan is built by the same builders the reference uses, with the same
+// blob and parameter names (mirrored one for one by pps_amd/model.py):
+//   add_ResNet50_conv5_body  detectron/modeling/ResNet.py:39-40,91-126
+//     basic_bn_stem          ResNet.py:246-256
+//     add_stage              ResNet.py:60-88
+//     add_residual_block     ResNet.py:153-195 (stride rule :169-171)
+//     bottleneck_transformation ResNet.py:276-333 (STRIDE_1X1 :290)
+//     basic_bn_shortcut      ResNet.py:203-220
+//   FPN coarsest level       detectron/modeling/FPN_reid.py:160-174 (gated)
+//   add_pps_part_head        detectron/modeling/pps_heads.py:38-96
+//     add_uniform_partition  detectron/modeling/bpm_heads.py:18-55
+//   add_reid_outputs         detectron/modeling/reid_heads.py:34-127
+// and compiled into the fused launches of the op-level ABI (test-mode BN
+// folded into conv epilogues, projection shortcuts K-concatenated into their
+// branch2c GEMM, stem conv + pool fused, part pooling in the last conv's
+// epilogue, 31 heads as one split-K batched GEMM + one BN/ReLU/Normalize
+// pass).  Each launch goes through the same pps_* entry point, with the same
+// arguments, as the Python orchestrator (pps_amd/model.py PPSModel), so the
+// two give identical bits for the same tile / plane / split-K table.
+//
+// This replaces the reference's `workspace.RunNet(model.net)` of the test net
+// (detectron/core/test.py:163-165) behind a C ABI.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pps_internal.hpp"
+
+namespace pps {
+namespace {
+
+constexpr double kBnEps = 1e-5;  // Caffe2 SpatialBN default epsilon (pytorch v1.0.1)
+constexpr int kHeadSplitK = 8;   // K = 2048 head GEMMs cut 8 ways (pps_amd/model.py HEAD_SPLITK)
+constexpr int kMaxSplitK = 4;    // conv split-K factors the autotune tries
+
+enum class Op { Conv, ConvDual, MaxPool, StemPool, Pps, ConvPps, Heads, Normalize };
+
+const char* op_name(Op op) {
+  switch (op) {
+    case Op::Conv: return "conv";
+    case Op::ConvDual: return "conv_dual";
+    case Op::MaxPool: return "maxpool";
+    case Op::StemPool: return "stem_pool";
+    case Op::Pps: return "pps";
+    case Op::ConvPps: return "conv_pps";
+    case Op::Heads: return "heads";
+    case Op::Normalize: return "normalize";
+  }
+  return "?";
+}
+
+struct ModelError : std::runtime_error {
+  int code;
+  ModelError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define PPS_MCHECK(cond, msg)                                                         \
+  do {                                                                                \
+    if (!(cond))                                                                      \
+      throw ModelError(PPS_ERR_INVALID_ARG, std::string("[enforce fail at ") +       \
+                                                __func__ + "] " + #cond + ". " + (msg)); \
+  } while (0)
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw ModelError(PPS_ERR_LAUNCH, std::string(what) + ": " + hipGetErrorString(e));
+}
+void rc_check(int rc) {  // an op-level entry point failed: its message is already set
+  if (rc != PPS_OK) throw ModelError(rc, pps_last_error());
+}
+
+// ---- plan (structure only) -------------------------------------------------
+struct PlanLayer {
+  Op op;
+  std::string name, bn, input, output, residual;
+  int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, dil = 1;
+  bool relu = false;
+  std::vector<int> split;  // pps
+  bool max_ave = false;
+  std::vector<std::string> prefixes;
+  int dim = 0, dim_inner = 0;
+};
+
+struct Plan {
+  std::vector<PlanLayer> layers;
+  std::map<std::string, std::vector<int64_t>> params;
+  std::string output;
+  int feat_dim = 0;
+
+  std::string conv(const std::string& in, const std::string& prefix, int din, int dout, int k,
+                   int stride, int pad, int dil = 1, bool relu = false,
+                   const std::string& residual = "", const std::string& out = "",
+                   bool bias = false, const std::string& bn_name = "") {
+    params[prefix + "_w"] = {dout, din, k, k};
+    if (bias) params[prefix + "_b"] = {dout};
+    const std::string bn = bn_name.empty() ? prefix + "_bn" : bn_name;
+    for (const char* s : {"_s", "_b", "_rm", "_riv"}) params[bn + s] = {dout};
+    PlanLayer L;
+    L.op = Op::Conv; L.name = prefix; L.bn = bn; L.input = in;
+    L.output = out.empty() ? bn : out;
+    L.cin = din; L.cout = dout; L.k = k; L.stride = stride; L.pad = pad; L.dil = dil;
+    L.relu = relu; L.residual = residual;
+    layers.push_back(L);
+    return L.output;
+  }
+};
+
+// model.py basic_bn_stem (ResNet.py:246-256)
+std::string basic_bn_stem(Plan& p) {
+  const std::string c = p.conv("data", "conv1", 3, 64, 7, 2, 3, 1, true, "", "", false, "res_conv1_bn");
+  PlanLayer L;
+  L.op = Op::MaxPool; L.input = c; L.output = "pool1"; L.k = 3; L.stride = 2; L.pad = 1;
+  p.layers.push_back(L);
+  return "pool1";
+}
+
+// ResNet.py:276-333 (+ the Sum/Relu of add_residual_block :186-195)
+std::string bottleneck(Plan& p, const PpsModelConfig& c, const std::string& in, int din, int dout,
+                       int stride, const std::string& prefix, int dinner, int dil,
+                       const std::string& shortcut, const std::string& out) {
+  const int s1 = c.stride_1x1 ? stride : 1, s3 = c.stride_1x1 ? 1 : stride;
+  std::string cur = p.conv(in, prefix + "_branch2a", din, dinner, 1, s1, 0, 1, true);
+  cur = p.conv(cur, prefix + "_branch2b", dinner, dinner, 3, s3, dil, dil, true);
+  return p.conv(cur, prefix + "_branch2c", dinner, dout, 1, 1, 0, 1, true, shortcut, out);
+}
+
+// ResNet.py:153-195 with basic_bn_shortcut :203-220
+std::string residual_block(Plan& p, const PpsModelConfig& c, const std::string& prefix,
+                           const std::string& in, int din, int dout, int dinner, int dil,
+                           int stride_init, bool inplace_sum) {
+  const int stride = (din != dout && din != 64 && dil == 1) ? stride_init : 1;
+  std::string sc = in;
+  if (din != dout) sc = p.conv(in, prefix + "_branch1", din, dout, 1, stride, 0);
+  const std::string out = prefix + (inplace_sum ? "_branch2c_bn" : "_sum");
+  return bottleneck(p, c, in, din, dout, stride, prefix, dinner, dil, sc, out);
+}
+
+// ResNet.py:60-88
+std::string add_stage(Plan& p, const PpsModelConfig& c, const std::string& prefix,
+                      std::string in, int n, int& din, int dout, int dinner, int dil,
+                      int stride_init) {
+  for (int i = 0; i < n; ++i) {
+    in = residual_block(p, c, prefix + "_" + std::to_string(i), in, din, dout, dinner, dil,
+                        stride_init, i < n - 1);
+    din = dout;
+  }
+  return in;
+}
+
+// bpm_heads.py:18-35: strip heights along H
+std::vector<int> uniform_partition_split(const PpsModelConfig& c, double spatial_scale) {
+  static const std::map<int, std::vector<int>> table = {
+      {7, {3, 3, 4, 4, 4, 3, 3}}, {5, {5, 5, 4, 5, 5}},
+      {9, {2, 3, 3, 3, 3, 3, 3, 2, 2}}, {10, {2, 2, 2, 3, 3, 3, 3, 2, 2, 2}}};
+  std::vector<int> out;
+  auto it = table.find(c.strip_num);
+  if (it != table.end() && c.height == 16 * 24) {
+    const double scale = 16 * spatial_scale;
+    for (int s : it->second) out.push_back((int)(s * scale));
+    return out;
+  }
+  const int h = (int)(c.height * spatial_scale / c.strip_num);
+  out.assign(c.strip_num, h);
+  return out;
+}
+
+Plan build_plan(const PpsModelConfig& c) {
+  Plan p;
+  std::string s = basic_bn_stem(p);
+  int din = 64;
+  const int db = c.num_groups * c.width_per_group;
+  s = add_stage(p, c, "res2", s, 3, din, 256, db, 1, 2);
+  s = add_stage(p, c, "res3", s, 4, din, 512, db * 2, 1, 2);
+  s = add_stage(p, c, "res4", s, 6, din, 1024, db * 4, 1, 2);
+  s = add_stage(p, c, "res5", s, 3, din, 2048, db * 8, c.res5_dilation, c.res5_stride);
+  const double scale = 1. / 16. * c.res5_dilation / c.res5_stride;
+  int dim = din;
+  if (c.fpn_on && dim != c.fpn_dim) {  // FPN_reid.py:160-174 (coarsest level only)
+    s = p.conv(s, "fpn_inner_" + s, dim, c.fpn_dim, 1, 1, 0, 1, true, "", "", true,
+               "fpn_inner_" + s + "_bn");
+    dim = c.fpn_dim;
+  }
+  // pps_heads.py:38-96: subset i = bits of i; blob prefix pps + digits
+  PlanLayer P;
+  P.op = Op::Pps; P.input = s; P.output = "pps_pool2_all"; P.dim = dim;
+  P.split = uniform_partition_split(c, scale);
+  P.max_ave = c.max_ave != 0;
+  for (int i = 1; i < (1 << c.strip_num); ++i) {
+    std::string pre = "pps";
+    for (int j = 0; j < c.strip_num; ++j)
+      if (i & (1 << j)) pre += std::to_string(j);
+    P.prefixes.push_back(pre);
+  }
+  p.layers.push_back(P);
+  // reid_heads.py:34-127 (test branch; the unused FC logits are not built)
+  for (const auto& pre : P.prefixes) {
+    p.params[pre + "_conv_w"] = {c.bpm_dim, dim, 1, 1};
+    p.params[pre + "_conv_b"] = {c.bpm_dim};
+    for (const char* sfx : {"_s", "_b", "_rm", "_riv"}) p.params[pre + "_bn" + sfx] = {c.bpm_dim};
+  }
+  PlanLayer H;
+  H.op = Op::Heads; H.input = P.output; H.prefixes = P.prefixes; H.dim = dim;
+  H.dim_inner = c.bpm_dim; H.output = "reid_feature_concat";
+  p.layers.push_back(H);
+  p.output = H.output;
+  if (c.normalize) {
+    PlanLayer N;
+    N.op = Op::Normalize; N.input = H.output; N.output = "reid_feature_concat_norm";
+    p.layers.push_back(N);
+    p.output = N.output;
+  }
+  p.feat_dim = (int)P.prefixes.size() * c.bpm_dim;
+  return p;
+}
+
+// ---- device memory ------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  explicit DevBuf(size_t n) : bytes(n) {
+    if (n) hip_check(hipMalloc(&p, n), "hipMalloc");
+  }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+using Buf = std::shared_ptr<DevBuf>;
+
+Buf upload(const std::vector<float>& h, hipStream_t st) {
+  auto b = std::make_shared<DevBuf>(h.size() * sizeof(float));
+  hip_check(hipMemcpyAsync(b->p, h.data(), b->bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");  // h may die after return
+  return b;
+}
+
+// f32 weights -> bf16x3 planes [nbatch][3][n] (pps_split_bf16x3)
+Buf split3(const Buf& w, int64_t n, int nbatch, hipStream_t st) {
+  auto b = std::make_shared<DevBuf>((size_t)n * nbatch * 3 * sizeof(uint16_t));
+  rc_check(pps_split_bf16x3(w->as<float>(), n, nbatch, b->as<uint16_t>(), st));
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return b;
+}
+
+// ---- weights (host) -------------------------------------------------------------
+struct Blob {
+  const float* data;
+  std::vector<int64_t> shape;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+// model.py fold_bn: test-mode SpatialBN y = (x - rm) * s / sqrt(riv + eps) + b as
+// y = x * scale + shift, in float64 then rounded to float32 (conv bias in shift)
+void fold_bn(const std::map<std::string, Blob>& blobs, const std::string& bn, const Blob* bias,
+             std::vector<float>& scale, std::vector<float>& shift) {
+  const Blob& s = blobs.at(bn + "_s");
+  const Blob& b = blobs.at(bn + "_b");
+  const Blob& rm = blobs.at(bn + "_rm");
+  const Blob& riv = blobs.at(bn + "_riv");
+  const int64_t n = s.numel();
+  scale.resize(n);
+  shift.resize(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const double sc = (double)s.data[i] / std::sqrt((double)riv.data[i] + kBnEps);
+    const double cb = bias ? (double)bias->data[i] : 0.0;
+    scale[i] = (float)sc;
+    shift[i] = (float)((cb - (double)rm.data[i]) * sc + (double)b.data[i]);
+  }
+}
+
+// [Cout][Cin][KH][KW] -> [Cout][Kpad], K ordered (kh, kw, cin), Kpad % 16 == 0
+std::vector<float> pack_conv(const Blob& w, int cin_pad, int& kpad) {
+  const int64_t co = w.shape[0], ci = w.shape[1], kh = w.shape[2], kw = w.shape[3];
+  const int64_t cp = std::max<int64_t>(cin_pad, ci);
+  const int64_t k = kh * kw * cp;
+  kpad = (int)((k + 15) / 16 * 16);
+  std::vector<float> out((size_t)co * kpad, 0.f);
+  for (int64_t o = 0; o < co; ++o)
+    for (int64_t y = 0; y < kh; ++y)
+      for (int64_t x = 0; x < kw; ++x)
+        for (int64_t c = 0; c < ci; ++c)
+          out[o * kpad + (y * kw + x) * cp + c] = w.data[((o * ci + c) * kh + y) * kw + x];
+  return out;
+}
+
+// conv1 [64][3][7][7] -> the fused stem's [64][pps_stem_k()] layout: K index
+// (kh * 3 + c) * 8 + kw, kw = 7 and the tail zero (stem.hip, model.py pack_stem_weight)
+std::vector<float> pack_stem(const Blob& w) {
+  const int K = pps_stem_k();
+  std::vector<float> out((size_t)64 * K, 0.f);
+  for (int o = 0; o < 64; ++o)
+    for (int kh = 0; kh < 7; ++kh)
+      for (int c = 0; c < 3; ++c)
+        for (int kw = 0; kw < 7; ++kw)
+          out[(size_t)o * K + (kh * 3 + c) * 8 + kw] = w.data[((o * 3 + c) * 7 + kh) * 7 + kw];
+  return out;
+}
+
+// ---- compiled layers ----------------------------------------------------------
+struct Layer {
+  Op op;
+  std::string name;  // tuning key: conv name, or the output blob for heads / pooling
+  std::string input, input2, output, residual, conv_output;
+  int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, dil = 1, stride2 = 1;
+  bool relu = false;
+  int cin_eff = 0, kpad = 0, shortcut_cin = 0;
+  Buf w, scale, shift;  // w: f32 [Cout][Kpad] or bf16x3 planes
+  std::vector<int> split;
+  bool max_ave = false, normalize = false;
+  int nsub = 0, dim = 0, dim_inner = 0;
+  int tile = 0, splitk = 1;
+  bool planes_in = false, planes_out = false;
+};
+
+struct Shape {
+  int64_t d[4] = {0, 0, 0, 0};
+  int64_t numel() const { return d[0] * d[1] * d[2] * d[3]; }
+};
+
+struct Workspace {
+  int N = 0;
+  std::map<std::string, Shape> shapes;
+  std::map<std::string, Buf> bufs;  // plane-capable tensors hold 6 B per element
+  Buf part;                         // conv split-K partials
+  size_t part_floats = 0;
+  Buf nhwc4;                        // input staging for pps_forward_nchw / _bgr
+};
+
+}  // namespace
+}  // namespace pps
+
+struct PpsModel {
+  PpsModelConfig cfg;
+  pps::Plan plan;
+  std::vector<pps::Layer> layers;
+  std::vector<std::pair<int, int>> edges;  // plane-eligible (producer, consumer) layer indices
+  std::set<std::string> plane_capable;     // outputs of edge producers
+  bool x3 = true, fused_stem = false, fused_pps = false, act_planes = false;
+  mutable std::map<int, pps::Workspace> ws;
+  mutable std::vector<std::string> names;  // storage for pps_model_layer_info
+};
+
+namespace pps {
+namespace {
+
+int conv_out(int h, int pad, int dil, int k, int stride) {
+  return (h + 2 * pad - dil * (k - 1) - 1) / stride + 1;
+}
+
+int count_readers(const PpsModel& m, const std::string& blob, bool all_keys) {
+  int n = 0;
+  for (const auto& L : m.layers) {
+    if (L.input == blob) ++n;
+    if (all_keys && (L.input2 == blob || L.residual == blob)) ++n;
+  }
+  return n;
+}
+
+void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t st) {
+  const Plan& plan = m.plan;
+  // projection shortcuts fused into their block's branch2c GEMM (K concat)
+  std::map<std::string, const PlanLayer*> shortcut_of;
+  for (const auto& L : plan.layers)
+    if (L.op == Op::Conv && L.name.size() > 8 &&
+        L.name.compare(L.name.size() - 8, 8, "_branch1") == 0 && L.k == 1)
+      shortcut_of[L.output] = &L;
+  auto bias_of = [&](const std::string& n) -> const Blob* {
+    auto it = blobs.find(n);
+    return it == blobs.end() ? nullptr : &it->second;
+  };
+  for (const auto& P : plan.layers) {
+    Layer L;
+    L.op = P.op; L.name = P.name.empty() ? P.output : P.name;
+    L.input = P.input; L.output = P.output; L.residual = P.residual;
+    L.cin = P.cin; L.cout = P.cout; L.k = P.k; L.stride = P.stride; L.pad = P.pad; L.dil = P.dil;
+    L.relu = P.relu;
+    if (P.op == Op::Conv && shortcut_of.count(P.output)) continue;  // inside its branch2c
+    if (P.op == Op::Conv && shortcut_of.count(P.residual)) {
+      const PlanLayer& S = *shortcut_of.at(P.residual);
+      int kpad1 = 0, kpad2 = 0;
+      std::vector<float> w1 = pack_conv(blobs.at(P.name + "_w"), 0, kpad1);
+      std::vector<float> w2 = pack_conv(blobs.at(S.name + "_w"), 0, kpad2);
+      PPS_MCHECK(kpad1 == P.cin && kpad2 == S.cin, "fused shortcut needs Cin % 16 == 0");
+      std::vector<float> s1, h1, s2, h2;
+      fold_bn(blobs, P.bn, nullptr, s1, h1);
+      fold_bn(blobs, S.bn, nullptr, s2, h2);
+      const int K = kpad1 + kpad2;
+      std::vector<float> w((size_t)P.cout * K), sh(P.cout);
+      for (int o = 0; o < P.cout; ++o) {
+        for (int k = 0; k < kpad1; ++k) w[(size_t)o * K + k] = w1[(size_t)o * kpad1 + k] * s1[o];
+        for (int k = 0; k < kpad2; ++k)
+          w[(size_t)o * K + kpad1 + k] = w2[(size_t)o * kpad2 + k] * s2[o];
+        sh[o] = h1[o] + h2[o];
+      }
+      L.op = Op::ConvDual;
+      L.w = upload(w, st); L.shift = upload(sh, st);
+      L.kpad = kpad1; L.cin_eff = P.cin;
+      L.input2 = S.input; L.stride2 = S.stride; L.residual.clear(); L.shortcut_cin = S.cin;
+      m.layers.push_back(L);
+      continue;
+    }
+    if (P.op == Op::Conv) {
+      const int cin_pad = P.cin == 3 ? 4 : 0;
+      std::vector<float> w = pack_conv(blobs.at(P.name + "_w"), cin_pad, L.kpad);
+      std::vector<float> sc, sh;
+      fold_bn(blobs, P.bn, bias_of(P.name + "_b"), sc, sh);
+      L.w = upload(w, st); L.scale = upload(sc, st); L.shift = upload(sh, st);
+      L.cin_eff = cin_pad ? cin_pad : P.cin;
+    } else if (P.op == Op::Heads) {
+      const int nb = (int)P.prefixes.size();
+      std::vector<float> w((size_t)nb * P.dim_inner * P.dim), sc, sh, s1, h1;
+      for (int b = 0; b < nb; ++b) {
+        const Blob& wb = blobs.at(P.prefixes[b] + "_conv_w");
+        std::copy(wb.data, wb.data + (size_t)P.dim_inner * P.dim,
+                  w.begin() + (size_t)b * P.dim_inner * P.dim);
+        fold_bn(blobs, P.prefixes[b] + "_bn", bias_of(P.prefixes[b] + "_conv_b"), s1, h1);
+        sc.insert(sc.end(), s1.begin(), s1.end());
+        sh.insert(sh.end(), h1.begin(), h1.end());
+      }
+      L.w = upload(w, st); L.scale = upload(sc, st); L.shift = upload(sh, st);
+      L.dim = P.dim; L.dim_inner = P.dim_inner; L.nsub = nb;
+    } else if (P.op == Op::Pps) {
+      L.split = P.split; L.max_ave = P.max_ave; L.nsub = (int)P.prefixes.size();
+    } else if (P.op == Op::Normalize && !m.layers.empty() && m.layers.back().op == Op::Heads) {
+      // heads as split-K partials + one reduce/BN/ReLU/Normalize pass
+      m.layers.back().normalize = true;
+      m.layers.back().output = P.output;
+      m.layers.back().name = P.output;
+      continue;
+    }
+    m.layers.push_back(L);
+  }
+  if (m.x3) {
+    for (auto& L : m.layers) {
+      if (L.op == Op::Conv || L.op == Op::ConvDual)
+        L.w = split3(L.w, (int64_t)L.cout * (L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad), 1, st);
+      else if (L.op == Op::Heads)
+        L.w = split3(L.w, (int64_t)L.dim_inner * L.dim, L.nsub, st);
+    }
+  }
+  // conv1 + BN + ReLU + pool1 as one kernel (x3, input width 128 only)
+  if (m.fused_stem) {
+    bool done = false;
+    for (size_t i = 0; i + 1 < m.layers.size() && !done; ++i) {
+      Layer& L = m.layers[i];
+      const Layer& P = m.layers[i + 1];
+      if (L.op == Op::Conv && L.input == "data" && L.k == 7 && L.stride == 2 && L.pad == 3 &&
+          L.dil == 1 && L.cin == 3 && L.cout == 64 && L.relu && L.residual.empty() &&
+          P.op == Op::MaxPool && P.input == L.output && P.k == 3 && P.stride == 2 && P.pad == 1 &&
+          count_readers(m, L.output, false) == 1) {
+        Layer F = L;
+        F.op = Op::StemPool; F.output = P.output; F.conv_output = L.output;
+        F.w = split3(upload(pack_stem(blobs.at(L.name + "_w")), st), 64LL * pps_stem_k(), 1, st);
+        m.layers[i] = F;
+        m.layers.erase(m.layers.begin() + i + 1);
+        done = true;
+      }
+    }
+    m.fused_stem = done;
+  }
+  // the last conv (+ residual + ReLU) and the part pooling that is its only
+  // reader as one conv_pps layer (x3)
+  if (m.fused_pps) {
+    bool done = false;
+    for (size_t i = 0; i + 1 < m.layers.size() && !done; ++i) {
+      Layer& L = m.layers[i];
+      const Layer& P = m.layers[i + 1];
+      if (L.op == Op::Conv && !L.residual.empty() && L.relu && P.op == Op::Pps &&
+          P.input == L.output && L.output != m.plan.output && L.cin_eff % 32 == 0 &&
+          L.kpad == L.k * L.k * L.cin_eff && count_readers(m, L.output, true) == 1) {
+        Layer F = L;
+        F.op = Op::ConvPps; F.output = P.output; F.conv_output = L.output;
+        F.split = P.split; F.max_ave = P.max_ave; F.nsub = P.nsub;
+        m.layers[i] = F;
+        m.layers.erase(m.layers.begin() + i + 1);
+        done = true;
+      }
+    }
+    m.fused_pps = done;
+  }
+  // (producer, consumer) conv pairs whose tensor may travel as bf16x3 planes:
+  // one reader, a plain conv / conv_pps taking it as main input, Cin % 32 == 0
+  if (m.act_planes) {
+    for (size_t i = 0; i < m.layers.size(); ++i) {
+      const Layer& L = m.layers[i];
+      if (L.op != Op::Conv || L.cin_eff % 4 || L.cout % 4 || L.output == m.plan.output) continue;
+      int nread = 0, j = -1;
+      bool main_input = false;
+      for (size_t r = 0; r < m.layers.size(); ++r) {
+        const Layer& R = m.layers[r];
+        if (R.input == L.output) { ++nread; j = (int)r; main_input = true; }
+        if (R.input2 == L.output) { ++nread; j = (int)r; main_input = false; }
+        if (R.residual == L.output) { ++nread; j = (int)r; main_input = false; }
+      }
+      if (nread == 1 && main_input &&
+          (m.layers[j].op == Op::Conv || m.layers[j].op == Op::ConvPps) &&
+          m.layers[j].cin_eff % 32 == 0) {
+        m.edges.emplace_back((int)i, j);
+        m.plane_capable.insert(L.output);
+      }
+    }
+    // heuristic before any autotune: the 3x3 consumers with Cin >= 256
+    for (auto& e : m.edges) {
+      const Layer& C = m.layers[e.second];
+      const bool on = C.k > 1 && C.cin >= 256;
+      m.layers[e.first].planes_out = m.layers[e.second].planes_in = on;
+    }
+  }
+}
+
+// ---- shapes / workspaces ------------------------------------------------------
+std::map<std::string, Shape> infer_shapes(const PpsModel& m, int N) {
+  std::map<std::string, Shape> s;
+  s["data"] = Shape{{N, m.cfg.height, m.cfg.width, 4}};
+  for (const auto& L : m.layers) {
+    const Shape& x = s.at(L.input);
+    switch (L.op) {
+      case Op::Conv: case Op::ConvDual:
+        s[L.output] = Shape{{x.d[0], conv_out((int)x.d[1], L.pad, L.dil, L.k, L.stride),
+                             conv_out((int)x.d[2], L.pad, L.dil, L.k, L.stride), L.cout}};
+        break;
+      case Op::MaxPool:
+        s[L.output] = Shape{{x.d[0], (x.d[1] + 2 * L.pad - L.k) / L.stride + 1,
+                             (x.d[2] + 2 * L.pad - L.k) / L.stride + 1, x.d[3]}};
+        break;
+      case Op::StemPool: {
+        const int64_t hc = (x.d[1] - 1) / 2 + 1, wc = (x.d[2] - 1) / 2 + 1;
+        s[L.output] = Shape{{x.d[0], (hc - 1) / 2 + 1, (wc - 1) / 2 + 1, L.cout}};
+        break;
+      }
+      case Op::Pps:
+        s[L.output] = Shape{{L.nsub, x.d[0], x.d[3], 1}};
+        break;
+      case Op::ConvPps:
+        s[L.conv_output] = Shape{{x.d[0], conv_out((int)x.d[1], L.pad, L.dil, L.k, L.stride),
+                                  conv_out((int)x.d[2], L.pad, L.dil, L.k, L.stride), L.cout}};
+        s[L.output] = Shape{{L.nsub, x.d[0], L.cout, 1}};
+        break;
+      case Op::Heads:
+        s[L.output] = Shape{{N, (int64_t)L.nsub * L.dim_inner, 1, 1}};
+        s[L.output + "_partials"] = Shape{{kHeadSplitK, N, (int64_t)L.nsub * L.dim_inner, 1}};
+        break;
+      case Op::Normalize:
+        s[L.output] = x;
+        break;
+    }
+  }
+  return s;
+}
+
+std::vector<int> pps_tiles(const PpsModel& m, const Layer& L, const Shape& conv_shape) {
+  std::vector<int> out;
+  const int rows = (int)(conv_shape.d[1] * conv_shape.d[2]);
+  for (int t = GEMM_TILE_P_FIRST; t < GEMM_NUM_TILES; ++t) {
+    const int r = x3p_tile_rows(t, L.planes_in), c = x3p_tile_cols(t, L.planes_in);
+    if (r == rows && c > 0 && c <= 128) out.push_back(t);
+  }
+  (void)m;
+  return out;
+}
+
+size_t part_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) {
+  size_t need = 0;
+  for (const auto& L : m.layers)
+    if (L.op == Op::Conv && L.splitk > 1)
+      need = std::max(need, (size_t)L.splitk * (size_t)shapes.at(L.output).numel());
+  return need;
+}
+
+bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+  return cs != hipStreamCaptureStatusNone;
+}
+
+Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc) {
+  auto it = m.ws.find(N);
+  if (it != m.ws.end()) {
+    Workspace& w = it->second;
+    const size_t need = part_need(m, w.shapes);
+    if (need > w.part_floats) {
+      PPS_MCHECK(allow_alloc && !capturing(st),
+                 "split-K partials grew after pps_model_reserve: reserve again outside capture");
+      w.part = std::make_shared<DevBuf>(need * sizeof(float));
+      w.part_floats = need;
+    }
+    return w;
+  }
+  PPS_MCHECK(allow_alloc && !capturing(st),
+             "no workspace for batch " + std::to_string(N) +
+                 ": call pps_model_reserve before capturing pps_forward");
+  Workspace w;
+  w.N = N;
+  w.shapes = infer_shapes(m, N);
+  bool need_conv_out = false;
+  for (const auto& L : m.layers)
+    if (L.op == Op::ConvPps && pps_tiles(m, L, w.shapes.at(L.conv_output)).empty())
+      need_conv_out = true;
+  for (const auto& kv : w.shapes) {
+    if (kv.first == "data") continue;
+    bool fused_away = false;
+    for (const auto& L : m.layers)
+      if (L.op == Op::ConvPps && L.conv_output == kv.first && !need_conv_out) fused_away = true;
+    if (fused_away) continue;
+    const size_t esz = m.plane_capable.count(kv.first) ? 6 : 4;
+    w.bufs[kv.first] = std::make_shared<DevBuf>((size_t)kv.second.numel() * esz);
+  }
+  w.part_floats = part_need(m, w.shapes);
+  if (w.part_floats) w.part = std::make_shared<DevBuf>(w.part_floats * sizeof(float));
+  return m.ws.emplace(N, std::move(w)).first->second;
+}
+
+float* nhwc4_buffer(const PpsModel& m, Workspace& w, hipStream_t st) {
+  if (!w.nhwc4) {
+    PPS_MCHECK(!capturing(st), "input staging buffer: call pps_model_reserve before capture");
+    w.nhwc4 = std::make_shared<DevBuf>((size_t)w.N * m.cfg.height * m.cfg.width * 4 * sizeof(float));
+  }
+  return w.nhwc4->as<float>();
+}
+
+// ---- one layer ----------------------------------------------------------------
+struct Act {  // an activation operand: f32 NHWC or bf16x3 planes
+  const float* f = nullptr;
+  const uint16_t* pl = nullptr;
+  int64_t plane = 0;
+  Shape s;
+};
+
+void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, float* feat,
+               bool last, int tile, int sk, hipStream_t st) {
+  auto act = [&](const std::string& name, bool planes) {
+    Act a;
+    a.s = w.shapes.at(name);
+    if (name == "data") { a.f = x; return a; }
+    void* p = w.bufs.at(name)->p;
+    if (planes) { a.pl = static_cast<const uint16_t*>(p); a.plane = a.s.numel(); }
+    else a.f = static_cast<const float*>(p);
+    return a;
+  };
+  auto fbuf = [&](const std::string& name) { return w.bufs.at(name)->as<float>(); };
+  const uint16_t* w3 = m.x3 && L.w ? L.w->as<uint16_t>() : nullptr;
+  const float* wf = !m.x3 && L.w ? L.w->as<float>() : nullptr;
+  const float* sc = L.scale ? L.scale->as<float>() : nullptr;
+  const float* sh = L.shift ? L.shift->as<float>() : nullptr;
+  const int N = w.N;
+  switch (L.op) {
+    case Op::Conv: {
+      const Act a = act(L.input, L.planes_in);
+      const Shape ys = w.shapes.at(L.output);
+      const float* res = L.residual.empty() ? nullptr : fbuf(L.residual);
+      const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
+      const int Ho = (int)ys.d[1], Wo = (int)ys.d[2];
+      if (m.x3 && (L.planes_in || L.planes_out || sk > 1)) {
+        const int t = tile >= GEMM_TILE_P_FIRST ? tile : 0;
+        float* yf = L.planes_out ? nullptr : fbuf(L.output);
+        uint16_t* y3 = L.planes_out ? w.bufs.at(L.output)->as<uint16_t>() : nullptr;
+        const int64_t ypl = L.planes_out ? ys.numel() : 0;
+        if (sk > 1)
+          rc_check(pps_conv2d_bn_act_x3p_splitk(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
+                                                L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil,
+                                                sc, sh, res, L.relu, yf, y3, ypl, Ho, Wo, L.cout,
+                                                sk, w.part->as<float>(), t, st));
+        else
+          rc_check(pps_conv2d_bn_act_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout,
+                                         L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res,
+                                         L.relu, yf, y3, ypl, Ho, Wo, L.cout, t, st));
+      } else if (m.x3) {
+        rc_check(pps_conv2d_bn_act_x3(a.f, n, H, W, L.cin_eff, ldx, w3, L.cout, L.kpad, L.k, L.k,
+                                      L.stride, L.pad, L.dil, sc, sh, res, L.relu,
+                                      fbuf(L.output), Ho, Wo, L.cout, tile, st));
+      } else {
+        rc_check(pps_conv2d_bn_act(a.f, n, H, W, L.cin_eff, ldx, wf, L.cout, L.kpad, L.k, L.k,
+                                   L.stride, L.pad, L.dil, sc, sh, res, L.relu, fbuf(L.output),
+                                   Ho, Wo, L.cout, tile, st));
+      }
+      return;
+    }
+    case Op::ConvDual: {
+      const Act a = act(L.input, false), b = act(L.input2, false);
+      const Shape ys = w.shapes.at(L.output);
+      const int C2 = (int)b.s.d[3];
+      if (m.x3)
+        rc_check(pps_conv2d_dual_bn_act_x3(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2],
+                                           L.cin_eff, (int)a.s.d[3], L.k, L.k, L.stride, L.pad,
+                                           b.f, (int)b.s.d[1], (int)b.s.d[2], C2, C2, L.stride2,
+                                           w3, L.cout, L.kpad, C2, sh, L.relu, fbuf(L.output),
+                                           (int)ys.d[1], (int)ys.d[2], L.cout, tile, st));
+      else
+        rc_check(pps_conv2d_dual_bn_act(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2],
+                                        L.cin_eff, (int)a.s.d[3], L.k, L.k, L.stride, L.pad, b.f,
+                                        (int)b.s.d[1], (int)b.s.d[2], C2, C2, L.stride2, wf,
+                                        L.cout, L.kpad, C2, sh, L.relu, fbuf(L.output),
+                                        (int)ys.d[1], (int)ys.d[2], L.cout, tile, st));
+      return;
+    }
+    case Op::MaxPool: {
+      const Act a = act(L.input, false);
+      const Shape ys = w.shapes.at(L.output);
+      rc_check(pps_maxpool2d(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], (int)a.s.d[3],
+                             L.k, L.stride, L.pad, fbuf(L.output), (int)ys.d[1], (int)ys.d[2], st));
+      return;
+    }
+    case Op::StemPool: {
+      const Act a = act(L.input, false);
+      const Shape ys = w.shapes.at(L.output);
+      rc_check(pps_stem_conv_pool_x3(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], w3, sc,
+                                     sh, fbuf(L.output), (int)ys.d[1], (int)ys.d[2], st));
+      return;
+    }
+    case Op::Pps: {
+      const Act a = act(L.input, false);
+      rc_check(pps_part_power_set(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2],
+                                  (int)a.s.d[3], L.split.data(), (int)L.split.size(), L.max_ave,
+                                  fbuf(L.output), st));
+      return;
+    }
+    case Op::ConvPps: {
+      const Act a = act(L.input, L.planes_in);
+      const Shape cs = w.shapes.at(L.conv_output);
+      const float* res = fbuf(L.residual);
+      const std::vector<int> ok = pps_tiles(m, L, cs);
+      const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
+      if (!ok.empty()) {
+        const int t = std::find(ok.begin(), ok.end(), tile) != ok.end() ? tile : ok[0];
+        rc_check(pps_conv2d_bn_act_pps_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
+                                           L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc,
+                                           sh, res, nullptr, (int)cs.d[1], (int)cs.d[2],
+                                           L.split.data(), (int)L.split.size(), L.max_ave,
+                                           fbuf(L.output), t, st));
+      } else {  // no tile holds exactly one image: conv, then the pooling kernel
+        float* y = fbuf(L.conv_output);
+        rc_check(pps_conv2d_bn_act_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout,
+                                       L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, 1,
+                                       y, nullptr, 0, (int)cs.d[1], (int)cs.d[2], L.cout,
+                                       tile >= GEMM_TILE_P_FIRST ? tile : 0, st));
+        rc_check(pps_part_power_set(y, n, (int)cs.d[1], (int)cs.d[2], L.cout, L.split.data(),
+                                    (int)L.split.size(), L.max_ave, fbuf(L.output), st));
+      }
+      return;
+    }
+    case Op::Heads: {
+      float* part = fbuf(L.output + "_partials");
+      const float* xin = fbuf(L.input);
+      if (m.x3)
+        rc_check(pps_gemm_splitk_batched_x3(xin, N, L.dim, w3, L.dim_inner, L.nsub, kHeadSplitK,
+                                            part, tile, st));
+      else
+        rc_check(pps_gemm_splitk_batched(xin, N, L.dim, wf, L.dim_inner, L.nsub, kHeadSplitK,
+                                         part, tile, st));
+      float* y = last ? feat : fbuf(L.output);
+      rc_check(pps_splitk_bn_act_normalize(part, kHeadSplitK, N, L.nsub * L.dim_inner, sc, sh, 1,
+                                           L.normalize ? 1 : 0, y, st));
+      return;
+    }
+    case Op::Normalize: {
+      const Act a = act(L.input, false);
+      rc_check(pps_l2_normalize(a.f, a.s.d[0], (int)a.s.d[1], last ? feat : fbuf(L.output), st));
+      return;
+    }
+  }
+}
+
+void forward_range(const PpsModel& m, const float* x, int N, float* feat, int first, int last,
+                   hipStream_t st) {
+  Workspace& w = workspace(m, N, st, true);
+  for (int i = first; i < last; ++i) {
+    const Layer& L = m.layers[i];
+    run_layer(m, L, w, x, feat, i + 1 == (int)m.layers.size(), L.tile, L.splitk, st);
+  }
+}
+
+bool tunable(const Layer& L) {
+  return L.op == Op::Conv || L.op == Op::ConvDual || L.op == Op::Heads || L.op == Op::ConvPps;
+}
+
+double layer_flops(const PpsModel& m, const Layer& L, const std::map<std::string, Shape>& s, int N) {
+  switch (L.op) {
+    case Op::StemPool: {
+      const Shape& x = s.at(L.input);
+      const double hc = (double)((x.d[1] - 1) / 2 + 1), wc = (double)((x.d[2] - 1) / 2 + 1);
+      return 2.0 * N * hc * wc * L.cout * L.k * L.k * L.cin;  // true Cin = 3
+    }
+    case Op::Conv: case Op::ConvDual: case Op::ConvPps: {
+      const Shape& y = s.at(L.op == Op::ConvPps ? L.conv_output : L.output);
+      return 2.0 * y.d[0] * y.d[1] * y.d[2] * y.d[3] * ((double)L.k * L.k * L.cin + L.shortcut_cin);
+    }
+    case Op::Heads:
+      return 2.0 * N * L.nsub * L.dim_inner * L.dim;
+    default:
+      return 0.0;
+  }
+  (void)m;
+}
+
+// algorithmic HBM bytes per launch: every operand read once, the output
+// written once (model.py PPSModel._alloc)
+double layer_bytes(const PpsModel& m, const Layer& L, const std::map<std::string, Shape>& s, int N) {
+  const double wb = m.x3 ? 6.0 : 4.0;
+  switch (L.op) {
+    case Op::StemPool:
+      return 4.0 * s.at(L.input).numel() + 4.0 * s.at(L.output).numel() +
+             wb * L.cout * pps_stem_k();
+    case Op::Conv: case Op::ConvDual: {
+      const Shape& y = s.at(L.output);
+      double b = 4.0 * s.at(L.input).numel() + 4.0 * y.numel() +
+                 wb * L.cout * ((double)L.k * L.k * L.cin + L.shortcut_cin);
+      if (!L.residual.empty()) b += 4.0 * y.numel();
+      if (L.op == Op::ConvDual) b += 4.0 * s.at(L.input2).numel();
+      return b;
+    }
+    case Op::ConvPps: {
+      const Shape& y = s.at(L.conv_output);
+      return 4.0 * s.at(L.input).numel() + 4.0 * y.numel() +
+             wb * L.cout * (double)L.k * L.k * L.cin + 4.0 * s.at(L.output).numel();
+    }
+    case Op::Heads:
+      return 4.0 * s.at(L.input).numel() + wb * L.nsub * L.dim_inner * L.dim +
+             4.0 * kHeadSplitK * N * L.nsub * L.dim_inner;
+    default:
+      return 0.0;
+  }
+}
+
+// ---- autotune (the reference's cudnn_exhaustive_search analogue,
+// modeling/detector.py:58; same procedure as PPSModel.autotune) --------------
+struct Timer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  Timer() {
+    hip_check(hipEventCreate(&e0), "hipEventCreate");
+    hip_check(hipEventCreate(&e1), "hipEventCreate");
+  }
+  ~Timer() {
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+};
+
+float time_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, int tile,
+                 int sk, int reps, hipStream_t st, Timer& t) {
+  for (int i = 0; i < 2; ++i) run_layer(m, L, w, x, nullptr, false, tile, sk, st);
+  hip_check(hipEventRecord(t.e0, st), "hipEventRecord");
+  for (int i = 0; i < reps; ++i) run_layer(m, L, w, x, nullptr, false, tile, sk, st);
+  hip_check(hipEventRecord(t.e1, st), "hipEventRecord");
+  hip_check(hipEventSynchronize(t.e1), "hipEventSynchronize");
+  float ms = 0.f;
+  hip_check(hipEventElapsedTime(&ms, t.e0, t.e1), "hipEventElapsedTime");
+  return ms / reps;
+}
+
+}  // namespace
+}  // namespace pps
+
+using namespace pps;
+
+namespace {
+template <class F> int guarded(F&& f) {
+  try {
+    f();
+    return PPS_OK;
+  } catch (const ModelError& e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_error(std::string("pps model: ") + e.what());
+    return PPS_ERR_INVALID_ARG;
+  }
+}
+
+Layer* find_layer(PpsModel* m, const char* name) {
+  PPS_MCHECK(m && name, "null argument");
+  for (auto& L : m->layers)
+    if (L.name == name) return &L;
+  throw ModelError(PPS_ERR_INVALID_ARG, std::string("no layer named '") + name + "'");
+}
+
+__global__ void nchw_to_nhwc4_kernel(const float* __restrict__ x, int64_t npix_img, int64_t total,
+                                     float4* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = i / npix_img, p = i - n * npix_img;
+    const float* src = x + n * 3 * npix_img + p;
+    y[i] = make_float4(src[0], src[npix_img], src[2 * npix_img], 0.f);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int pps_model_config_default(PpsModelConfig* c) {
+  if (!c) return PPS_ERR_INVALID_ARG;
+  std::memset(c, 0, sizeof(*c));
+  c->struct_size = (int)sizeof(PpsModelConfig);
+  // configs/market1501/pps_crm_triplet_R-50_1x.yaml (the reference's PPS
+  // Market-1501 test configuration)
+  c->height = 384; c->width = 128;
+  c->strip_num = 5; c->bpm_dim = 128;
+  c->num_groups = 1; c->width_per_group = 64; c->stride_1x1 = 1;
+  c->res5_stride = 1; c->res5_dilation = 1;
+  c->fpn_on = 0; c->fpn_dim = 256;
+  c->max_ave = 1; c->normalize = 1;
+  c->math = PPS_MATH_X3;
+  c->fused_stem = 1; c->fused_pps = 1; c->act_planes = 1;
+  c->pixel_means[0] = 102.9801f; c->pixel_means[1] = 115.9465f; c->pixel_means[2] = 122.7717f;
+  return PPS_OK;
+}
+
+int pps_model_create(const PpsBlob* blobs, int nblobs, const PpsModelConfig* cfg,
+                     PpsModel** out) {
+  return guarded([&] {
+    PPS_MCHECK(out && cfg && (blobs || nblobs == 0) && nblobs >= 0, "null argument");
+    PPS_MCHECK(cfg->struct_size == (int)sizeof(PpsModelConfig),
+               "PpsModelConfig.struct_size mismatch (use pps_model_config_default)");
+    *out = nullptr;
+    const PpsModelConfig& c = *cfg;
+    PPS_MCHECK(c.height > 0 && c.width > 0 && c.strip_num >= 1 && c.strip_num <= 10 &&
+                   c.bpm_dim > 0 && c.num_groups > 0 && c.width_per_group > 0 &&
+                   c.res5_stride >= 1 && c.res5_dilation >= 1 && c.fpn_dim > 0,
+               "bad config");
+    PPS_MCHECK(c.math == PPS_MATH_X3 || c.math == PPS_MATH_F32, "math must be PPS_MATH_X3 or _F32");
+    auto m = std::make_unique<PpsModel>();
+    m->cfg = c;
+    m->plan = build_plan(c);
+    m->x3 = c.math == PPS_MATH_X3;
+    m->fused_stem = m->x3 && c.fused_stem && c.width == 128;  // the fused stem's kernel is W = 128
+    m->fused_pps = m->x3 && c.fused_pps;
+    m->act_planes = m->x3 && c.act_planes;
+    std::map<std::string, Blob> bmap;
+    for (int i = 0; i < nblobs; ++i) {
+      const PpsBlob& b = blobs[i];
+      PPS_MCHECK(b.name && (b.data || b.ndim == 0) && b.ndim >= 0 && b.ndim <= 4, "bad blob entry");
+      Blob B{b.data, std::vector<int64_t>(b.shape, b.shape + b.ndim)};
+      bmap[b.name] = B;
+    }
+    std::vector<std::string> missing;
+    for (const auto& kv : m->plan.params) {
+      auto it = bmap.find(kv.first);
+      const bool optional = kv.first.size() > 7 &&
+                            kv.first.compare(kv.first.size() - 7, 7, "_conv_b") == 0;
+      if (it == bmap.end()) {
+        if (!optional) missing.push_back(kv.first);
+        continue;
+      }
+      int64_t want = 1;
+      for (auto s : kv.second) want *= s;
+      PPS_MCHECK(it->second.numel() == want,
+                 "blob " + kv.first + " has " + std::to_string(it->second.numel()) +
+                     " elements, the net needs " + std::to_string(want));
+      it->second.shape = kv.second;
+    }
+    PPS_MCHECK(missing.empty(), "weights missing " + std::to_string(missing.size()) +
+                                    " blobs, e.g. " + (missing.empty() ? "" : missing[0]));
+    hipStream_t st = nullptr;
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    try {
+      compile(*m, bmap, st);
+    } catch (...) {
+      (void)hipStreamDestroy(st);
+      throw;
+    }
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    (void)hipStreamDestroy(st);
+    *out = m.release();
+  });
+}
+
+int pps_model_destroy(PpsModel* m) {
+  return guarded([&] {
+    if (!m) return;
+    (void)hipDeviceSynchronize();  // no launch of this model may still read its buffers
+    delete m;
+  });
+}
+
+int pps_model_feat_dim(const PpsModel* m) { return m ? m->plan.feat_dim : -1; }
+int pps_model_num_layers(const PpsModel* m) { return m ? (int)m->layers.size() : -1; }
+
+int pps_model_layer_info(const PpsModel* m, int i, int N, PpsLayerInfo* info) {
+  return guarded([&] {
+    PPS_MCHECK(m && info, "null argument");
+    PPS_MCHECK(i >= 0 && i < (int)m->layers.size(), "layer index out of range");
+    PPS_MCHECK(N > 0, "N must be positive");
+    const Layer& L = m->layers[i];
+    const auto shapes = infer_shapes(*m, N);
+    std::memset(info, 0, sizeof(*info));
+    info->name = L.name.c_str();
+    info->op = op_name(L.op);
+    info->tile = L.tile;
+    info->splitk = L.splitk;
+    info->planes_in = L.planes_in;
+    info->planes_out = L.planes_out;
+    info->gemm = tunable(L) || L.op == Op::StemPool;
+    info->flops = layer_flops(*m, L, shapes, N);
+    info->bytes = layer_bytes(*m, L, shapes, N);
+    const Shape& y = shapes.at(L.op == Op::ConvPps ? L.output : L.output);
+    for (int d = 0; d < 4; ++d) info->out_shape[d] = y.d[d];
+  });
+}
+
+int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
+  return guarded([&] {
+    Layer* L = find_layer(m, layer);
+    PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
+    PPS_MCHECK(tile >= 0 && tile < GEMM_NUM_TILES, "tile out of range");
+    L->tile = tile;
+  });
+}
+
+int pps_model_set_splitk(PpsModel* m, const char* layer, int splitk) {
+  return guarded([&] {
+    Layer* L = find_layer(m, layer);
+    PPS_MCHECK(L->op == Op::Conv, std::string("split-K applies to plain convs, not '") + layer + "'");
+    PPS_MCHECK(splitk >= 1 && splitk <= kMaxSplitK, "splitk must be in [1, 4]");
+    PPS_MCHECK(splitk == 1 || (m->x3 && L->cin_eff % 32 == 0 && L->kpad == L->k * L->k * L->cin_eff &&
+                               L->kpad % (32 * splitk) == 0),
+               "split-K " + std::to_string(splitk) + " not possible for " + layer);
+    L->splitk = splitk;
+  });
+}
+
+int pps_model_num_plane_edges(const PpsModel* m) { return m ? (int)m->edges.size() : -1; }
+
+int pps_model_plane_edge(const PpsModel* m, int i, const char** producer, const char** consumer,
+                         int* on) {
+  return guarded([&] {
+    PPS_MCHECK(m && producer && consumer && on, "null argument");
+    PPS_MCHECK(i >= 0 && i < (int)m->edges.size(), "edge index out of range");
+    const Layer& P = m->layers[m->edges[i].first];
+    *producer = P.name.c_str();
+    *consumer = m->layers[m->edges[i].second].name.c_str();
+    *on = P.planes_out;
+  });
+}
+
+int pps_model_set_planes(PpsModel* m, const char* producer, int on) {
+  return guarded([&] {
+    PPS_MCHECK(m && producer, "null argument");
+    for (auto& e : m->edges)
+      if (m->layers[e.first].name == producer) {
+        m->layers[e.first].planes_out = m->layers[e.second].planes_in = on != 0;
+        return;
+      }
+    throw ModelError(PPS_ERR_INVALID_ARG,
+                     std::string("not a plane-eligible producer: '") + producer + "'");
+  });
+}
+
+int pps_model_reserve(PpsModel* m, int N) {
+  return guarded([&] {
+    PPS_MCHECK(m && N > 0, "bad arguments");
+    Workspace& w = workspace(*m, N, nullptr, true);
+    nhwc4_buffer(*m, w, nullptr);
+  });
+}
+
+int pps_model_release(PpsModel* m, int N) {
+  return guarded([&] {
+    PPS_MCHECK(m, "null argument");
+    (void)hipDeviceSynchronize();
+    if (N > 0) m->ws.erase(N);
+    else m->ws.clear();
+  });
+}
+
+int pps_model_tensor(const PpsModel* m, int N, const char* blob, void** ptr, int* planes,
+                     int64_t* shape4) {
+  return guarded([&] {
+    PPS_MCHECK(m && blob && ptr && planes && shape4, "null argument");
+    auto it = m->ws.find(N);
+    PPS_MCHECK(it != m->ws.end(), "no workspace for this batch size (pps_model_reserve)");
+    auto b = it->second.bufs.find(blob);
+    PPS_MCHECK(b != it->second.bufs.end(), std::string("no device tensor '") + blob + "'");
+    *ptr = b->second->p;
+    *planes = 0;
+    for (const auto& L : m->layers)
+      if (L.output == blob && L.planes_out) *planes = 1;
+    const Shape& s = it->second.shapes.at(blob);
+    for (int d = 0; d < 4; ++d) shape4[d] = s.d[d];
+  });
+}
+
+int pps_forward_layers(const PpsModel* m, const float* x, int N, float* feat, int first,
+                       int last, void* stream) {
+  return guarded([&] {
+    PPS_MCHECK(m && x && feat, "null pointer");
+    PPS_MCHECK(N > 0, "N must be positive");
+    PPS_MCHECK(0 <= first && first <= last && last <= (int)m->layers.size(), "bad layer range");
+    PPS_MCHECK(aligned16(x) && aligned16(feat), "x / feat must be 16-byte aligned");
+    forward_range(*m, x, N, feat, first, last, as_stream(stream));
+  });
+}
+
+int pps_forward(const PpsModel* m, const float* nhwc4, int N, float* feat, void* stream) {
+  return pps_forward_layers(m, nhwc4, N, feat, 0, m ? (int)m->layers.size() : 0, stream);
+}
+
+int pps_forward_nchw(const PpsModel* m, const float* nchw, int N, float* feat, void* stream) {
+  return guarded([&] {
+    PPS_MCHECK(m && nchw && feat, "null pointer");
+    PPS_MCHECK(N > 0, "N must be positive");
+    const hipStream_t st = as_stream(stream);
+    Workspace& w = workspace(*m, N, st, true);
+    float* x = nhwc4_buffer(*m, w, st);
+    const int64_t npix = (int64_t)m->cfg.height * m->cfg.width, total = npix * N;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65535);
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, nchw, npix,
+                       total, reinterpret_cast<float4*>(x));
+    hip_check(hipGetLastError(), "nchw_to_nhwc4_kernel");
+    forward_range(*m, x, N, feat, 0, (int)m->layers.size(), st);
+  });
+}
+
+int pps_forward_bgr(const PpsModel* m, const uint8_t* img, int N, int Hi, int Wi, float* feat,
+                    void* stream) {
+  return guarded([&] {
+    PPS_MCHECK(m && img && feat, "null pointer");
+    PPS_MCHECK(N > 0, "N must be positive");
+    const hipStream_t st = as_stream(stream);
+    Workspace& w = workspace(*m, N, st, true);
+    float* x = nhwc4_buffer(*m, w, st);
+    rc_check(pps_preprocess_bgr(img, N, Hi, Wi, m->cfg.pixel_means, m->cfg.height, m->cfg.width,
+                                x, st));
+    forward_range(*m, x, N, feat, 0, (int)m->layers.size(), st);
+  });
+}
+
+int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stream) {
+  return guarded([&] {
+    PPS_MCHECK(m && x, "null pointer");
+    PPS_MCHECK(N > 0, "N must be positive");
+    const hipStream_t st = as_stream(stream);
+    PPS_MCHECK(!capturing(st), "autotune cannot run inside a graph capture");
+    const int reps = 3, finalists = 4, final_reps = 10;
+    Workspace* w = &workspace(*m, N, st, true);
+    std::vector<float> scratch((size_t)N * m->plan.feat_dim);
+    DevBuf feat(scratch.size() * sizeof(float));
+    forward_range(*m, x, N, feat.as<float>(), 0, (int)m->layers.size(), st);
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Timer t;
+    auto cands_of = [&](const Layer& L) {
+      std::vector<int> c;
+      if (L.op == Op::ConvPps) {
+        c = pps_tiles(*m, L, w->shapes.at(L.conv_output));
+      } else {
+        const bool pipelined_only = L.planes_in || L.planes_out;
+        for (int tl = pipelined_only ? GEMM_TILE_P_FIRST : 1; tl < GEMM_NUM_TILES; ++tl)
+          c.push_back(tl);
+      }
+      if (c.empty()) c.push_back(0);
+      return c;
+    };
+    auto tune = [&](Layer& L) {
+      std::vector<std::pair<float, int>> screen;
+      for (int tl : cands_of(L)) screen.emplace_back(time_layer(*m, L, *w, x, tl, L.splitk, reps, st, t), tl);
+      std::sort(screen.begin(), screen.end());
+      float best = 1e30f;
+      for (int i = 0; i < (int)screen.size() && i < finalists; ++i) {
+        const float ms = time_layer(*m, L, *w, x, screen[i].second, L.splitk, final_reps, st, t);
+        if (ms < best) { best = ms; L.tile = screen[i].second; }
+      }
+      return best;
+    };
+    const bool tune_planes = (flags & PPS_AUTOTUNE_NO_PLANES) == 0 && m->act_planes;
+    if (tune_planes)
+      for (auto& e : m->edges) m->layers[e.first].planes_out = m->layers[e.second].planes_in = false;
+    std::vector<float> cost(m->layers.size(), 0.f);
+    for (size_t i = 0; i < m->layers.size(); ++i)
+      if (tunable(m->layers[i])) cost[i] = tune(m->layers[i]);
+    if (tune_planes) {
+      for (auto& e : m->edges) {
+        Layer& P = m->layers[e.first];
+        Layer& C = m->layers[e.second];
+        const float before = cost[e.first] + cost[e.second];
+        const int tp = P.tile, tc = C.tile;
+        P.planes_out = C.planes_in = true;
+        const float cp = tune(P), cc = tune(C);
+        if (cp + cc < 0.98f * before) {
+          cost[e.first] = cp; cost[e.second] = cc;
+        } else {
+          P.planes_out = C.planes_in = false;
+          P.tile = tp; C.tile = tc;
+        }
+      }
+    }
+    if (m->x3 && (flags & PPS_AUTOTUNE_SPLITK)) {
+      for (size_t i = 0; i < m->layers.size(); ++i) {
+        Layer& L = m->layers[i];
+        if (L.op != Op::Conv || L.cin_eff % 32 || L.kpad != L.k * L.k * L.cin_eff) continue;
+        std::vector<std::pair<float, std::pair<int, int>>> screen;
+        for (int sk = 2; sk <= kMaxSplitK; ++sk) {
+          if (L.kpad % (32 * sk)) continue;
+          const int save = L.splitk;
+          L.splitk = sk;
+          w = &workspace(*m, N, st, true);  // grow the partials buffer
+          L.splitk = save;
+          for (int tl = GEMM_TILE_P_FIRST; tl < GEMM_NUM_TILES; ++tl)
+            screen.push_back({time_layer(*m, L, *w, x, tl, sk, reps, st, t), {tl, sk}});
+        }
+        if (screen.empty()) continue;
+        std::sort(screen.begin(), screen.end());
+        float best = 1e30f;
+        std::pair<int, int> pick{0, 1};
+        for (int j = 0; j < (int)screen.size() && j < finalists; ++j) {
+          const auto o = screen[j].second;
+          const float ms = time_layer(*m, L, *w, x, o.first, o.second, final_reps, st, t);
+          if (ms < best) { best = ms; pick = o; }
+        }
+        if (best < 0.98f * cost[i]) {
+          L.tile = pick.first; L.splitk = pick.second; cost[i] = best;
+        }
+      }
+    }
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  });
+}
+
+}  // extern "C"

@@ -185,6 +185,15 @@ int pick_tile(const GemmParams& p, int batch);
 
 // ---- retrieval (rank.hip) ---------------------------------------------------
 constexpr int kMergeMaxLists = 64;
+// rank_count_stream / cmc_counts: gallery entries per workgroup (grid.y =
+// chunks of a row, <= 65535)
+constexpr int kRankStreamChunk = 8192;
+// rank_prepare merges R*Pmax positives in dynamic LDS (4 int arrays):
+// 16 B per merged positive, 128 KiB at the cap -- within gfx950's 160 KiB
+// LDS per workgroup (this library is built for gfx950 only)
+constexpr int kRankMergeCap = 8192;
+constexpr int kLdsBytesGfx950 = 160 * 1024;
+static_assert(16 * kRankMergeCap <= kLdsBytesGfx950, "rank_prepare LDS exceeds the CU's LDS");
 struct MergeOffsets {  // kernel-argument copy of the per-list global offsets
   int64_t off[kMergeMaxLists];
 };

@@ -469,7 +469,8 @@ int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* 
 #endif
 constexpr int kStreamThreads = 256;
 constexpr int kStreamU = RANK_STREAM_U;                      // float4 per thread in flight
-constexpr int kStreamChunk = kStreamThreads * kStreamU * 4;  // 4096 entries per block
+constexpr int kStreamChunk = kStreamThreads * kStreamU * 4;  // 8192 entries per block
+static_assert(kStreamChunk == kRankStreamChunk, "pps_internal.hpp kRankStreamChunk");
 constexpr int kStreamLdsCap = 6144;                          // positives held in LDS
 
 template <bool KLDS>
@@ -701,6 +702,157 @@ int ap_finalize(int64_t Q, int Ptot, const float* sorted_d, const int32_t* pos_t
   hipLaunchKernelGGL(ap_finalize_kernel, dim3((unsigned)Q), dim3(64), 0, st, Q, Ptot,
                      sorted_d, pos_total, hist, before, ap, valid, first_rank);
   PPS_CHECK_LAUNCH("ap_finalize_kernel");
+  return PPS_OK;
+}
+
+// ---- 4) CMC beyond the Market protocol (reid_dataset_evaluator.py:283-363) -------
+// The reference's cmc defaults to first_match_break=False: for the j-th true
+// match (in rank order) at position k among the valid entries it adds
+// 1/#matches to ret[k - j], k - j = the number of valid NON-matches ranked
+// before it (:349-356); separate_camera_set=True also drops every gallery
+// entry from the query's camera (:329-331).  Both need, per positive p, the
+// exact count of valid entries ordered before it.  Entry e is binned at
+// b(e) = #positives whose (distance, global index) key is below e's, so
+// H[p] = sum_{b <= p} hist[b] counts the valid entries ranked before positive
+// p plus the positives 0..p: k - j = H[p] - p - 1.  Exact under the stable
+// (distance, index) order, ties included; additive over gallery shards.
+constexpr int kCmcLdsCap = 4096;
+
+template <bool KLDS, bool SEP>
+__global__ void __launch_bounds__(kStreamThreads)
+cmc_count_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int64_t g_offset,
+                 int Ptot, const float* __restrict__ sorted_d,
+                 const int32_t* __restrict__ sorted_idx, const int32_t* __restrict__ pos_total,
+                 const int32_t* __restrict__ qcam, const int32_t* __restrict__ gcam, int Jmax,
+                 const float* __restrict__ junk_d, const int32_t* __restrict__ junk_idx,
+                 const int32_t* __restrict__ junk_cnt, int32_t* __restrict__ hist) {
+  const int64_t q = blockIdx.x;
+  const int P = pos_total[q];
+  if (P == 0) return;
+  extern __shared__ int slds[];
+  float* sd = reinterpret_cast<float*>(slds);
+  int* si = slds + (KLDS ? P : 0);
+  int* hs = slds + (KLDS ? 2 * P : 0);
+  const float* gsd = sorted_d + q * Ptot;
+  const int32_t* gsi = sorted_idx + q * Ptot;
+  int32_t* ghist = hist + q * Ptot;
+  if (KLDS) {
+    for (int p = threadIdx.x; p < P; p += kStreamThreads) {
+      sd[p] = gsd[p];
+      si[p] = gsi[p];
+      hs[p] = 0;
+    }
+    __syncthreads();
+  }
+  const float* S = KLDS ? sd : gsd;
+  const int32_t* I = KLDS ? si : gsi;
+  const float dmax = S[P - 1];
+  // b = #positives with key < (d, gi); entries ordered after every positive
+  // (b == P) do not count
+  auto key_bin = [&](float d, int64_t gi) {
+    int lo = 0, hi = P;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (S[mid] < d || (S[mid] == d && (int64_t)I[mid] < gi)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  auto add = [&](int b, int v) {
+    if (b < P) {
+      if (KLDS) atomicAdd(&hs[b], v); else atomicAdd(&ghist[b], v);
+    }
+  };
+  const int qc = SEP ? qcam[q] : 0;
+  const int64_t c0 = (int64_t)blockIdx.y * kStreamChunk;
+  const int64_t c1 = c0 + kStreamChunk < G ? c0 + kStreamChunk : G;
+  const float* row = dist + q * ldd;
+  for (int64_t i = c0 + threadIdx.x; i < c1; i += kStreamThreads) {
+    const float d = row[i];
+    if (d > dmax) continue;
+    if (SEP && gcam[i] == qc) continue;  // same camera: never valid
+    add(key_bin(d, g_offset + i), 1);
+  }
+  if (!SEP && blockIdx.y == 0) {  // this shard's junk (same id, same camera) back out
+    const int nj = junk_cnt[q] < Jmax ? junk_cnt[q] : Jmax;
+    for (int j = threadIdx.x; j < nj; j += kStreamThreads) {
+      const float d = junk_d[q * Jmax + j];
+      if (d <= dmax) add(key_bin(d, (int64_t)junk_idx[q * Jmax + j]), -1);
+    }
+  }
+  if (KLDS) {
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += kStreamThreads)
+      if (hs[p]) atomicAdd(&ghist[p], hs[p]);
+  }
+}
+
+int cmc_counts(const float* dist, int64_t Q, int64_t G, int64_t ldd, int64_t g_offset, int Ptot,
+               const float* sorted_d, const int32_t* sorted_idx, const int32_t* pos_total,
+               const int32_t* qcam, const int32_t* gcam, int Jmax, const float* junk_d,
+               const int32_t* junk_idx, const int32_t* junk_cnt, int32_t* hist,
+               hipStream_t st) {
+  if (Q <= 0 || G <= 0) return PPS_OK;
+  const int64_t nchunk = (G + kStreamChunk - 1) / kStreamChunk;
+  const bool lds = Ptot <= kCmcLdsCap, sep = gcam != nullptr;
+  const size_t shm = lds ? (size_t)3 * Ptot * sizeof(int) : 0;
+  for (int64_t q0 = 0; q0 < Q; q0 += 65535) {  // grid.x limit
+    const int64_t qn = Q - q0 < 65535 ? Q - q0 : 65535;
+    const dim3 grid((unsigned)qn, (unsigned)nchunk);
+    auto launch = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, grid, dim3(kStreamThreads), shm, st, dist + q0 * ldd, G, ldd,
+                         g_offset, Ptot, sorted_d + q0 * Ptot, sorted_idx + q0 * Ptot,
+                         pos_total + q0, sep ? qcam + q0 : nullptr, gcam, Jmax,
+                         junk_d + q0 * Jmax, junk_idx + q0 * Jmax, junk_cnt + q0,
+                         hist + q0 * Ptot);
+    };
+    if (lds && sep) launch(cmc_count_kernel<true, true>);
+    else if (lds) launch(cmc_count_kernel<true, false>);
+    else if (sep) launch(cmc_count_kernel<false, true>);
+    else launch(cmc_count_kernel<false, false>);
+    PPS_CHECK_LAUNCH("cmc_count_kernel");
+  }
+  return PPS_OK;
+}
+
+// Per query (one wave): ret[q][0..topk) = the reference's CMC row after its
+// cumsum (:358-360): for positives p = 0.. in rank order, c = H[p] - p - 1;
+// stop at c >= topk; first_match_break adds 1 once, else 1/P each, summed in
+// the reference's order (float64, same rounding).  valid[q] = P > 0.
+__global__ void cmc_finalize_kernel(int Ptot, const int32_t* __restrict__ pos_total,
+                                    const int32_t* __restrict__ hist, int topk, int fmb,
+                                    double* __restrict__ ret, int32_t* __restrict__ valid) {
+  const int64_t q = blockIdx.x;
+  const int P = pos_total[q];
+  double* r = ret + q * topk;
+  for (int t = threadIdx.x; t < topk; t += 64) r[t] = 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    valid[q] = P > 0 ? 1 : 0;
+    if (P > 0) {
+      const int32_t* h = hist + q * Ptot;
+      const double delta = 1.0 / (double)P;
+      int64_t H = 0;
+      for (int p = 0; p < P; ++p) {
+        H += h[p];
+        const int64_t c = H - p - 1;
+        if (c >= topk) break;
+        if (fmb) {
+          r[c] += 1.0;
+          break;
+        }
+        r[c] += delta;
+      }
+      for (int t = 1; t < topk; ++t) r[t] += r[t - 1];
+    }
+  }
+}
+
+int cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_t* hist, int topk,
+                 int fmb, double* ret, int32_t* valid, hipStream_t st) {
+  if (Q <= 0) return PPS_OK;
+  hipLaunchKernelGGL(cmc_finalize_kernel, dim3((unsigned)Q), dim3(64), 0, st, Ptot, pos_total,
+                     hist, topk, fmb, ret, valid);
+  PPS_CHECK_LAUNCH("cmc_finalize_kernel");
   return PPS_OK;
 }
 

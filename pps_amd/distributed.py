@@ -103,6 +103,36 @@ def all_gather_rows(x, sizes):
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(x.device).contiguous()
 
 
+def _padded(x, mx, dim):
+    """x padded with zeros to mx along dim (0 = rows, 1 = columns), on the
+    collective's device."""
+    dev = _coll_device(x)
+    shape = list(x.shape)
+    shape[dim] = mx
+    pad = torch.zeros(shape, dtype=x.dtype, device=dev)
+    pad.narrow(dim, 0, x.shape[dim]).copy_(x)
+    return pad
+
+
+def gather_blocks(x, sizes, dim=0, dst=0):
+    """Gather blocks of unequal extent sizes[r] along `dim` (0: rows [n_r, ...],
+    1: columns [m, n_r]) to rank `dst` only, concatenated in rank order;
+    None on the other ranks.  For tensors only one rank consumes (the
+    features.npy dump, the re-ranking inputs): 1/world of an all-gather's
+    traffic."""
+    world = len(sizes)
+    if not _active(world):
+        return x
+    pad = _padded(x, max(max(sizes), 1), dim)
+    me = torch.distributed.get_rank()
+    bufs = [torch.empty_like(pad) for _ in range(world)] if me == dst else None
+    torch.distributed.gather(pad, bufs, dst=dst)
+    if me != dst:
+        return None
+    return torch.cat([b.narrow(dim, 0, s) for b, s in zip(bufs, sizes)],
+                     dim).to(x.device).contiguous()
+
+
 def broadcast_object(obj, world, src=0):
     if not _active(world):
         return obj
@@ -341,18 +371,20 @@ def evaluate_sharded(q_local, g_local, mq_local, ids, cams, marks, rank, world,
         r = ev_mq.run(None, g_local, dist=mq_g)
         mq_mAP, mq_cmc = r['mAP'], r['cmc']
     if rerank:
-        # the whole (Q+G)^2 neighbour structure: gathered to rank 0
+        # the whole (Q+G)^2 neighbour structure on rank 0: the gallery
+        # features (for g x g) and the shards' q x g blocks already computed
+        # above, gathered there only (not recomputed, not sent to every rank)
         g_sizes = [b - a for a, b in ev.g_ranges]
-        g_all = all_gather_rows(g_local, g_sizes)
+        g_all = gather_blocks(g_local, g_sizes)
+        qg_full = gather_blocks(q_g.contiguous(), g_sizes, dim=1)
+        mqg_full = gather_blocks(mq_g.contiguous(), g_sizes, dim=1) if mq.any() else None
         scores = None
         if rank == 0:
-            qg_full = be.distmat(q_all, g_all, metric)
             g_g = be.self_dist(g_all, metric)
             rr = be.re_ranking(qg_full, be.self_dist(q_all, metric), g_g)
             s_sq = _score(*be.rank_eval(rr, ids[q], ids[g], cams[q], cams[g]))
             s_mq = None
             if mq.any():
-                mqg_full = be.distmat(pooled, g_all, metric)
                 rr_mq = be.re_ranking(mqg_full, be.self_dist(pooled, metric), g_g)
                 s_mq = _score(*be.rank_eval(rr_mq, keys[:, 0], ids[g], keys[:, 1], cams[g]))
             scores = (s_sq, s_mq)

@@ -391,7 +391,11 @@ class PPSModel(object):
         self._batch = None
 
     def _fuse_stem(self, blobs):
-        """Replace the stem conv + maxpool pair by one 'stem_pool' layer."""
+        """Replace the stem conv + maxpool pair by one 'stem_pool' layer (its
+        kernel takes 128-wide inputs: REID.SCALE[0] == 128, else the conv and
+        maxpool stay separate)."""
+        if int(cfg.REID.SCALE[0]) != ops.STEM_WIDTH:
+            return
         for i, L in enumerate(self.layers[:-1]):
             P = self.layers[i + 1]
             if (L['op'] == 'conv' and L['input'] == 'data' and L['k'] == 7 and

@@ -27,6 +27,7 @@ Layout: NHWC activations; the graph input 'data' is NHWC with 4 channels
 (BGR minus means, 4th zero), as ops.preprocess_bgr writes it.
 """
 import json
+import weakref
 
 import numpy as np
 import torch
@@ -44,6 +45,10 @@ def _host(t):
     return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
 
 
+# packed device copies per weight object: id(w) -> (weakref to w, {cin:
+# (version, packed, kpad)}).  The weakref's callback drops the entry when the
+# weight dies, and an in-place change of a torch weight (its version
+# counter) repacks it.
 _PACKED = {}
 
 
@@ -51,14 +56,21 @@ def _packed_conv(w, cin):
     """Caffe2 conv weight [Cout][Cin][k][k] -> the GEMM layout [Cout][Kpad]
     (K ordered kh, kw, cin; cin padded to the input's channels), cached per
     weight tensor."""
-    key = (id(w), cin)
-    hit = _PACKED.get(key)
-    if hit is not None and hit[0] is w:
+    version = getattr(w, '_version', 0)
+    key = id(w)
+    entry = _PACKED.get(key)
+    if entry is not None and entry[0]() is not w:
+        entry = None
+    hit = entry[1].get(cin) if entry is not None else None
+    if hit is not None and hit[0] == version:
         return hit[1], hit[2]
     wn = _host(w).astype(np.float32)
     packed, kpad = pmodel.pack_conv_weight(wn, cin if cin != wn.shape[1] else None)
     dev = torch.from_numpy(packed).cuda()
-    _PACKED[key] = (w, dev, kpad)
+    if entry is None:
+        entry = (weakref.ref(w, lambda _r, k=key: _PACKED.pop(k, None)), {})
+        _PACKED[key] = entry
+    entry[1][cin] = (version, dev, kpad)
     return dev, kpad
 
 

@@ -313,6 +313,38 @@ def rank_count_stream(dist, g_offset, sp, junk, hist=None, before=None):
     return hist, before
 
 
+def cmc_counts(dist, g_offset, sp, junk, index=None, separate_camera_set=False, hist=None):
+    """Per-positive exact-rank bins for the reference's general cmc
+    (pps_cmc_counts); with separate_camera_set the MatchIndex's qcam / gcam
+    drop every same-camera entry.  hist accumulates when given."""
+    Q, G = dist.shape
+    Ptot = sp.sorted_d.shape[1]
+    junk_d, junk_idx, junk_cnt = junk
+    if hist is None:
+        hist = torch.zeros((Q, Ptot), dtype=torch.int32, device=dist.device)
+    qc = gc = 0
+    if separate_camera_set:
+        qc = _dev(index.qcam, 'qcam', torch.int32)
+        gc = _dev(index.gcam, 'gcam', torch.int32)
+    call('pps_cmc_counts', _dev_rows(dist, 'dist'), Q, G, _ld(dist), int(g_offset), Ptot,
+         _dev(sp.sorted_d, 'sorted_d'), _dev(sp.sorted_idx, 'sorted_idx', torch.int32),
+         _dev(sp.pos_total, 'pos_total', torch.int32), qc, gc, junk_d.shape[1],
+         _dev(junk_d, 'junk_d'), _dev(junk_idx, 'junk_idx', torch.int32),
+         _dev(junk_cnt, 'junk_cnt', torch.int32), _dev(hist, 'hist', torch.int32), _stream())
+    return hist
+
+
+def cmc_finalize(pos_total, hist, topk, first_match_break):
+    """(ret [Q, topk] float64 after the reference's cumsum, valid [Q] int32)."""
+    Q, Ptot = hist.shape
+    ret = torch.empty((Q, topk), dtype=torch.float64, device=hist.device)
+    valid = torch.empty((Q,), dtype=torch.int32, device=hist.device)
+    call('pps_cmc_finalize', Q, Ptot, _dev(pos_total, 'pos_total', torch.int32),
+         _dev(hist, 'hist', torch.int32), int(topk), int(bool(first_match_break)),
+         ret.data_ptr(), valid.data_ptr(), _stream())
+    return ret, valid
+
+
 def collect_positives(dist, qid, qcam, gid, gcam, g_offset, Pmax):
     Q, G = dist.shape
     pos_d = torch.empty((Q, Pmax), dtype=torch.float32, device=dist.device)
@@ -567,6 +599,9 @@ def splitk_bn_act_normalize(part, scale, shift, relu, normalize, y):
     call('pps_splitk_bn_act_normalize', _dev(part, 'part'), S, M, N, _dev(scale, 'scale'),
          _dev(shift, 'shift'), int(bool(relu)), int(bool(normalize)), _dev(y, 'y'), _stream())
     return y
+
+
+STEM_WIDTH = 128  # input width the fused stem kernel takes (stem.hip kStemW)
 
 
 def stem_k():

@@ -62,7 +62,9 @@ def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams, index=N
     true matches listed from a per-identity gallery index (ops.MatchIndex,
     built from the ids unless given), then one streaming count pass over the
     distance rows (pps_collect_matches / pps_rank_prepare /
-    pps_rank_count_stream / pps_ap_finalize)."""
+    pps_rank_count_stream / pps_ap_finalize).  Capacity: a query's identity
+    may have at most 8192 same-id gallery entries (pps_rank_prepare's LDS
+    merge; RuntimeError with PPS_ERR_CAPACITY beyond)."""
     d = distmat if isinstance(distmat, torch.Tensor) and distmat.is_cuda and \
         distmat.dtype == torch.float32 and distmat.dim() == 2 and \
         (distmat.shape[0] < 2 or distmat.stride(1) == 1) else _to_dev(distmat)
@@ -104,19 +106,36 @@ def mean_ap(distmat, query_ids=None, gallery_ids=None, query_cams=None,
 def cmc(distmat, query_ids=None, gallery_ids=None, query_cams=None, gallery_cams=None,
         topk=100, separate_camera_set=False, single_gallery_shot=False,
         first_match_break=False, average=True):
-    if separate_camera_set or single_gallery_shot or not first_match_break:
-        raise NotImplementedError(
-            'GPU cmc implements the Market-1501 protocol used by evaluate() '
-            '(separate_camera_set=False, single_gallery_shot=False, '
-            'first_match_break=True; reid_dataset_evaluator.py:35-37)')
-    _, valid, first = rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams)
-    valid, first = _np(valid).astype(bool), _np(first)
+    """reid_dataset_evaluator.py:283-363 with the same defaults and outputs:
+    the fractional CMC (first_match_break=False), the first-match CMC, and
+    separate_camera_set, from per-positive counts on the device
+    (pps_cmc_counts / pps_cmc_finalize; the Market protocol evaluate() uses
+    takes the mAP pass's first-match ranks instead).  The ranking is the
+    stable (distance, index) order.  single_gallery_shot draws random gallery
+    samples 100 times per query (:334-346) and is not built."""
+    if single_gallery_shot:
+        raise NotImplementedError('single_gallery_shot (random per-identity sampling, '
+                                  'reid_dataset_evaluator.py:334-346) is not built')
+    d = distmat if isinstance(distmat, torch.Tensor) and distmat.is_cuda and \
+        distmat.dtype == torch.float32 and distmat.dim() == 2 and \
+        (distmat.shape[0] < 2 or distmat.stride(1) == 1) else _to_dev(distmat)
+    if first_match_break and not separate_camera_set:
+        _, valid, first = rank_eval(d, query_ids, gallery_ids, query_cams, gallery_cams)
+        valid, first = _np(valid).astype(bool), _np(first)
+        ret = np.zeros((len(valid), topk))
+        rows = np.nonzero(valid & (first < topk))[0]
+        ret[rows, first[rows]] = 1
+        ret = ret.cumsum(axis=1)
+    else:
+        index = ops.MatchIndex(_host_ids(query_ids), _host_ids(query_cams),
+                               _host_ids(gallery_ids), _host_ids(gallery_cams), d.device)
+        pos_d, pos_idx, pos_cnt, junk = ops.collect_matches(d, index)
+        sp = ops.rank_prepare(pos_d[None], pos_idx[None], pos_cnt[None])
+        hist = ops.cmc_counts(d, 0, sp, junk, index, separate_camera_set)
+        ret, valid = ops.cmc_finalize(sp.pos_total, hist, topk, first_match_break)
+        ret, valid = _np(ret), _np(valid).astype(bool)
     if not valid.any():
         raise RuntimeError('No valid query')
-    ret = np.zeros((len(valid), topk))
-    rows = np.nonzero(valid & (first < topk))[0]
-    ret[rows, first[rows]] = 1
-    ret = ret.cumsum(axis=1)
     if average:
         return np.sum(ret, axis=0) / valid.sum()
     return ret, valid.astype(np.float64)

@@ -31,6 +31,7 @@ import torch
 
 from . import distributed as pdist
 from . import model as pmodel
+from . import native
 from . import ops
 from . import reid_dataset_evaluator as rde
 from .config import cfg
@@ -49,13 +50,22 @@ def get_output_dir(dataset_name, training=False):
 
 
 def initialize_model_from_cfg(weights_file, gpu_id=0, trusted=False, blobs=None):
-    """test_engine.py:390-405: build the test net and load its weights."""
+    """test_engine.py:390-405: build the test net and load its weights -- as
+    one handle of the whole-network C ABI (pps_model_create; every forward
+    is one pps_forward call).  PPS_TILES_FILE: apply a saved autotune table
+    (bench.py --tiles-file)."""
     torch.cuda.set_device(gpu_id)
     plan = pmodel.build_plan()
     if blobs is None:
         blobs = load_weights(weights_file, trusted=trusted)
     check_complete(blobs, plan)
-    return pmodel.PPSModel(blobs, device='cuda:%d' % gpu_id, plan=plan)
+    m = native.NativeModel(blobs)
+    tf = os.environ.get('PPS_TILES_FILE')
+    if tf:
+        import json
+        with open(tf) as f:
+            m.apply_table(json.load(f))
+    return m
 
 
 def _decode_bgr(path):
@@ -120,12 +130,13 @@ class BatchFeeder(object):
             yield s, x
 
 
-def extract_features(model, source, n, batch=None, out=None):
-    """Features [n, D] (device tensor) for images source(0..n-1)."""
+def extract_features(model, source, n, batch=None, out=None, workers=8):
+    """Features [n, D] (device tensor) for images source(0..n-1), decoded on
+    `workers` host threads."""
     batch = batch or int(cfg.TEST.get('IMS_PER_BATCH', 64))
     feats = out if out is not None else torch.empty((n, model.feat_dim),
                                                     dtype=torch.float32, device='cuda')
-    for s, x in BatchFeeder(source, n, batch):
+    for s, x in BatchFeeder(source, n, batch, workers=workers):
         f = model.forward(x)
         feats[s:s + x.shape[0]].copy_(f)
     return feats
@@ -230,16 +241,21 @@ def multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir, truste
         sp = [paths[i] for i in rows[a:b]]
         shards.append(extract_features(model, lambda i, sp=sp: _decode_bgr(sp[i]), len(sp)))
         rows_of.append(rows)
-    # features in dataset order, written by rank 0 (test_engine.py:216-227)
-    full = torch.empty((len(paths), model.feat_dim), dtype=torch.float32, device='cuda')
+    # features in dataset order, written by rank 0 (test_engine.py:216-227):
+    # gathered to rank 0 only
+    full = None
     for m in (0, 1, 2):
         n = len(rows_of[m])
         if n == 0:
             continue
         sizes = [b - a for a, b in (pdist.shard_range(n, r, world) for r in range(world))]
-        allm = pdist.all_gather_rows(shards[m], sizes)
-        full[torch.from_numpy(rows_of[m]).cuda()] = allm
-    if rank == 0:
+        allm = pdist.gather_blocks(shards[m], sizes)
+        if rank == 0:
+            if full is None:
+                full = torch.empty((len(paths), model.feat_dim), dtype=torch.float32,
+                                   device='cuda')
+            full[torch.from_numpy(rows_of[m]).cuda()] = allm
+    if rank == 0 and full is not None:
         np.save(os.path.join(output_dir, 'features.npy'), full.cpu().numpy())
     del full
     s = pdist.evaluate_sharded(shards[0], shards[1], shards[2], ids, cams, marks, rank,

@@ -146,6 +146,38 @@ def case_rerank(ev):
     return dict(name='rerank', Q=len(qid), G=len(gid), mAP=float(mAP))
 
 
+def case_cmc_modes(ev):
+    """The reference `cmc` beyond the Market protocol: its own defaults
+    (topk=100, first_match_break=False: fractional CMC, delta = 1/#matches,
+    :283-292,349-356) and separate_camera_set=True (:329-331), with and
+    without first_match_break, averaged and per query."""
+    out = {}
+    for tag, args in (('market_small', dict(n_ids=60, per_id=8, D=128, noise=1.6, seed=0,
+                                            n_distract=80, q_frac=0.2)),
+                      ('dense', dict(n_ids=15, per_id=12, D=32, noise=2.5, seed=4,
+                                     n_distract=30, q_frac=0.2))):
+        x, ids, cams = synth_features(args['n_ids'], args['per_id'], args['D'], args['noise'],
+                                      args['seed'], args['n_distract'])
+        (qf, qid, qcam), (gf, gid, gcam) = split_qg(x, ids, cams, args['q_frac'], args['seed'])
+        dist, _ = quiet(ev.compute_dist, qf, gf, type='euclidean')
+        out[tag + '_qid'], out[tag + '_gid'] = qid, gid
+        out[tag + '_qcam'], out[tag + '_gcam'] = qcam, gcam
+        out[tag + '_dist'] = dist.astype(np.float32)
+        for sep in (False, True):
+            for fmb in (False, True):
+                key = '%s_sep%d_fmb%d' % (tag, sep, fmb)
+                out[key] = ev.cmc(dist, qid, gid, qcam, gcam, separate_camera_set=sep,
+                                  first_match_break=fmb)
+                out[key + '_all'], out[key + '_valid'] = ev.cmc(
+                    dist, qid, gid, qcam, gcam, separate_camera_set=sep,
+                    first_match_break=fmb, average=False)
+        out[tag + '_default'] = ev.cmc(dist, qid, gid, qcam, gcam)   # the signature defaults
+        out[tag + '_sep1_fmb0_top5'] = ev.cmc(dist, qid, gid, qcam, gcam, topk=5,
+                                              separate_camera_set=True)
+    np.savez_compressed(os.path.join(HERE, 'cmc_modes.npz'), **out)
+    return dict(name='cmc_modes', keys=len(out))
+
+
 class _FakeJsonDataset(object):
     def __init__(self, entries):
         self.entries = entries
@@ -181,6 +213,10 @@ def case_evaluate(ev):
 
 def main():
     ev, _ = load_reference_evaluator(rerank=False)
+    if '--only' in sys.argv:   # one case, the other fixtures untouched
+        name = sys.argv[sys.argv.index('--only') + 1]
+        print(globals()['case_' + name](ev))
+        return
     meta = []
     meta.append(case_retrieval(ev, 'market_small', n_ids=60, per_id=8, D=128,
                                noise=1.6, seed=0, n_distract=80, q_frac=0.2))
@@ -189,6 +225,7 @@ def main():
     meta.append(case_ties(ev))
     meta.append(case_rerank(ev))
     meta.append(case_evaluate(ev))
+    meta.append(case_cmc_modes(ev))
     import sklearn
     meta = dict(cases=meta, numpy=np.__version__, sklearn=sklearn.__version__,
                 python=sys.version.split()[0],

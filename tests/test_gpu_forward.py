@@ -2,7 +2,9 @@
 against the CPU fp32 oracle (oracle/forward.py, driven by the recorded
 reference graph).  fp32 tolerance: every kernel computes in fp32 with a
 different summation order than the CPU, so per-layer results agree to
-~1e-6 relative; the end-to-end normalised feature within 2e-5 absolute."""
+~1e-6 relative; the end-to-end normalised feature within FWD_ATOL absolute."""
+import os
+
 import numpy as np
 from _tiles import check_tile_bits
 import pytest
@@ -10,6 +12,13 @@ import torch
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
+
+# Parity bounds (round 3): what the kernels deliver plus a margin.
+FWD_ATOL = 1e-6     # normalised 3968-d features vs the oracle (observed ~6e-8)
+LAYER_RTOL = 1e-5   # intermediate stage outputs, relative to their max
+PRE_ATOL = 2e-4     # preprocess (values up to ~255) vs the float64 oracle
+BENCH_TILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           'profiles', 'r03', 'tiles_v0.json')
 
 
 def _cuda(x):
@@ -153,8 +162,11 @@ def test_full_forward_vs_oracle(math):
         got = bufs[name].cpu().numpy()
         want = kept[name].numpy().transpose(0, 2, 3, 1)
         err = np.abs(got - want).max() / max(1e-6, np.abs(want).max())
-        assert err < 1e-4, (name, err)
-    np.testing.assert_allclose(out, ref.numpy(), rtol=0, atol=2e-5)
+        print('%s %s max|err| / max|ref| = %.3g' % (math, name, err))
+        assert err < LAYER_RTOL, (name, err)
+    err = float(np.abs(out - ref.numpy()).max())
+    print('%s forward max|err| vs oracle %.3g' % (math, err))
+    assert err <= FWD_ATOL
     np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
 
 
@@ -168,7 +180,9 @@ def test_preprocess_vs_oracle():
     assert np.all(y[..., 3] == 0)
     for n in range(3):
         ref = pre.prep_im_for_blob(imgs[n])
-        np.testing.assert_allclose(y[n, ..., :3], ref, rtol=0, atol=4e-3)
+        err = float(np.abs(y[n, ..., :3] - ref).max())
+        print('preprocess image %d max|err| vs oracle %.3g' % (n, err))
+        assert err <= PRE_ATOL
 
 
 def test_preprocess_ragged_matches_dense():
@@ -185,7 +199,8 @@ def test_preprocess_ragged_matches_dense():
                                   torch.tensor([s[1] for s in shapes], dtype=torch.int32).cuda(),
                                   pre.PIXEL_MEANS, (384, 128)).cpu().numpy()
     for n, im in enumerate(ims):
-        np.testing.assert_allclose(y[n, ..., :3], pre.prep_im_for_blob(im), rtol=0, atol=4e-3)
+        np.testing.assert_allclose(y[n, ..., :3], pre.prep_im_for_blob(im), rtol=0,
+                                   atol=PRE_ATOL)
 
 
 @pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(2, 24, 8, 128, 256, 512, 2),
@@ -269,7 +284,9 @@ def test_fpn_variant_forward_vs_oracle():
     xin = np.zeros((2, 384, 128, 4), np.float32)
     xin[..., :3] = x.transpose(0, 2, 3, 1)
     out = model.PPSModel(blobs, plan=plan).forward(_cuda(xin)).cpu().numpy()
-    np.testing.assert_allclose(out, ref, rtol=0, atol=2e-5)
+    err = float(np.abs(out - ref).max())
+    print('FPN forward max|err| vs oracle %.3g' % err)
+    assert err <= FWD_ATOL
 
 
 def test_bench_configuration_vs_oracle():
@@ -282,8 +299,7 @@ def test_bench_configuration_vs_oracle():
     from oracle.forward import GraphForward
     from oracle import preprocess as pre
     from pps_amd import model, ops
-    tf = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                      'profiles', 'r02', 'tiles_v4.json')
+    tf = BENCH_TILES
     if not os.path.exists(tf):
         pytest.skip('no committed tiles file')
     _market_cfg()
@@ -296,6 +312,9 @@ def test_bench_configuration_vs_oracle():
     m.set_planes(saved.get('__planes__', []))
     m.set_splitks(saved.get('__splitk__', {}))
     assert len(m.planes()) > 0
+    # the run uses exactly the tile ids the autotune chose (incl. 50-53)
+    want = {v for k, v in saved.items() if not k.startswith('__')}
+    assert set(m.tiles().values()) == want, (sorted(want), sorted(set(m.tiles().values())))
     rng = np.random.RandomState(64)
     imgs = rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)
     x = ops.preprocess_bgr(torch.from_numpy(imgs).cuda(), pre.PIXEL_MEANS, (384, 128))
@@ -305,7 +324,9 @@ def test_bench_configuration_vs_oracle():
     # parity is test_preprocess_vs_oracle's)
     xin = x[pick, :, :, :3].cpu().numpy().transpose(0, 3, 1, 2)
     ref = GraphForward(blobs)(np.ascontiguousarray(xin, np.float32)).numpy()
-    np.testing.assert_allclose(feat[pick], ref, rtol=0, atol=2e-5)
+    err = float(np.abs(feat[pick] - ref).max())
+    print('bench configuration forward max|err| vs oracle %.3g' % err)
+    assert err <= FWD_ATOL
 
 
 @pytest.mark.parametrize('N,H', [(2, 384), (3, 100), (1, 30), (2, 7), (1, 390)])

@@ -1,0 +1,182 @@
+"""The whole-network C entry point (pps_model_create / pps_forward, include/
+pps_abi.h) against the Python orchestrator (bit for bit, same tuning table)
+and the CPU oracle (tight bound): the forward a C/C++ caller gets through the
+ABI with no pps_amd/model.py orchestration."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TILES = os.path.join(ROOT, 'profiles', 'r03', 'tiles_v0.json')
+FWD_ATOL = 1e-6   # normalised features vs the oracle (observed ~6e-8)
+
+
+def _market_cfg():
+    from tests.test_gpu_forward import _market_cfg as f
+    return f()
+
+
+def _models(seed=0, **kw):
+    from pps_amd import model, native
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=seed)
+    return blobs, model.PPSModel(blobs, plan=plan, **kw), native.NativeModel(blobs, **kw)
+
+
+def _input(N, seed=0):
+    rng = np.random.RandomState(seed)
+    x = (rng.randn(N, 3, 384, 128) * 50).astype(np.float32)
+    xin = np.zeros((N, 384, 128, 4), np.float32)
+    xin[..., :3] = x.transpose(0, 2, 3, 1)
+    return x, torch.from_numpy(xin).cuda()
+
+
+def test_native_plan_matches_python():
+    """Same layers, names, ops, FLOPs, bytes and default plane edges as the
+    Python orchestrator (both mirror the reference builders)."""
+    _, pm, nm = _models()
+    _, x = _input(2)
+    pm.forward(x)
+    nl = nm.layers(N=2)
+    assert [L.get('name', L['output']) for L in pm.layers] == [L['name'] for L in nl]
+    assert [L['op'] for L in pm.layers] == [L['op'] for L in nl]
+    for a, b in zip(pm.layers, nl):
+        assert a['flops'] == pytest.approx(b['flops'], rel=1e-12), b['name']
+        assert a['bytes'] == pytest.approx(b['bytes'], rel=1e-12), b['name']
+    assert sorted(pm.planes()) == sorted(nm.planes())
+    assert len(nm.plane_edges()) == len(pm._edges)
+    assert nm.feat_dim == pm.feat_dim == 3968
+
+
+@pytest.mark.parametrize('math', ['x3', 'f32'])
+def test_native_forward_bit_identical_and_vs_oracle(math):
+    from oracle.forward import GraphForward
+    blobs, pm, nm = _models(math=math)
+    x, xd = _input(3)
+    a = pm.forward(xd).cpu().numpy()
+    b = nm.forward(xd).cpu().numpy()
+    assert np.array_equal(a, b)
+    ref = GraphForward(blobs)(x).numpy()
+    err = float(np.abs(b - ref).max())
+    print('native forward (%s) max|err| vs oracle %.3g' % (math, err))
+    assert err <= FWD_ATOL
+
+
+def test_native_bench_table_bit_identical():
+    """Batch 64 with the committed autotune table (tiles of both rounding
+    groups, plane edges): pps_forward == PPSModel.forward bit for bit, and
+    the uint8 / NCHW entry points equal preprocess + pps_forward."""
+    if not os.path.exists(TILES):
+        pytest.skip('no committed tiles file')
+    from oracle import preprocess as pre
+    from pps_amd import ops
+    _, pm, nm = _models()
+    with open(TILES) as f:
+        saved = json.load(f)
+    pm.set_tiles(saved)
+    pm.set_planes(saved.get('__planes__', []))
+    pm.set_splitks(saved.get('__splitk__', {}))
+    nm.apply_table(pm)
+    assert nm.tiles() == pm.tiles() and sorted(nm.planes()) == sorted(pm.planes())
+    rng = np.random.RandomState(64)
+    imgs = torch.from_numpy(rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)).cuda()
+    x = ops.preprocess_bgr(imgs, pre.PIXEL_MEANS, (384, 128))
+    a = pm.forward(x).cpu().numpy()
+    b = nm.forward(x).cpu().numpy()
+    assert np.array_equal(a, b)
+    c = nm.forward_bgr(imgs).cpu().numpy()
+    assert np.array_equal(b, c)
+    nchw = x[..., :3].permute(0, 3, 1, 2).contiguous()
+    d = nm.forward_nchw(nchw).cpu().numpy()
+    assert np.array_equal(b, d)
+
+
+def test_native_graph_capture():
+    """pps_forward is stream-ordered and capturable once N is reserved."""
+    _, pm, nm = _models()
+    _, x = _input(4, seed=1)
+    nm.reserve(4)
+    out = torch.empty((4, nm.feat_dim), device='cuda')
+    nm.forward(x, out=out)
+    torch.cuda.synchronize()
+    want = out.clone()
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nm.forward(x, out=out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
+
+
+def test_native_autotune_then_python_twin():
+    """The C autotune fills the table; the Python orchestrator given that
+    table computes the same bits."""
+    _, pm, nm = _models(seed=1)
+    _, x = _input(2, seed=2)
+    tiles = nm.autotune(x)
+    assert all(0 <= t <= 53 for t in tiles.values())
+    assert any(t != 0 for t in tiles.values())
+    pm.set_tiles(tiles)
+    pm.set_planes(nm.planes())
+    assert np.array_equal(pm.forward(x).cpu().numpy(), nm.forward(x).cpu().numpy())
+
+
+def test_native_intermediate_tensor_and_layer_range():
+    _, pm, nm = _models(fused_pps=False)
+    _, x = _input(2, seed=3)
+    pm.forward(x)
+    nm.forward(x)
+    torch.cuda.synchronize()
+    for name in ('pool1', 'res3_3_sum', 'res5_2_sum'):
+        assert np.array_equal(pm.buffers()[name].cpu().numpy(), nm.tensor(2, name)), name
+    # layers [0, n) in two ranges == one forward
+    n = len(nm.layers())
+    a = nm.forward(x).clone()
+    nm.forward_layers(x, 0, n // 2)
+    b = nm.forward_layers(x, n // 2, n)
+    assert torch.equal(a, b)
+
+
+def test_native_fpn_variant_bit_identical():
+    from pps_amd import config, model, native
+    _market_cfg()
+    config.merge_cfg_from_list(['FPN.FPN_ON', 'True', 'MODEL.CONV_BODY',
+                                'FPN_reid.add_fpn_ResNet50_conv5_body'])
+    try:
+        plan = model.build_plan()
+        blobs = model.synthetic_weights(plan, seed=3)
+        pm = model.PPSModel(blobs, plan=plan)
+        nm = native.NativeModel(blobs)
+        _, x = _input(2, seed=4)
+        assert [L['name'] for L in nm.layers()][-3].startswith('fpn_inner_')
+        assert np.array_equal(pm.forward(x).cpu().numpy(), nm.forward(x).cpu().numpy())
+    finally:
+        config.merge_cfg_from_list(['FPN.FPN_ON', 'False', 'MODEL.CONV_BODY',
+                                    'ResNet.add_ResNet50_conv5_body'])
+
+
+def test_native_errors_are_enforce_style():
+    from pps_amd import model, native
+    _market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=0)
+    bad = dict(blobs)
+    bad['res2_0_branch2a_w'] = bad['res2_0_branch2a_w'][:10]
+    with pytest.raises(RuntimeError, match='res2_0_branch2a_w has'):
+        native.NativeModel(bad)
+    missing = dict(blobs)
+    del missing['res4_3_branch2b_bn_riv']
+    with pytest.raises(RuntimeError, match='weights missing 1 blobs'):
+        native.NativeModel(missing)
+    nm = native.NativeModel(blobs)
+    with pytest.raises(RuntimeError, match='no layer named'):
+        native.call('pps_model_set_tile', nm.handle, b'res9_branch2a', 3)
+    with pytest.raises(RuntimeError, match='not a plane-eligible producer'):
+        nm.set_planes(['res2_0_branch2c'])

@@ -121,5 +121,8 @@ def test_eager_net_vs_oracle():
     for name in ('res5_2_sum', 'pps013_pool2'):
         got, want = _nchw(kept[name]), rk[name].numpy()
         err = np.abs(got - want).max() / max(1e-6, np.abs(want).max())
-        assert err < 1e-4, (name, err)
-    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=0, atol=2e-5)
+        print('eager net %s max|err| / max|ref| = %.3g' % (name, err))
+        assert err < 1e-5, (name, err)
+    err = float(np.abs(out.cpu().numpy() - ref.numpy()).max())
+    print('eager net forward max|err| vs oracle %.3g' % err)
+    assert err <= 1e-6

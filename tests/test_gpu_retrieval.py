@@ -322,3 +322,59 @@ def test_rank_eval_padded_rows_view(golden):
     for x, y in zip(a1, a2):
         np.testing.assert_array_equal(x, y)
     np.testing.assert_allclose(a1[0], g['aps'], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('tag', ['market_small', 'dense'])
+def test_cmc_all_modes_vs_reference_golden(golden, tag):
+    """The reference `cmc` with its own defaults (topk=100, fractional
+    first_match_break=False) and with separate_camera_set=True, on the
+    reference's distances (cmc_modes.npz): per-query rows bit-exact."""
+    from pps_amd import reid_dataset_evaluator as gev
+    g = golden('cmc_modes')
+    d, qid, gid = g[tag + '_dist'], g[tag + '_qid'], g[tag + '_gid']
+    qcam, gcam = g[tag + '_qcam'], g[tag + '_gcam']
+    for sep in (0, 1):
+        for fmb in (0, 1):
+            key = '%s_sep%d_fmb%d' % (tag, sep, fmb)
+            ret, valid = gev.cmc(d, qid, gid, qcam, gcam, separate_camera_set=bool(sep),
+                                 first_match_break=bool(fmb), average=False)
+            np.testing.assert_array_equal(valid, g[key + '_valid'], err_msg=key)
+            np.testing.assert_array_equal(ret, g[key + '_all'], err_msg=key)
+            avg = gev.cmc(d, qid, gid, qcam, gcam, separate_camera_set=bool(sep),
+                          first_match_break=bool(fmb))
+            np.testing.assert_array_equal(avg, g[key], err_msg=key)
+    np.testing.assert_array_equal(gev.cmc(d, qid, gid, qcam, gcam), g[tag + '_default'])
+    np.testing.assert_array_equal(gev.cmc(d, qid, gid, qcam, gcam, topk=5,
+                                          separate_camera_set=True),
+                                  g[tag + '_sep1_fmb0_top5'])
+    with pytest.raises(NotImplementedError, match='single_gallery_shot'):
+        gev.cmc(d, qid, gid, qcam, gcam, single_gallery_shot=True)
+
+
+def test_cmc_counts_sharded_equal_unsharded(golden):
+    """pps_cmc_counts is additive over gallery shards (global indices)."""
+    from pps_amd import ops
+    g = golden('cmc_modes')
+    d = torch.from_numpy(g['dense_dist']).cuda()
+    qid, gid, qcam, gcam = g['dense_qid'], g['dense_gid'], g['dense_qcam'], g['dense_gcam']
+    G = d.shape[1]
+    full_idx = ops.MatchIndex(qid, qcam, gid, gcam)
+    pd, pi, pc, junk = ops.collect_matches(d, full_idx)
+    sp = ops.rank_prepare(pd[None], pi[None], pc[None])
+    want = ops.cmc_counts(d, 0, sp, junk)
+    cuts = [0, G // 3, G]
+    lists, shards = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ds = d[:, a:b].contiguous()
+        idx = ops.MatchIndex(qid, qcam, gid[a:b], gcam[a:b])
+        p = ops.collect_matches(ds, idx, a, full_idx.capacity)
+        lists.append(p[:3])
+        shards.append((ds, a, p[3]))
+    sp2 = ops.rank_prepare(torch.stack([l[0] for l in lists]), torch.stack([l[1] for l in lists]),
+                           torch.stack([l[2] for l in lists]))
+    hist = None
+    for ds, a, junk_s in shards:
+        hist = ops.cmc_counts(ds, a, sp2, junk_s, hist=hist)
+    r1, v1 = ops.cmc_finalize(sp.pos_total, want, 100, False)
+    r2, v2 = ops.cmc_finalize(sp2.pos_total, hist, 100, False)
+    assert torch.equal(v1, v2) and torch.equal(r1, r2)

@@ -84,3 +84,28 @@ def test_pairwise_distance_oracle_matches_norm_form():
     Z = ev.pairwise_distance(X)
     assert np.all(np.diag(Z) == 0)
     np.testing.assert_allclose(Z, ev.compute_dist(X, X, 'sqeuclidean'), atol=1e-4)
+
+
+def test_oracle_cmc_all_modes_vs_reference(golden):
+    """The reference `cmc` beyond the Market protocol (cmc_modes.npz, made by
+    the reference evaluator itself): its defaults (topk=100, fractional
+    first_match_break=False) and separate_camera_set=True."""
+    g = golden('cmc_modes')
+    for tag in ('market_small', 'dense'):
+        d, qid, gid = g[tag + '_dist'], g[tag + '_qid'], g[tag + '_gid']
+        qcam, gcam = g[tag + '_qcam'], g[tag + '_gcam']
+        for sep in (0, 1):
+            for fmb in (0, 1):
+                key = '%s_sep%d_fmb%d' % (tag, sep, fmb)
+                got = ev.cmc(d, qid, gid, qcam, gcam, separate_camera_set=bool(sep),
+                             first_match_break=bool(fmb))
+                np.testing.assert_allclose(got, g[key], rtol=0, atol=1e-12, err_msg=key)
+                ret, valid = ev.cmc(d, qid, gid, qcam, gcam, separate_camera_set=bool(sep),
+                                    first_match_break=bool(fmb), average=False)
+                np.testing.assert_allclose(ret, g[key + '_all'], rtol=0, atol=1e-12)
+                np.testing.assert_array_equal(valid, g[key + '_valid'])
+        np.testing.assert_allclose(ev.cmc(d, qid, gid, qcam, gcam), g[tag + '_default'],
+                                   rtol=0, atol=1e-12)
+        np.testing.assert_allclose(ev.cmc(d, qid, gid, qcam, gcam, topk=5,
+                                          separate_camera_set=True),
+                                   g[tag + '_sep1_fmb0_top5'], rtol=0, atol=1e-12)
