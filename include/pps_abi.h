@@ -388,8 +388,8 @@ int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w
 /* The last res5 conv with the part pooling fused into its epilogue
  * (ResNet.py:276-333 res5_2 branch2c + Sum + Relu feeding bpm_heads.py:18-55
  * and pps_heads.py:38-80): conv + BN (scale/shift) + residual + ReLU on a
- * pipelined bf16x3 tile whose rows are exactly one image (Ho*Wo rows, <= 128
- * columns; pps_x3p_tile_shape tells a tile's rows/columns); every tile pools
+ * pipelined bf16x3 tile whose rows are exactly one image (Ho*Wo rows, <= 256
+ * columns, the 192x256 tile pooling in two column passes; pps_x3p_tile_shape tells a tile's rows/columns); every tile pools
  * its image's S horizontal strips (heights `splits`, average and max) and
  * writes the 2^S - 1 part subsets to pps_out [2^S - 1][N][Cout] with
  * pps_part_power_set's arithmetic (same bits).  Exactly one of x (f32 NHWC)

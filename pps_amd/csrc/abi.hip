@@ -582,9 +582,9 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   PPS_ENFORCE(hsum == Ho, "strip heights must sum to the output height");
   const bool pl = x3 != nullptr;
   if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
-  PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= 128,
+  PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= kPpsFuseMaxCols,
               "the fused pooling needs a pipelined tile of exactly Ho*Wo = " +
-                  std::to_string(Ho * Wo) + " rows and <= 128 columns, tile " +
+                  std::to_string(Ho * Wo) + " rows and <= 256 columns, tile " +
                   std::to_string(tile) + " has " + std::to_string(x3p_tile_rows(tile, pl)));
   PPS_ENFORCE((int64_t)N * H * W * ldx * (pl ? 2 : 4) < kMaxBufBytes, "input larger than 2 GiB");
   PPS_ENFORCE((int64_t)(1 << S) * N * Cout < (1ll << 31), "part output too large");

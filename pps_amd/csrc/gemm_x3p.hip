@@ -181,200 +181,214 @@ constexpr int lds_epi_bytes() { return BM * (BN + 4) * 4; }
 #define X3P_RES_PREFETCH 16  // residual vectors per thread requested early (0: off)
 #endif
 
-template <int EPI, int BM, int BN, int WM, int WN, int S>
+// HB column passes: the fused part pooling of a tile too wide for one
+// [BM][BN+4] LDS image (192 x 256) parks, finishes and pools BN / HB columns
+// at a time -- per element the same arithmetic in the same order.
+template <int EPI, int BM, int BN, int WM, int WN, int S, int HB = 1>
 __device__ inline void conv_epilogue_lds(const GemmParams& p,
                                          typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
                                          unsigned char* lds, int batch, int kslice, int m0,
                                          int n0, int wm, int wn, int r32, int h) {
   constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
-  constexpr int LD = BN + 4;
+  constexpr int BNH = BN / HB;  // columns per pass
+  constexpr int LD = BNH + 4;
   constexpr int NT = 64 * WM * WN;
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool PPS = (EPI & EPI_F_PPS) != 0;
+  static_assert(HB == 1 || (PPS && (BN / WN) % S == 0 && BNH % (BN / WN) == 0),
+                "column passes: PPS tiles whose wave columns fall in one pass");
   float* t = reinterpret_cast<float*>(lds);
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
-  float* __restrict__ out = p.out + obase;
   const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0, nrem = p.Ncol - n0;
-  const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0;
-  const float* sh = p.shift + batch * p.ss_bstride + n0;
-  const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
+  const int mrem = p.M - m0;
   const int ldr = (int)p.ldr;
-  constexpr int C4 = BN / 4;
+  constexpr int C4 = BNH / 4;
   // the residual tile is requested before the accumulators are parked, so
   // its HBM latency overlaps the LDS round trip (up to 8 vectors per thread)
   constexpr int IT = (BM * C4) / NT;
   constexpr bool PRE = HAS_RES && (BM * C4) % NT == 0 && IT <= X3P_RES_PREFETCH;
-  f32x4 rpre[PRE ? IT : 1];
-  if constexpr (PRE) {
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = it * NT + threadIdx.x;
-      const int row = idx / C4, col = 4 * (idx - row * C4);
-      rpre[it] = (row < mrem && col < nrem)
-                     ? *reinterpret_cast<const f32x4*>(res + row * ldr + col)
-                     : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  __syncthreads();  // every wave is done reading the last stage
+  for (int hb = 0; hb < HB; ++hb) {
+    const int c0h = hb * BNH;
+    float* __restrict__ out = p.out + obase + c0h;
+    const int nrem = p.Ncol - n0 - c0h;
+    const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0 + c0h;
+    const float* sh = p.shift + batch * p.ss_bstride + n0 + c0h;
+    const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 + c0h : nullptr;
+    f32x4 rpre[PRE ? IT : 1];
+    if constexpr (PRE) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int rr = wm * (BM / WM) + i * S + r32;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cb = wn * (BN / WN) + j * S + 4 * h;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-        *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
-      }
-    }
-  }
-  __syncthreads();
-  auto finish = [&](int idx, const f32x4& rv) {
-    const int row = idx / C4, col = 4 * (idx - row * C4);
-    if (row >= mrem || col >= nrem) return;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
-    const f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
-    const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + col);
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = __builtin_fmaf(a[e], s4[e], t4[e]);
-      if (HAS_RES) v[e] += rv[e];
-      if (RELU) v[e] = fmaxf(v[e], 0.f);
-    }
-    if (PPS) {  // the pooling below reads the tile back from LDS
-      *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
-      if (p.pps_write_y) *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
-    } else {
-      *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
-    }
-  };
-  if constexpr (PRE) {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) finish(it * NT + threadIdx.x, rpre[it]);
-  } else {
-    for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
-      f32x4 rv = {0.f, 0.f, 0.f, 0.f};
-      if (HAS_RES) {
+      for (int it = 0; it < IT; ++it) {
+        const int idx = it * NT + threadIdx.x;
         const int row = idx / C4, col = 4 * (idx - row * C4);
-        if (row < mrem && col < nrem) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
+        rpre[it] = (row < mrem && col < nrem)
+                       ? *reinterpret_cast<const f32x4*>(res + row * ldr + col)
+                       : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      finish(idx, rv);
     }
-  }
-  if constexpr (PPS) {
-    // The tile is one image (BM = Ho * Wo rows, row-major positions) x BN
-    // channels.  Per (strip, channel): sum and max over the strip's rows in
-    // row-major order, then the 2^S - 1 subsets -- the arithmetic of
-    // part_power_set_v3_kernel (feature_ops.hip), so the bits are the same.
-    __syncthreads();
-    float* s_ave = t + BM * LD;
-    float* s_max = s_ave + kPpsFuseMaxStrips * BN;
-    // (work split by whole waves: the strip / subset group is wave-uniform,
-    // so the strip table is read with scalar loads)
-    const int W = p.Wo, NS5 = p.pps_S;
-    constexpr int CB = BN / 64;  // 64-channel slices per tile
-    static_assert(BN % 64 == 0, "fused pooling: BN must be a multiple of 64");
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ln = threadIdx.x & 63;
-    for (int it = wv; it < ((X3P_PPS_ABL & 1) ? 0 : NS5 * CB); it += NT / 64) {
-      const int j = it / CB, c = (it - j * CB) * 64 + ln;
-      int r0 = 0;
-      for (int q = 0; q < j; ++q) r0 += p.pps_h[q];
-      const int cnt = p.pps_h[j] * W;
-      const float* colp = t + (r0 * W) * LD + c;
-      float sum = 0.f, mx = -INFINITY;
-#pragma unroll 16
-      for (int e = 0; e < cnt; ++e) {
-        const float v = colp[e * LD];
-        sum += v;
-        mx = fmaxf(mx, v);
-      }
-      s_ave[j * BN + c] = sum / (float)cnt;
-      s_max[j * BN + c] = mx;
-    }
-    __syncthreads();
-    // subsets.  S <= 5 (Market: 5 strips): one lane per channel builds all
-    // 2^S - 1 subsets in increasing order, each from the subset without its
-    // highest strip plus that strip -- the same ascending-order sum as the
-    // standalone kernel, one add and one max per subset.  Larger S: thread
-    // (channel, group of 8 subsets) with the standalone loop.
-    const int img = m0 / (p.Ho * p.Wo);
-    const int nsub = (1 << NS5) - 1;
-    float* po = p.pps_out + (int64_t)img * p.Ncol + n0;
-    const int64_t sub_stride = (int64_t)p.pps_nimg * p.Ncol;
-    if (NS5 <= 5) {
-      for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : CB); o += NT / 64) {
-        const int cc = o * 64 + ln;
-        if (cc >= nrem) continue;
-        float av[5], mv[5], ss[32], sm[32];
+    __syncthreads();  // every wave is done reading the last stage / the last pass
+    const int wc0 = wn * (BN / WN);  // this wave's first column (wave-uniform)
+    if (HB == 1 || (wc0 >= c0h && wc0 < c0h + BNH)) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          av[q] = q < NS5 ? s_ave[q * BN + cc] : 0.f;
-          mv[q] = q < NS5 ? s_max[q * BN + cc] : 0.f;
-        }
+      for (int i = 0; i < TM; ++i) {
+        const int rr = wm * (BM / WM) + i * S + r32;
 #pragma unroll
-        for (int i = 1; i < 32; ++i) {
-          const int top = 31 - __builtin_clz(i), rest = i & ~(1 << top);
-          ss[i] = rest ? ss[rest] + av[top] : av[top];
-          sm[i] = rest ? fmaxf(sm[rest], mv[top]) : mv[top];
-          if (i <= nsub) {
-            const float v = p.pps_max_ave
-                                ? ss[i] * (1.f / (float)__builtin_popcount(i)) + sm[i]
-                                : 0.f;
-            if (p.pps_max_ave) po[(int64_t)(i - 1) * sub_stride + cc] = v;
+        for (int j = 0; j < TN; ++j) {
+          const int cb = wc0 + j * S + 4 * h - c0h;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+            *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
           }
         }
-        if (!p.pps_max_ave) {  // Max-only: the max of the strip averages
-          float mx[32];
+      }
+    }
+    __syncthreads();
+    auto finish = [&](int idx, const f32x4& rv) {
+      const int row = idx / C4, col = 4 * (idx - row * C4);
+      if (row >= mrem || col >= nrem) return;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
+      const f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
+      const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + col);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = __builtin_fmaf(a[e], s4[e], t4[e]);
+        if (HAS_RES) v[e] += rv[e];
+        if (RELU) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (PPS) {  // the pooling below reads the tile back from LDS
+        *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
+        if (p.pps_write_y) *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+      } else {
+        *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+      }
+    };
+    if constexpr (PRE) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) finish(it * NT + threadIdx.x, rpre[it]);
+    } else {
+      for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+        f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+        if (HAS_RES) {
+          const int row = idx / C4, col = 4 * (idx - row * C4);
+          if (row < mrem && col < nrem) rv = *reinterpret_cast<const f32x4*>(res + row * ldr + col);
+        }
+        finish(idx, rv);
+      }
+    }
+    if constexpr (PPS) {
+      // The tile is one image (BM = Ho * Wo rows, row-major positions) x BNH
+      // channels.  Per (strip, channel): sum and max over the strip's rows in
+      // row-major order, then the 2^S - 1 subsets -- the arithmetic of
+      // part_power_set_v3_kernel (feature_ops.hip), so the bits are the same.
+      __syncthreads();
+      float* s_ave = t + BM * LD;
+      float* s_max = s_ave + kPpsFuseMaxStrips * BNH;
+      // (work split by whole waves: the strip / subset group is wave-uniform,
+      // so the strip table is read with scalar loads)
+      const int W = p.Wo, NS5 = p.pps_S;
+      constexpr int CB = BNH / 64;  // 64-channel slices per pass
+      static_assert(BNH % 64 == 0, "fused pooling: BN / HB must be a multiple of 64");
+      const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const int ln = threadIdx.x & 63;
+      for (int it = wv; it < ((X3P_PPS_ABL & 1) ? 0 : NS5 * CB); it += NT / 64) {
+        const int j = it / CB, c = (it - j * CB) * 64 + ln;
+        int r0 = 0;
+        for (int q = 0; q < j; ++q) r0 += p.pps_h[q];
+        const int cnt = p.pps_h[j] * W;
+        const float* colp = t + (r0 * W) * LD + c;
+        float sum = 0.f, mx = -INFINITY;
+#pragma unroll 16
+        for (int e = 0; e < cnt; ++e) {
+          const float v = colp[e * LD];
+          sum += v;
+          mx = fmaxf(mx, v);
+        }
+        s_ave[j * BNH + c] = sum / (float)cnt;
+        s_max[j * BNH + c] = mx;
+      }
+      __syncthreads();
+      // subsets.  S <= 5 (Market: 5 strips): one lane per channel builds all
+      // 2^S - 1 subsets in increasing order, each from the subset without its
+      // highest strip plus that strip -- the same ascending-order sum as the
+      // standalone kernel, one add and one max per subset.  Larger S: thread
+      // (channel, group of 8 subsets) with the standalone loop.
+      const int img = m0 / (p.Ho * p.Wo);
+      const int nsub = (1 << NS5) - 1;
+      float* po = p.pps_out + (int64_t)img * p.Ncol + n0 + c0h;
+      const int64_t sub_stride = (int64_t)p.pps_nimg * p.Ncol;
+      if (NS5 <= 5) {
+        for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : CB); o += NT / 64) {
+          const int cc = o * 64 + ln;
+          if (cc >= nrem) continue;
+          float av[5], mv[5], ss[32], sm[32];
+#pragma unroll
+          for (int q = 0; q < 5; ++q) {
+            av[q] = q < NS5 ? s_ave[q * BNH + cc] : 0.f;
+            mv[q] = q < NS5 ? s_max[q * BNH + cc] : 0.f;
+          }
 #pragma unroll
           for (int i = 1; i < 32; ++i) {
             const int top = 31 - __builtin_clz(i), rest = i & ~(1 << top);
-            mx[i] = rest ? fmaxf(mx[rest], av[top]) : av[top];
-            if (i <= nsub) po[(int64_t)(i - 1) * sub_stride + cc] = mx[i];
+            ss[i] = rest ? ss[rest] + av[top] : av[top];
+            sm[i] = rest ? fmaxf(sm[rest], mv[top]) : mv[top];
+            if (i <= nsub) {
+              const float v = p.pps_max_ave
+                                  ? ss[i] * (1.f / (float)__builtin_popcount(i)) + sm[i]
+                                  : 0.f;
+              if (p.pps_max_ave) po[(int64_t)(i - 1) * sub_stride + cc] = v;
+            }
+          }
+          if (!p.pps_max_ave) {  // Max-only: the max of the strip averages
+            float mx[32];
+#pragma unroll
+            for (int i = 1; i < 32; ++i) {
+              const int top = 31 - __builtin_clz(i), rest = i & ~(1 << top);
+              mx[i] = rest ? fmaxf(mx[rest], av[top]) : av[top];
+              if (i <= nsub) po[(int64_t)(i - 1) * sub_stride + cc] = mx[i];
+            }
           }
         }
-      }
-    } else {
-      const int ngrp = (nsub + 7) / 8;
-      for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : ngrp * CB); o += NT / 64) {
-        const int g = o / CB, cc = (o - g * CB) * 64 + ln;
-        if (cc >= nrem) continue;
-        float av[kPpsFuseMaxStrips], mv[kPpsFuseMaxStrips];
+      } else {
+        const int ngrp = (nsub + 7) / 8;
+        for (int o = wv; o < ((X3P_PPS_ABL & 2) ? 0 : ngrp * CB); o += NT / 64) {
+          const int g = o / CB, cc = (o - g * CB) * 64 + ln;
+          if (cc >= nrem) continue;
+          float av[kPpsFuseMaxStrips], mv[kPpsFuseMaxStrips];
 #pragma unroll
-        for (int q = 0; q < kPpsFuseMaxStrips; ++q) {
-          av[q] = q < NS5 ? s_ave[q * BN + cc] : 0.f;
-          mv[q] = q < NS5 ? s_max[q * BN + cc] : 0.f;
-        }
-        for (int i = 8 * g + 1; i <= 8 * g + 8 && i <= nsub; ++i) {
-          float v;
-          if (p.pps_max_ave) {
-            float sm = 0.f, mx = -INFINITY;
-            int k = 0;
-            bool first = true;
-#pragma unroll
-            for (int q = 0; q < kPpsFuseMaxStrips; ++q)
-              if (q < NS5 && (i & (1 << q))) {
-                sm = first ? av[q] : sm + av[q];
-                first = false;
-                mx = fmaxf(mx, mv[q]);
-                ++k;
-              }
-            v = sm * (1.f / (float)k) + mx;
-          } else {
-            float mx = -INFINITY;
-#pragma unroll
-            for (int q = 0; q < kPpsFuseMaxStrips; ++q)
-              if (q < NS5 && (i & (1 << q))) mx = fmaxf(mx, av[q]);
-            v = mx;
+          for (int q = 0; q < kPpsFuseMaxStrips; ++q) {
+            av[q] = q < NS5 ? s_ave[q * BNH + cc] : 0.f;
+            mv[q] = q < NS5 ? s_max[q * BNH + cc] : 0.f;
           }
-          po[(int64_t)(i - 1) * sub_stride + cc] = v;
+          for (int i = 8 * g + 1; i <= 8 * g + 8 && i <= nsub; ++i) {
+            float v;
+            if (p.pps_max_ave) {
+              float sm = 0.f, mx = -INFINITY;
+              int k = 0;
+              bool first = true;
+#pragma unroll
+              for (int q = 0; q < kPpsFuseMaxStrips; ++q)
+                if (q < NS5 && (i & (1 << q))) {
+                  sm = first ? av[q] : sm + av[q];
+                  first = false;
+                  mx = fmaxf(mx, mv[q]);
+                  ++k;
+                }
+              v = sm * (1.f / (float)k) + mx;
+            } else {
+              float mx = -INFINITY;
+#pragma unroll
+              for (int q = 0; q < kPpsFuseMaxStrips; ++q)
+                if (q < NS5 && (i & (1 << q))) mx = fmaxf(mx, av[q]);
+              v = mx;
+            }
+            po[(int64_t)(i - 1) * sub_stride + cc] = v;
+          }
         }
       }
     }
@@ -598,12 +612,16 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #define X3P_LDSEPI 1
 #endif
   constexpr bool PPSEPI = (EPI & EPI_F_PPS) != 0;  // needs the LDS epilogue
-  constexpr int PPS_BYTES = PPSEPI ? 2 * kPpsFuseMaxStrips * BN * 4 : 0;
-  static_assert(!PPSEPI || lds_epi_bytes<BM, BN>() + PPS_BYTES <= 160 * 1024,
+  // PPS tiles whose [BM][BN+4] image + pooling scratch exceed the LDS (192 x
+  // 256) park, finish and pool in two column passes
+  constexpr int EHB = (PPSEPI && lds_epi_bytes<BM, BN>() + 2 * kPpsFuseMaxStrips * BN * 4 >
+                                     160 * 1024) ? 2 : 1;
+  constexpr int PPS_BYTES = PPSEPI ? 2 * kPpsFuseMaxStrips * (BN / EHB) * 4 : 0;
+  static_assert(!PPSEPI || lds_epi_bytes<BM, BN / EHB>() + PPS_BYTES <= 160 * 1024,
                 "part-power-set epilogue does not fit in LDS");
   constexpr bool LDSEPI = (X3P_LDSEPI || PPSEPI) &&
                           !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
-                          lds_epi_bytes<BM, BN>() <= 160 * 1024 &&
+                          lds_epi_bytes<BM, BN / EHB>() <= 160 * 1024 &&
                           (PPSEPI || !(BM == 192 && BN == 128 && NW == 8));
 #ifndef X3P_DISTLDS
 #define X3P_DISTLDS 1
@@ -611,8 +629,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool DISTLDS = X3P_DISTLDS && (EPI & EPI_DIST) != 0 &&
                            lds_epi_bytes<BM, BN>() <= NS * STAGE;
   constexpr int LDS_BYTES =
-      (LDSEPI && lds_epi_bytes<BM, BN>() + PPS_BYTES > NS * STAGE)
-          ? lds_epi_bytes<BM, BN>() + PPS_BYTES
+      (LDSEPI && lds_epi_bytes<BM, BN / EHB>() + PPS_BYTES > NS * STAGE)
+          ? lds_epi_bytes<BM, BN / EHB>() + PPS_BYTES
           : NS * STAGE;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -1004,7 +1022,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   } else if constexpr ((EPI & EPI_DIST) != 0)
     dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
   else if constexpr (LDSEPI)
-    conv_epilogue_lds<EPI, BM, BN, WM, WN, S>(p, acc, lds, batch, kslice, m0, n0, wm, wn, r32, h);
+    conv_epilogue_lds<EPI, BM, BN, WM, WN, S, EHB>(p, acc, lds, batch, kslice, m0, n0, wm, wn, r32,
+                                                  h);
   else
     conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
 }
@@ -1034,7 +1053,7 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
   if (epi & EPI_F_PPS) {
     // the fused part-power-set epilogue: conv + BN + residual + ReLU, one
     // image per 192-row tile (Market's 24 x 8 res5 output)
-    if constexpr (BM == 192 && BN <= 128) {
+    if constexpr (BM == 192 && BN <= 256) {
       if (epi != (C | RS | RL | EPI_F_PPS)) {
         set_error("part-power-set epilogue: conv + BN + residual + ReLU only");
         return PPS_ERR_INVALID_ARG;
@@ -1048,7 +1067,7 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
       PPS_CHECK_LAUNCH("gemm_x3p_kernel");
       return PPS_OK;
     } else {
-      set_error("part-power-set epilogue needs a 192-row tile with at most 128 columns");
+      set_error("part-power-set epilogue needs a 192-row tile with at most 256 columns");
       return PPS_ERR_INVALID_ARG;
     }
   }

@@ -570,7 +570,7 @@ std::vector<int> pps_tiles(const PpsModel& m, const Layer& L, const Shape& conv_
   const int rows = (int)(conv_shape.d[1] * conv_shape.d[2]);
   for (int t = GEMM_TILE_P_FIRST; t < GEMM_NUM_TILES; ++t) {
     const int r = x3p_tile_rows(t, L.planes_in), c = x3p_tile_cols(t, L.planes_in);
-    if (r == rows && c > 0 && c <= 128) out.push_back(t);
+    if (r == rows && c > 0 && c <= kPpsFuseMaxCols) out.push_back(t);
   }
   (void)m;
   return out;

@@ -170,6 +170,7 @@ struct GemmParams {
   int pps_h[10];
 };
 constexpr int kPpsFuseMaxStrips = 10;
+constexpr int kPpsFuseMaxCols = 256;  // widest tile the fused pooling takes (two column passes)
 
 int launch_gemm(const GemmParams& p, int epi, int batch, hipStream_t stream);
 int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream);

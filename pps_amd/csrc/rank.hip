@@ -7,6 +7,8 @@
 // distances -- one streaming read of the distance row, no sort.  The result
 // equals a stable (distance, gallery index) sort; counts are additive over
 // gallery shards, which is what the multi-GPU path all-reduces.
+#include <cstdlib>
+
 #include "gemm_common.hpp"
 
 namespace pps {
@@ -892,6 +894,85 @@ __device__ inline void block_bitonic(unsigned long long* buf, int n2) {
   }
 }
 
+// cut: keep the k best of the n candidates cand[0, n) at the front (block-
+// wide).  The k-th best packed key T is found by an 8-pass radix select
+// (8-bit digits from the top; packed keys are unique, so exactly k entries
+// are <= T) and the k entries are compacted to the front -- a full bitonic
+// sort of the buffer (78 LDS-bound stages for 4096 entries, shared by the
+// CU's blocks) cost ~150 us per row block on short rows.  Only the final
+// cut sorts, and only those k entries.  Returns T (~0 when n <= k).
+struct TopkSmem {
+  unsigned hist[256];
+  unsigned long long pref;
+  int rank, cnt;
+};
+__device__ unsigned long long block_cut(unsigned long long* cand, int n, int k, bool final,
+                                        TopkSmem& sm) {
+  constexpr int kPerThr = kTopkBuf / kTopkThreads;
+  unsigned long long T = ~0ull;
+  int keep = n;
+  if (n > k) {
+    if (threadIdx.x == 0) { sm.pref = 0ull; sm.rank = k; }
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = 56 - 8 * pass;
+      for (int i = threadIdx.x; i < 256; i += blockDim.x) sm.hist[i] = 0u;
+      __syncthreads();
+      const unsigned long long pre = sm.pref;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long v = cand[i];
+        if (pass == 0 || (v >> (shift + 8)) == pre)
+          atomicAdd(&sm.hist[(unsigned)(v >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x < 64) {  // one wave: the bin holding rank sm.rank
+        const int l = threadIdx.x;
+        unsigned h[4], sum = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) { h[b] = sm.hist[4 * l + b]; sum += h[b]; }
+        unsigned incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned t = __shfl_up(incl, o);
+          if (l >= o) incl += t;
+        }
+        const unsigned r = (unsigned)sm.rank;
+        const unsigned long long hit = __ballot(incl >= r);
+        const int hl = __ffsll((long long)hit) - 1;
+        if (l == hl) {
+          unsigned before = incl - sum;
+          int b = 0;
+          while (b < 3 && before + h[b] < r) before += h[b++];
+          sm.pref = (pre << 8) | (unsigned long long)(4 * l + b);
+          sm.rank = (int)(r - before);
+        }
+      }
+      __syncthreads();
+    }
+    T = sm.pref;  // the k-th best packed key
+    unsigned long long mine[kPerThr];
+#pragma unroll
+    for (int j = 0; j < kPerThr; ++j) {
+      const int i = threadIdx.x + j * kTopkThreads;
+      mine[j] = i < n ? cand[i] : ~0ull;
+    }
+    if (threadIdx.x == 0) sm.cnt = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPerThr; ++j)
+      if (mine[j] <= T) cand[atomicAdd(&sm.cnt, 1)] = mine[j];
+    __syncthreads();
+    keep = k;
+  }
+  if (final) {
+    int n2 = 1;
+    while (n2 < keep) n2 <<= 1;
+    for (int i = keep + threadIdx.x; i < n2; i += blockDim.x) cand[i] = ~0ull;
+    __syncthreads();
+    block_bitonic(cand, n2);
+  }
+  return T;
+}
+
 // One pass over the row.  Entries are packed as (order-preserving key << 32 |
 // index), so comparing packed values is the stable (distance, index) order.
 // An entry enters the LDS candidate buffer only if it beats the current
@@ -915,79 +996,12 @@ topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
   if (threadIdx.x == 0) { s_n = 0; s_thr = ~0ull; }
   __syncthreads();
   const int64_t chunk = (int64_t)blockDim.x * kTopkUnroll;
-  // cut(n, final): keep the k best of the n candidates.  The k-th best
-  // packed key T is found by an 8-pass radix select (8-bit digits from the
-  // top; packed keys are unique, so exactly k entries are <= T) and the k
-  // entries are compacted to the front -- a full bitonic sort of the
-  // buffer (78 LDS-bound stages for 4096 entries, shared by the CU's
-  // blocks) cost ~150 us per row block on short rows.  Only the final cut
-  // sorts, and only those k entries.
-  __shared__ unsigned s_hist[256];
-  __shared__ unsigned long long s_pref;
-  __shared__ int s_rank, s_cnt;
-  constexpr int kPerThr = kTopkBuf / kTopkThreads;
+  __shared__ TopkSmem sm;
   auto cut = [&](int n, bool final) {
-    int keep = n;
-    if (n > k) {
-      if (threadIdx.x == 0) { s_pref = 0ull; s_rank = k; }
-      for (int pass = 0; pass < 8; ++pass) {
-        const int shift = 56 - 8 * pass;
-        for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0u;
-        __syncthreads();
-        const unsigned long long pre = s_pref;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-          const unsigned long long v = cand[i];
-          if (pass == 0 || (v >> (shift + 8)) == pre)
-            atomicAdd(&s_hist[(unsigned)(v >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {  // one wave: the bin holding rank s_rank
-          const int l = threadIdx.x;
-          unsigned h[4], sum = 0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) { h[b] = s_hist[4 * l + b]; sum += h[b]; }
-          unsigned incl = sum;
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const unsigned t = __shfl_up(incl, o);
-            if (l >= o) incl += t;
-          }
-          const unsigned r = (unsigned)s_rank;
-          const unsigned long long hit = __ballot(incl >= r);
-          const int hl = __ffsll((long long)hit) - 1;
-          if (l == hl) {
-            unsigned before = incl - sum;
-            int b = 0;
-            while (b < 3 && before + h[b] < r) before += h[b++];
-            s_pref = (pre << 8) | (unsigned long long)(4 * l + b);
-            s_rank = (int)(r - before);
-          }
-        }
-        __syncthreads();
-      }
-      const unsigned long long T = s_pref;  // the k-th best packed key
-      unsigned long long mine[kPerThr];
-#pragma unroll
-      for (int j = 0; j < kPerThr; ++j) {
-        const int i = threadIdx.x + j * kTopkThreads;
-        mine[j] = i < n ? cand[i] : ~0ull;
-      }
-      if (threadIdx.x == 0) s_cnt = 0;
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kPerThr; ++j)
-        if (mine[j] <= T) cand[atomicAdd(&s_cnt, 1)] = mine[j];
-      __syncthreads();
-      keep = k;
-      if (threadIdx.x == 0) s_thr = T;
-    }
-    if (threadIdx.x == 0) s_n = keep;
-    if (final) {
-      int n2 = 1;
-      while (n2 < keep) n2 <<= 1;
-      for (int i = keep + threadIdx.x; i < n2; i += blockDim.x) cand[i] = ~0ull;
-      __syncthreads();
-      block_bitonic(cand, n2);
+    const unsigned long long T = block_cut(cand, n, k, final, sm);
+    if (threadIdx.x == 0) {
+      s_n = n > k ? k : n;
+      if (n > k) s_thr = T;
     }
     __syncthreads();
   };
@@ -1089,11 +1103,197 @@ topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
   }
 }
 
+// Long rows (the 1M-gallery shards: 125k entries per row): every WAVE streams
+// its own contiguous quarter of the row with its own threshold and its own
+// candidate buffer in LDS, so the streaming loop has no block barrier and no
+// LDS atomic (a wave appends at its own uniform count).  A wave cuts its
+// buffer back to its k best by a wave-level radix select when the next
+// iteration could overflow it, and once right after its first iteration (so
+// the rest of the row is filtered against a real threshold: ~k ln(G/4k)
+// insertions per wave).  The four k-lists are then merged by the block
+// select + sort of topk_kernel.  Same result (the stable (distance, index)
+// top-k is unique), 20 KB of LDS per block instead of 34 KB.
+constexpr int kTkwU = 2;                    // float4 per lane per iteration
+constexpr int kTkwIter = 64 * 4 * kTkwU;    // row entries per wave iteration (512)
+constexpr int kTkwWaves = kTopkThreads / 64;
+constexpr int kTkwMinRow = 16384;           // rows at least this long take this kernel
+constexpr int kTkwMaxK = 256;
+
+__device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// k-th smallest packed value of buf[0, n) (unique values, n > k) by a wave:
+// 8 passes of 8-bit digits from the top, the histogram in wave-private LDS;
+// then compacts the k values <= T to the front, in place.  Returns T.
+__device__ unsigned long long wave_cut(unsigned long long* buf, int n, int k, unsigned* hist) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pre = 0ull;
+  unsigned rank = (unsigned)k;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) hist[4 * lane + b] = 0u;
+    wave_lds_sync();
+    for (int j = lane; j < n; j += 64) {
+      const unsigned long long v = buf[j];
+      if (pass == 0 || (v >> (shift + 8)) == pre) atomicAdd(&hist[(unsigned)(v >> shift) & 255u], 1u);
+    }
+    wave_lds_sync();
+    unsigned h[4], sum = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) { h[b] = hist[4 * lane + b]; sum += h[b]; }
+    unsigned incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    const unsigned long long hit = __ballot(incl >= rank);
+    const int hl = __ffsll((long long)hit) - 1;
+    unsigned before = incl - sum;
+    int b = 0;
+    while (b < 3 && before + h[b] < rank) before += h[b++];
+    const int bin = __shfl(4 * lane + b, hl);
+    const unsigned r2 = __shfl(rank - before, hl);
+    pre = (pre << 8) | (unsigned long long)bin;
+    rank = r2;
+    wave_lds_sync();
+  }
+  // in-place compaction, 64 entries at a time: every lane reads its entry of
+  // the block before any lane writes, and writes land at or below the block
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int m = 0;
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    const int j = j0 + lane;
+    const unsigned long long v = j < n ? buf[j] : ~0ull;
+    wave_lds_sync();
+    const bool keep = j < n && v <= pre;
+    const unsigned long long bal = __ballot(keep);
+    if (keep) buf[m + __popcll(bal & below)] = v;
+    m += __popcll(bal);
+  }
+  wave_lds_sync();
+  return pre;
+}
+
+__global__ void __launch_bounds__(kTopkThreads)
+topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, int cap,
+                 float* __restrict__ vals, int32_t* __restrict__ idx) {
+  extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers, then hists
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned long long* buf = tkw + wave * cap;
+  unsigned* hist = reinterpret_cast<unsigned*>(tkw + kTkwWaves * cap) + wave * 256;
+  const int64_t q = blockIdx.x;
+  const float* row = dist + q * ldd;
+  // this wave's segment [s0, s1): whole float4s of the 16-byte-aligned row
+  const int64_t GV = G & ~(int64_t)3;
+  const int64_t per = ((GV / 4 + kTkwWaves - 1) / kTkwWaves) * 4;
+  const int64_t s0 = min(GV, (int64_t)wave * per), s1 = min(GV, s0 + per);
+  const rsrc_t rrow = make_rsrc(row, (uint32_t)(GV * 4));  // past GV: reads zero (masked)
+  const unsigned long long below = (1ull << lane) - 1ull;
+  auto load = [&](int64_t it, f32x4 (&dst)[kTkwU]) {
+#pragma unroll
+    for (int u = 0; u < kTkwU; ++u) {
+      const int64_t i = s0 + it * kTkwIter + 4 * (u * 64 + lane);
+      dst[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rrow, (int)(i < s1 ? i * 4 : GV * 4), 0, 0));
+    }
+  };
+  const int64_t niter = (s1 - s0 + kTkwIter - 1) / kTkwIter;
+  f32x4 a[kTkwU], b[kTkwU];
+  load(0, a);
+  load(1, b);
+  int n = 0;
+  unsigned long long thr = ~0ull;
+  for (int64_t it = 0; it < niter; ++it) {
+    if (n + kTkwIter > cap || (it == 1 && n > k)) {
+      thr = wave_cut(buf, n, k, hist);
+      n = k;
+    }
+    f32x4 c[kTkwU];
+    load(it + 2, c);
+#pragma unroll
+    for (int u = 0; u < kTkwU; ++u) {
+      const int64_t i0 = s0 + it * kTkwIter + 4 * (u * 64 + lane);
+      const float e[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int64_t i = i0 + t;
+        const unsigned long long packed = ((unsigned long long)float_key(e[t]) << 32) | (uint32_t)i;
+        const bool take = i < s1 && packed < thr;
+        const unsigned long long bal = __ballot(take);
+        if (take) buf[n + __popcll(bal & below)] = packed;
+        n += __popcll(bal);
+      }
+      a[u] = b[u];
+      b[u] = c[u];
+    }
+  }
+  if (n > k) {
+    wave_cut(buf, n, k, hist);
+    n = k;
+  }
+  // the < 4 entries past the last float4: wave 0 takes them (scalar loads)
+  if (wave == 0 && GV < G) {
+    const int64_t i = GV + lane;
+    const bool take = i < G;
+    const unsigned long long packed =
+        take ? (((unsigned long long)float_key(row[take ? i : 0]) << 32) | (uint32_t)i) : ~0ull;
+    const unsigned long long bal = __ballot(take);
+    if (take) buf[n + __popcll(bal & below)] = packed;
+    n += __popcll(bal);
+  }
+  // merge: the waves' lists into one array at the front of the LDS, then
+  // the block select + sort of topk_kernel
+  __shared__ int s_cnt[kTkwWaves];
+  if (lane == 0) s_cnt[wave] = n;
+  unsigned long long mine[(kTkwMaxK + 4 + 63) / 64];
+#pragma unroll
+  for (int j = 0; j < (kTkwMaxK + 4 + 63) / 64; ++j) {
+    const int p = j * 64 + lane;
+    mine[j] = p < n ? buf[p] : ~0ull;
+  }
+  __syncthreads();
+  int off = 0, total = 0;
+  for (int w = 0; w < kTkwWaves; ++w) {
+    off += w < wave ? s_cnt[w] : 0;
+    total += s_cnt[w];
+  }
+#pragma unroll
+  for (int j = 0; j < (kTkwMaxK + 4 + 63) / 64; ++j) {
+    const int p = j * 64 + lane;
+    if (p < n) tkw[off + p] = mine[j];
+  }
+  __syncthreads();
+  __shared__ TopkSmem sm;
+  block_cut(tkw, total, k, true, sm);
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const unsigned long long v = tkw[i];
+    vals[q * k + i] = key_float((uint32_t)(v >> 32));
+    idx[q * k + i] = (int32_t)(v & 0xffffffffu);
+  }
+}
+
+// PPS_TOPK_WAVE=0: keep long rows on topk_kernel (A/B runs)
+static bool topk_wave_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PPS_TOPK_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* vals,
          int32_t* idx, hipStream_t st) {
   if (Q <= 0) return PPS_OK;
   const bool v4 = (reinterpret_cast<uintptr_t>(dist) & 15) == 0 && (ldd & 3) == 0;
-  if (v4)
+  if (v4 && G >= kTkwMinRow && k <= kTkwMaxK && topk_wave_enabled()) {
+    // per-wave buffer: k kept + one iteration's worst-case inflow
+    const int cap = (k + kTkwIter + 63) / 64 * 64;
+    const size_t lds = (size_t)kTkwWaves * cap * 8 + kTkwWaves * 256 * 4;
+    hipLaunchKernelGGL(topk_wave_kernel, dim3((unsigned)Q), dim3(kTopkThreads), lds, st, dist,
+                       G, ldd, k, cap, vals, idx);
+  } else if (v4)
     hipLaunchKernelGGL(topk_kernel<true>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
                        ldd, k, vals, idx);
   else

@@ -431,7 +431,7 @@ class PPSModel(object):
 
     def pps_tiles(self, L):
         """Tiles the fused conv + pooling can run on: pipelined, exactly one
-        image (Ho x Wo rows) per tile, <= 128 columns (empty: unfused fallback)."""
+        image (Ho x Wo rows) per tile, <= 256 columns (empty: unfused fallback)."""
         n, ho, wo, co = self._shapes[L['conv_output']]
         planes = bool(L.get('planes_in'))
         key = (ho * wo, planes)
@@ -439,7 +439,7 @@ class PPSModel(object):
         if key not in cache:
             cache[key] = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)
                           if ops.tile_shape(t, planes)[0] == ho * wo and
-                          0 < ops.tile_shape(t, planes)[1] <= 128]
+                          0 < ops.tile_shape(t, planes)[1] <= ops.PPS_FUSE_MAX_COLS]
         return cache[key]
 
     def _plane_edges(self):

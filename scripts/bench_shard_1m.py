@@ -71,6 +71,24 @@ def main():
             for k, (s, t) in dict(index_ms=(0, 1), distmat_ms=(1, 2), topk_ms=(2, 3)).items():
                 res.setdefault(k, []).append(e[s].elapsed_time(e[t]))
     med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+    # the memory-bound kernel of this config on its own: the stable top-k
+    # over the resident [Q, G] block, timed over 10 launches between HIP
+    # events (algorithmic bytes: every distance read once + the k-lists)
+    for _ in range(2):
+        ops.topk(out, a.topk)
+    e0, e1 = ev(), ev()
+    e0.record()
+    for _ in range(10):
+        ops.topk(out, a.topk)
+    e1.record()
+    e1.synchronize()
+    tk_us = e0.elapsed_time(e1) * 100.0
+    tk_bytes = a.queries * a.shard * 4 + a.queries * a.topk * 8
+    roof_topk = dict(bound='hbm', achieved=round(tk_bytes / tk_us / 1e3, 1), peak=8000.0,
+                     unit='GB/s', frac=round(tk_bytes / tk_us / 1e3 / 8000.0, 4), traffic=None,
+                     kernel='topk_wave_kernel (per-wave streaming stable top-%d)' % a.topk
+                     if a.shard >= 16384 and a.topk <= 256 else 'topk_kernel',
+                     avg_launch_us=round(tk_us, 2), algorithmic_bytes_per_launch=tk_bytes)
     flops = 2.0 * a.queries * a.shard * a.dim
     byt = (a.queries + a.shard) * a.dim * 4 + a.queries * a.shard * 4
     print(json.dumps(dict(
@@ -80,7 +98,8 @@ def main():
         topk_ms=round(med['topk_ms'], 3),
         distmat_TFLOPs=round(flops / med['distmat_ms'] / 1e9, 1),
         distmat_GBps=round(byt / med['distmat_ms'] / 1e6, 1),
-        topk_GBps=round(a.queries * a.shard * 4 / med['topk_ms'] / 1e6, 1))), flush=True)
+        topk_GBps=round(a.queries * a.shard * 4 / med['topk_ms'] / 1e6, 1),
+        roofline_topk=roof_topk)), flush=True)
 
 
 if __name__ == '__main__':

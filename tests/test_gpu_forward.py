@@ -404,8 +404,10 @@ def test_conv_pps_matches_conv_then_pooling(planes):
     split = [5, 5, 4, 5, 5]
     xa = ops.split_bf16x3(x) if planes else x
     tiles = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1)
-             if ops.tile_shape(t, planes)[0] == H * W and ops.tile_shape(t, planes)[1] <= 128]
-    assert len(tiles) >= (4 if planes else 7), tiles
+             if ops.tile_shape(t, planes)[0] == H * W and
+             ops.tile_shape(t, planes)[1] <= ops.PPS_FUSE_MAX_COLS]
+    assert len(tiles) >= (4 if planes else 8), tiles
+    assert planes or 35 in tiles  # the 192x256 tile (two column passes)
     for tile in tiles:
         y = torch.empty(N, H, W, Cout, device='cuda')
         ops.conv2d_bn_act_x3p(xa, Cin, w3, kpad, 1, 1, 0, 1, sc, sh, res, True, y, tile=tile)

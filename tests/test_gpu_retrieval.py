@@ -378,3 +378,29 @@ def test_cmc_counts_sharded_equal_unsharded(golden):
     r1, v1 = ops.cmc_finalize(sp.pos_total, want, 100, False)
     r2, v2 = ops.cmc_finalize(sp2.pos_total, hist, 100, False)
     assert torch.equal(v1, v2) and torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize('G,k', [(16384, 1), (40003, 100), (40000, 256), (125001, 100),
+                                 (20001, 257)])
+def test_topk_long_rows_wave_kernel(G, k):
+    """Long rows (>= 16384 entries, k <= 256: the per-wave streaming kernel of
+    the 1M-gallery shards; k = 257 stays on the block kernel): the stable
+    (distance, index) top-k equals NumPy's, with heavy ties, negative values,
+    the < 4-entry tail (odd G, padded rows), and adversarial rows whose
+    values only decrease (every entry beats the running threshold, so every
+    iteration cuts)."""
+    from pps_amd import ops
+    rng = np.random.RandomState(G + k)
+    Q = 24
+    d = rng.randint(-40, 40, size=(Q, G)).astype(np.float32) / 4   # many ties
+    d[1] = rng.rand(G).astype(np.float32)
+    d[2] = -np.arange(G, dtype=np.float32)                            # strictly decreasing
+    d[3] = 1.0                                                        # all tied
+    d[4, -1] = -1e9                                                   # best entry in the tail
+    d[5, :G // 2] = np.linspace(1, 0, G // 2, dtype=np.float32)       # decreasing first half
+    buf = ops.dist_buffer(Q, G, 'cuda')
+    buf.copy_(torch.from_numpy(d))
+    vals, idx = ops.topk(buf, k)
+    ref = np.argsort(d, axis=1, kind='stable')[:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, ref, axis=1))

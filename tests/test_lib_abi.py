@@ -53,7 +53,7 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 def test_pipelined_tile_shapes():
     """pps_x3p_tile_shape (host-only) mirrors the pipelined tile table
     (pps_internal.hpp): the ids the fused part pooling may use are exactly
-    the 192-row tiles with <= 128 columns, with f32 or plane activations."""
+    the 192-row tiles with <= 256 columns (192x256: f32 activations only)."""
     from pps_amd import ops
     want = {29: (128, 128), 30: (192, 128), 31: (128, 64), 32: (192, 64), 33: (256, 128),
             34: (128, 256), 35: (192, 256), 36: (128, 128), 37: (192, 128), 38: (128, 128),
@@ -70,7 +70,8 @@ def test_pipelined_tile_shapes():
     assert ops.tile_shape(35, True) == (128, 256) and ops.tile_shape(37, True)[0] == 192
     assert ops.tile_shape(47, True)[0] == 192 and ops.tile_shape(49, True)[0] == 96
     assert ops.tile_shape(50, True) == (96, 128)
-    pps_f32 = [t for t in want if ops.tile_shape(t)[0] == 192 and ops.tile_shape(t)[1] <= 128]
+    pps_f32 = [t for t in want if ops.tile_shape(t)[0] == 192 and ops.tile_shape(t)[1] <= 256]
     pps_pl = [t for t in want if ops.tile_shape(t, True)[0] == 192 and
-              ops.tile_shape(t, True)[1] <= 128]
-    assert pps_f32 == [30, 32, 37, 39, 41, 46, 47, 48, 52] and pps_pl == pps_f32
+              ops.tile_shape(t, True)[1] <= 256]
+    assert pps_f32 == [30, 32, 35, 37, 39, 41, 46, 47, 48, 52]
+    assert pps_pl == [30, 32, 37, 39, 41, 46, 47, 48, 52]
