@@ -58,7 +58,9 @@ const char* pps_registered_ops(void);
  * 192x128 (8 waves, 4 x 2), 48 = 192x64 (4 waves), 49 = 96x128 (4 waves),
  * 50 = 96x128 (8 waves, 2 x 4), 51 / 52 = 128x128 / 192x128 (8 waves,
  * 4 x 2) with three LDS stages, 53 = tile 50 with three stages, all on
- * 16x16x32 blocks.  Results
+ * 16x16x32 blocks; 54 = the weight-stationary persistent kernel for 1x1
+ * convs with K = 64 / 128 / 256 (stationary weight columns in LDS,
+ * activations streamed to registers; other shapes run tile 38).  Results
  * are identical for every tile below 38 (same per-element fp32 MFMA
  * accumulation order) and identical among the tiles from 38 on (one MFMA
  * sums a 32-wide K chunk: a different rounding

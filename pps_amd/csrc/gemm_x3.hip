@@ -263,10 +263,19 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     set_error("bf16x3 distance GEMM needs both squared-norm vectors");
     return PPS_ERR_INVALID_ARG;
   }
+  const int epi_in = epi;
   if (!(epi & EPI_DIST) && !(epi & EPI_F_RAW)) {
     if (p.residual) epi |= EPI_F_RES;
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
+  }
+  if (p.tile == GEMM_TILE_WS) {
+    // the weight-stationary kernel where it applies, else the 128x128
+    // pipelined tile of the same (16x16x32) rounding group
+    if (ws_eligible(p, epi, batch)) return launch_gemm_ws(p, epi, stream);
+    GemmParams q = p;
+    q.tile = GEMM_TILE_P16_FIRST;
+    return launch_gemm_x3(q, epi_in, batch, stream);
   }
   if (p.ksplit_conv && (p.tile < GEMM_TILE_P_FIRST || !x3p_eligible(p, epi))) {
     set_error("conv split-K runs on the pipelined tiles only (tile >= " +

@@ -56,6 +56,26 @@ __device__ inline f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32
   return c;
 }
 
+// The same six terms on v_mfma_f32_16x16x32_bf16 (the S = 16 tiles of
+// gemm_x3p.hip and gemm_ws.hip) with the MFMA operands swapped (weights as
+// the MFMA "A"): one MFMA covers a whole 32-wide K chunk, so its rounding
+// differs from the 32x32x16 form -- S = 16 kernels agree bit for bit with
+// each other, not with S = 32.  Transposed accumulator: lane l keeps output
+// row (l & 15) and columns 4 (l >> 4) + e, e = 0..3 (one 16-byte vector per
+// block).
+__device__ inline f32x4 mfma16_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = mfma16_bf16(b[0], a[0], c);
+  c = mfma16_bf16(b[0], a[1], c);
+  c = mfma16_bf16(b[1], a[0], c);
+  c = mfma16_bf16(b[0], a[2], c);
+  c = mfma16_bf16(b[1], a[1], c);
+  c = mfma16_bf16(b[2], a[0], c);
+  return c;
+}
+
 // Distance epilogue from precomputed squared row norms (pps_row_sqnorm):
 //   sqeuclid = (-2 q.g + |q|^2) + |g|^2 clamped at 0 [sqrt]; cosine = 1 - q.g/(|q||g|)
 template <int BM, int BN, int WM, int WN>

@@ -60,24 +60,6 @@ __device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
   return c;
 }
 
-// The same six terms on v_mfma_f32_16x16x32_bf16 (S = 16 tiles): one MFMA
-// covers a whole 32-wide K chunk, so its rounding differs from the 32x32x16
-// form -- S = 16 tiles agree bit for bit with each other, not with S = 32.
-// Transposed accumulator: lane l keeps output row (l & 15) and columns
-// 4 (l >> 4) + e, e = 0..3 (one 16-byte vector per block).
-__device__ inline f32x4 mfma16_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
-  c = mfma16_bf16(b[0], a[0], c);
-  c = mfma16_bf16(b[0], a[1], c);
-  c = mfma16_bf16(b[1], a[0], c);
-  c = mfma16_bf16(b[0], a[2], c);
-  c = mfma16_bf16(b[1], a[1], c);
-  c = mfma16_bf16(b[2], a[0], c);
-  return c;
-}
-
 // grouped tile order of the distance GEMMs: MB of query panels per group
 #ifndef X3P_GM_MB
 #define X3P_GM_MB 32
@@ -1169,7 +1151,7 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 // Rows (BM) of the tile a pipelined id launches (as launch_variant /
 // launch_gemm_x3p map it), 0 for a non-pipelined id.
 int x3p_tile_rows(int tile, bool a3) {
-  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
+  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41 ||
       tile == GEMM_TILE_P16_192x128W42S3)
     return 192;
@@ -1192,7 +1174,7 @@ int x3p_tile_rows(int tile, bool a3) {
 
 // Columns (BN) of that tile.
 int x3p_tile_cols(int tile, bool a3) {
-  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_NUM_TILES) return 0;
+  if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
       tile == GEMM_TILE_P16_96x128W24 || tile == GEMM_TILE_P16_128x128W42S3 ||
       tile == GEMM_TILE_P16_192x128W42S3 || tile == GEMM_TILE_P16_96x128W24S3)

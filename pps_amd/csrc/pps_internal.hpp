@@ -95,7 +95,10 @@ enum GemmTile {
   GEMM_TILE_P16_192x128W42S3 = 52,
   // 53 (16x16x32): 96x128 with 8 waves as 2 x 4 and three LDS stages
   GEMM_TILE_P16_96x128W24S3 = 53,
-  GEMM_NUM_TILES = 54
+  // 54 (16x16x32 rounding): weight-stationary persistent kernel (gemm_ws.hip)
+  // for 1x1 convs with K = 64 / 128 / 256; other shapes run tile 38
+  GEMM_TILE_WS = 54,
+  GEMM_NUM_TILES = 55
 };
 
 struct GemmParams {
@@ -183,6 +186,8 @@ int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipS
 int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,
                  hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
+bool ws_eligible(const GemmParams& p, int epi, int batch);
+int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream);
 
 // ---- retrieval (rank.hip) ---------------------------------------------------
 constexpr int kMergeMaxLists = 64;

@@ -179,4 +179,6 @@ def test_native_errors_are_enforce_style():
     with pytest.raises(RuntimeError, match='no layer named'):
         native.call('pps_model_set_tile', nm.handle, b'res9_branch2a', 3)
     with pytest.raises(RuntimeError, match='not a plane-eligible producer'):
+        native.call('pps_model_set_planes', nm.handle, b'res2_0_branch2c', 1)
+    with pytest.raises(ValueError, match='not a plane-eligible producer'):
         nm.set_planes(['res2_0_branch2c'])

@@ -75,6 +75,13 @@ def test_split_sqnorm_fused_equals_separate(R, D):
     (1, 11, 9, 16, 33, 3, 2, 1),       # ragged, strided, Cin < 32 (BK32 falls back)
     (1, 9, 7, 20, 24, 3, 1, 1),        # Cin not a power of two and < 32
     (2, 384, 128, 4, 64, 7, 2, 3),     # stem conv1 (Cin 3 packed to 4)
+    # the weight-stationary tile 54 (1x1, K = 64 / 128 / 256): res2 / res3 /
+    # res4 branch2c shapes, ragged M, Cout < the column block
+    (2, 96, 32, 64, 256, 1, 1, 0),
+    (1, 48, 16, 128, 512, 1, 1, 0),
+    (2, 24, 8, 256, 1024, 1, 1, 0),
+    (3, 7, 5, 64, 128, 1, 1, 0),
+    (1, 9, 9, 128, 64, 1, 1, 0),
 ])
 @pytest.mark.parametrize('residual', [False, True])
 def test_conv_x3_error_and_tiles(N, H, W, Cin, Cout, k, s, p, residual):
@@ -118,7 +125,9 @@ def test_conv_x3_error_and_tiles(N, H, W, Cin, Cout, k, s, p, residual):
 
 @pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(2, 24, 8, 128, 256, 512, 2),
                                                  (1, 24, 8, 512, 1024, 2048, 1),
-                                                 (3, 5, 7, 16, 32, 40, 1)])
+                                                 (3, 5, 7, 16, 32, 40, 1),
+                                                 (2, 96, 32, 64, 64, 256, 1),   # res2_0 (tile 54)
+                                                 (1, 12, 8, 32, 32, 64, 2)])
 def test_conv_dual_x3(N, H, W, C1, C2, Cout, s2):
     from pps_amd import model, ops
     rng = np.random.RandomState(C1 + Cout)
