@@ -27,19 +27,22 @@
 
 namespace pps {
 
-constexpr int kWsWaves = 8;
 constexpr int kWsCUs = 256;  // MI355X compute units (one workgroup each)
-template <int BN2> constexpr int ws_rows() { return 16 * kWsWaves / (BN2 / 64); }
+constexpr int kWsLd = 64 + 4;  // epilogue scratch row (floats): 64 columns + bank padding
+template <int BN2, int W> constexpr int ws_rows() { return 16 * W / (BN2 / 64); }
 
-// NCH: 32-wide K chunks (K = 32 NCH); BN2: the stationary column block.
-template <int NCH, int BN2, int EPI>
-__global__ void __launch_bounds__(64 * kWsWaves)
+// NCH: 32-wide K chunks (K = 32 NCH); BN2: the stationary column block;
+// W: waves per workgroup (8: two per SIMD -- 16 waves measured no faster).
+template <int NCH, int BN2, int EPI, int W>
+__global__ void __launch_bounds__(64 * W)
 gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
-  constexpr int PD = NCH <= 2 ? 3 : (NCH <= 4 ? 2 : 1);  // tiles in flight ahead
+  constexpr int kWsWaves = W;
+  // tiles in flight ahead of the one computing
+  constexpr int PD = NCH <= 2 ? 3 : (NCH <= 4 ? 2 : 1);
   extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
   constexpr int TN = 4;              // 16-column MFMA blocks per wave (64 columns)
   constexpr int WC = BN2 / 64;       // waves across the column block
-  constexpr int ROWS = ws_rows<BN2>();
+  constexpr int ROWS = ws_rows<BN2, W>();
   static_assert(BN2 % 64 == 0 && kWsWaves % WC == 0, "column block");
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
@@ -78,6 +81,11 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   }
   __syncthreads();
 
+  // the wave's epilogue scratch and its lanes' (row layout) scale / shift
+  float* wsc = reinterpret_cast<float*>(ws_lds + WBYTES + 2 * BN2 * 4) + wave * 16 * kWsLd;
+  const f32x4 s4r = *reinterpret_cast<const f32x4*>(s_sc + wcol + 4 * (lane & 15));
+  const f32x4 t4r = *reinterpret_cast<const f32x4*>(s_sh + wcol + 4 * (lane & 15));
+
   // 2) row tiles rt = g / n_cb + k * rg
   const rsrc_t ra = make_rsrc(p.a, p.a_bytes);
   const rsrc_t ra2 = DUAL ? make_rsrc(p.a2, p.a2_bytes) : ra;
@@ -97,7 +105,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   // HBM latency x 25 GB/s per CU).
   struct Ops {
     f32x4 a[NCH][2];
-    f32x4 r[HAS_RES ? TN : 1];
+    f32x4 r[HAS_RES ? 4 : 1];
   };
   // Every memory access is a buffer op whose offset is kOOB for a row past M
   // or a tile past this workgroup's share (loads read zero, stores are
@@ -123,12 +131,13 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
       o.a[kc][1] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off == kOOB ? kOOB : off + 16, 0, 0));
     }
-    if constexpr (HAS_RES) {
-      const int ro = ok ? (m * p.ldr + n0 + wcol + 4 * h) * 4 : kOOB;
+    if constexpr (HAS_RES) {  // row layout (see process): 4 rows x 256 B per load
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        o.r[j] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rres, ro == kOOB ? kOOB : ro + 64 * j, 0, 0));
+      for (int it = 0; it < 4; ++it) {
+        const int mr = rt * ROWS + wr * 16 + 4 * it + (lane >> 4);
+        const int ro = (valid && mr < p.M) ? (mr * p.ldr + n0 + wcol + 4 * (lane & 15)) * 4 : kOOB;
+        o.r[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rres, ro, 0, 0));
+      }
     }
   };
 
@@ -156,22 +165,33 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
       // every chunk's LDS reads and run out of registers)
       asm volatile("" ::: "memory");
     }
-    const int oo = ok ? (m * (int)p.ldo + n0 + wcol + 4 * h) * 4 : kOOB;
+    // Epilogue in row layout: the wave parks its 16 x 64 accumulator block in
+    // its own LDS scratch and reads it back so that lane l holds columns
+    // 4 (l & 15) .. +3 of row 4 it + (l >> 4): every residual load and
+    // output store then covers 4 whole 256-byte row segments (the
+    // accumulator layout would scatter 64-byte pieces over 16 rows).  Wave-
+    // private: LDS ops of one wave complete in order, no barrier.
+    (void)ok;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = wcol + 16 * j + 4 * h;
-      const f32x4 s4 = *reinterpret_cast<const f32x4*>(s_sc + c);
-      const f32x4 t4 = *reinterpret_cast<const f32x4*>(s_sh + c);
+    for (int j = 0; j < TN; ++j)
+      *reinterpret_cast<f32x4*>(wsc + r16 * kWsLd + 16 * j + 4 * h) = acc[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = 4 * it + (lane >> 4);
+      const f32x4 a = *reinterpret_cast<const f32x4*>(wsc + row * kWsLd + 4 * (lane & 15));
+      const int mr = rt * ROWS + wr * 16 + row;
+      const int oo = (valid && mr < p.M) ? (mr * (int)p.ldo + n0 + wcol + 4 * (lane & 15)) * 4 : kOOB;
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = __builtin_fmaf(acc[j][e], s4[e], t4[e]);
-        if (HAS_RES) v[e] += o.r[j][e];
+        v[e] = __builtin_fmaf(a[e], s4r[e], t4r[e]);
+        if (HAS_RES) v[e] += o.r[it][e];
         if (RELU) v[e] = fmaxf(v[e], 0.f);
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout,
-                                             oo == kOOB ? kOOB : oo + 64 * j, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, 0);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next park
   };
 
   Ops ring[PD + 1];
@@ -207,21 +227,22 @@ bool ws_eligible(const GemmParams& p, int epi, int batch) {
   return true;
 }
 
-template <int NCH, int BN2>
+template <int NCH, int BN2, int W>
 static int launch_ws_cfg(const GemmParams& p, int epi, hipStream_t stream) {
   const int n_cb = (p.Ncol + BN2 - 1) / BN2;
-  const int n_rt = (p.M + ws_rows<BN2>() - 1) / ws_rows<BN2>();
+  const int n_rt = (p.M + ws_rows<BN2, W>() - 1) / ws_rows<BN2, W>();
   const int rg = n_cb >= kWsCUs ? 1 : (kWsCUs / n_cb < n_rt ? kWsCUs / n_cb : n_rt);
-  const size_t lds = (size_t)NCH * 3 * BN2 * 64 + 2 * BN2 * sizeof(float);
-  const dim3 grid((unsigned)(n_cb * rg)), block(64 * kWsWaves);
+  const size_t lds = (size_t)NCH * 3 * BN2 * 64 + 2 * BN2 * sizeof(float) +
+                     (size_t)W * 16 * kWsLd * sizeof(float);
+  const dim3 grid((unsigned)(n_cb * rg)), block(64 * W);
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, DU = EPI_F_DUAL;
   switch (epi) {
-    case C: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
-    case C | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
-    case C | RS: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RS>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
-    case C | RS | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RS | RL>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
-    case C | RL | DU: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL | DU>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
-    case C | DU: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | DU>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C | RS: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RS, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C | RS | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RS | RL, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C | RL | DU: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL | DU, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+    case C | DU: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | DU, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
     default:
       set_error("weight-stationary GEMM: epilogue not built");
       return PPS_ERR_INVALID_ARG;
@@ -235,15 +256,15 @@ static int launch_ws_cfg(const GemmParams& p, int epi, hipStream_t stream) {
 int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream) {
   const int K = p.Kloop;
   if (K == 64) {
-    if (p.Ncol % 256 == 0) return launch_ws_cfg<2, 256>(p, epi, stream);
-    if (p.Ncol % 128 == 0) return launch_ws_cfg<2, 128>(p, epi, stream);
-    return launch_ws_cfg<2, 64>(p, epi, stream);
+    if (p.Ncol % 256 == 0) return launch_ws_cfg<2, 256, 8>(p, epi, stream);
+    if (p.Ncol % 128 == 0) return launch_ws_cfg<2, 128, 8>(p, epi, stream);
+    return launch_ws_cfg<2, 64, 8>(p, epi, stream);
   }
   if (K == 128) {
-    if (p.Ncol % 128 == 0) return launch_ws_cfg<4, 128>(p, epi, stream);
-    return launch_ws_cfg<4, 64>(p, epi, stream);
+    if (p.Ncol % 128 == 0) return launch_ws_cfg<4, 128, 8>(p, epi, stream);
+    return launch_ws_cfg<4, 64, 8>(p, epi, stream);
   }
-  return launch_ws_cfg<8, 64>(p, epi, stream);
+  return launch_ws_cfg<8, 64, 8>(p, epi, stream);
 }
 
 }  // namespace pps

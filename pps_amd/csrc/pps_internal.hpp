@@ -95,8 +95,9 @@ enum GemmTile {
   GEMM_TILE_P16_192x128W42S3 = 52,
   // 53 (16x16x32): 96x128 with 8 waves as 2 x 4 and three LDS stages
   GEMM_TILE_P16_96x128W24S3 = 53,
-  // 54 (16x16x32 rounding): weight-stationary persistent kernel (gemm_ws.hip)
-  // for 1x1 convs with K = 64 / 128 / 256; other shapes run tile 38
+  // 54 (16x16x32 rounding): weight-stationary persistent kernel
+  // (gemm_ws.hip) for 1x1 convs with K = 64 / 128 / 256; other shapes run
+  // tile 38
   GEMM_TILE_WS = 54,
   GEMM_NUM_TILES = 55
 };

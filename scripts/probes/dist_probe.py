@@ -18,7 +18,9 @@ def main():
     out = ops.dist_buffer(Q, G, 'cuda') if os.environ.get('PAD', '1') == '1' else \
         torch.empty(Q, G, device='cuda')
     flops = 2.0 * Q * G * D
-    for tile in range(ops.TILE_P_FIRST, ops.num_tiles() + 1):
+    tiles = [int(t) for t in os.environ['TILES'].split(',')] if os.environ.get('TILES') else \
+        range(ops.TILE_P_FIRST, ops.num_tiles() + 1)
+    for tile in tiles:
         row = []
         for qp in (False, True):
             for _ in range(2):
