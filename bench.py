@@ -31,7 +31,7 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA
 PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # bf16 MFMA = 16x the f32 rate (~2.5 PF)
 # bf16x3 path: every f32 product costs 6 bf16 MFMA terms -> its own MFMA roof
 PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
-TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r02', 'pmc_traffic.json')
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r03', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -165,14 +165,56 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         t_rank.append(res['t_rank_ms'])
         t_total.append(res['t_total_ms'])
     rank_roof = rank_roofline(ev, res['dist'])
+    dist_roof = distmat_roofline(q_local, g_local, world)
     del res['dist']
-    out = dict(rank_roofline=rank_roof, distmat_tile=pdist.HipBackend.distmat_tile,
+    out = dict(rank_roofline=rank_roof, dist_roofline=dist_roof,
+               distmat_tile=pdist.HipBackend.distmat_tile,
                distmat_qplanes=pdist.HipBackend.distmat_qplanes,
                distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
                retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
                cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
                cmc10=float(res['cmc'][9]), G_local=gsl[1] - gsl[0])
     return out
+
+
+def distmat_roofline(q_local, g_local, world, reps=10):
+    """The distance GEMM launch alone (gemm_x3p_kernel EPI_DIST on the bench's
+    tile), the way a gallery index is used: gallery planes + norms prepared
+    once (GalleryIndex), queries split once; `reps` launches between HIP
+    events on the kernel's stream.  Algorithmic work 2 Q G_r D FLOP."""
+    from pps_amd import ops
+    from pps_amd import distributed as pdist
+    be = pdist.HipBackend
+    if ops.default_math() != 'x3':
+        return None
+    q_all = pdist.all_gather_rows(q_local, [q_local.shape[0]] * world) if world > 1 else q_local
+    idx = ops.GalleryIndex(g_local)
+    Q, D = q_all.shape
+    out = ops.dist_buffer(Q, g_local.shape[0], q_all.device)
+    qp = bool(be.distmat_qplanes)
+    if qp:
+        q3, qsq = ops.split_sqnorm(q_all)
+        launch = lambda: ops.distmat_planes(q3, qsq, idx, out, tile=be.distmat_tile)
+    else:
+        launch = lambda: ops.compute_dist(q_all, idx, out=out, tile=be.distmat_tile)
+    for _ in range(2):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    G = g_local.shape[0]
+    flops = 2.0 * Q * G * D
+    byt = (Q + G) * D * 6 + Q * G * 4   # the bf16x3 operand planes read once + the matrix
+    tf = flops / (us * 1e-6) / 1e12
+    return dict(achieved=round(tf, 2), frac=round(tf / PEAK_X3_TFLOPS, 4),
+                avg_launch_us=round(us, 2), flops_per_launch=flops,
+                operand_and_output_bytes_per_launch=byt, queries_as_planes=bool(qp),
+                timing='%d launches between HIP events, gallery index and query planes '
+                       'prepared once' % reps)
 
 
 def rank_roofline(ev, dist, reps=20):
@@ -207,7 +249,7 @@ def rank_roofline(ev, dist, reps=20):
 
 def _pmc_traffic(key, math, batch):
     """HBM bytes per launch measured by rocprofv3 PMC passes of this bench
-    (scripts/pmc_traffic.py -> profiles/r01/pmc_traffic.json): FETCH_SIZE x 2
+    (scripts/pmc_traffic.py -> profiles/r03/pmc_traffic.json): FETCH_SIZE x 2
     (gfx950 reports half of wide streaming reads) + WRITE_SIZE, per launch.
     None unless the file was measured for the same math and batch."""
     try:
@@ -633,15 +675,22 @@ def main():
         'roofline': roof,
         'roofline_rank': ret['rank_roofline'],
         'roofline_distmat': dict(
-            bound='mfma', achieved=round(dist_tflops, 2),
+            bound='mfma',
+            achieved=(ret['dist_roofline'] or {}).get('achieved', round(dist_tflops, 2)),
             peak=round(PEAK_X3_TFLOPS if dist_math == 'x3' else PEAK_FP32_MFMA_TFLOPS, 1),
             unit='TFLOP/s',
-            frac=round(dist_tflops / (PEAK_X3_TFLOPS if dist_math == 'x3'
-                                      else PEAK_FP32_MFMA_TFLOPS), 4),
+            frac=(ret['dist_roofline'] or {}).get(
+                'frac', round(dist_tflops / (PEAK_X3_TFLOPS if dist_math == 'x3'
+                                             else PEAK_FP32_MFMA_TFLOPS), 4)),
+            avg_launch_us=(ret['dist_roofline'] or {}).get('avg_launch_us'),
+            with_index_prep=dict(ms=round(ret['distmat_ms'], 3), TFLOPs=round(dist_tflops, 2),
+                                 note='gallery shard split + norms + query gather + GEMM, '
+                                      'as retrieval_ms runs it'),
             hbm_GBps=round(dist_bytes / (ret['distmat_ms'] * 1e-3) / 1e9, 2),
             traffic=_pmc_traffic('distmat', dist_math, Q_MARKET),
             algorithmic_bytes_per_launch=dist_bytes,
-            kernel='%s EPI_DIST, tile %d (+ split/norm of the gallery shard)' % (
+            timing=(ret['dist_roofline'] or {}).get('timing'),
+            kernel='%s EPI_DIST, tile %d' % (
                 'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
                 ret['distmat_tile']) + (', queries as bf16x3 planes'
                                         if ret['distmat_qplanes'] else '')),

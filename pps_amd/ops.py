@@ -170,12 +170,21 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
         return out
     if q_planes:
         q3, qsq = split_sqnorm(q) if q.is_contiguous() else (split_bf16x3(q), row_sqnorm(q))
-        call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
-             _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
-             METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
-        return out
+        return distmat_planes(q3, qsq, idx, out, metric, tile)
     qsq = row_sqnorm(q)
     call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
+         _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
+         METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
+    return out
+
+
+def distmat_planes(q3, qsq, idx, out, metric='euclidean', tile=0):
+    """The distance GEMM alone (pps_distmat_x3p) on queries already split into
+    bf16x3 planes q3 [3, Q, D] with squared norms qsq, against a
+    GalleryIndex: what compute_dist(q_planes=True) launches after the split."""
+    _, Q, D = q3.shape
+    G = idx.shape[0]
+    call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
          METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
     return out

@@ -43,6 +43,8 @@ def epi_of(name):
     if '<' not in name:
         return 0   # the fused stem: a conv epilogue
     args = name.split('<', 1)[1].split('>', 1)[0].split(',')
+    if 'gemm_ws_kernel' in name:   # <NCH, BN2, EPI, W>
+        return int(args[2])
     return int(args[4])
 
 
@@ -51,7 +53,8 @@ def main():
     fetch = load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0], 'FETCH_SIZE')
     write = load(glob.glob(os.path.join(d, 'p2', '*counter_collection.csv'))[0], 'WRITE_SIZE')
     # the x3 path launches both the register-staged and the pipelined family
-    knames = ('gemm_x3_kernel', 'gemm_x3p_kernel') if math == 'x3' else ('gemm_f32_kernel',)
+    knames = ('gemm_x3_kernel', 'gemm_x3p_kernel', 'gemm_ws_kernel') if math == 'x3' \
+        else ('gemm_f32_kernel',)
 
     def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
         return any(k + '<' in nm for k in knames) or ('stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)

@@ -16,8 +16,9 @@ pytestmark = pytest.mark.gpu
 # Parity bounds (round 3): what the kernels deliver plus a margin.
 FWD_ATOL = 1e-6     # normalised 3968-d features vs the oracle (observed ~6e-8)
 LAYER_RTOL = 1e-5   # intermediate stage outputs, relative to their max
-PRE_ATOL = 2e-3     # preprocess vs the float64 oracle: f32 separable passes, observed
-                    # 9.0e-4 on values up to ~255 (4e-6 relative)
+PRE_ATOL = 3e-3     # preprocess vs the float64 oracle, f32 separable passes: observed
+                    # 9.7e-4 at Market size, 2.0e-3 on the ragged up-scales (values up
+                    # to ~255: ~1e-5 of the range)
 BENCH_TILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                            'profiles', 'r03', 'tiles_v0.json')
 
