@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session that produces the round's measurement artefacts:
 #   1. bench (autotune; tiles saved)            -> gpurun_out/bench_tuned.log
-#   2. rocprofv3 --kernel-trace --stats (same tiles) -> gpurun_out/prof/
+#   2. rocprofv3 --kernel-trace --stats (same tiles, no e2e stage: its ragged
+#      last batch would be the "last forward") -> gpurun_out/prof/
 #   3. PMC passes FETCH_SIZE / WRITE_SIZE / GRBM_GUI_ACTIVE+MFMA busy (same tiles)
 #      -> gpurun_out/pmc_traffic.json
 #   4. bench again (same tiles, traffic filled)  -> gpurun_out/bench_final.log
@@ -12,18 +13,20 @@ OUT=$PWD/gpurun_out
 mkdir -p $OUT profiles/r03
 TILES=$OUT/tiles.json
 rm -f $TILES
+# TILES_IN=<committed table>: skip the tuning run, profile that table
+if [ -n "$TILES_IN" ]; then cp "$TILES_IN" $TILES; fi
 MATH=${PPS_MATH:-x3}
 step() { echo "== $1"; }
 step bench-tune
-timeout -k 10 600 python bench.py --tiles-file $TILES > $OUT/bench_tuned.log 2>&1 || { tail -5 $OUT/bench_tuned.log; exit 1; }
-tail -1 $OUT/bench_tuned.log | cut -c1-300
+[ -n "$TILES_IN" ] || timeout -k 10 600 python bench.py --tiles-file $TILES > $OUT/bench_tuned.log 2>&1 || { tail -5 $OUT/bench_tuned.log; exit 1; }
+[ -n "$TILES_IN" ] || tail -1 $OUT/bench_tuned.log | cut -c1-300
 step stats
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline > $OUT/prof.log 2>&1 || { tail -5 $OUT/prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e > $OUT/prof.log 2>&1 || { tail -5 $OUT/prof.log; exit 1; }
 step pmc
 rm -rf $OUT/pmcb
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmcb/p1 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc1.log 2>&1 || { tail -5 $OUT/pmc1.log; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc2.log 2>&1 || { tail -5 $OUT/pmc2.log; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmcb/p1 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc1.log 2>&1 || { tail -5 $OUT/pmc1.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc2.log 2>&1 || { tail -5 $OUT/pmc2.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
 python scripts/pmc_traffic.py $OUT/pmcb $MATH 64 50 > $OUT/pmc_traffic.json || exit 1
 cat $OUT/pmc_traffic.json
 cp $OUT/pmc_traffic.json profiles/r03/pmc_traffic.json   # bench-final reads it (box copy)
