@@ -1106,82 +1106,123 @@ topk_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k,
 // Long rows (the 1M-gallery shards: 125k entries per row): every WAVE streams
 // its own contiguous quarter of the row with its own threshold and its own
 // candidate buffer in LDS, so the streaming loop has no block barrier and no
-// LDS atomic (a wave appends at its own uniform count).  A wave cuts its
-// buffer back to its k best by a wave-level radix select when the next
-// iteration could overflow it, and once right after its first iteration (so
-// the rest of the row is filtered against a real threshold: ~k ln(G/4k)
-// insertions per wave).  The four k-lists are then merged by the block
-// select + sort of topk_kernel.  Same result (the stable (distance, index)
-// top-k is unique), 20 KB of LDS per block instead of 34 KB.
-constexpr int kTkwU = 2;                    // float4 per lane per iteration
+// LDS atomic (a wave appends at its own uniform count).  When the next
+// iteration could overflow the buffer (and once right after the first
+// iteration, so the rest of the row is filtered against a real threshold) the
+// wave cuts it back to between k and k + kTkwSlack entries; at the end to
+// exactly its k best.  Wave 0 then selects the row's k best of the four lists
+// and the block sorts them.  Same result as topk_kernel (the stable
+// (distance, index) top-k is unique).
+//
+// Selection is a bisection on the packed value with the buffer held in
+// registers: each step is one compare per register, a ballot and a scalar
+// popcount -- no LDS atomics.  (A radix select's LDS histogram serialises
+// here: after the first cut the buffered keys share their top bytes, so 64
+// lanes add into one bin.)
+#ifndef PPS_TKW_U
+#define PPS_TKW_U 2
+#endif
+#ifndef PPS_TKW_D
+#define PPS_TKW_D 2   // iterations loaded ahead of the one filtering
+#endif
+#ifndef PPS_TKW_PROBE
+#define PPS_TKW_PROBE 0
+#endif
+constexpr int kTkwU = PPS_TKW_U;            // float4 per lane per iteration
 constexpr int kTkwIter = 64 * 4 * kTkwU;    // row entries per wave iteration (512)
 constexpr int kTkwWaves = kTopkThreads / 64;
 constexpr int kTkwMinRow = 16384;           // rows at least this long take this kernel
 constexpr int kTkwMaxK = 256;
+constexpr int kTkwSlack = 64;               // a streaming cut keeps k .. k + slack entries
+// per-wave buffer: what a cut keeps + one iteration's worst-case inflow
+__host__ __device__ constexpr int tkw_cap(int k) { return (k + kTkwSlack + kTkwIter + 63) / 64 * 64; }
+// registers per lane for a wave's buffer / the four merged lists, for k <= KM
+template <int KM> constexpr int tkw_j() { return tkw_cap(KM) / 64; }
+template <int KM> constexpr int tkw_merge_j() { return kTkwWaves * KM / 64 + 1; }
 
 __device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// k-th smallest packed value of buf[0, n) (unique values, n > k) by a wave:
-// 8 passes of 8-bit digits from the top, the histogram in wave-private LDS;
-// then compacts the k values <= T to the front, in place.  Returns T.
-__device__ unsigned long long wave_cut(unsigned long long* buf, int n, int k, unsigned* hist) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long pre = 0ull;
-  unsigned rank = (unsigned)k;
-  for (int pass = 0; pass < 8; ++pass) {
-    const int shift = 56 - 8 * pass;
+__device__ inline unsigned long long wave_min_u64(unsigned long long x) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) hist[4 * lane + b] = 0u;
-    wave_lds_sync();
-    for (int j = lane; j < n; j += 64) {
-      const unsigned long long v = buf[j];
-      if (pass == 0 || (v >> (shift + 8)) == pre) atomicAdd(&hist[(unsigned)(v >> shift) & 255u], 1u);
-    }
-    wave_lds_sync();
-    unsigned h[4], sum = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) { h[b] = hist[4 * lane + b]; sum += h[b]; }
-    unsigned incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
-    }
-    const unsigned long long hit = __ballot(incl >= rank);
-    const int hl = __ffsll((long long)hit) - 1;
-    unsigned before = incl - sum;
-    int b = 0;
-    while (b < 3 && before + h[b] < rank) before += h[b++];
-    const int bin = __shfl(4 * lane + b, hl);
-    const unsigned r2 = __shfl(rank - before, hl);
-    pre = (pre << 8) | (unsigned long long)bin;
-    rank = r2;
-    wave_lds_sync();
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_xor(x, o);
+    x = y < x ? y : x;
   }
-  // in-place compaction, 64 entries at a time: every lane reads its entry of
-  // the block before any lane writes, and writes land at or below the block
-  const unsigned long long below = (1ull << lane) - 1ull;
+  return x;
+}
+__device__ inline unsigned long long wave_max_u64(unsigned long long x) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_xor(x, o);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+template <int J>
+__device__ inline int wave_count_le(const unsigned long long (&v)[J], unsigned long long t) {
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) c += __popcll(__ballot(v[j] <= t));
+  return c;
+}
+
+// v[j] holds entry j*64 + lane of a wave's n > k unique packed values (~0ull
+// past n; no real entry is ~0ull: indices are < 2^31).  Returns a T with
+// k <= count(v <= T) <= k + slack; slack 0 gives the k-th smallest value.
+// Invariant count(<= lo) < k <= count(<= hi); every value is wave-uniform.
+template <int J>
+__device__ unsigned long long wave_select(const unsigned long long (&v)[J], int k, int slack) {
+  unsigned long long mn = ~0ull, mx = 0ull;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    mn = v[j] < mn ? v[j] : mn;
+    mx = (v[j] != ~0ull && v[j] > mx) ? v[j] : mx;
+  }
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if (k <= 1) return mn;
+  unsigned long long lo = mn, hi = mx;   // count(<= mn) = 1 < k
+  while (hi - lo > 1) {
+    const unsigned long long mid = lo + ((hi - lo) >> 1);
+    const int c = wave_count_le(v, mid);
+    if (c >= k && c <= k + slack) return mid;
+    if (c < k) lo = mid; else hi = mid;
+  }
+  return hi;
+}
+
+// Cuts a wave's buffer buf[0, n) to the entries <= T of wave_select: reads
+// it into registers, selects, writes the kept entries back to the front.
+// Returns T; n becomes the kept count.
+template <int J>
+__device__ unsigned long long wave_cut(unsigned long long* buf, int& n, int k, int slack) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) v[j] = j * 64 + lane < n ? buf[j * 64 + lane] : ~0ull;
+  const unsigned long long T = wave_select(v, k, slack);
   int m = 0;
-  for (int j0 = 0; j0 < n; j0 += 64) {
-    const int j = j0 + lane;
-    const unsigned long long v = j < n ? buf[j] : ~0ull;
-    wave_lds_sync();
-    const bool keep = j < n && v <= pre;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const bool keep = v[j] <= T;
     const unsigned long long bal = __ballot(keep);
-    if (keep) buf[m + __popcll(bal & below)] = v;
+    if (keep) buf[m + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = v[j];
     m += __popcll(bal);
   }
   wave_lds_sync();
-  return pre;
+  n = m;
+  return T;
 }
 
-__global__ void __launch_bounds__(kTopkThreads)
+template <int KM>
+__global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
 topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, int cap,
                  float* __restrict__ vals, int32_t* __restrict__ idx) {
-  extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers, then hists
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers
+  // wave-uniform: segment bounds, buffer base and counts live in SGPRs
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   unsigned long long* buf = tkw + wave * cap;
-  unsigned* hist = reinterpret_cast<unsigned*>(tkw + kTkwWaves * cap) + wave * 256;
   const int64_t q = blockIdx.x;
   const float* row = dist + q * ldd;
   // this wave's segment [s0, s1): whole float4s of the 16-byte-aligned row
@@ -1199,39 +1240,108 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
     }
   };
   const int64_t niter = (s1 - s0 + kTkwIter - 1) / kTkwIter;
-  f32x4 a[kTkwU], b[kTkwU];
-  load(0, a);
-  load(1, b);
   int n = 0;
-  unsigned long long thr = ~0ull;
-  for (int64_t it = 0; it < niter; ++it) {
-    if (n + kTkwIter > cap || (it == 1 && n > k)) {
-      thr = wave_cut(buf, n, k, hist);
-      n = k;
+  unsigned long long thr = ~0ull;   // inclusive: entries <= thr stay candidates
+  // Float pre-filter: an entry can only be <= thr if its distance is not
+  // above thr's distance, !(e > thr_f) -- a superset of the exact test (NaN
+  // entries and the initial NaN threshold pass it).  One compare per entry;
+  // the append runs only for the entry slots where some lane passed.
+  float thr_f = key_float((uint32_t)(thr >> 32));
+  // one iteration: refill `nxt` (consumed by the previous iteration) with
+  // iteration it + PPS_TKW_D, then filter `cur`.  Named buffers in a loop
+  // unrolled by the rotation length: a rotating a = b, b = c would make the
+  // compiler copy the registers at the end of every iteration and so wait for
+  // the load it had just issued (vmcnt(0)).
+  auto step = [&](int64_t it, const f32x4 (&cur)[kTkwU], f32x4 (&nxt)[kTkwU]) {
+    if (n + kTkwIter > cap || (it == 1 && n > k + kTkwSlack)) {
+      thr = wave_cut<tkw_j<KM>()>(buf, n, k, kTkwSlack);
+      thr_f = key_float((uint32_t)(thr >> 32));
+#if PPS_TKW_PROBE
+      thr_f = -__builtin_huge_valf();   // timing probe only: stream, take nothing
+#endif
     }
-    f32x4 c[kTkwU];
-    load(it + 2, c);
+    // keep each step's refill in its step: a load hoisted above the previous
+    // step's filter would overlap `nxt` with live buffers, and the loop head
+    // would then wait for every load in flight
+    asm volatile("" ::: "memory");
+    load(it + PPS_TKW_D, nxt);
+    unsigned long long m[kTkwU][4], any = 0ull;
 #pragma unroll
     for (int u = 0; u < kTkwU; ++u) {
-      const int64_t i0 = s0 + it * kTkwIter + 4 * (u * 64 + lane);
-      const float e[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+      const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int64_t i = i0 + t;
-        const unsigned long long packed = ((unsigned long long)float_key(e[t]) << 32) | (uint32_t)i;
-        const bool take = i < s1 && packed < thr;
-        const unsigned long long bal = __ballot(take);
-        if (take) buf[n + __popcll(bal & below)] = packed;
-        n += __popcll(bal);
+        m[u][t] = __ballot(!(e[t] > thr_f));
+        any |= m[u][t];
       }
-      a[u] = b[u];
-      b[u] = c[u];
     }
+    if (!any) return;
+    if ((it + 1) * kTkwIter > s1 - s0) {   // the segment's last iteration: exact, bounded
+#pragma unroll
+      for (int u = 0; u < kTkwU; ++u) {
+        const int64_t i0 = s0 + it * kTkwIter + 4 * (u * 64 + lane);
+        const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (!m[u][t]) continue;
+          const int64_t i = i0 + t;
+          const unsigned long long packed = ((unsigned long long)float_key(e[t]) << 32) | (uint32_t)i;
+          const bool take = i < s1 && packed <= thr;
+          const unsigned long long bal = __ballot(take);
+          if (take) buf[n + __popcll(bal & below)] = packed;
+          n += __popcll(bal);
+        }
+      }
+      return;
+    }
+    // inside the segment every pre-filter passer is appended: an entry with
+    // thr's distance but a larger index is a harmless extra candidate (cuts
+    // rank packed values), so the slot costs the key, the lane's rank in the
+    // pass mask and one LDS store
+#pragma unroll
+    for (int u = 0; u < kTkwU; ++u) {
+      const uint32_t i0 = (uint32_t)(s0 + it * kTkwIter) + 4u * (uint32_t)(u * 64 + lane);
+      const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const unsigned long long mm = m[u][t];
+        if (!mm) continue;
+        if (!(e[t] > thr_f)) {
+          const uint32_t ub = __float_as_uint(e[t]);
+          const uint32_t key = ub ^ ((uint32_t)((int32_t)ub >> 31) | 0x80000000u);
+          const int pos = n + (int)__builtin_amdgcn_mbcnt_hi(
+                                  (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+          buf[pos] = ((unsigned long long)key << 32) | (i0 + (uint32_t)t);
+        }
+        n += __popcll(mm);
+      }
+    }
+  };
+  // Whole rounds: the iterations past the segment read zeros (buffer loads
+  // past GV) and take nothing (i >= s1).
+#if PPS_TKW_D == 3
+  f32x4 a[kTkwU], b[kTkwU], c[kTkwU], d4[kTkwU];
+  load(0, a);
+  load(1, b);
+  load(2, c);
+  for (int64_t it = 0; it < niter; it += 4) {
+    step(it, a, d4);
+    step(it + 1, b, a);
+    step(it + 2, c, b);
+    step(it + 3, d4, c);
   }
-  if (n > k) {
-    wave_cut(buf, n, k, hist);
-    n = k;
+#else
+  f32x4 a[kTkwU], b[kTkwU], c[kTkwU];
+  load(0, a);
+  asm volatile("" ::: "memory");   // issue order a, b: the first step waits for a only
+  load(1, b);
+  for (int64_t it = 0; it < niter; it += 3) {
+    step(it, a, c);
+    step(it + 1, b, a);
+    step(it + 2, c, b);
   }
+#endif
+  if (n > k) wave_cut<tkw_j<KM>()>(buf, n, k, 0);
   // the < 4 entries past the last float4: wave 0 takes them (scalar loads)
   if (wave == 0 && GV < G) {
     const int64_t i = GV + lane;
@@ -1242,30 +1352,42 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
     if (take) buf[n + __popcll(bal & below)] = packed;
     n += __popcll(bal);
   }
-  // merge: the waves' lists into one array at the front of the LDS, then
-  // the block select + sort of topk_kernel
+  // merge: wave 0 reads the four lists (<= k + 3 entries each) and keeps the
+  // row's k best at the front of the LDS; the block sorts them
   __shared__ int s_cnt[kTkwWaves];
   if (lane == 0) s_cnt[wave] = n;
-  unsigned long long mine[(kTkwMaxK + 4 + 63) / 64];
+  __syncthreads();
+  if (wave == 0) {
+    constexpr int MJ = tkw_merge_j<KM>();
+    unsigned long long v[MJ];
 #pragma unroll
-  for (int j = 0; j < (kTkwMaxK + 4 + 63) / 64; ++j) {
-    const int p = j * 64 + lane;
-    mine[j] = p < n ? buf[p] : ~0ull;
+    for (int j = 0; j < MJ; ++j) {
+      const int p = j * 64 + lane;   // merged position
+      int ww = 0, off = p;
+      for (; ww < kTkwWaves && off >= s_cnt[ww]; ++ww) off -= s_cnt[ww];
+      v[j] = ww < kTkwWaves ? tkw[ww * cap + off] : ~0ull;
+    }
+    int total = 0;
+    for (int ww = 0; ww < kTkwWaves; ++ww) total += s_cnt[ww];
+    const unsigned long long T = total > k ? wave_select(v, k, 0) : ~0ull - 1;
+    wave_lds_sync();
+    int m = 0;
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const bool keep = v[j] <= T;
+      const unsigned long long bal = __ballot(keep);
+      if (keep) tkw[m + __popcll(bal & below)] = v[j];
+      m += __popcll(bal);
+    }
+    // pad to the sort length
+    int n2 = 1;
+    while (n2 < k) n2 <<= 1;
+    for (int i = m + lane; i < n2; i += 64) tkw[i] = ~0ull;
   }
   __syncthreads();
-  int off = 0, total = 0;
-  for (int w = 0; w < kTkwWaves; ++w) {
-    off += w < wave ? s_cnt[w] : 0;
-    total += s_cnt[w];
-  }
-#pragma unroll
-  for (int j = 0; j < (kTkwMaxK + 4 + 63) / 64; ++j) {
-    const int p = j * 64 + lane;
-    if (p < n) tkw[off + p] = mine[j];
-  }
-  __syncthreads();
-  __shared__ TopkSmem sm;
-  block_cut(tkw, total, k, true, sm);
+  int n2 = 1;
+  while (n2 < k) n2 <<= 1;
+  block_bitonic(tkw, n2);
   __syncthreads();
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const unsigned long long v = tkw[i];
@@ -1288,11 +1410,14 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
   if (Q <= 0) return PPS_OK;
   const bool v4 = (reinterpret_cast<uintptr_t>(dist) & 15) == 0 && (ldd & 3) == 0;
   if (v4 && G >= kTkwMinRow && k <= kTkwMaxK && topk_wave_enabled()) {
-    // per-wave buffer: k kept + one iteration's worst-case inflow
-    const int cap = (k + kTkwIter + 63) / 64 * 64;
-    const size_t lds = (size_t)kTkwWaves * cap * 8 + kTkwWaves * 256 * 4;
-    hipLaunchKernelGGL(topk_wave_kernel, dim3((unsigned)Q), dim3(kTopkThreads), lds, st, dist,
-                       G, ldd, k, cap, vals, idx);
+    const int cap = tkw_cap(k);
+    const size_t lds = (size_t)kTkwWaves * cap * 8;
+    if (k <= 128)
+      hipLaunchKernelGGL(topk_wave_kernel<128>, dim3((unsigned)Q), dim3(kTopkThreads), lds, st,
+                         dist, G, ldd, k, cap, vals, idx);
+    else
+      hipLaunchKernelGGL(topk_wave_kernel<kTkwMaxK>, dim3((unsigned)Q), dim3(kTopkThreads), lds,
+                         st, dist, G, ldd, k, cap, vals, idx);
   } else if (v4)
     hipLaunchKernelGGL(topk_kernel<true>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
                        ldd, k, vals, idx);
