@@ -30,11 +30,19 @@ __device__ inline float rr_m(const float* qg, const float* qq, const float* gg, 
   return c < Q ? qg[c * G + (r - Q)] : gg[(r - Q) * G + (c - Q)];
 }
 
+// OD rows are padded to a multiple of 4 floats: 16-byte aligned rows let the
+// top-k over OD take its 16-byte-load kernels (the wave-streaming one at
+// Duke size, N >= 16384)
+static int64_t od_stride(int64_t N) { return (N + 3) / 4 * 4; }
+
 // The column maxima of M^2 by blocks: column c of M is column c of qq plus
 // row c of qg (c < Q), or column c-Q of qg plus column c-Q of gg (c >= Q).
 // Squares are >= 0, so their float bits order as unsigned integers and an
-// integer atomicMax into a zeroed vector is an exact, order-free max.
-constexpr int kCmRows = 256;  // rows per block of the column-max kernel
+// integer atomicMax into a zeroed vector is an exact, order-free max.  A
+// thread owns one column of a kCmRows-row block and keeps kCmBatch loads in
+// flight (one load at a time left the 1.2 GB of Duke's blocks at ~2.3 TB/s).
+constexpr int kCmRows = 256;   // rows per block of the column-max kernel
+constexpr int kCmBatch = 16;   // loads in flight per thread
 __global__ void rerank_colmax_sq_kernel(const float* __restrict__ x, int64_t R, int64_t C,
                                         int64_t ld, unsigned* __restrict__ out) {
   const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -42,7 +50,15 @@ __global__ void rerank_colmax_sq_kernel(const float* __restrict__ x, int64_t R, 
   const int64_t r0 = blockIdx.y * (int64_t)kCmRows;
   const int64_t r1 = r0 + kCmRows < R ? r0 + kCmRows : R;
   float m = 0.f;
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  for (; r + kCmBatch <= r1; r += kCmBatch) {
+    float v[kCmBatch];
+#pragma unroll
+    for (int u = 0; u < kCmBatch; ++u) v[u] = __builtin_nontemporal_load(x + (r + u) * ld + c);
+#pragma unroll
+    for (int u = 0; u < kCmBatch; ++u) m = fmaxf(m, v[u] * v[u]);
+  }
+  for (; r < r1; ++r) {
     const float v = x[r * ld + c];
     m = fmaxf(m, v * v);
   }
@@ -53,51 +69,81 @@ __global__ void rerank_colmax_sq_kernel(const float* __restrict__ x, int64_t R, 
 __global__ void rerank_rowmax_sq_kernel(const float* __restrict__ x, int64_t C, int64_t ld,
                                         unsigned* __restrict__ out) {
   const int64_t r = blockIdx.x;
+  const float* row = x + r * ld;
   float m = 0.f;
-  for (int64_t c = threadIdx.x; c < C; c += blockDim.x) {
-    const float v = x[r * ld + c];
+  int64_t c = threadIdx.x;
+  for (; c + (kCmBatch - 1) * (int64_t)blockDim.x < C; c += kCmBatch * (int64_t)blockDim.x) {
+    float v[kCmBatch];
+#pragma unroll
+    for (int u = 0; u < kCmBatch; ++u) v[u] = row[c + u * (int64_t)blockDim.x];
+#pragma unroll
+    for (int u = 0; u < kCmBatch; ++u) m = fmaxf(m, v[u] * v[u]);
+  }
+  for (; c < C; c += blockDim.x) {
+    const float v = row[c];
     m = fmaxf(m, v * v);
   }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) atomicMax(out + r, __float_as_uint(m));
 }
 
-// OD[i][j] = M[j][i]^2 / colmax[i], via 64x64 LDS tiles (the transpose of
-// :454); a wave moves one 256-byte tile row per access
+// OD[i][j] = M[j][i]^2 / colmax[i], via T x T LDS tiles (the transpose of
+// :454).  256 threads; a wave moves T/64 consecutive 256-byte pieces of a
+// tile row per access round, so HBM sees T*4-byte row segments both ways.
+#ifndef PPS_OD_TILE
+#define PPS_OD_TILE 64
+#endif
+template <int T>
 __global__ void __launch_bounds__(256)
 rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
                        const float* __restrict__ gg, int64_t Q, int64_t G,
-                       const float* __restrict__ colmax, float* __restrict__ od) {
-  __shared__ float tile[64][65];
+                       const float* __restrict__ colmax, float* __restrict__ od, int64_t ldo) {
+  constexpr int H = T / 64;
+  __shared__ float tile[T][T + 1];
   const int64_t N = Q + G;
-  const int64_t i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int64_t i0 = blockIdx.y * (int64_t)T, j0 = blockIdx.x * (int64_t)T;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: ty 0..3
-  if (i0 + 64 <= Q && j0 >= Q) {
+  if (i0 + T <= Q && j0 >= Q) {
     // query rows x gallery columns: M[j][i] = qg[i][j - Q], i.e. OD here is
     // qg itself (squared, scaled) -- read it row-wise, no transpose (the
     // generic path below would read qg down its columns, stride G)
-    for (int k = ty; k < 64; k += 4) {
-      const int64_t i = i0 + k, j = j0 + tx;
-      if (j < N) {
-        const float m = qg[i * G + (j - Q)];
-        od[i * N + j] = (m * m) / colmax[i];
+    for (int k = ty; k < T; k += 4) {
+      const int64_t i = i0 + k;
+      const float cm = colmax[i];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int64_t j = j0 + tx + 64 * h;
+        if (j < N) {
+          const float m = qg[i * G + (j - Q)];
+          od[i * ldo + j] = (m * m) / cm;
+        }
       }
     }
     return;
   }
-  for (int k = ty; k < 64; k += 4) {  // read M[j0+k][i0+tx] (row j, col i)
-    const int64_t r = j0 + k, c = i0 + tx;
-    float v = 0.f;
-    if (r < N && c < N) {
-      const float m = rr_m(qg, qq, gg, Q, G, r, c);
-      v = m * m;
+  for (int k = ty; k < T; k += 4) {  // read M[j0+k][i0+tx..] (row j, col i)
+    const int64_t r = j0 + k;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int64_t c = i0 + tx + 64 * h;
+      float v = 0.f;
+      if (r < N && c < N) {
+        const float m = rr_m(qg, qq, gg, Q, G, r, c);
+        v = m * m;
+      }
+      tile[k][tx + 64 * h] = v;
     }
-    tile[k][tx] = v;
   }
   __syncthreads();
-  for (int k = ty; k < 64; k += 4) {  // write OD[i0+k][j0+tx] = tile[tx][k] / colmax
-    const int64_t i = i0 + k, j = j0 + tx;
-    if (i < N && j < N) od[i * N + j] = tile[tx][k] / colmax[i];
+  for (int k = ty; k < T; k += 4) {  // write OD[i0+k][j0+tx..] = tile[tx..][k] / colmax
+    const int64_t i = i0 + k;
+    if (i >= N) continue;
+    const float cm = colmax[i];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int64_t j = j0 + tx + 64 * h;
+      if (j < N) od[i * ldo + j] = tile[tx + 64 * h][k] / cm;
+    }
   }
 }
 
@@ -112,7 +158,7 @@ __device__ inline bool in_row(const int32_t* rank, int K1, int row, int len, int
   return false;
 }
 
-__global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N,
+__global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, int64_t ldo,
                                      const int32_t* __restrict__ rank, int K1, int Kh,
                                      int vcap, int32_t* __restrict__ v_idx,
                                      float* __restrict__ v_val, int32_t* __restrict__ v_cnt) {
@@ -181,12 +227,12 @@ __global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N,
   float wsum = 0.f;
   if (lane == 0) {
     // weight = exp(-OD[i, idx]); V = weight / sum(weight) (float32, in index order)
-    for (int t = 0; t < u; ++t) wsum += expf(-od[i * N + exp_[t]]);
+    for (int t = 0; t < u; ++t) wsum += expf(-od[i * ldo + exp_[t]]);
   }
   wsum = __shfl(wsum, 0);
   const int cap = min(u, vcap);
   for (int t = lane; t < cap; t += 64) {
-    const float w = expf(-od[i * N + exp_[t]]);
+    const float w = expf(-od[i * ldo + exp_[t]]);
     v_idx[i * vcap + t] = exp_[t];
     v_val[i * vcap + t] = w / wsum;
   }
@@ -337,6 +383,7 @@ __global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_
 
 // ---- 6) Jaccard + blend for the query rows ------------------------------------
 __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restrict__ od,
+                                      int64_t ldo,
                                       const int32_t* __restrict__ q_idx,
                                       const float* __restrict__ q_val,
                                       const int32_t* __restrict__ q_cnt, int qcap,
@@ -362,7 +409,7 @@ __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restr
     const float t = tm[j];
     const float jac = 1.f - __fdiv_rn(t, 2.f - t);
     out[i * (N - Q) + (j - Q)] = __fadd_rn(__fmul_rn(jac, one_m_lam),
-                                           __fmul_rn(od[i * N + j], lam));
+                                           __fmul_rn(od[i * ldo + j], lam));
   }
 }
 
@@ -373,6 +420,7 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   // NumPy (NEP 50) casts the Python-float factors to float32: lambda and 1-lambda
   const float lam = (float)lambda, one_m_lam = (float)(1.0 - lambda);
   const int64_t N = Q + G;
+  const int64_t ldo = od_stride(N);
   const int K1 = k1 + 1;
   const int Kh = (int)lrint(k1 / 2.0) + 1;  // int(np.around(k1 / 2.)) + 1
   const int vbound = K1 + K1 * Kh;
@@ -385,7 +433,7 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
     p += (bytes + 255) / 256 * 256;
     return r;
   };
-  float* od = reinterpret_cast<float*>(take(sizeof(float) * N * N));
+  float* od = reinterpret_cast<float*>(take(sizeof(float) * N * ldo));
   float* colmax = reinterpret_cast<float*>(take(sizeof(float) * N));
   float* topv = reinterpret_cast<float*>(take(sizeof(float) * N * K1));
   int32_t* rank = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * K1));
@@ -420,11 +468,12 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, G,
                      cm);       // columns c < Q: rows r >= Q (qg^T)
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
-  hipLaunchKernelGGL(rerank_build_od_kernel, dim3((unsigned)((N + 63) / 64),
-                                                  (unsigned)((N + 63) / 64)),
-                     dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od);
+  constexpr int T = PPS_OD_TILE;
+  hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((N + T - 1) / T),
+                                                     (unsigned)((N + T - 1) / T)),
+                     dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo);
   PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
-  int rc = topk(od, N, N, N, K1, topv, rank, st);
+  int rc = topk(od, N, N, ldo, K1, topv, rank, st);
   if (rc != PPS_OK) return rc;
   PPS_CHECK_LAUNCH_S("rerank topk", st);
   if (debug_sync()) {  // every neighbour index must address a row of OD
@@ -437,7 +486,7 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
         return PPS_ERR_LAUNCH;
       }
   }
-  hipLaunchKernelGGL(rerank_v_rows_kernel, dim3((unsigned)N), dim3(64), 0, st, od, N, rank,
+  hipLaunchKernelGGL(rerank_v_rows_kernel, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo, rank,
                      K1, Kh, vcap, v_idx, v_val, v_cnt);
   PPS_CHECK_LAUNCH_S("rerank_v_rows_kernel", st);
   if (k2 != 1) {
@@ -461,7 +510,7 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
                      q_val, q_cnt, qc, start, fill, csc_row, csc_val);
   PPS_CHECK_LAUNCH_S("rerank_csc_fill_kernel", st);
   hipLaunchKernelGGL(rerank_jaccard_kernel, dim3((unsigned)Q), dim3(256), sizeof(float) * N, st,
-                     Q, N, od, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam, one_m_lam,
+                     Q, N, od, ldo, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam, one_m_lam,
                      out);
   PPS_CHECK_LAUNCH_S("rerank_jaccard_kernel", st);
   return PPS_OK;
@@ -476,7 +525,7 @@ size_t rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   const int64_t qcap = (int64_t)k2 * vcap;
   auto r = [](size_t b) { return (b + 255) / 256 * 256; };
   size_t s = 0;
-  s += r(4 * N * N) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
+  s += r(4 * N * od_stride(N)) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
   s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
   return s;
 }
