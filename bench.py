@@ -365,9 +365,10 @@ def e2e_stage(nm, rank, world, n_images, batch, threads):
     """End-to-end images/s from image FILES (north_star "end-to-end
     images/sec"; the reference's loop is detectron/core/test_engine.py:
     282-315): Market-sized 128x64 JPEGs written to local disk, then the
-    product loop pps_amd.test_engine.extract_features -- PIL decode on
-    `threads` host threads, one pinned H2D copy per batch, the preprocessing
-    kernel and pps_forward on the GPU -- followed (one rank) by the
+    product loop pps_amd.test_engine.extract_features -- PIL decode in the
+    decode processes main() started before touching the GPU (threads if
+    none), one pinned H2D copy per batch, the preprocessing kernel and
+    pps_forward on the GPU -- followed (one rank) by the
     distance matrix + mAP/CMC of the first 3368 images as queries against
     the rest.  Images are split over ranks; the rate is all images / the
     slowest rank's time."""
@@ -396,20 +397,25 @@ def e2e_stage(nm, rank, world, n_images, batch, threads):
         feats = torch.empty((n, nm.feat_dim), dtype=torch.float32, device='cuda')
         # warm: the decode pool, pinned allocations, the batch shapes
         test_engine.extract_features(nm, lambda i: test_engine._decode_bgr(paths[i]),
-                                     min(n, 2 * batch), batch=batch, out=feats, workers=threads)
+                                     min(n, 2 * batch), batch=batch, out=feats, workers=threads,
+                                     paths=paths)
         pdist.barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         test_engine.extract_features(nm, lambda i: test_engine._decode_bgr(paths[i]), n,
-                                     batch=batch, out=feats, workers=threads)
+                                     batch=batch, out=feats, workers=threads, paths=paths)
         torch.cuda.synchronize()
         t_ext = time.perf_counter() - t0
         t_max = pdist.max_over_ranks(t_ext, world)
-        out = dict(images=n_images, decode_threads=threads, jpeg_MB=round(jpeg_bytes / 1e6, 2),
+        from pps_amd import decode_pool
+        procs = decode_pool.workers()
+        out = dict(images=n_images, decode='%d processes' % procs if procs else
+                   '%d threads' % threads, jpeg_MB=round(jpeg_bytes / 1e6, 2),
                    extract_s=round(t_max, 4), images_per_s=round(n_images / t_max, 2),
-                   note='JPEG files on local disk -> PIL decode on host threads -> pinned H2D '
-                        '-> pps_preprocess_bgr_ragged -> pps_forward (test_engine.'
-                        'extract_features); rate = all images / slowest rank')
+                   note='JPEG files on local disk (page-cached after writing) -> PIL decode '
+                        'in worker processes -> pinned H2D -> pps_preprocess_bgr_ragged -> '
+                        'pps_forward (test_engine.extract_features); rate = all images / '
+                        'slowest rank')
         if world == 1 and n > Q_MARKET:
             from pps_amd.distributed import ShardedEvaluator
             rs = np.random.RandomState(0)
@@ -543,6 +549,13 @@ def main():
     backend = os.environ.get('PPS_DIST_BACKEND', 'nccl')
     if backend == 'gloo':
         local = local % torch.cuda.device_count()
+    if not args.no_e2e:
+        # JPEG decode processes for the e2e stage, forked from a server started
+        # before this process touches the GPU; the host's CPUs split over the
+        # node's ranks
+        from pps_amd import decode_pool
+        lw = int(os.environ.get('LOCAL_WORLD_SIZE', world))
+        decode_pool.start(decode_pool.default_workers(share=max(1, lw)))
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist

@@ -12,8 +12,9 @@ detectron/core/test_engine.py:
 and the result dict of task_evaluation.py:54-60,345-359.
 
 MI355X-first differences (SURVEY §3.1 hot loop): the reference runs one image
-per RunNet with two host<->device copies per image (test.py:163-185).  Here a
-thread pool decodes JPEGs for batch b+1 while the GPU runs batch b; each batch
+per RunNet with two host<->device copies per image (test.py:163-185).  Here
+decode processes (decode_pool, or threads) decode JPEGs for the next batches
+while the GPU runs batch b; each batch
 is one pinned-memory H2D copy of the raw uint8 pixels, then the preprocessing
 kernel (mean-subtract + bicubic), the ResNet-50 / PPS kernels and the
 normalisation run on the device, and features stay in HBM for the
@@ -29,6 +30,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
+from . import decode_pool
 from . import distributed as pdist
 from . import model as pmodel
 from . import native
@@ -68,22 +70,22 @@ def initialize_model_from_cfg(weights_file, gpu_id=0, trusted=False, blobs=None)
     return m
 
 
-def _decode_bgr(path):
-    """cv2.imread(path, IMREAD_COLOR) equivalent: uint8 HxWx3, BGR order."""
-    from PIL import Image
-    with Image.open(path) as im:
-        rgb = np.asarray(im.convert('RGB'), dtype=np.uint8)
-    return np.ascontiguousarray(rgb[..., ::-1])
+_decode_bgr = decode_pool.decode_bgr
 
 
 class BatchFeeder(object):
-    """Decode on CPU threads, stage raw pixels in pinned memory, one async H2D
+    """Decode on the host, stage raw pixels in pinned memory, one async H2D
     copy per batch, preprocess on the GPU.  `source(i)` returns image i as a
-    uint8 BGR array (a path list uses _decode_bgr)."""
+    uint8 BGR array (a path list uses _decode_bgr).  Given the image `paths`
+    and a running decode process pool (decode_pool.start), the decode runs in
+    those processes, `depth` batches ahead; otherwise on `workers` threads
+    one batch ahead (PIL holds the GIL for most of a small image's decode)."""
 
-    def __init__(self, source, n, batch, workers=8):
+    def __init__(self, source, n, batch, workers=8, paths=None, depth=4):
         self.source, self.n, self.batch = source, n, batch
-        self.pool = futures.ThreadPoolExecutor(max_workers=workers)
+        self.procs = decode_pool.pool() if paths is not None else None
+        self.paths, self.depth = paths, depth
+        self.pool = None if self.procs is not None else futures.ThreadPoolExecutor(max_workers=workers)
         self.H, self.W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
         self.means = np.asarray(cfg.PIXEL_MEANS, np.float32).ravel()
         self.copy_stream = torch.cuda.Stream()
@@ -91,6 +93,12 @@ class BatchFeeder(object):
     def _decode_batch(self, start):
         idx = range(start, min(start + self.batch, self.n))
         return list(self.pool.map(self.source, idx))
+
+    def _submit_procs(self, start):
+        ps = self.paths[start:min(start + self.batch, self.n)]
+        per = max(2, -(-len(ps) // max(1, decode_pool.workers())))
+        return self.procs.map_async(decode_pool.decode_many,
+                                    [ps[i:i + per] for i in range(0, len(ps), per)])
 
     def _stage(self, ims):
         sizes = [im.size for im in ims]
@@ -109,13 +117,26 @@ class BatchFeeder(object):
             done.record()
         return dblob, dmeta, done, blob, meta
 
-    def __iter__(self):
-        starts = list(range(0, self.n, self.batch))
+    def _decoded(self, starts):
+        """Decoded batches in order, the next ones already in flight."""
+        if self.procs is not None:
+            inflight = [self._submit_procs(s) for s in starts[:self.depth]]
+            for k in range(len(starts)):
+                chunks = inflight.pop(0).get()
+                if k + self.depth < len(starts):
+                    inflight.append(self._submit_procs(starts[k + self.depth]))
+                yield [im for c in chunks for im in c]
+            return
         pending = self.pool.submit(self._decode_batch, starts[0]) if starts else None
-        for k, s in enumerate(starts):
+        for k in range(len(starts)):
             ims = pending.result()
             if k + 1 < len(starts):
                 pending = self.pool.submit(self._decode_batch, starts[k + 1])
+            yield ims
+
+    def __iter__(self):
+        starts = list(range(0, self.n, self.batch))
+        for s, ims in zip(starts, self._decoded(starts)):
             dblob, dmeta, done, _hb, _hm = self._stage(ims)
             torch.cuda.current_stream().wait_event(done)
             offs = dmeta[0].contiguous()
@@ -130,15 +151,15 @@ class BatchFeeder(object):
             yield s, x
 
 
-def extract_features(model, source, n, batch=None, out=None, workers=8):
-    """Features [n, D] (device tensor) for images source(0..n-1), decoded on
-    `workers` host threads."""
+def extract_features(model, source, n, batch=None, out=None, workers=8, paths=None):
+    """Features [n, D] (device tensor) for images source(0..n-1): decoded by
+    the decode processes when `paths` is given and decode_pool.start() ran,
+    else on `workers` host threads."""
     batch = batch or int(cfg.TEST.get('IMS_PER_BATCH', 64))
     feats = out if out is not None else torch.empty((n, model.feat_dim),
                                                     dtype=torch.float32, device='cuda')
-    for s, x in BatchFeeder(source, n, batch, workers=workers):
-        f = model.forward(x)
-        feats[s:s + x.shape[0]].copy_(f)
+    for s, x in BatchFeeder(source, n, batch, workers=workers, paths=paths):
+        model.forward(x, out=feats[s:s + x.shape[0]])
     return feats
 
 
@@ -165,7 +186,7 @@ def test_net(weights_file, dataset_name, proposal_file, output_dir, ind_range=No
         model = initialize_model_from_cfg(weights_file, gpu_id, trusted=trusted)
     paths = [e['image'] for e in roidb]
     t0 = time.time()
-    feats = extract_features(model, lambda i: _decode_bgr(paths[i]), len(paths))
+    feats = extract_features(model, lambda i: _decode_bgr(paths[i]), len(paths), paths=paths)
     torch.cuda.synchronize()
     logger.info('im_detect: %d images in %.2fs (%.1f img/s)', len(paths),
                 time.time() - t0, len(paths) / max(time.time() - t0, 1e-9))
@@ -239,7 +260,8 @@ def multi_gpu_test_net_on_dataset(weights_file, dataset_name, output_dir, truste
         rows = np.nonzero(marks == m)[0]
         a, b = pdist.shard_range(len(rows), rank, world)
         sp = [paths[i] for i in rows[a:b]]
-        shards.append(extract_features(model, lambda i, sp=sp: _decode_bgr(sp[i]), len(sp)))
+        shards.append(extract_features(model, lambda i, sp=sp: _decode_bgr(sp[i]), len(sp),
+                                       paths=sp))
         rows_of.append(rows)
     # features in dataset order, written by rank 0 (test_engine.py:216-227):
     # gathered to rank 0 only

@@ -68,3 +68,27 @@ def test_bench_gpus_must_match_world_size():
     """Under a launcher (WORLD_SIZE set) --gpus must agree with it."""
     rc, lines, err = _bench(['--gpus', '4', '--dry-run'], env={'WORLD_SIZE': '2'})
     assert rc != 0 and not lines and '--gpus 4 but WORLD_SIZE=2' in err
+
+
+def test_decode_pool_matches_in_process_decode(tmp_path):
+    """The decode processes return exactly what decode_bgr returns in the
+    calling process (BGR uint8, source shapes kept), in order."""
+    from PIL import Image
+    from pps_amd import decode_pool
+    rng = np.random.RandomState(7)
+    paths = []
+    for i, (h, w) in enumerate([(128, 64), (97, 41), (128, 64), (200, 90), (64, 32)]):
+        p = str(tmp_path / ('%d.jpg' % i))
+        Image.fromarray(rng.randint(0, 256, (h, w, 3)).astype(np.uint8)).save(p, quality=90)
+        paths.append(p)
+    try:
+        pool = decode_pool.start(2)
+        assert decode_pool.workers() == 2 and decode_pool.start(3) is pool
+        got = [im for c in pool.map(decode_pool.decode_many, [paths[:2], paths[2:]]) for im in c]
+    finally:
+        decode_pool.stop()
+    assert decode_pool.pool() is None
+    for p, g in zip(paths, got):
+        want = decode_pool.decode_bgr(p)
+        assert g.dtype == np.uint8 and g.shape == want.shape and np.array_equal(g, want)
+    assert decode_pool.default_workers(share=1000) == 1

@@ -39,6 +39,11 @@ def main(argv=None):
         config.merge_cfg_from_list(args.opts)
     cfg = config.assert_and_infer_cfg()
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    # JPEG decode processes, forked from a server started before this process
+    # touches the GPU (pps_amd/decode_pool.py); the CPUs split over the ranks
+    from pps_amd import decode_pool
+    decode_pool.start(decode_pool.default_workers(
+        share=int(os.environ.get('LOCAL_WORLD_SIZE', world))))
     if world > 1:
         local = int(os.environ.get('LOCAL_RANK', '0'))
         torch.cuda.set_device(local)
