@@ -94,6 +94,19 @@ def main():
                 mfma_busy_frac=round(busy / (1024.0 * act), 4),
                 mfma_busy_frac_at_2p4GHz=round(busy / (1024.0 * dur * 2.4), 4),
                 source='rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (third pass)')
+        # the same for the last distance-matrix launch (the distmat roofline's
+        # kernel): its clock and MFMA-busy fraction
+        rows = [(nm, c, dur) for nm, c, dur in load_all(p3[0])
+                if is_gemm(nm) and epi_of(nm) == 1 and 'GRBM_GUI_ACTIVE' in c][-1:]
+        if rows:
+            nm, c, dur = rows[0]
+            act = c['GRBM_GUI_ACTIVE'] / 8.0
+            busy = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0)
+            out['distmat_mfma'] = dict(
+                math=math, duration_us=round(dur / 1e3, 1), clock_GHz=round(act / dur, 3),
+                mfma_busy_frac=round(busy / (1024.0 * act), 4),
+                mfma_busy_frac_at_2p4GHz=round(busy / (1024.0 * dur * 2.4), 4),
+                source='rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (third pass)')
     print(json.dumps(out, indent=1))
 
 

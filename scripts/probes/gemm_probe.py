@@ -27,6 +27,7 @@ LAYERS = {
     'res4c': (64, 24, 8, 256, 1024, 1, 1, 0),
     'res4a': (64, 24, 8, 1024, 256, 1, 1, 0),
     'res2a': (64, 96, 32, 256, 64, 1, 1, 0),
+    'res3a': (64, 48, 16, 512, 128, 1, 1, 0),
     'stemgemm': (64, 192, 64, 224, 64, 1, 1, 0),  # the stem as a plain K=224 GEMM
     # full-chip shapes (thousands of tiles): the kernel's own ceiling
     'big3x3': (64, 64, 64, 512, 512, 3, 1, 1),
