@@ -254,6 +254,15 @@ int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2);
 int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
                    int64_t G, int k1, int k2, double lambda_value, void* workspace,
                    int64_t ws_bytes, float* out, void* stream);
+/* The same with flags.  PPS_RERANK_SYMMETRIC: the caller guarantees q_q and
+ * g_g are exactly symmetric (q_q[a][b] == q_q[b][a] bit for bit -- e.g. both
+ * from the mirrored self-distance GEMM, pps_distmat_x3_self), so the N x N
+ * matrix is built from M's rows and only its q_g^T block is transposed.  Same
+ * result as pps_re_ranking on such inputs. */
+#define PPS_RERANK_SYMMETRIC 1
+int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                         int64_t G, int k1, int k2, double lambda_value, int flags,
+                         void* workspace, int64_t ws_bytes, float* out, void* stream);
 
 /* ---- feature extractor ----------------------------------------------------
  * Implicit-GEMM convolution + test-mode SpatialBN + optional residual Sum +

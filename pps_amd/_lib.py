@@ -88,6 +88,8 @@ SIGNATURES = {
                                     c_ptr, c_ptr],
     'pps_re_ranking': [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int, ctypes.c_double,
                        c_ptr, c_i64, c_ptr, c_ptr],
+    'pps_re_ranking_flags': [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int, ctypes.c_double,
+                             c_int, c_ptr, c_i64, c_ptr, c_ptr],
     'pps_stem_conv_pool_x3': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
                               c_int, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,

@@ -52,7 +52,7 @@ int rank_count_stream(const float*, int64_t, int64_t, int64_t, int64_t, int, con
                       const int32_t*, const int32_t*, const int32_t*, int, const float*,
                       const int32_t*, const int32_t*, int32_t*, int32_t*, hipStream_t);
 int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int, double,
-           void*, size_t, float*, hipStream_t);
+           void*, size_t, float*, hipStream_t, int);
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
 int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
                             const float*, int, int, float*, hipStream_t);
@@ -399,9 +399,9 @@ int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   return (int64_t)rerank_workspace_bytes(Q, G, k1, k2);
 }
 
-int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
-                   int64_t G, int k1, int k2, double lambda_value, void* workspace,
-                   int64_t ws_bytes, float* out, void* stream) {
+int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                         int64_t G, int k1, int k2, double lambda_value, int flags,
+                         void* workspace, int64_t ws_bytes, float* out, void* stream) {
   PPS_ENFORCE(q_g && q_q && g_g && workspace && out, "null pointer");
   PPS_ENFORCE(Q > 0 && G > 0, "bad shape");
   PPS_ENFORCE(k1 >= 1 && k1 + 1 <= 64, "k1 + 1 must be <= 64");
@@ -411,9 +411,17 @@ int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t
   PPS_ENFORCE(k2 * (K1 + K1 * Kh <= 256 ? 256 : (K1 + K1 * Kh <= 512 ? 512 : 1024)) <= 4096,
               "k2 * V row capacity must be <= 4096");
   PPS_ENFORCE((Q + G) * 4 <= 160 * 1024, "Q + G must be <= 40960 (LDS accumulator)");
-  PPS_ENFORCE(Q + G <= Q + G && (Q + G) >= K1, "need Q + G >= k1 + 1");
+  PPS_ENFORCE((Q + G) >= K1, "need Q + G >= k1 + 1");
+  PPS_ENFORCE((flags & ~PPS_RERANK_SYMMETRIC) == 0, "unknown re-ranking flags");
   return rerank(q_g, q_q, g_g, Q, G, k1, k2, lambda_value, workspace, (size_t)ws_bytes, out,
-                as_stream(stream));
+                as_stream(stream), flags);
+}
+
+int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                   int64_t G, int k1, int k2, double lambda_value, void* workspace,
+                   int64_t ws_bytes, float* out, void* stream) {
+  return pps_re_ranking_flags(q_g, q_q, g_g, Q, G, k1, k2, lambda_value, 0, workspace,
+                              ws_bytes, out, stream);
 }
 
 // weights either f32 [Cout][Kpad] (x3 = 0) or bf16x3 planes [3][Cout][Kpad]

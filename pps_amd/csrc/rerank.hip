@@ -97,11 +97,13 @@ template <int T>
 __global__ void __launch_bounds__(256)
 rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
                        const float* __restrict__ gg, int64_t Q, int64_t G,
-                       const float* __restrict__ colmax, float* __restrict__ od, int64_t ldo) {
+                       const float* __restrict__ colmax, float* __restrict__ od, int64_t ldo,
+                       int64_t i_min, int64_t j_max) {
+  // writes OD[i][j] for i >= i_min, j < j_max (tiles cover that window)
   constexpr int H = T / 64;
   __shared__ float tile[T][T + 1];
   const int64_t N = Q + G;
-  const int64_t i0 = blockIdx.y * (int64_t)T, j0 = blockIdx.x * (int64_t)T;
+  const int64_t i0 = (i_min / T) * T + blockIdx.y * (int64_t)T, j0 = blockIdx.x * (int64_t)T;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: ty 0..3
   if (i0 + T <= Q && j0 >= Q) {
     // query rows x gallery columns: M[j][i] = qg[i][j - Q], i.e. OD here is
@@ -113,7 +115,7 @@ rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ q
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         const int64_t j = j0 + tx + 64 * h;
-        if (j < N) {
+        if (j < N && j < j_max && i >= i_min) {
           const float m = qg[i * G + (j - Q)];
           od[i * ldo + j] = (m * m) / cm;
         }
@@ -137,13 +139,49 @@ rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ q
   __syncthreads();
   for (int k = ty; k < T; k += 4) {  // write OD[i0+k][j0+tx..] = tile[tx..][k] / colmax
     const int64_t i = i0 + k;
-    if (i >= N) continue;
+    if (i >= N || i < i_min) continue;
     const float cm = colmax[i];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const int64_t j = j0 + tx + 64 * h;
-      if (j < N) od[i * ldo + j] = tile[tx + 64 * h][k] / cm;
+      if (j < N && j < j_max) od[i * ldo + j] = tile[tx + 64 * h][k] / cm;
     }
+  }
+}
+
+// Symmetric q_q and g_g (both self-distances from the mirrored GEMM, exactly
+// symmetric): M is symmetric, so OD[i][j] = M[j][i]^2 / colmax[i] =
+// M[i][j]^2 / colmax[i] is a row-major scaled copy of M's rows -- except the
+// block i >= Q, j < Q, which is qg^T and keeps the tiled transpose above.
+// One block streams kOdRowChunk entries of one OD row, 8 loads in flight per
+// thread; same arithmetic (m * m, then / colmax) as the transposing kernel.
+constexpr int kOdRowChunk = 2048;
+__global__ void __launch_bounds__(256)
+rerank_build_od_rows_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
+                            const float* __restrict__ gg, int64_t Q, int64_t G,
+                            const float* __restrict__ colmax, float* __restrict__ od,
+                            int64_t ldo) {
+  const int64_t N = Q + G;
+  const int64_t i = blockIdx.y;
+  // row i's sources: [0, Q) from qq (i < Q) -- none for i >= Q (qg^T, tiled
+  // kernel); [Q, N) from qg (i < Q) or gg (i >= Q)
+  const int64_t jlo = i < Q ? 0 : Q;
+  const int64_t j0 = jlo + blockIdx.x * (int64_t)kOdRowChunk;
+  if (j0 >= N) return;
+  const float cm = colmax[i];
+  float* orow = od + i * ldo;
+  float m[kOdRowChunk / 256];
+#pragma unroll
+  for (int u = 0; u < kOdRowChunk / 256; ++u) {
+    const int64_t j = j0 + u * 256 + threadIdx.x;
+    m[u] = 0.f;
+    if (j < N)
+      m[u] = j < Q ? qq[i * Q + j] : (i < Q ? qg[i * G + (j - Q)] : gg[(i - Q) * G + (j - Q)]);
+  }
+#pragma unroll
+  for (int u = 0; u < kOdRowChunk / 256; ++u) {
+    const int64_t j = j0 + u * 256 + threadIdx.x;
+    if (j < N) orow[j] = (m[u] * m[u]) / cm;
   }
 }
 
@@ -250,41 +288,55 @@ __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, i
                                   int32_t* __restrict__ q_cnt) {
   __shared__ unsigned long long key[kQeCap];  // (column << 32) | (t << 16) | slot
   __shared__ float val[kQeCap];
-  __shared__ int s_n;
+  __shared__ int32_t lc[kQeCap];              // the k2 rows' columns, concatenated
+  __shared__ int s_off[65], s_row[64];
   const int64_t i = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) s_n = 0;
-  __syncthreads();
-  for (int t = 0; t < k2; ++t) {
-    const int r = rank[i * K1 + t];
-    const int c = min(v_cnt[r], vcap);
-    const int base = s_n;
-    for (int e = tid; e < c; e += nt) {
-      if (base + e < kQeCap) {
-        key[base + e] = ((unsigned long long)(uint32_t)v_idx[(int64_t)r * vcap + e] << 32) |
-                        ((unsigned long long)t << 16) | (unsigned)(base + e);
-        val[base + e] = v_val[(int64_t)r * vcap + e];
-      }
+  if (tid == 0) {
+    int o = 0;
+    for (int t = 0; t < k2; ++t) {
+      const int r = rank[i * K1 + t];
+      s_row[t] = r;
+      s_off[t] = o;
+      o += min(v_cnt[r], vcap);
     }
-    __syncthreads();
-    if (tid == 0) s_n = base + c;
-    __syncthreads();
+    s_off[k2] = o;
   }
-  const int n = min(s_n, kQeCap);
-  int n2 = 1;
-  while (n2 < n) n2 <<= 1;
-  for (int e = n + tid; e < n2; e += nt) key[e] = ~0ull;
   __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int e = tid; e < n2 / 2; e += nt) {
-        const int a = 2 * stride * (e / stride) + (e % stride), b = a + stride;
-        const bool up = (a & size) == 0;
-        const unsigned long long x = key[a], y = key[b];
-        if ((x > y) == up) { key[a] = y; key[b] = x; }
+  const int n = min(s_off[k2], kQeCap);
+  auto list_of = [&](int e) {   // the row t holding concatenated entry e
+    int t = 0;
+    while (t + 1 < k2 && s_off[t + 1] <= e) ++t;
+    return t;
+  };
+  for (int e = tid; e < n; e += nt) {
+    const int t = list_of(e);
+    lc[e] = v_idx[(int64_t)s_row[t] * vcap + (e - s_off[t])];
+  }
+  __syncthreads();
+  // Each V row is sorted by column (np.unique), so the (column, t) order of
+  // all entries is a k2-way merge: an entry's position is its index in its
+  // own row plus, in every other row t2, the entries with a smaller column
+  // (or the same column and t2 < t) -- binary searches in LDS, no sort.
+  for (int e = tid; e < n; e += nt) {
+    const int t = list_of(e);
+    const int32_t c = lc[e];
+    int pos = e - s_off[t];
+    for (int t2 = 0; t2 < k2; ++t2) {
+      if (t2 == t) continue;
+      int lo = s_off[t2], hi = min(s_off[t2 + 1], n);
+      while (lo < hi) {   // first entry of row t2 with column > c (t2 < t) / >= c (t2 > t)
+        const int mid = (lo + hi) >> 1;
+        const bool before = t2 < t ? lc[mid] <= c : lc[mid] < c;
+        if (before) lo = mid + 1; else hi = mid;
       }
-      __syncthreads();
+      pos += lo - s_off[t2];
     }
+    key[pos] = ((unsigned long long)(uint32_t)c << 32) | ((unsigned long long)t << 16) |
+               (unsigned)pos;
+    val[pos] = v_val[(int64_t)s_row[t] * vcap + (e - s_off[t])];
+  }
+  __syncthreads();
   // segmented sums per column in row order t (key order), then / k2.  Each
   // thread owns a contiguous run of entries; a segment is summed left to
   // right by the thread owning its first entry (the serial order), at the
@@ -416,7 +468,8 @@ __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restr
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
 
 int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t G, int k1,
-           int k2, double lambda, void* ws, size_t ws_bytes, float* out, hipStream_t st) {
+           int k2, double lambda, void* ws, size_t ws_bytes, float* out, hipStream_t st,
+           int flags) {
   // NumPy (NEP 50) casts the Python-float factors to float32: lambda and 1-lambda
   const float lam = (float)lambda, one_m_lam = (float)(1.0 - lambda);
   const int64_t N = Q + G;
@@ -469,9 +522,21 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
                      cm);       // columns c < Q: rows r >= Q (qg^T)
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
   constexpr int T = PPS_OD_TILE;
-  hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((N + T - 1) / T),
-                                                     (unsigned)((N + T - 1) / T)),
-                     dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo);
+  if (flags & PPS_RERANK_SYMMETRIC) {
+    // rows streamed from M's rows; only the qg^T block (i >= Q, j < Q) is
+    // transposed
+    hipLaunchKernelGGL(rerank_build_od_rows_kernel,
+                       dim3((unsigned)((N + kOdRowChunk - 1) / kOdRowChunk), (unsigned)N),
+                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo);
+    PPS_CHECK_LAUNCH_S("rerank_build_od_rows_kernel", st);
+    const int64_t ti = (N + T - 1) / T - Q / T;   // row tiles covering [Q, N)
+    hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((Q + T - 1) / T), (unsigned)ti),
+                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo, Q, Q);
+  } else {
+    hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((N + T - 1) / T),
+                                                       (unsigned)((N + T - 1) / T)),
+                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo, (int64_t)0, N);
+  }
   PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
   int rc = topk(od, N, N, ldo, K1, topv, rank, st);
   if (rc != PPS_OK) return rc;

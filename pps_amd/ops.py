@@ -167,6 +167,7 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
         call('pps_distmat_x3_self', _dev(q, 'x'), Q, D, _dev(idx.sqnorm, 'xsq'),
              _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric],
              _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
+        out._pps_symmetric = True   # mirrored tiles: exactly symmetric (re_ranking uses it)
         return out
     if q_planes:
         q3, qsq = split_sqnorm(q) if q.is_contiguous() else (split_bf16x3(q), row_sqnorm(q))
@@ -404,18 +405,29 @@ def ap_finalize(sorted_d, pos_total, hist, before):
     return ap, valid, first
 
 
-def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3):
-    """k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519) -> [Q, G]."""
+def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None):
+    """k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519) -> [Q, G].
+    symmetric: q_q and g_g are exactly symmetric (PPS_RERANK_SYMMETRIC: the
+    N x N matrix is built from rows, only q_g^T is transposed); None = both
+    came from compute_dist's mirrored self-distance (tagged
+    `_pps_symmetric`).  Same result either way on symmetric inputs."""
     Q, G = q_g.shape
     assert tuple(q_q.shape) == (Q, Q) and tuple(g_g.shape) == (G, G)
+    if symmetric is None:
+        symmetric = bool(getattr(q_q, '_pps_symmetric', False) and
+                         getattr(g_g, '_pps_symmetric', False))
     nbytes = _lib.lib().pps_rerank_workspace_bytes(Q, G, k1, k2)
     if nbytes < 0:
         raise RuntimeError('bad re-ranking arguments')
     ws = torch.empty((int(nbytes),), dtype=torch.uint8, device=q_g.device)
     out = torch.empty((Q, G), dtype=torch.float32, device=q_g.device)
-    call('pps_re_ranking', _dev(q_g, 'q_g'), _dev(q_q, 'q_q'), _dev(g_g, 'g_g'), Q, G, k1, k2,
-         float(lambda_value), ws.data_ptr(), int(nbytes), out.data_ptr(), _stream())
+    call('pps_re_ranking_flags', _dev(q_g, 'q_g'), _dev(q_q, 'q_q'), _dev(g_g, 'g_g'), Q, G,
+         k1, k2, float(lambda_value), RERANK_SYMMETRIC if symmetric else 0, ws.data_ptr(),
+         int(nbytes), out.data_ptr(), _stream())
     return out
+
+
+RERANK_SYMMETRIC = 1   # pps_abi.h PPS_RERANK_SYMMETRIC
 
 
 def max_positives(qid, qcam, gid, gcam):

@@ -60,7 +60,7 @@ def main():
         g_g = ops.compute_dist(gf, gf, metric='cosine')
         mark('g_g')
         e[2].record()
-        rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+        rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)   # q_q, g_g mirrored: symmetric path
         e[3].record()
         mark('re_ranking')
         res = gev.rank_eval(rr, qid, gid, qcam, gcam)
@@ -95,7 +95,8 @@ def main():
                       'synthetic features' % (Q, G, D),
                math=ops.default_math(), mAP_plain=round(mAP0, 6), cmc1_plain=round(float(cmc0[0]), 6),
                mAP_reranked=round(mAP, 6), cmc1_reranked=round(float(cmc[0]), 6),
-               gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr)
+               gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr,
+               rerank_symmetric=bool(getattr(g_g, '_pps_symmetric', False)))
     print(json.dumps(out), flush=True)
 
 

@@ -257,6 +257,30 @@ def test_re_ranking_vs_oracle_params(k1, k2):
     np.testing.assert_allclose(rr, ref, rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize('Q,G,metric', [(300, 1700, 'cosine'), (77, 2100, 'euclidean')])
+def test_re_ranking_symmetric_path_bit_identical(Q, G, metric):
+    """PPS_RERANK_SYMMETRIC (row-streamed N x N build, only q_g^T transposed)
+    gives the same bits as the transposing build on the mirrored self-distance
+    GEMM's exactly symmetric q_q / g_g, and both match the oracle."""
+    from pps_amd import ops
+    rng = np.random.RandomState(Q)
+    x = rng.randn(Q + G, 64).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    xd = torch.from_numpy(x).cuda()
+    q, g = xd[:Q].contiguous(), xd[Q:].contiguous()
+    qg = ops.compute_dist(q, g, metric=metric)
+    qq = ops.compute_dist(q, q, metric=metric)
+    gg = ops.compute_dist(g, g, metric=metric)
+    assert getattr(qq, '_pps_symmetric', False) and getattr(gg, '_pps_symmetric', False)
+    assert torch.equal(gg, gg.t()) and torch.equal(qq, qq.t())
+    sym = ops.re_ranking(qg, qq, gg)
+    asym = ops.re_ranking(qg, qq, gg, symmetric=False)
+    assert torch.equal(sym, asym)
+    ref = ev.re_ranking(qg.cpu().numpy(), qq.cpu().numpy(), gg.cpu().numpy(), k1=20, k2=6,
+                        lambda_value=0.3)
+    np.testing.assert_allclose(sym.cpu().numpy(), ref, rtol=0, atol=1e-5)
+
+
 def test_evaluate_with_rerank_vs_oracle(golden):
     from pps_amd import reid_dataset_evaluator as gev
     from pps_amd.config import cfg
