@@ -60,7 +60,8 @@ const char* pps_registered_ops(void);
  * 4 x 2) with three LDS stages, 53 = tile 50 with three stages, all on
  * 16x16x32 blocks; 54 = the weight-stationary persistent kernel for 1x1
  * convs with K = 64 / 128 / 256 (stationary weight columns in LDS,
- * activations streamed to registers; other shapes run tile 38).  Results
+ * activations streamed to registers; other shapes run tile 38); 55 = 64x128
+ * (8 waves, 2 x 4, four LDS stages: short-M split-K head GEMMs).  Results
  * are identical for every tile below 38 (same per-element fp32 MFMA
  * accumulation order) and identical among the tiles from 38 on (one MFMA
  * sums a 32-wide K chunk: a different rounding

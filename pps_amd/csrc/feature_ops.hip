@@ -228,6 +228,9 @@ __global__ void splitk_bn_act_normalize_kernel(const float* __restrict__ part, i
 
 // Vectorised single-pass form for N % 4 == 0, N <= 4096: one float4 column
 // group per thread, kept in registers between the norm and the scaling.
+// SC > 0: the slice count as a constant, so all SC partial loads are issued
+// before the first add (a runtime-count loop waits for each load in turn).
+template <int SC>
 __global__ void __launch_bounds__(1024)
 splitk_bn_act_normalize_v4_kernel(const float* __restrict__ part, int S, int64_t sstride,
                                   int N, const float* __restrict__ scale,
@@ -238,9 +241,20 @@ splitk_bn_act_normalize_v4_kernel(const float* __restrict__ part, int S, int64_t
   const bool on = j < N;
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (on) {
-    v = *reinterpret_cast<const f32x4*>(part + m * N + j);
-    for (int s = 1; s < S; ++s)
-      v += *reinterpret_cast<const f32x4*>(part + s * sstride + m * N + j);
+    if constexpr (SC > 0) {
+      f32x4 ps[SC];
+#pragma unroll
+      for (int s = 0; s < SC; ++s)
+        ps[s] = __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(part + s * sstride + m * N + j));
+      v = ps[0];
+#pragma unroll
+      for (int s = 1; s < SC; ++s) v += ps[s];
+    } else {
+      v = *reinterpret_cast<const f32x4*>(part + m * N + j);
+      for (int s = 1; s < S; ++s)
+        v += *reinterpret_cast<const f32x4*>(part + s * sstride + m * N + j);
+    }
     const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + j);
     const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + j);
 #pragma unroll
@@ -276,8 +290,12 @@ int splitk_bn_act_normalize(const float* part, int S, int64_t sstride, int M, in
                                    reinterpret_cast<uintptr_t>(scale) |
                                    reinterpret_cast<uintptr_t>(shift)) & 15) == 0) {
     const int threads = ((N / 4 + 63) / 64) * 64;
-    hipLaunchKernelGGL(splitk_bn_act_normalize_v4_kernel, dim3(M), dim3(threads), 0, st,
-                       part, S, sstride, N, scale, shift, relu, normalize, y);
+    if (S == 8)
+      hipLaunchKernelGGL(splitk_bn_act_normalize_v4_kernel<8>, dim3(M), dim3(threads), 0, st,
+                         part, S, sstride, N, scale, shift, relu, normalize, y);
+    else
+      hipLaunchKernelGGL(splitk_bn_act_normalize_v4_kernel<0>, dim3(M), dim3(threads), 0, st,
+                         part, S, sstride, N, scale, shift, relu, normalize, y);
     PPS_CHECK_LAUNCH("splitk_bn_act_normalize_v4_kernel");
     return PPS_OK;
   }

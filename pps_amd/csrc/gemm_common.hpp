@@ -35,6 +35,32 @@ __device__ inline u32x2 bload64(rsrc_t r, int byte_off) {
   return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
 }
 
+// Cache policy of the layer-output stores (vector stores only): 0 plain,
+// 1 nt, 2 sc1 (write-through: the line leaves the XCD's L2, so the kernel
+// ends with little dirty L2 to write back at its boundary).
+#ifndef PPS_STPOL
+#define PPS_STPOL 0
+#endif
+constexpr int kStAux = PPS_STPOL == 1 ? 2 : PPS_STPOL == 2 ? 16 : 0;  // gfx950 CPol bits
+__device__ inline void st_out4(float* p, f32x4 v) {
+  if constexpr (PPS_STPOL == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  } else if constexpr (PPS_STPOL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *reinterpret_cast<f32x4*>(p) = v;
+  }
+}
+__device__ inline void st_out2(void* p, u32x2 v) {
+  if constexpr (PPS_STPOL == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+  } else if constexpr (PPS_STPOL == 2) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *reinterpret_cast<u32x2*>(p) = v;
+  }
+}
+
 // XCD-aware bijective remap of the flat block id: the hardware deals blocks
 // round-robin over the 8 XCDs; renumber so consecutive tiles (which share an
 // A panel) run on the same XCD / L2.

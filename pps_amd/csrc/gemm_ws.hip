@@ -189,7 +189,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
         if (HAS_RES) v[e] += o.r[it][e];
         if (RELU) v[e] = fmaxf(v[e], 0.f);
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, kStAux);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next park
   };

@@ -66,7 +66,28 @@ __device__ inline f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32
 __device__ inline f32x4 mfma16_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+#ifndef PPS_X3_ORDER
+#define PPS_X3_ORDER 0  // probes: 1 / 2 = weight- / activation-plane-major term order
+#endif
 __device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  if constexpr (PPS_X3_ORDER == 1) {
+    c = mfma16_bf16(b[0], a[0], c);
+    c = mfma16_bf16(b[0], a[1], c);
+    c = mfma16_bf16(b[0], a[2], c);
+    c = mfma16_bf16(b[1], a[0], c);
+    c = mfma16_bf16(b[1], a[1], c);
+    c = mfma16_bf16(b[2], a[0], c);
+    return c;
+  }
+  if constexpr (PPS_X3_ORDER == 2) {
+    c = mfma16_bf16(b[0], a[0], c);
+    c = mfma16_bf16(b[1], a[0], c);
+    c = mfma16_bf16(b[2], a[0], c);
+    c = mfma16_bf16(b[0], a[1], c);
+    c = mfma16_bf16(b[1], a[1], c);
+    c = mfma16_bf16(b[0], a[2], c);
+    return c;
+  }
   c = mfma16_bf16(b[0], a[0], c);
   c = mfma16_bf16(b[0], a[1], c);
   c = mfma16_bf16(b[1], a[0], c);

@@ -51,6 +51,24 @@ __device__ inline void wait_vmcnt() {
 // moves 16-byte vectors (4 stores per block instead of 16).  Same products,
 // same term order.
 __device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  if constexpr (PPS_X3_ORDER == 1) {
+    c = mfma_bf16(b[0], a[0], c);
+    c = mfma_bf16(b[0], a[1], c);
+    c = mfma_bf16(b[0], a[2], c);
+    c = mfma_bf16(b[1], a[0], c);
+    c = mfma_bf16(b[1], a[1], c);
+    c = mfma_bf16(b[2], a[0], c);
+    return c;
+  }
+  if constexpr (PPS_X3_ORDER == 2) {
+    c = mfma_bf16(b[0], a[0], c);
+    c = mfma_bf16(b[1], a[0], c);
+    c = mfma_bf16(b[2], a[0], c);
+    c = mfma_bf16(b[0], a[1], c);
+    c = mfma_bf16(b[1], a[1], c);
+    c = mfma_bf16(b[0], a[2], c);
+    return c;
+  }
   c = mfma_bf16(b[0], a[0], c);
   c = mfma_bf16(b[0], a[1], c);
   c = mfma_bf16(b[1], a[0], c);
@@ -137,11 +155,11 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
           split2(v[0], v[1], h0, m0_, l0);
           split2(v[2], v[3], h1, m1, l1);
           uint16_t* o = out3 + rr * ldo + cb + 8 * q;
-          *reinterpret_cast<u32x2*>(o) = (u32x2){h0, h1};
-          *reinterpret_cast<u32x2*>(o + p.out_plane) = (u32x2){m0_, m1};
-          *reinterpret_cast<u32x2*>(o + 2 * p.out_plane) = (u32x2){l0, l1};
+          st_out2(o, (u32x2){h0, h1});
+          st_out2(o + p.out_plane, (u32x2){m0_, m1});
+          st_out2(o + 2 * p.out_plane, (u32x2){l0, l1});
         } else {
-          *reinterpret_cast<f32x4*>(out + rr * ldo + cb + 8 * q) = v;
+          st_out4(out + rr * ldo + cb + 8 * q, v);
         }
       }
     }
@@ -245,9 +263,9 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       }
       if (PPS) {  // the pooling below reads the tile back from LDS
         *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
-        if (p.pps_write_y) *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+        if (p.pps_write_y) st_out4(out + row * ldo + col, v);
       } else {
-        *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+        st_out4(out + row * ldo + col, v);
       }
     };
     if constexpr (PRE) {
@@ -1151,6 +1169,7 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 // Rows (BM) of the tile a pipelined id launches (as launch_variant /
 // launch_gemm_x3p map it), 0 for a non-pipelined id.
 int x3p_tile_rows(int tile, bool a3) {
+  if (tile == GEMM_TILE_P16_64x128W24S4) return 64;
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41 ||
       tile == GEMM_TILE_P16_192x128W42S3)
@@ -1174,6 +1193,7 @@ int x3p_tile_rows(int tile, bool a3) {
 
 // Columns (BN) of that tile.
 int x3p_tile_cols(int tile, bool a3) {
+  if (tile == GEMM_TILE_P16_64x128W24S4) return 128;
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
       tile == GEMM_TILE_P16_96x128W24 || tile == GEMM_TILE_P16_128x128W42S3 ||
@@ -1208,13 +1228,20 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
   // the 8-wave 128x128 / 192x128 tiles, for long-K GEMMs whose operands come
   // from the Infinity Cache rather than L2 (distance matrix, res5);
   // 192-row plane A keeps two stages (uneven pieces)
+#ifndef X3P_DEEP
+#define X3P_DEEP 0  // probes: 1 = four LDS stages for f32 A on tiles 51 / 53
+#endif
   if (variant == GEMM_TILE_P16_128x128W42S3 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<128, 128, 4, 2, 3, 3, 16>(p, epi, batch, stream);
+    return launch_tile_p<128, 128, 4, 2, X3P_DEEP ? 4 : 3, 3, 16>(p, epi, batch, stream);
   if (variant == GEMM_TILE_P16_192x128W42S3 - GEMM_TILE_P_FIRST)
     return launch_tile_p<192, 128, 4, 2, 3, 2, 16>(p, epi, batch, stream);
   // 96x128 as 2 x 4 waves with three stages (uneven pieces, per-wave waits)
   if (variant == GEMM_TILE_P16_96x128W24S3 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<96, 128, 2, 4, 3, 3, 16>(p, epi, batch, stream);
+    return launch_tile_p<96, 128, 2, 4, X3P_DEEP ? 4 : 3, 3, 16>(p, epi, batch, stream);
+  // 64x128, 8 waves as 2 x 4, four stages (three chunks in flight): the
+  // 64-row split-K head GEMMs, whose 8-chunk slices are all pipeline fill
+  if (variant == GEMM_TILE_P16_64x128W24S4 - GEMM_TILE_P_FIRST)
+    return launch_tile_p<64, 128, 2, 4, 4, 4, 16>(p, epi, batch, stream);
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }

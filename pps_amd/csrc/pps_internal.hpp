@@ -99,7 +99,10 @@ enum GemmTile {
   // (gemm_ws.hip) for 1x1 convs with K = 64 / 128 / 256; other shapes run
   // tile 38
   GEMM_TILE_WS = 54,
-  GEMM_NUM_TILES = 55
+  // 55 (16x16x32): 64x128 with 8 waves as 2 x 4 and four LDS stages -- short
+  // M (the 64-row head GEMMs: 248 split-K workgroups, three chunks in flight)
+  GEMM_TILE_P16_64x128W24S4 = 55,
+  GEMM_NUM_TILES = 56
 };
 
 struct GemmParams {
