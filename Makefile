@@ -13,7 +13,7 @@ all: $(LIB)
 # scalar (SLP-packed v_pk_add_f32 issues at half rate beside MFMAs)
 build/gemm_x3p.o: HIPFLAGS += -fno-slp-vectorize
 
-build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp pps_amd/csrc/gemm_common.hpp pps_amd/csrc/gemm_x3_common.hpp include/pps_abi.h
+build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp pps_amd/csrc/gemm_common.hpp pps_amd/csrc/gemm_x3_common.hpp pps_amd/csrc/gemm_x3p_common.hpp include/pps_abi.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -277,6 +277,13 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     q.tile = GEMM_TILE_P16_FIRST;
     return launch_gemm_x3(q, epi_in, batch, stream);
   }
+  if (p.tile >= GEMM_TILE_C16_FIRST) {
+    // patch-staged 3x3 tiles where they apply, else tile 38
+    if (x3c_eligible(p, epi, batch, p.tile)) return launch_gemm_x3c(p, epi, stream, p.tile);
+    GemmParams q = p;
+    q.tile = GEMM_TILE_P16_FIRST;
+    return launch_gemm_x3(q, epi_in, batch, stream);
+  }
   if (p.ksplit_conv && (p.tile < GEMM_TILE_P_FIRST || !x3p_eligible(p, epi))) {
     set_error("conv split-K runs on the pipelined tiles only (tile >= " +
               std::to_string((int)GEMM_TILE_P_FIRST) + ", Cin % 32 == 0)");

@@ -1209,7 +1209,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
           L.splitk = sk;
           w = &workspace(*m, N, st, true);  // grow the partials buffer
           L.splitk = save;
-          for (int tl = GEMM_TILE_P_FIRST; tl < GEMM_NUM_TILES; ++tl)
+          for (int tl = GEMM_TILE_P_FIRST; tl < GEMM_TILE_C16_FIRST; ++tl)  // not 3x3-patch ids
             screen.push_back({time_layer(*m, L, *w, x, tl, sk, reps, st, t), {tl, sk}});
         }
         if (screen.empty()) continue;

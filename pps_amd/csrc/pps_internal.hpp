@@ -102,7 +102,14 @@ enum GemmTile {
   // 55 (16x16x32): 64x128 with 8 waves as 2 x 4 and four LDS stages -- short
   // M (the 64-row head GEMMs: 248 split-K workgroups, three chunks in flight)
   GEMM_TILE_P16_64x128W24S4 = 55,
-  GEMM_NUM_TILES = 56
+  // 56..58 (16x16x32, own rounding group: K in (channel chunk, tap) order):
+  // patch-staged stride-1 3x3 convs (gemm_x3c.hip) -- 192x128 (8 waves),
+  // 192x64 (4 waves), 96x128 (8 waves); other shapes run tile 38
+  GEMM_TILE_C16_FIRST = 56,
+  GEMM_TILE_C16_192x128 = 56,
+  GEMM_TILE_C16_192x64 = 57,
+  GEMM_TILE_C16_96x128 = 58,
+  GEMM_NUM_TILES = 59
 };
 
 struct GemmParams {
@@ -192,6 +199,10 @@ int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3
 int pick_tile(const GemmParams& p, int batch);
 bool ws_eligible(const GemmParams& p, int epi, int batch);
 int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream);
+bool x3c_eligible(const GemmParams& p, int epi, int batch, int tile);
+int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
+int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
+int x3c_tile_cols(int tile);
 
 // ---- retrieval (rank.hip) ---------------------------------------------------
 constexpr int kMergeMaxLists = 64;
