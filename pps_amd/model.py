@@ -733,7 +733,7 @@ class PPSModel(object):
         if self.math == 'x3' and splitk:
             # split-K (conv_bn_act_x3p_splitk) where it beats the one-pass
             # kernel by > 2 % -- the res5 3x3/1x1 layers at batch 64
-            ptiles = [t for t in cands if t >= ops.TILE_P_FIRST]
+            ptiles = [t for t in cands if ops.TILE_P_FIRST <= t < ops.TILE_C16_FIRST]
 
             def time_split(L, t, sk, n):
                 bufs = dict(self._bufs)

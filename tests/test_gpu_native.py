@@ -121,7 +121,8 @@ def test_native_autotune_then_python_twin():
     _, pm, nm = _models(seed=1)
     _, x = _input(2, seed=2)
     tiles = nm.autotune(x)
-    assert all(0 <= t <= 53 for t in tiles.values())
+    from pps_amd import ops
+    assert all(0 <= t <= ops.num_tiles() for t in tiles.values())
     assert any(t != 0 for t in tiles.values())
     pm.set_tiles(tiles)
     pm.set_planes(nm.planes())
