@@ -325,7 +325,9 @@ def conv_roofline(nm, x, reps=20):
            for L, t in zip(layers, eager)}
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if nm.math == 'x3':
-        peak, kernel = PEAK_X3_TFLOPS, ('gemm_x3p_kernel<*> (LDS-DMA pipelined; gemm_x3_kernel where autotune prefers it) implicit-GEMM conv + the fused stem (stem_ring_x3_kernel), f32 products as 6 '
+        peak, kernel = PEAK_X3_TFLOPS, ('implicit-GEMM conv: gemm_x3p_kernel<*> (LDS-DMA pipelined), gemm_x3c_kernel<*> (3x3 '
+                                        'from LDS input patches), gemm_ws_kernel<*> (weight-stationary 1x1), per-layer autotune; '
+                                        '+ the fused stem (stem_ring_x3_kernel); f32 products as 6 '
                                         'bf16 MFMA terms (%d launches/forward, run by pps_forward)' % n_launch)
     else:
         peak, kernel = PEAK_FP32_MFMA_TFLOPS, ('gemm_f32_kernel<*> implicit-GEMM conv '

@@ -62,8 +62,8 @@ const char* pps_registered_ops(void);
  * convs with K = 64 / 128 / 256 (stationary weight columns in LDS,
  * activations streamed to registers; other shapes run tile 38); 55 = 64x128
  * (8 waves, 2 x 4, four LDS stages: short-M split-K head GEMMs); 56 / 57 /
- * 58 = patch-staged stride-1 3x3 convs (192x128 8 waves / 192x64 4 waves /
- * 96x128 8 waves; the tile's input patch staged once per 32-channel chunk,
+ * 58 / 59 = patch-staged stride-1 3x3 convs (192x128 8 waves / 192x64 4
+ * waves / 96x128 8 waves / 192x64 8 waves; the tile's input patch staged once per 32-channel chunk,
  * K in (channel chunk, tap) order: their own rounding group; other shapes
  * run tile 38).  Results
  * are identical for every tile below 38 (same per-element fp32 MFMA

@@ -1,5 +1,5 @@
 // Patch-staged bf16x3 GEMM for the stride-1 3x3 convolutions (bottleneck
-// branch2b, ResNet.py:291-306; GEMM tile ids 56-58).
+// branch2b, ResNet.py:291-306; GEMM tile ids 56-59).
 //
 // The pipelined kernel (gemm_x3p.hip) stages the im2col A operand per
 // 32-wide K chunk, i.e. per (tap, channel chunk): every input pixel of a tile
@@ -43,8 +43,9 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   constexpr int B_PLANE = BN * BK * 2;
   constexpr int B_STAGE = 3 * B_PLANE;
   constexpr int NPB = BN / 16;  // weight pieces per plane and chunk
-  static_assert(NPB % NW == 0, "weight pieces must split evenly over the waves");
-  constexpr int BPW = NPB / NW;
+  // pieces per wave; with fewer pieces than waves the spare waves load zeros
+  // into the dummy KiB, so every wave issues the same count
+  constexpr int BPW = (NPB + NW - 1) / NW;
   constexpr int PXP = A3 ? 16 : 8;                    // patch pixels per DMA piece
   constexpr int PMR = (PMAX + PXP - 1) / PXP * PXP;   // pixels, whole pieces
   constexpr int PX_BYTES = A3 ? 64 : 128;             // per pixel (and plane)
@@ -104,7 +105,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int col = n0 + (wave * BPW + j) * 16 + (lane >> 2);
-    boff[j] = col < p.Ncol ? (col * p.ldb + bcl * 8) * 2 : kOOB;
+    boff[j] = (wave * BPW + j < NPB && col < p.Ncol) ? (col * p.ldb + bcl * 8) * 2 : kOOB;
   }
 
   // patch piece q of channel chunk c into buffer c & 1: lane l fills pixel
@@ -150,10 +151,12 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
       const int off = (valid && boff[j] != kOOB) ? boff[j] + koff : kOOB;
-      const unsigned char* d = st + (wave * BPW + j) * 1024;
+      const bool mine = wave * BPW + j < NPB;  // wave-uniform
+      const unsigned char* d = mine ? st + (wave * BPW + j) * 1024 : lds + OFF_D;
+      const int pstep = mine ? B_PLANE : 0;
       glds16(rb0, d, off);
-      glds16(rb1, d + B_PLANE, off);
-      glds16(rb2, d + 2 * B_PLANE, off);
+      glds16(rb1, d + pstep, off);
+      glds16(rb2, d + 2 * pstep, off);
     }
     int pc = -1, s = 0;  // patch chunk this issue serves, its slot
     if (it == 0) {
@@ -315,12 +318,13 @@ static int launch_c(const GemmParams& p, int epi, hipStream_t stream) {
   return PPS_OK;
 }
 
-// Rows / columns / patch pixels of tiles 56-58.
+// Rows / columns / patch pixels of tiles 56-59.
 static void x3c_shape(int tile, int& bm, int& bn, int& pmax) {
   switch (tile) {
     case GEMM_TILE_C16_192x128: bm = 192; bn = 128; pmax = 272; return;
     case GEMM_TILE_C16_192x64: bm = 192; bn = 64; pmax = 272; return;
     case GEMM_TILE_C16_96x128: bm = 96; bn = 128; pmax = 144; return;
+    case GEMM_TILE_C16_192x64W42: bm = 192; bn = 64; pmax = 272; return;
     default: bm = bn = pmax = 0; return;
   }
 }
@@ -367,6 +371,11 @@ int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile) 
     case GEMM_TILE_C16_96x128:
       return a3 ? launch_c<96, 128, 2, 4, 4, true, 144>(p, epi, stream)
                 : launch_c<96, 128, 2, 4, 4, false, 144>(p, epi, stream);
+    case GEMM_TILE_C16_192x64W42:
+      // 8 waves as 4 x 2 (48 x 32 each): half the weight bytes per tile of
+      // tile 57's neighbours at 256+ tiles for N = 256 (res4) / 128 (res3)
+      return a3 ? launch_c<192, 64, 4, 2, 4, true, 272>(p, epi, stream)
+                : launch_c<192, 64, 4, 2, 4, false, 272>(p, epi, stream);
     default:
       set_error("unknown patch-staged tile " + std::to_string(tile));
       return PPS_ERR_INVALID_ARG;

@@ -102,14 +102,15 @@ enum GemmTile {
   // 55 (16x16x32): 64x128 with 8 waves as 2 x 4 and four LDS stages -- short
   // M (the 64-row head GEMMs: 248 split-K workgroups, three chunks in flight)
   GEMM_TILE_P16_64x128W24S4 = 55,
-  // 56..58 (16x16x32, own rounding group: K in (channel chunk, tap) order):
-  // patch-staged stride-1 3x3 convs (gemm_x3c.hip) -- 192x128 (8 waves),
-  // 192x64 (4 waves), 96x128 (8 waves); other shapes run tile 38
+  // 56..59 (16x16x32, own rounding group: K in (channel chunk, tap) order):
+  // patch-staged stride-1 3x3 convs (gemm_x3c.hip) -- 192x128 (8 waves), 192x64 (4 waves), 96x128 (8 waves),
+  // 192x64 (8 waves); other shapes run tile 38
   GEMM_TILE_C16_FIRST = 56,
   GEMM_TILE_C16_192x128 = 56,
   GEMM_TILE_C16_192x64 = 57,
   GEMM_TILE_C16_96x128 = 58,
-  GEMM_NUM_TILES = 59
+  GEMM_TILE_C16_192x64W42 = 59,  // 192x64 with 8 waves (4 x 2)
+  GEMM_NUM_TILES = 60
 };
 
 struct GemmParams {

@@ -20,7 +20,8 @@ PEAK_X3 = 2516.8 / 6  # bf16 dense MFMA peak / 6 product terms (bench.py)
 
 
 def is_mfma(nm):
-    return ('gemm_x3_kernel<' in nm or 'gemm_x3p_kernel<' in nm or 'gemm_ws_kernel<' in nm or
+    return ('gemm_x3_kernel<' in nm or 'gemm_x3p_kernel<' in nm or 'gemm_x3c_kernel<' in nm or
+            'gemm_ws_kernel<' in nm or
             ('stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)) and epi_of(nm) != 1
 
 

@@ -53,7 +53,7 @@ def main():
     fetch = load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0], 'FETCH_SIZE')
     write = load(glob.glob(os.path.join(d, 'p2', '*counter_collection.csv'))[0], 'WRITE_SIZE')
     # the x3 path launches both the register-staged and the pipelined family
-    knames = ('gemm_x3_kernel', 'gemm_x3p_kernel', 'gemm_ws_kernel') if math == 'x3' \
+    knames = ('gemm_x3_kernel', 'gemm_x3p_kernel', 'gemm_x3c_kernel', 'gemm_ws_kernel') if math == 'x3' \
         else ('gemm_f32_kernel',)
 
     def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
