@@ -30,162 +30,6 @@
 
 namespace pps {
 
-// The distance epilogue staged through LDS (not for self-distance tiles,
-// which also write their mirror): the dot products are parked as a
-// [BM][BN+4] f32 tile and the workgroup then writes whole output rows, 16 B
-// per lane with consecutive lanes on consecutive columns, so each store
-// instruction covers full 64-256 B row segments instead of 16-B pieces of 16-32
-// rows (PMC: the direct epilogue wrote 1.56x the matrix).  Same per-element
-// formulas as dist_epilogue_t (identical bits).
-template <int BM, int BN, int WM, int WN, int S>
-__device__ inline void dist_epilogue_lds(const GemmParams& p,
-                                         typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
-                                         unsigned char* lds, int m0, int n0, int wm, int wn,
-                                         int r32, int h) {
-  constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
-  constexpr int LD = BN + 4;
-  constexpr int NT = 64 * WM * WN;
-  float* t = reinterpret_cast<float*>(lds);
-  __syncthreads();  // every wave is done reading the last stage
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int rr = wm * (BM / WM) + i * S + r32;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cb = wn * (BN / WN) + j * S + 4 * h;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-        *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
-      }
-    }
-  }
-  __syncthreads();
-  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
-  const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0, nrem = p.Ncol - n0;
-  const bool vec = (p.ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-  constexpr int C4 = BN / 4;
-  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
-    const int row = idx / C4, col = 4 * (idx - row * C4);
-    if (row >= mrem || col >= nrem) continue;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
-    const float qn = p.norm_a[m0 + row];
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gn = col + e < nrem ? p.norm_b[n0 + col + e] : 0.f;
-      const float dot = a[e];
-      float d;
-      if (p.metric == PPS_METRIC_COSINE) {
-        const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
-        d = 1.f - dot / den;
-      } else {
-        d = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
-        if (p.metric == PPS_METRIC_EUCLIDEAN) d = sqrtf(d);
-      }
-      if (p.zero_diag && m0 + row == n0 + col + e) d = 0.f;
-      v[e] = d;
-    }
-    float* o = out + row * ldo + col;
-    if (vec && col + 3 < nrem) {
-      *reinterpret_cast<f32x4*>(o) = v;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (col + e < nrem) o[e] = v[e];
-    }
-  }
-}
-
-// Distance epilogue on transposed accumulators: same formulas as
-// dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
-template <int BM, int BN, int WM, int WN, int S = 32>
-__device__ inline void dist_epilogue_t(const GemmParams& p,
-                                       typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
-                                       int m0, int n0, int wm, int wn, int r32, int h) {
-  constexpr int TM = BM / WM / S;
-  constexpr int TN = BN / WN / S;
-  constexpr int NQ = S * S / 256;
-  float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
-  const bool mirror = p.sym && m0 < n0;  // strictly-upper tile of a self-distance
-  const bool diag = p.sym && m0 == n0;   // diagonal tile: its own upper half, mirrored
-  float* __restrict__ outT = p.out + (int64_t)n0 * p.ldo + m0;
-  const int ldo = (int)p.ldo;
-  const int mrem = p.M - m0;
-  const int nrem = p.Ncol - n0;
-  const bool vec = (p.ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-  const float* qsq = p.norm_a + m0;
-  float qn[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int rr = wm * (BM / WM) + i * S + r32;
-    qn[i] = rr < mrem ? qsq[rr] : 0.f;
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int cb = wn * (BN / WN) + j * S + 4 * h;
-    float gn[4 * NQ];
-#pragma unroll
-    for (int r = 0; r < 4 * NQ; ++r) {
-      const int c = cb + 8 * (r >> 2) + (r & 3);
-      gn[r] = c < nrem ? p.norm_b[n0 + c] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rr = wm * (BM / WM) + i * S + r32;
-      if (rr >= mrem) continue;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int c = cb + 8 * q;
-        if (c >= nrem) continue;
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float dot = acc[i][j][4 * q + e];
-          float d;
-          if (p.metric == PPS_METRIC_COSINE) {
-            const float den =
-                fmaxf(sqrtf(qn[i]), 1e-12f) * fmaxf(sqrtf(gn[4 * q + e]), 1e-12f);
-            d = 1.f - dot / den;
-          } else {
-            d = fmaxf(__builtin_fmaf(-2.f, dot, qn[i]) + gn[4 * q + e], 0.f);
-            if (p.metric == PPS_METRIC_EUCLIDEAN) d = sqrtf(d);
-          }
-          if (p.zero_diag && m0 + rr == n0 + c + e) d = 0.f;
-          v[e] = d;
-        }
-        float* o = out + rr * ldo + c;
-        if (diag) {  // diagonal tile of a self-distance: upper half, mirrored
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int cc = c + e;
-            if (cc < nrem && rr <= cc) {
-              o[e] = v[e];
-              if (rr < cc) outT[cc * ldo + rr] = v[e];
-            }
-          }
-          continue;
-        }
-        if (vec && c + 3 < nrem) {
-          *reinterpret_cast<f32x4*>(o) = v;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (c + e < nrem) o[e] = v[e];
-        }
-        if (mirror) {  // out[n0 + c + e][m0 + rr]: consecutive lanes, consecutive rows
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (c + e < nrem) outT[(c + e) * ldo + rr] = v[e];
-        }
-      }
-    }
-  }
-}
-
 // A3 = false: A is f32 NHWC, staged as 128-byte f32 rows and split after the
 // fragment read.  A3 = true: A is three bf16 planes (written by a producer
 // epilogue with EPI_F_PLANES), staged like B as 64-byte rows per plane --
