@@ -133,8 +133,7 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
         cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
         if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
-            cands += [(t, True) for t in list(range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)) +
-                      [ops.TILE_D32]]
+            cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)]
 
         def time_dist(t, qp, n):
             ops.compute_dist(qa, g_local, tile=t, q_planes=qp, pad_rows=True)

@@ -65,9 +65,7 @@ const char* pps_registered_ops(void);
  * 58 / 59 = patch-staged stride-1 3x3 convs (192x128 8 waves / 192x64 4
  * waves / 96x128 8 waves / 192x64 8 waves; the tile's input patch staged once per 32-channel chunk,
  * K in (channel chunk, tap) order: their own rounding group; other shapes
- * run tile 38); 60 = 256x256 distance tile on query planes (pps_distmat_x3p;
- * 8 waves, 16-wide K stages, same bits as the ids below 38; any other use
- * runs tile 29).  Results
+ * run tile 38).  Results
  * are identical for every tile below 38 (same per-element fp32 MFMA
  * accumulation order) and identical among the tiles from 38 on (one MFMA
  * sums a 32-wide K chunk: a different rounding

@@ -277,13 +277,6 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     q.tile = GEMM_TILE_P16_FIRST;
     return launch_gemm_x3(q, epi_in, batch, stream);
   }
-  if (p.tile == GEMM_TILE_D32_256x256) {
-    // the 256x256 distance tile on plane queries, else tile 29 (same bits)
-    if (x3d_eligible(p, epi, batch)) return launch_gemm_x3d(p, stream);
-    GemmParams q = p;
-    q.tile = GEMM_TILE_P_FIRST;
-    return launch_gemm_x3(q, epi_in, batch, stream);
-  }
   if (p.tile >= GEMM_TILE_C16_FIRST) {
     // patch-staged 3x3 tiles where they apply, else tile 38
     if (x3c_eligible(p, epi, batch, p.tile)) return launch_gemm_x3c(p, epi, stream, p.tile);

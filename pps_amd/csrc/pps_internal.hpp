@@ -110,11 +110,7 @@ enum GemmTile {
   GEMM_TILE_C16_192x64 = 57,
   GEMM_TILE_C16_96x128 = 58,
   GEMM_TILE_C16_192x64W42 = 59,  // 192x64 with 8 waves (4 x 2)
-  // 60 (32x32x16 rounding, the ids-below-38 group): 256x256 distance GEMM on
-  // query and gallery planes, 16-wide K stages (gemm_x3d.hip); any other use
-  // runs tile 29
-  GEMM_TILE_D32_256x256 = 60,
-  GEMM_NUM_TILES = 61
+  GEMM_NUM_TILES = 60
 };
 
 struct GemmParams {
@@ -207,8 +203,6 @@ int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream);
 bool x3c_eligible(const GemmParams& p, int epi, int batch, int tile);
 int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
 int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
-bool x3d_eligible(const GemmParams& p, int epi, int batch);
-int launch_gemm_x3d(const GemmParams& p, hipStream_t stream);
 int x3c_tile_cols(int tile);
 
 // ---- retrieval (rank.hip) ---------------------------------------------------
