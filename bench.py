@@ -130,6 +130,7 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         # distance-GEMM tile choice on this shard's shape (outside the timed runs)
         from pps_amd import ops
         qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
+        gidx = ops.GalleryIndex(g_local)   # prepared once: the tiles compete on the GEMM
         # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
         cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
         if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
@@ -195,7 +196,8 @@ def distmat_roofline(q_local, g_local, world, reps=10):
     qp = bool(be.distmat_qplanes)
     if qp:
         q3, qsq = ops.split_sqnorm(q_all)
-        launch = lambda: ops.distmat_planes(q3, qsq, idx, out, tile=be.distmat_tile)
+        q3t = ops.tile_planes(q3) if D % 32 == 0 else None
+        launch = lambda: ops.distmat_planes(q3, qsq, idx, out, tile=be.distmat_tile, q_tiled=q3t)
     else:
         launch = lambda: ops.compute_dist(q_all, idx, out=out, tile=be.distmat_tile)
     for _ in range(2):
@@ -708,7 +710,8 @@ def main():
             timing=(ret['dist_roofline'] or {}).get('timing'),
             kernel='%s EPI_DIST, tile %d' % (
                 'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
-                ret['distmat_tile']) + (', queries as bf16x3 planes'
+                ret['distmat_tile']) + (', queries and gallery as chunk-tiled bf16x3 planes '
+                                        '(pps_distmat_x3p_tiled)'
                                         if ret['distmat_qplanes'] else '')),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

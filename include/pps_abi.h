@@ -107,6 +107,23 @@ int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq
                     const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg,
                     int D, int metric, float* out, int64_t ldo, int tile,
                     void* stream);
+/* Chunk-tiled planes (experimental layout for the distance GEMM): planes
+ * [3][rows][ld] (plane stride plane_stride) -> out [3][rows16/16][D/32][16][32],
+ * rows16 = rows rounded up to 16, padding rows zero; D % 32 == 0.  out holds
+ * 3 * rows16 * D bf16. */
+int pps_tile_planes(const uint16_t* planes, int64_t rows, int D, int64_t ld,
+                    int64_t plane_stride, uint16_t* out, void* stream);
+/* pps_split_bf16x3_sqnorm writing the planes chunk-tiled (the layout of
+ * pps_tile_planes; out3t holds 3 * rows16 * D bf16, padding rows zero):
+ * one read of x, the same bits. */
+int pps_split_bf16x3_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld,
+                                  uint16_t* out3t, float* sqnorm, void* stream);
+/* pps_distmat_x3p on tiled query and gallery planes (pps_tile_planes): each
+ * 16-row DMA piece of a 32-wide K chunk is one contiguous KiB.  Same bits as
+ * pps_distmat_x3p on the same tile; pipelined tiles 29..53 (0 = 42). */
+int pps_distmat_x3p_tiled(const uint16_t* q3t, int64_t Q, const float* qsq,
+                          const uint16_t* g3t, const float* gsq, int64_t G, int D,
+                          int metric, float* out, int64_t ldo, int tile, void* stream);
 /* Self-distance of one feature set x [N][ld] (the reference's
  * compute_dist(g, g) / compute_dist(q, q) of re-ranking and multi-query,
  * reid_dataset_evaluator.py:169-175, 195-206): out [N][N] from the

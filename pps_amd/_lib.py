@@ -29,6 +29,10 @@ SIGNATURES = {
                        c_ptr, c_i64, c_int, c_ptr],
     'pps_distmat_x3p': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int,
                         c_ptr, c_i64, c_int, c_ptr],
+    'pps_tile_planes': [c_ptr, c_i64, c_int, c_i64, c_i64, c_ptr, c_ptr],
+    'pps_split_bf16x3_sqnorm_tiled': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr, c_ptr],
+    'pps_distmat_x3p_tiled': [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_int, c_int, c_ptr,
+                              c_i64, c_int, c_ptr],
     'pps_distmat_x3_self': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_i64,
                             c_int, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,

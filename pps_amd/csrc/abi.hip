@@ -132,6 +132,16 @@ int pps_split_bf16x3_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uin
   return split_sqnorm(x, rows, D, ld, out3, sqnorm, as_stream(stream));
 }
 
+int pps_split_bf16x3_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld,
+                                  uint16_t* out3t, float* sqnorm, void* stream) {
+  PPS_ENFORCE(x && out3t && sqnorm, "null pointer");
+  PPS_ENFORCE(rows >= 0 && D > 0 && D % 32 == 0 && ld >= D && ld % 4 == 0,
+              "bad shape (D % 32 == 0)");
+  PPS_ENFORCE(aligned16(x), "x must be 16-byte aligned");
+  PPS_ENFORCE(((uintptr_t)out3t & 7) == 0, "out3t must be 8-byte aligned");
+  return split_sqnorm_tiled(x, rows, D, ld, out3t, sqnorm, as_stream(stream));
+}
+
 int pps_distmat_x3(const float* q, int64_t Q, int64_t ldq, const float* qsq,
                    const uint16_t* g3, const float* gsq, int64_t G, int64_t ldg, int D,
                    int metric, float* out, int64_t ldo, int tile, void* stream) {
@@ -202,6 +212,37 @@ int pps_distmat_x3p(const uint16_t* q3, int64_t Q, int64_t ldq, const float* qsq
     }
   }
   return PPS_OK;
+}
+
+// Both operands' planes chunk-tiled ([rows16 / 16][D / 32][16][32] per
+// plane, rows padded to a multiple of 16 with zeros: pps_tile_planes).
+int pps_distmat_x3p_tiled(const uint16_t* q3t, int64_t Q, const float* qsq,
+                          const uint16_t* g3t, const float* gsq, int64_t G, int D, int metric,
+                          float* out, int64_t ldo, int tile, void* stream) {
+  PPS_ENFORCE(q3t && qsq && g3t && gsq && out, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && D > 0 && D % 32 == 0, "bad shape (D % 32 == 0)");
+  PPS_ENFORCE(ldo >= G, "ldo < G");
+  PPS_ENFORCE(aligned16(q3t) && aligned16(g3t), "planes must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_WS),
+              "tiled planes need a pipelined tile (0 or 29..53)");
+  const int64_t Qp = (Q + 15) / 16 * 16, Gp = (G + 15) / 16 * 16;
+  PPS_ENFORCE(Qp * D * 2 < kMaxBufBytes && Gp * D * 2 < kMaxBufBytes, "planes over 2 GiB");
+  if (Q == 0 || G == 0) return PPS_OK;
+  GemmParams p{};
+  p.splitk = 1;
+  p.tiled = 3;
+  p.a3 = q3t; p.a_plane = Qp * D; p.a_bytes = (uint32_t)(Qp * D * 2);
+  p.H = 1; p.W = (int)Q; p.Cin = D; p.lda = D;
+  p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)Q;
+  p.M = (int)Q;
+  p.b3 = g3t; p.b_plane = Gp * D; p.b_bytes = (uint32_t)(Gp * D * 2);
+  p.ldb = D; p.kb_valid = D; p.Ncol = (int)G;
+  p.Kloop = D;
+  p.norm_a = qsq; p.norm_b = gsq;
+  p.out = out; p.ldo = ldo; p.metric = metric;
+  p.tile = tile ? tile : GEMM_TILE_P16_FIRST + 4;
+  return launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
 }
 
 int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,

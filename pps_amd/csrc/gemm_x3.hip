@@ -423,19 +423,25 @@ __global__ void row_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int
 // ---- gallery / query index in one pass: bf16x3 planes [3][rows][D] and
 // squared row norms, reading x once.  The norm uses row_sqnorm_kernel's lane
 // order and xor tree, the split is elementwise: bits equal to the two
-// separate kernels.
+// separate kernels.  TILED: the planes in the chunk-tiled layout
+// [rows16 / 16][D / 32][16][32] (pps_tile_planes; rows16 = rows rounded up to
+// 16, the padding rows written as zeros, D % 32 == 0).
+template <bool TILED>
 __global__ void split_sqnorm_kernel(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
                                     unsigned short* __restrict__ out3,
                                     float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const float* r = x + row * ld;
-  const int64_t plane = rows * (int64_t)D;
-  unsigned short* o = out3 + row * (int64_t)D;
+  const int64_t rows16 = TILED ? (rows + 15) / 16 * 16 : rows;
+  if (row >= rows16) return;
+  const bool real = row < rows;
+  const float* r = x + (real ? row : 0) * ld;
+  const int64_t plane = rows16 * (int64_t)D;
+  unsigned short* o = TILED ? out3 + (row >> 4) * 16 * (int64_t)D + (row & 15) * 32
+                            : out3 + row * (int64_t)D;
   float s = 0.f;
   for (int k = lane * 4; k < D; k += 256) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
+    const f32x4 v = real ? *reinterpret_cast<const f32x4*>(r + k) : (f32x4){0.f, 0.f, 0.f, 0.f};
     s = __builtin_fmaf(v[0], v[0], s);
     s = __builtin_fmaf(v[1], v[1], s);
     s = __builtin_fmaf(v[2], v[2], s);
@@ -444,21 +450,32 @@ __global__ void split_sqnorm_kernel(const float* __restrict__ x, int64_t rows, i
     unsigned a, m, l;
     split2(v[0], v[1], a, m, l); hi[0] = a; mid[0] = m; lo[0] = l;
     split2(v[2], v[3], a, m, l); hi[1] = a; mid[1] = m; lo[1] = l;
-    *reinterpret_cast<u32x2*>(o + k) = hi;
-    *reinterpret_cast<u32x2*>(o + plane + k) = mid;
-    *reinterpret_cast<u32x2*>(o + 2 * plane + k) = lo;
+    const int64_t ko = TILED ? (int64_t)(k >> 5) * 512 + (k & 31) : k;
+    *reinterpret_cast<u32x2*>(o + ko) = hi;
+    *reinterpret_cast<u32x2*>(o + plane + ko) = mid;
+    *reinterpret_cast<u32x2*>(o + 2 * plane + ko) = lo;
   }
 #pragma unroll
   for (int o2 = 32; o2 >= 1; o2 >>= 1) s += __shfl_xor(s, o2);
-  if (lane == 0) out[row] = s;
+  if (lane == 0 && real) out[row] = s;
 }
 
 int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,
                  hipStream_t stream) {
   if (rows <= 0) return PPS_OK;
   const int64_t blocks = (rows + 3) / 4;
-  hipLaunchKernelGGL(split_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, rows,
-                     D, ld, reinterpret_cast<unsigned short*>(out3), out);
+  hipLaunchKernelGGL(split_sqnorm_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, x,
+                     rows, D, ld, reinterpret_cast<unsigned short*>(out3), out);
+  PPS_CHECK_LAUNCH("split_sqnorm_kernel");
+  return PPS_OK;
+}
+
+int split_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3t,
+                       float* out, hipStream_t stream) {
+  if (rows <= 0) return PPS_OK;
+  const int64_t blocks = ((rows + 15) / 16 * 16 + 3) / 4;
+  hipLaunchKernelGGL(split_sqnorm_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, x,
+                     rows, D, ld, reinterpret_cast<unsigned short*>(out3t), out);
   PPS_CHECK_LAUNCH("split_sqnorm_kernel");
   return PPS_OK;
 }
@@ -491,3 +508,50 @@ int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream
 }
 
 }  // namespace pps
+
+namespace pps {
+// Chunk-tiled copy of bf16x3 planes for the distance GEMM's tiled path:
+// in [3][rows][ld] (plane stride ps) -> out [3][rows16 / 16][D / 32][16][32]
+// with rows16 = rows rounded up to 16 (padding rows zero).  One thread per
+// 16-byte vector of the output.
+__global__ void tile_planes_kernel(const uint16_t* __restrict__ in, int64_t rows, int D,
+                                   int64_t ld, int64_t ps, uint16_t* __restrict__ out,
+                                   int64_t nvec) {
+  const int64_t rows16 = (rows + 15) / 16 * 16;
+  const int nkc = D / 32;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = v * 8;                  // output element
+    const int64_t per_plane = rows16 * D;
+    const int pl = (int)(e / per_plane);
+    const int64_t r = e - pl * per_plane;     // within the plane
+    const int64_t blk = r / 512;              // (row block, chunk)
+    const int w = (int)(r - blk * 512);       // within the KiB: row * 32 + k
+    const int64_t rb = blk / nkc;
+    const int kc = (int)(blk - rb * nkc);
+    const int64_t row = rb * 16 + (w >> 5);
+    const int k = kc * 32 + (w & 31);
+    uint4 x = make_uint4(0u, 0u, 0u, 0u);
+    if (row < rows) x = *reinterpret_cast<const uint4*>(in + pl * ps + row * ld + k);
+    *reinterpret_cast<uint4*>(out + e) = x;
+  }
+}
+}  // namespace pps
+
+int pps_tile_planes(const uint16_t* planes, int64_t rows, int D, int64_t ld, int64_t plane_stride,
+                    uint16_t* out, void* stream) {
+  using namespace pps;
+  if (!planes || !out) { set_error("null pointer"); return PPS_ERR_INVALID_ARG; }
+  if (rows < 0 || D <= 0 || D % 32 != 0 || ld < D || ld % 8 != 0 || plane_stride < rows * ld) {
+    set_error("pps_tile_planes: bad shape (D % 32 == 0, ld % 8 == 0)");
+    return PPS_ERR_INVALID_ARG;
+  }
+  const int64_t rows16 = (rows + 15) / 16 * 16;
+  const int64_t nvec = 3 * rows16 * D / 8;
+  if (nvec == 0) return PPS_OK;
+  const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipLaunchKernelGGL(tile_planes_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), planes, rows, D, ld, plane_stride, out, nvec);
+  PPS_CHECK_LAUNCH("tile_planes_kernel");
+  return PPS_OK;
+}

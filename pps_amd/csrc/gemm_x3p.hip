@@ -225,6 +225,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const int ih0 = oh * p.stride - p.pad;
       const int iw0 = ow * p.stride - p.pad;
       abase[i] = ((n * p.H + ih0) * p.W + iw0) * p.lda + ce;
+      if (A3 && (p.tiled & 1))  // plain rows (distance): [row / 16][K / 32][16][32]
+        abase[i] = (rowc >> 4) * (p.lda / 32) * 512 + (rowc & 15) * 32 + ce;
       uint64_t m = 0;
       for (int t = 0, kh = 0, kw = 0; t < ntaps; ++t) {
         const int ih = ih0 + kh * p.dil, iw = iw0 + kw * p.dil;
@@ -251,9 +253,15 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int col = n0 + bpiece(j) * 16 + (lane >> 2);
-    boff[j] = col < p.Ncol ? (col * p.ldb + bcl * 8) * 2 : kOOB;
+    boff[j] = col < p.Ncol ? ((p.tiled & 2) ? ((col >> 4) * (p.ldb / 32) * 512 + (col & 15) * 32 +
+                                                bcl * 8) * 2
+                                             : (col * p.ldb + bcl * 8) * 2)
+                           : kOOB;
   }
 
+  // chunk strides: tiled planes advance a KiB per 32-wide chunk
+  const int tcm = (A3 && (p.tiled & 1)) ? 16 : 1;
+  const int bstep = (p.tiled & 2) ? 1024 : BK * 2;
   // ---- wave-uniform im2col tracker of the next chunk to request
   int tc = 0, tt = 0, tkw = 0, toff = 0;
   const int step_w = p.dil * p.lda;
@@ -282,7 +290,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
         if (!AEVEN && apiece(i) >= NPA) continue;  // wave-uniform: an empty slot
         const bool ok = tt < 64 && ((amask[i] >> tt) & 1ull);
         if (A3) {
-          const int off = ok ? (abase[i] + toff + tc) * 2 : kOOB;
+          const int off = ok ? (abase[i] + toff + tc * tcm) * 2 : kOOB;
           const unsigned char* d = st + apiece(i) * 1024;
           glds16(ra, d, off);
           glds16(ra1, d + A_PLANE, off);
@@ -303,7 +311,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
       if (!BEVEN && bpiece(j) >= NPB) continue;
-      const int off = (kok && boff[j] != kOOB) ? boff[j] + kiss * BK * 2 : kOOB;
+      const int off = (kok && boff[j] != kOOB) ? boff[j] + kiss * bstep : kOOB;
       const unsigned char* d = st + A_BYTES + bpiece(j) * 1024;
       glds16(rb0, d, off);
       glds16(rb1, d + B_PLANE, off);

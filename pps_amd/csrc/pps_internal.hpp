@@ -156,6 +156,10 @@ struct GemmParams {
   // (tap t0 = k0 / Cin, channel k0 % Cin); the A pointer is NOT offset (the
   // plain-GEMM split-K of the heads offsets it instead)
   int ksplit_conv;
+  // pipelined distance GEMM on chunk-tiled planes (pps_distmat_x3p_tiled):
+  // bit 0 = A, bit 1 = B stored [rows / 16][K / 32][16][32] per plane, so a
+  // 16-row DMA piece of one 32-wide K chunk is one contiguous KiB
+  int tiled;
   int tile;  // GemmTile; 0 = heuristic
   int splitk;           // >= 1; K slices enumerated with the batch on grid.y
   int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)
@@ -197,6 +201,8 @@ int split_bf16x3(const float* x, int64_t n, int nbatch, uint16_t* out, hipStream
 int row_sqnorm(const float* x, int64_t rows, int D, int64_t ld, float* out, hipStream_t stream);
 int split_sqnorm(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3, float* out,
                  hipStream_t stream);
+int split_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out3t,
+                       float* out, hipStream_t stream);
 int pick_tile(const GemmParams& p, int batch);
 bool ws_eligible(const GemmParams& p, int epi, int batch);
 int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream);

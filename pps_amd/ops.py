@@ -97,24 +97,55 @@ def split_sqnorm(x):
     return planes, sq
 
 
+def split_sqnorm_tiled(x):
+    """split_sqnorm writing the planes chunk-tiled (tile_planes' layout, as an
+    int16 [3, R16, D] tensor) from one read of x; D % 32 == 0.  Same bits."""
+    R, D = x.shape
+    r16 = (R + 15) // 16 * 16
+    planes = torch.empty((3, r16, D), dtype=torch.int16, device=x.device)
+    sq = torch.empty((R,), dtype=torch.float32, device=x.device)
+    call('pps_split_bf16x3_sqnorm_tiled', _dev(x, 'x'), R, D, x.stride(0),
+         _dev(planes, 'out3t', torch.int16), _dev(sq, 'sqnorm'), _stream())
+    return planes, sq
+
+
 class GalleryIndex(object):
     """A gallery prepared once for the bf16x3 distance GEMM: features split
     into three bf16 planes + squared norms; score any number of query
-    batches against it with compute_dist(q, index)."""
+    batches against it with compute_dist(q, index).  tiled=True prepares the
+    planes in the chunk-tiled layout the query-planes GEMM streams (one pass;
+    the row-major planes are then split on first use)."""
 
-    def __init__(self, g):
+    def __init__(self, g, tiled=False):
         if g.dim() != 2:
             raise RuntimeError('gallery must be [G, D], got %s' % (tuple(g.shape),))
         self.feats = g
-        if g.is_contiguous() and g.shape[1] % 4 == 0:
-            self.planes, self.sqnorm = split_sqnorm(g)
+        self._planes = self._tiled = None
+        if tiled and g.is_contiguous() and g.shape[1] % 32 == 0:
+            self._tiled, self.sqnorm = split_sqnorm_tiled(g)
+        elif g.is_contiguous() and g.shape[1] % 4 == 0:
+            self._planes, self.sqnorm = split_sqnorm(g)
         else:
-            self.planes = split_bf16x3(g)
+            self._planes = split_bf16x3(g)
             self.sqnorm = row_sqnorm(g)
 
     @property
     def shape(self):
         return self.feats.shape
+
+    @property
+    def planes(self):
+        """Row-major planes [3, G, D]."""
+        if self._planes is None:
+            self._planes = split_bf16x3(self.feats)
+        return self._planes
+
+    @property
+    def tiled_planes(self):
+        """The planes chunk-tiled (tile_planes' layout), built on first use."""
+        if self._tiled is None:
+            self._tiled = tile_planes(self.planes)
+        return self._tiled
 
 
 SELF_TILES = (0, TILE_P_FIRST, TILE_P_FIRST + 7, TILE_P16_FIRST, TILE_P16_FIRST + 7)
@@ -158,7 +189,9 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
         call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
              _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
-    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g)
+    tiled = bool(q_planes) and D % 32 == 0 and (tile == 0 or tile >= TILE_P_FIRST)
+    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g, tiled=tiled and not (
+        symmetric or (symmetric is None and g.data_ptr() == q.data_ptr())))
     if symmetric is None:
         f = idx.feats
         symmetric = (f.data_ptr() == q.data_ptr() and tuple(f.shape) == tuple(q.shape) and
@@ -171,6 +204,9 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
         out._pps_symmetric = True   # mirrored tiles: exactly symmetric (re_ranking uses it)
         return out
     if q_planes:
+        if tiled and q.is_contiguous():  # both operands chunk-tiled, queries in one pass
+            qt, qsq = split_sqnorm_tiled(q)
+            return distmat_planes(None, qsq, idx, out, metric, tile, q_tiled=qt, Q=Q, D=D)
         q3, qsq = split_sqnorm(q) if q.is_contiguous() else (split_bf16x3(q), row_sqnorm(q))
         return distmat_planes(q3, qsq, idx, out, metric, tile)
     qsq = row_sqnorm(q)
@@ -180,12 +216,44 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     return out
 
 
-def distmat_planes(q3, qsq, idx, out, metric='euclidean', tile=0):
-    """The distance GEMM alone (pps_distmat_x3p) on queries already split into
-    bf16x3 planes q3 [3, Q, D] with squared norms qsq, against a
-    GalleryIndex: what compute_dist(q_planes=True) launches after the split."""
-    _, Q, D = q3.shape
+def tile_planes(planes):
+    """bf16x3 planes [3, R, D] (D % 32 == 0) -> the chunk-tiled layout
+    [3][R16 / 16][D / 32][16][32] (R16 = R rounded up to 16, zero rows),
+    returned as an int16 [3, R16, D] tensor: a 16-row DMA piece of one
+    32-wide K chunk is then one contiguous KiB (pps_tile_planes)."""
+    _, R, D = planes.shape
+    r16 = (R + 15) // 16 * 16
+    out = torch.empty((3, r16, D), dtype=torch.int16, device=planes.device)
+    call('pps_tile_planes', _dev(planes, 'planes', torch.int16), R, D, D, R * D,
+         _dev(out, 'out', torch.int16), _stream())
+    return out
+
+
+def _tiled_tile(tile):
+    """The tile a tiled-plane distance GEMM runs: pipelined ids 29-53 as
+    given; ids 54+ (which a distance matrix runs as tile 38) -> 0 (tile 42,
+    the same 16x16x32 rounding group)."""
+    return int(tile) if TILE_P_FIRST <= tile < 54 else 0
+
+
+def distmat_planes(q3, qsq, idx, out, metric='euclidean', tile=0, q_tiled=None, Q=None,
+                   D=None):
+    """The distance GEMM alone on queries already split into bf16x3 planes
+    q3 [3, Q, D] with squared norms qsq, against a GalleryIndex: what
+    compute_dist(q_planes=True) launches after the split.  With D % 32 == 0
+    both operands go chunk-tiled (pps_distmat_x3p_tiled: same bits, Market
+    1.98 -> 1.83 ms on tile 52, scripts/probes/dist_tiled_probe.py); q_tiled
+    = tile_planes(q3) when the caller has it already (q3 may then be None,
+    with Q and D given)."""
+    if q3 is not None:
+        _, Q, D = q3.shape
     G = idx.shape[0]
+    if D % 32 == 0 and (tile == 0 or tile >= TILE_P_FIRST):
+        qt = q_tiled if q_tiled is not None else tile_planes(q3)
+        call('pps_distmat_x3p_tiled', _dev(qt, 'q3t', torch.int16), Q, _dev(qsq, 'qsq'),
+             _dev(idx.tiled_planes, 'g3t', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D,
+             METRICS[metric], _dev_rows(out, 'out'), _ld(out), _tiled_tile(tile), _stream())
+        return out
     call('pps_distmat_x3p', _dev(q3, 'q3', torch.int16), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
          METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())

@@ -63,6 +63,51 @@ def test_gallery_index_matches_plain_x3():
     np.testing.assert_allclose(sq, (g.double() ** 2).sum(1).cpu().numpy(), rtol=2e-6)
 
 
+@pytest.mark.parametrize('R,D', [(1, 32), (37, 96), (300, 2048), (33, 3968)])
+def test_tiled_planes_layout(R, D):
+    """split_sqnorm_tiled == tile_planes(split_sqnorm) bit for bit; the tiled
+    layout holds element (r, k) of plane p at [p][r // 16][k // 32][r % 16]
+    [k % 32] and zeros in the padding rows."""
+    from pps_amd import ops
+    x = _cuda(np.random.RandomState(R + D).randn(R, D).astype(np.float32))
+    planes, sq = ops.split_sqnorm(x)
+    t1 = ops.tile_planes(planes)
+    t2, sq2 = ops.split_sqnorm_tiled(x)
+    assert torch.equal(t1, t2) and torch.equal(sq, sq2)
+    r16 = (R + 15) // 16 * 16
+    want = torch.zeros((3, r16, D), dtype=torch.int16, device='cuda')
+    want[:, :R] = planes
+    want = want.reshape(3, r16 // 16, 16, D // 32, 32).permute(0, 1, 3, 2, 4).reshape(3, r16, D)
+    assert torch.equal(t2, want)
+
+
+@pytest.mark.parametrize('Q,G,D', [(45, 77, 96), (64, 1000, 3968), (3, 17, 32)])
+@pytest.mark.parametrize('metric', ['euclidean', 'cosine'])
+def test_distmat_tiled_planes_bits(Q, G, D, metric):
+    """compute_dist(q_planes=True) streams chunk-tiled planes of both operands
+    (pps_distmat_x3p_tiled); it equals the row-major planes GEMM
+    (pps_distmat_x3p) bit for bit on every tile, and the tiles keep their
+    rounding groups."""
+    from pps_amd import ops
+    rng = np.random.RandomState(Q + G)
+    q = _cuda(rng.randn(Q, D).astype(np.float32))
+    g = _cuda(rng.randn(G, D).astype(np.float32))
+    idx = ops.GalleryIndex(g)
+    q3, qsq = ops.split_sqnorm(q)
+    tiles = [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1))
+    outs = []
+    for tile in tiles:
+        a = ops.compute_dist(q, g, metric=metric, tile=tile, q_planes=True, pad_rows=True)
+        b = ops.dist_buffer(Q, G, 'cuda')
+        ops.call('pps_distmat_x3p', ops._dev(q3, 'q3', torch.int16), Q, D, ops._dev(qsq, 'qsq'),
+                 ops._dev(idx.planes, 'g3', torch.int16), ops._dev(idx.sqnorm, 'gsq'), G, D, D,
+                 ops.METRICS[metric], ops._dev_rows(b, 'out'), ops._ld(b),
+                 ops._tiled_tile(tile), ops._stream())
+        assert torch.equal(a, b), 'tile %d' % tile
+        outs.append(a.cpu().numpy())
+    check_tile_bits(tiles, outs, ops.TILE_P16_FIRST)
+
+
 def test_distmat_enforces_shapes():
     from pps_amd import ops
     with pytest.raises(RuntimeError):
