@@ -72,6 +72,11 @@ const char* pps_registered_ops(void);
  * sequence, same f32-level error); only speed differs, so callers may
  * autotune. */
 int pps_gemm_num_tiles(void);
+/* Or-ed into the `tile` of pps_conv2d_bn_act_x3 / _x3p / pps_conv2d_bn_act_pps_x3p
+ * (pipelined ids 29..53 and 55+): the bf16x3 weights are chunk-tiled,
+ * [3][Cout16/16][Kpad/32][16][32] (pps_tile_planes over the [3][Cout][Kpad]
+ * planes; Cout16 = Cout rounded up to 16, Cin % 32 == 0).  Same bits. */
+#define PPS_TILE_B_TILED 0x100
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,

@@ -477,6 +477,16 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       int splitk = 1, float* part = nullptr) {
   PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
               "exactly one of x / x planes and one of y / y planes must be given");
+  // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled
+  const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;
+  tile &= ~PPS_TILE_B_TILED;
+  if (wtiled) {
+    PPS_ENFORCE(x3 && splitk == 1, "tiled weights: bf16x3 weights, no split-K");
+    PPS_ENFORCE(Kpad % 32 == 0 && Cin % 32 == 0, "tiled weights need Cin % 32 == 0");
+    PPS_ENFORCE((tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_WS) ||
+                    (tile > GEMM_TILE_WS && tile < GEMM_NUM_TILES),
+                "tiled weights need a pipelined tile (29..53, 55+)");
+  }
   if (x_pl || y_pl) {
     PPS_ENFORCE(x3, "activation planes need the bf16x3 weights");
     PPS_ENFORCE(tile == 0 || tile >= GEMM_TILE_P_FIRST,
@@ -544,6 +554,10 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   if (y_pl) { p.out = nullptr; p.out3 = y_pl; p.out_plane = y_plane; }
   if (x3) {
     p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
+    if (wtiled) {  // [3][Cout16 / 16][Kpad / 32][16][32]
+      p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * Kpad;
+      p.tiled = 2;
+    }
     p.b_bytes = (uint32_t)(p.b_plane * 2);
     return launch_gemm_x3(p, y_pl ? EPI_CONV | EPI_F_PLANES : EPI_CONV, 1, as_stream(stream));
   }

@@ -269,6 +269,10 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
+  if ((p.tiled & 2) && (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST || p.splitk > 1)) {
+    set_error("chunk-tiled weights run on the pipelined / patch tiles only");
+    return PPS_ERR_INVALID_ARG;
+  }
   if (p.tile == GEMM_TILE_WS) {
     // the weight-stationary kernel where it applies, else the 128x128
     // pipelined tile of the same (16x16x32) rounding group

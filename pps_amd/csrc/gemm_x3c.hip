@@ -105,7 +105,10 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int col = n0 + (wave * BPW + j) * 16 + (lane >> 2);
-    boff[j] = (wave * BPW + j < NPB && col < p.Ncol) ? (col * p.ldb + bcl * 8) * 2 : kOOB;
+    boff[j] = (wave * BPW + j < NPB && col < p.Ncol)
+                  ? ((p.tiled & 2) ? ((col >> 4) * (p.ldb / 32) * 512 + (col & 15) * 32 + bcl * 8) * 2
+                                   : (col * p.ldb + bcl * 8) * 2)
+                  : kOOB;
   }
 
   // patch piece q of channel chunk c into buffer c & 1: lane l fills pixel
@@ -147,7 +150,9 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   auto issue = [&]() {
     const unsigned char* st = lds + siss * B_STAGE;
     const bool valid = kiss < nchunks;
-    const int koff = (it * p.Cin + 32 * ic) * 2;
+    // K offset of (tap it, channels 32 ic..): row-major 2 B per element;
+    // chunk-tiled weights 1 KiB per 32-wide chunk
+    const int koff = (p.tiled & 2) ? (it * (p.Cin / 32) + ic) * 1024 : (it * p.Cin + 32 * ic) * 2;
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
       const int off = (valid && boff[j] != kOOB) ? boff[j] + koff : kOOB;

@@ -44,6 +44,9 @@ def main():
     ap.add_argument('--residual', action='store_true', help='conv + BN + residual Sum + ReLU')
     ap.add_argument('--planes', action='store_true',
                     help='x3 only: input as bf16x3 activation planes (conv2d_bn_act_x3p)')
+    ap.add_argument('--wtiled', action='store_true',
+                    help='x3 only: also time chunk-tiled weights (tile | PPS_TILE_B_TILED) and '
+                         'check their bits against the row-major run')
     a = ap.parse_args()
     from pps_amd import model, ops
     for name in a.layers.split(','):
@@ -54,6 +57,7 @@ def main():
         wp, kpad = model.pack_conv_weight(w)
         wf = torch.from_numpy(wp).cuda()
         w3 = ops.split_bf16x3(wf)
+        w3t = ops.tile_planes(w3) if a.wtiled else None
         sc = torch.ones(Cout, device='cuda')
         sh = torch.zeros(Cout, device='cuda')
         y = torch.empty(N, Ho, Wo, Cout, device='cuda')
@@ -64,13 +68,15 @@ def main():
         for math in a.math.split(','):
             wt = w3 if math == 'x3' else wf
             res = []
-            def launch(tile):
+            def launch(tile, tiled=False):
+                wl = w3t if tiled else (w3 if a.planes else wt)
+                tl = tile | 0x100 if tiled else tile
                 if a.planes:
-                    ops.conv2d_bn_act_x3p(xp, Cin, w3, kpad, k, s, p, 1, sc, sh, resid, True, y,
-                                          tile=tile)
+                    ops.conv2d_bn_act_x3p(xp, Cin, wl, kpad, k, s, p, 1, sc, sh, resid, True, y,
+                                          tile=tl)
                 else:
-                    ops.conv2d_bn_act(x, Cin, wt, kpad, k, s, p, 1, sc, sh, resid, True, y,
-                                      tile=tile)
+                    ops.conv2d_bn_act(x, Cin, wl, kpad, k, s, p, 1, sc, sh, resid, True, y,
+                                      tile=tl)
             for tile in [int(t) for t in a.tiles.split(',')]:
                 launch(tile)
                 torch.cuda.synchronize()
@@ -82,6 +88,18 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps
                 res.append('%d:%.3f(%.0f)' % (tile, ms, flops / ms / 1e9))
+                if a.wtiled and math == 'x3':
+                    ref = y.clone()
+                    launch(tile, True)
+                    torch.cuda.synchronize()
+                    same = torch.equal(ref, y)
+                    e0.record()
+                    for _ in range(a.reps):
+                        launch(tile, True)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    mt = e0.elapsed_time(e1) / a.reps
+                    res.append('t%d:%.3f%s' % (tile, mt, '' if same else '(BITS DIFFER)'))
             print('%-6s %-4s M=%d N=%d K=%d  %s' % (name, math, N * Ho * Wo, Cout, k * k * Cin,
                                                     ' '.join(res)), flush=True)
 
