@@ -322,6 +322,8 @@ struct Layer {
   bool relu = false;
   int cin_eff = 0, kpad = 0, shortcut_cin = 0;
   Buf w, scale, shift;  // w: f32 [Cout][Kpad] or bf16x3 planes
+  Buf wt;               // x3 plain convs with Kpad % 32 == 0: the planes chunk-tiled
+                        // (pps_tile_planes), used when tile carries PPS_TILE_B_TILED
   std::vector<int> split;
   bool max_ave = false, normalize = false;
   int nsub = 0, dim = 0, dim_inner = 0;
@@ -451,6 +453,13 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
     for (auto& L : m.layers) {
       if (L.op == Op::Conv || L.op == Op::ConvDual)
         L.w = split3(L.w, (int64_t)L.cout * (L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad), 1, st);
+      if (L.op == Op::Conv && L.kpad % 32 == 0 && L.cin_eff % 32 == 0) {
+        const int64_t c16 = (L.cout + 15) / 16 * 16;
+        L.wt = std::make_shared<DevBuf>((size_t)3 * c16 * L.kpad * sizeof(uint16_t));
+        rc_check(pps_tile_planes(L.w->as<uint16_t>(), L.cout, L.kpad, L.kpad,
+                                 (int64_t)L.cout * L.kpad, L.wt->as<uint16_t>(), st));
+        hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+      }
       else if (L.op == Op::Heads)
         L.w = split3(L.w, (int64_t)L.dim_inner * L.dim, L.nsub, st);
     }
@@ -655,7 +664,10 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     return a;
   };
   auto fbuf = [&](const std::string& name) { return w.bufs.at(name)->as<float>(); };
-  const uint16_t* w3 = m.x3 && L.w ? L.w->as<uint16_t>() : nullptr;
+  // PPS_TILE_B_TILED in the tile: the chunk-tiled weight copy (plain convs)
+  const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) && L.wt;
+  if (!wtiled) tile &= ~PPS_TILE_B_TILED;
+  const uint16_t* w3 = m.x3 && L.w ? (wtiled ? L.wt->as<uint16_t>() : L.w->as<uint16_t>()) : nullptr;
   const float* wf = !m.x3 && L.w ? L.w->as<float>() : nullptr;
   const float* sc = L.scale ? L.scale->as<float>() : nullptr;
   const float* sh = L.shift ? L.shift->as<float>() : nullptr;
@@ -1017,7 +1029,10 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
-    PPS_MCHECK(tile >= 0 && tile < GEMM_NUM_TILES, "tile out of range");
+    const int base = tile & ~PPS_TILE_B_TILED;
+    PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
+    PPS_MCHECK(base == tile || (L->wt && base >= GEMM_TILE_P_FIRST && base != GEMM_TILE_WS),
+               "PPS_TILE_B_TILED: plain x3 conv with Cin % 32 == 0 on a pipelined tile only");
     L->tile = tile;
   });
 }
@@ -1173,6 +1188,12 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       for (int i = 0; i < (int)screen.size() && i < finalists; ++i) {
         const float ms = time_layer(*m, L, *w, x, screen[i].second, L.splitk, final_reps, st, t);
         if (ms < best) { best = ms; L.tile = screen[i].second; }
+        // the same tile on the chunk-tiled weight copy
+        const int tl = screen[i].second;
+        if (L.wt && L.splitk == 1 && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS) {
+          const float mt = time_layer(*m, L, *w, x, tl | PPS_TILE_B_TILED, 1, final_reps, st, t);
+          if (mt < best) { best = mt; L.tile = tl | PPS_TILE_B_TILED; }
+        }
       }
       return best;
     };

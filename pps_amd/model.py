@@ -586,17 +586,23 @@ class PPSModel(object):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
         sk = L.get('splitk', 1) if splitk is None else splitk
+        w = L.get('w')
+        if op == 'conv' and tile > 0 and tile & ops.TILE_B_TILED:
+            # the chunk-tiled weight copy (pps_model_autotune may pick it)
+            if '_wt' not in L:
+                L['_wt'] = ops.tile_planes(L['w'])
+            w = L['_wt']
         if op == 'conv' and (L.get('planes_in') or L.get('planes_out') or sk > 1):
             tile = tile if tile >= ops.TILE_P_FIRST else 0  # pipelined tiles only
             res = bufs[L['residual']] if L['residual'] else None
-            ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+            ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], w, L['kpad'], L['k'],
                                   L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                                   res, L['relu'], bufs[L['output']], tile=tile, splitk=sk,
                                   part=self._part_for(sk * np.prod(self._shapes[L['output']]))
                                   if sk > 1 else None)
         elif op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
-            ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+            ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], w, L['kpad'], L['k'],
                               L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                               res, L['relu'], bufs[L['output']], tile=tile)
         elif op == 'conv_dual':

@@ -403,3 +403,36 @@ def test_forward_splitk_layers():
     assert m.splitks() == sks
     got = m.forward(xd).cpu().numpy()
     np.testing.assert_allclose(got, base, rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,planes', [(1, 24, 8, 512, 512, 3, True),
+                                                     (2, 24, 8, 256, 256, 3, False),
+                                                     (1, 24, 8, 1024, 256, 1, False),
+                                                     (3, 7, 5, 64, 40, 1, False)])
+def test_conv_tiled_weights_bits(N, H, W, Cin, Cout, k, planes):
+    """Chunk-tiled bf16x3 weights (PPS_TILE_B_TILED, ops.tile_planes over the
+    [3][Cout][Kpad] planes) give the row-major weights' bits on every
+    pipelined and patch tile, and the other tiles refuse them."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(Cin + Cout + k)
+    x = _cuda(rng.randn(N, H, W, Cin).astype(np.float32))
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    w3t = ops.tile_planes(w3)
+    sc = _cuda(rng.uniform(0.5, 1.5, Cout).astype(np.float32))
+    sh = _cuda(rng.randn(Cout).astype(np.float32))
+    p = (k - 1) // 2
+    xin = ops.split_bf16x3(x.reshape(-1, Cin)).reshape(3, N, H, W, Cin) if planes else x
+    tiles = [t for t in range(ops.TILE_P_FIRST, ops.num_tiles() + 1) if t != 54]
+    for t in tiles:
+        ya = torch.empty((N, H, W, Cout), device='cuda')
+        yb = torch.full((N, H, W, Cout), float('nan'), device='cuda')
+        ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, 1, p, 1, sc, sh, None, True, ya, tile=t)
+        ops.conv2d_bn_act_x3p(xin, Cin, w3t, kpad, k, 1, p, 1, sc, sh, None, True, yb,
+                              tile=t | 0x100)
+        assert torch.equal(ya, yb), 'tile %d' % t
+    for t in (1, 28, 54):
+        with pytest.raises(RuntimeError):
+            ops.conv2d_bn_act_x3p(xin, Cin, w3t, kpad, k, 1, p, 1, sc, sh, None, True, yb,
+                                  tile=t | 0x100)
