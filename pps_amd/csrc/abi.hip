@@ -644,6 +644,8 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   }
   PPS_ENFORCE(hsum == Ho, "strip heights must sum to the output height");
   const bool pl = x3 != nullptr;
+  const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
+  tile &= ~PPS_TILE_B_TILED;
   if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
   PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= kPpsFuseMaxCols,
               "the fused pooling needs a pipelined tile of exactly Ho*Wo = " +
@@ -664,7 +666,9 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.dil = dil;
   p.Ho = Ho; p.Wo = Wo; p.M = N * Ho * Wo;
   p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
-  p.b3 = w3; p.b_plane = (int64_t)Cout * Kpad; p.b_bytes = (uint32_t)(p.b_plane * 2);
+  p.b3 = w3; p.b_plane = (int64_t)(wtiled ? (Cout + 15) / 16 * 16 : Cout) * Kpad;
+  p.b_bytes = (uint32_t)(p.b_plane * 2);
+  p.tiled = wtiled ? 2 : 0;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = Cout;
   p.out = y; p.ldo = Cout; p.relu = 1; p.tile = tile;
   p.pps_out = pps_out; p.pps_S = S; p.pps_max_ave = max_ave ? 1 : 0; p.pps_nimg = N;
@@ -682,6 +686,13 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                            float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
   PPS_ENFORCE(x && x2 && w && shift && y, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cin2 > 0, "bad shape");
+  const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
+  tile &= ~PPS_TILE_B_TILED;
+  if (wtiled)
+    PPS_ENFORCE(x3 && (Kpad1 + Kpad2) % 32 == 0 &&
+                    ((tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_WS) ||
+                     (tile > GEMM_TILE_WS && tile < GEMM_NUM_TILES)),
+                "tiled weights: bf16x3, K % 32 == 0, a pipelined tile");
   PPS_ENFORCE(Cin % 4 == 0 && ldx % 4 == 0 && Cin2 % 16 == 0 && ldx2 % 4 == 0,
               "channel counts must be multiples of 4 (second operand: 16)");
   PPS_ENFORCE(Kpad1 % 16 == 0 && Kpad1 >= KH * KW * Cin && Kpad2 == Cin2,
@@ -709,8 +720,10 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.scale = nullptr; p.shift = shift; p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   PPS_ENFORCE((int64_t)Cout * (Kpad1 + Kpad2) * 6 < kMaxBufBytes, "weights larger than 2 GiB");
   if (x3) {
-    p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * (Kpad1 + Kpad2);
+    p.b3 = static_cast<const uint16_t*>(w);
+    p.b_plane = (int64_t)(wtiled ? (Cout + 15) / 16 * 16 : Cout) * (Kpad1 + Kpad2);
     p.b_bytes = (uint32_t)(p.b_plane * 2);
+    p.tiled = wtiled ? 2 : 0;
     return launch_gemm_x3(p, EPI_CONV, 1, as_stream(stream));
   }
   p.b = static_cast<const float*>(w);

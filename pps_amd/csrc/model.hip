@@ -453,11 +453,12 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
     for (auto& L : m.layers) {
       if (L.op == Op::Conv || L.op == Op::ConvDual)
         L.w = split3(L.w, (int64_t)L.cout * (L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad), 1, st);
-      if (L.op == Op::Conv && L.kpad % 32 == 0 && L.cin_eff % 32 == 0) {
+      const int64_t kt = L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad;
+      if ((L.op == Op::Conv || L.op == Op::ConvDual) && kt % 32 == 0 && L.cin_eff % 32 == 0) {
         const int64_t c16 = (L.cout + 15) / 16 * 16;
-        L.wt = std::make_shared<DevBuf>((size_t)3 * c16 * L.kpad * sizeof(uint16_t));
-        rc_check(pps_tile_planes(L.w->as<uint16_t>(), L.cout, L.kpad, L.kpad,
-                                 (int64_t)L.cout * L.kpad, L.wt->as<uint16_t>(), st));
+        L.wt = std::make_shared<DevBuf>((size_t)3 * c16 * kt * sizeof(uint16_t));
+        rc_check(pps_tile_planes(L.w->as<uint16_t>(), L.cout, (int)kt, kt, (int64_t)L.cout * kt,
+                                 L.wt->as<uint16_t>(), st));
         hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
       }
       else if (L.op == Op::Heads)
@@ -750,7 +751,8 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const std::vector<int> ok = pps_tiles(m, L, cs);
       const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
       if (!ok.empty()) {
-        const int t = std::find(ok.begin(), ok.end(), tile) != ok.end() ? tile : ok[0];
+        int t = std::find(ok.begin(), ok.end(), tile) != ok.end() ? tile : ok[0];
+        if (wtiled) t |= PPS_TILE_B_TILED;
         rc_check(pps_conv2d_bn_act_pps_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
                                            L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc,
                                            sh, res, nullptr, (int)cs.d[1], (int)cs.d[2],
@@ -761,7 +763,7 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
         rc_check(pps_conv2d_bn_act_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout,
                                        L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, 1,
                                        y, nullptr, 0, (int)cs.d[1], (int)cs.d[2], L.cout,
-                                       tile >= GEMM_TILE_P_FIRST ? tile : 0, st));
+                                       tile >= GEMM_TILE_P_FIRST ? tile | (wtiled ? PPS_TILE_B_TILED : 0) : 0, st));
         rc_check(pps_part_power_set(y, n, (int)cs.d[1], (int)cs.d[2], L.cout, L.split.data(),
                                     (int)L.split.size(), L.max_ave, fbuf(L.output), st));
       }

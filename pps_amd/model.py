@@ -587,7 +587,7 @@ class PPSModel(object):
         tile = L.get('tile', 0) if tile is None else tile
         sk = L.get('splitk', 1) if splitk is None else splitk
         w = L.get('w')
-        if op == 'conv' and tile > 0 and tile & ops.TILE_B_TILED:
+        if op in ('conv', 'conv_dual', 'conv_pps') and tile > 0 and tile & ops.TILE_B_TILED:
             # the chunk-tiled weight copy (pps_model_autotune may pick it)
             if '_wt' not in L:
                 L['_wt'] = ops.tile_planes(L['w'])
@@ -607,7 +607,7 @@ class PPSModel(object):
                               res, L['relu'], bufs[L['output']], tile=tile)
         elif op == 'conv_dual':
             ops.conv2d_dual_bn_act(bufs[L['input']], L['cin_eff'], L['k'], L['stride'],
-                                   L['pad'], bufs[L['input2']], L['stride2'], L['w'],
+                                   L['pad'], bufs[L['input2']], L['stride2'], w,
                                    L['kpad'], L['shift'], L['relu'], bufs[L['output']],
                                    tile=tile)
         elif op == 'maxpool':
@@ -623,13 +623,14 @@ class PPSModel(object):
             res = bufs[L['residual']]
             ok = self.pps_tiles(L)
             if ok:
-                t = tile if tile in ok else ok[0]
-                ops.conv2d_bn_act_pps(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'], L['k'],
+                tb = tile & ~ops.TILE_B_TILED
+                t = (tb if tb in ok else ok[0]) | (tile & ops.TILE_B_TILED)
+                ops.conv2d_bn_act_pps(bufs[L['input']], L['cin_eff'], w, L['kpad'], L['k'],
                                       L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                                       res, L['split_arr'], L['max_ave'], bufs[L['output']],
                                       y=None, tile=t)
             else:   # no tile holds exactly one image: conv, then the pooling kernel
-                ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], L['w'], L['kpad'],
+                ops.conv2d_bn_act_x3p(bufs[L['input']], L['cin_eff'], w, L['kpad'],
                                       L['k'], L['stride'], L['pad'], L['dil'], L['scale'],
                                       L['shift'], res, True, bufs[L['conv_output']],
                                       tile=tile if tile >= ops.TILE_P_FIRST else 0)

@@ -20,7 +20,7 @@ PRE_ATOL = 3e-3     # preprocess vs the float64 oracle, f32 separable passes: ob
                     # 9.7e-4 at Market size, 2.0e-3 on the ragged up-scales (values up
                     # to ~255: ~1e-5 of the range)
 BENCH_TILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                           'profiles', 'r03', 'tiles_v0.json')
+                           'profiles', 'r03', 'tiles_v3.json')
 
 
 def _cuda(x):

@@ -436,3 +436,28 @@ def test_conv_tiled_weights_bits(N, H, W, Cin, Cout, k, planes):
         with pytest.raises(RuntimeError):
             ops.conv2d_bn_act_x3p(xin, Cin, w3t, kpad, k, 1, p, 1, sc, sh, None, True, yb,
                                   tile=t | 0x100)
+
+
+@pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(1, 24, 8, 512, 1024, 2048, 1),
+                                                 (2, 24, 8, 128, 256, 512, 2)])
+def test_conv_dual_tiled_weights_bits(N, H, W, C1, C2, Cout, s2):
+    """The K-concatenated shortcut conv on chunk-tiled weights (the
+    [3][Cout][Kpad1 + Cin2] planes through ops.tile_planes) equals the
+    row-major run bit for bit on the pipelined tiles."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(C1 + C2)
+    x = _cuda(rng.randn(N, H, W, C1).astype(np.float32))
+    x2 = _cuda(rng.randn(N, (H - 1) * s2 + 1, (W - 1) * s2 + 1, C2).astype(np.float32))
+    w1 = (rng.randn(Cout, C1, 1, 1) / np.sqrt(C1)).astype(np.float32)
+    w2 = (rng.randn(Cout, C2, 1, 1) / np.sqrt(C2)).astype(np.float32)
+    p1, k1 = model.pack_conv_weight(w1)
+    p2, _ = model.pack_conv_weight(w2)
+    w3 = ops.split_bf16x3(_cuda(np.concatenate([p1, p2], axis=1)))
+    w3t = ops.tile_planes(w3)
+    sh = _cuda(rng.randn(Cout).astype(np.float32))
+    for t in (29, 35, 36, 38, 42, 47, 52):
+        ya = torch.empty((N, H, W, Cout), device='cuda')
+        yb = torch.full((N, H, W, Cout), float('nan'), device='cuda')
+        ops.conv2d_dual_bn_act(x, C1, 1, 1, 0, x2, s2, w3, k1, sh, True, ya, tile=t)
+        ops.conv2d_dual_bn_act(x, C1, 1, 1, 0, x2, s2, w3t, k1, sh, True, yb, tile=t | 0x100)
+        assert torch.equal(ya, yb), 'tile %d' % t
