@@ -130,18 +130,29 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         # distance-GEMM tile choice on this shard's shape (outside the timed runs)
         from pps_amd import ops
         qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
-        gidx = ops.GalleryIndex(g_local)   # prepared once: the tiles compete on the GEMM
+        # gallery index and query planes prepared once: the tiles compete on the
+        # GEMM alone (what roofline_distmat times)
+        gidx = ops.GalleryIndex(g_local, tiled=D_FEAT % 32 == 0)
+        qt, qsq = ops.split_sqnorm_tiled(qa) if D_FEAT % 32 == 0 else (None, None)
+        dout = ops.dist_buffer(Q_MARKET, g_local.shape[0], 'cuda')
         # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
         cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
         if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
             cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)]
 
+        def launch_dist(t, qp):
+            if qp:
+                ops.distmat_planes(None, qsq, gidx, dout, tile=t, q_tiled=qt, Q=Q_MARKET,
+                                   D=D_FEAT)
+            else:
+                ops.compute_dist(qa, gidx, out=dout, tile=t)
+
         def time_dist(t, qp, n):
-            ops.compute_dist(qa, g_local, tile=t, q_planes=qp, pad_rows=True)
+            launch_dist(t, qp)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(n):
-                ops.compute_dist(qa, g_local, tile=t, q_planes=qp, pad_rows=True)
+                launch_dist(t, qp)
             e1.record()
             e1.synchronize()
             return e0.elapsed_time(e1) / n
@@ -153,7 +164,7 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         best = min(final, key=final.get)
         pdist.HipBackend.distmat_tile = best[0]
         pdist.HipBackend.distmat_qplanes = best[1]
-        del qa
+        del qa, gidx, qt, dout
     # warm-up
     res = ev.run(q_local, g_local)
     torch.cuda.synchronize()
