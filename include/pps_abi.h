@@ -77,6 +77,10 @@ int pps_gemm_num_tiles(void);
  * [3][Cout16/16][Kpad/32][16][32] (pps_tile_planes over the [3][Cout][Kpad]
  * planes; Cout16 = Cout rounded up to 16, Cin % 32 == 0).  Same bits. */
 #define PPS_TILE_B_TILED 0x100
+/* Or-ed into the same tiles: walk the output tiles column block by column
+ * block (consecutive workgroups -- one XCD -- share a weight block instead
+ * of an activation panel).  Same bits. */
+#define PPS_TILE_COL_ORDER 0x200
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,

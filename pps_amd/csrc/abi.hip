@@ -477,9 +477,11 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       int splitk = 1, float* part = nullptr) {
   PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
               "exactly one of x / x planes and one of y / y planes must be given");
-  // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled
+  // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled;
+  // PPS_TILE_COL_ORDER: column-major tile order
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;
-  tile &= ~PPS_TILE_B_TILED;
+  const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
+  tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (wtiled) {
     PPS_ENFORCE(x3 && splitk == 1, "tiled weights: bf16x3 weights, no split-K");
     PPS_ENFORCE(Kpad % 32 == 0 && Cin % 32 == 0, "tiled weights need Cin % 32 == 0");
@@ -525,6 +527,7 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.ldb = Kpad; p.kb_valid = Kpad; p.Ncol = Cout; p.Kloop = Kpad;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  p.colmajor = colmajor ? 1 : 0;
   if (x_pl) {
     p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
     p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
@@ -645,7 +648,8 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   PPS_ENFORCE(hsum == Ho, "strip heights must sum to the output height");
   const bool pl = x3 != nullptr;
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
-  tile &= ~PPS_TILE_B_TILED;
+  const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
+  tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
   PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= kPpsFuseMaxCols,
               "the fused pooling needs a pipelined tile of exactly Ho*Wo = " +
@@ -669,6 +673,7 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   p.b3 = w3; p.b_plane = (int64_t)(wtiled ? (Cout + 15) / 16 * 16 : Cout) * Kpad;
   p.b_bytes = (uint32_t)(p.b_plane * 2);
   p.tiled = wtiled ? 2 : 0;
+  p.colmajor = colmajor ? 1 : 0;
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = Cout;
   p.out = y; p.ldo = Cout; p.relu = 1; p.tile = tile;
   p.pps_out = pps_out; p.pps_S = S; p.pps_max_ave = max_ave ? 1 : 0; p.pps_nimg = N;
@@ -687,7 +692,8 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   PPS_ENFORCE(x && x2 && w && shift && y, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cin2 > 0, "bad shape");
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
-  tile &= ~PPS_TILE_B_TILED;
+  const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
+  tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (wtiled)
     PPS_ENFORCE(x3 && (Kpad1 + Kpad2) % 32 == 0 &&
                     ((tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_WS) ||
@@ -718,6 +724,7 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.ldb = Kpad1 + Kpad2; p.kb_valid = Kpad1 + Kpad2; p.Ncol = Cout;
   p.Kloop = Kpad1 + Kpad2;
   p.scale = nullptr; p.shift = shift; p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
+  p.colmajor = colmajor ? 1 : 0;
   PPS_ENFORCE((int64_t)Cout * (Kpad1 + Kpad2) * 6 < kMaxBufBytes, "weights larger than 2 GiB");
   if (x3) {
     p.b3 = static_cast<const uint16_t*>(w);

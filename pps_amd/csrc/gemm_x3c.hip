@@ -75,8 +75,10 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   const int h = lane / S;
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile_m = bid / tiles_n;  // consecutive ids share a patch (same XCD)
-  const int tile_n = bid - tile_m * tiles_n;
+  // consecutive ids (one XCD) share a patch, or with colmajor a weight block
+  const int tiles_m = gridDim.x / tiles_n;
+  const int tile_m = p.colmajor ? bid % tiles_m : bid / tiles_n;
+  const int tile_n = p.colmajor ? bid / tiles_m : bid - tile_m * tiles_n;
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;
   const int hw = p.Ho * p.Wo;

@@ -174,6 +174,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const int r = bid - grp * per;
       tile_n = r / gm;
       tile_m = first + (r - tile_n * gm);
+    } else if (p.colmajor) {  // consecutive ids (one XCD) share a weight block
+      tile_n = bid / tiles_m;
+      tile_m = bid - tile_n * tiles_m;
     } else {
       tile_m = bid / tiles_n;
       tile_n = bid - tile_m * tiles_n;

@@ -667,6 +667,7 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
   auto fbuf = [&](const std::string& name) { return w.bufs.at(name)->as<float>(); };
   // PPS_TILE_B_TILED in the tile: the chunk-tiled weight copy (plain convs)
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) && L.wt;
+  if (L.op == Op::Heads) tile &= ~PPS_TILE_COL_ORDER;
   if (!wtiled) tile &= ~PPS_TILE_B_TILED;
   const uint16_t* w3 = m.x3 && L.w ? (wtiled ? L.wt->as<uint16_t>() : L.w->as<uint16_t>()) : nullptr;
   const float* wf = !m.x3 && L.w ? L.w->as<float>() : nullptr;
@@ -751,7 +752,9 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const std::vector<int> ok = pps_tiles(m, L, cs);
       const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
       if (!ok.empty()) {
-        int t = std::find(ok.begin(), ok.end(), tile) != ok.end() ? tile : ok[0];
+        const int tb = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
+        int t = std::find(ok.begin(), ok.end(), tb) != ok.end() ? tb : ok[0];
+        t |= tile & PPS_TILE_COL_ORDER;
         if (wtiled) t |= PPS_TILE_B_TILED;
         rc_check(pps_conv2d_bn_act_pps_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
                                            L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc,
@@ -1031,10 +1034,14 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
-    const int base = tile & ~PPS_TILE_B_TILED;
+    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
     PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
-    PPS_MCHECK(base == tile || (L->wt && base >= GEMM_TILE_P_FIRST && base != GEMM_TILE_WS),
-               "PPS_TILE_B_TILED: plain x3 conv with Cin % 32 == 0 on a pipelined tile only");
+    PPS_MCHECK(!(tile & PPS_TILE_B_TILED) ||
+                   (L->wt && base >= GEMM_TILE_P_FIRST && base != GEMM_TILE_WS),
+               "PPS_TILE_B_TILED: x3 conv with Cin % 32 == 0 on a pipelined tile only");
+    PPS_MCHECK(!(tile & PPS_TILE_COL_ORDER) ||
+                   (L->op != Op::Heads && base >= GEMM_TILE_P_FIRST && base != GEMM_TILE_WS),
+               "PPS_TILE_COL_ORDER: conv layers on a pipelined tile only");
     L->tile = tile;
   });
 }
@@ -1190,11 +1197,16 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       for (int i = 0; i < (int)screen.size() && i < finalists; ++i) {
         const float ms = time_layer(*m, L, *w, x, screen[i].second, L.splitk, final_reps, st, t);
         if (ms < best) { best = ms; L.tile = screen[i].second; }
-        // the same tile on the chunk-tiled weight copy
+        // the same tile on the chunk-tiled weight copy and / or in column-major
+        // tile order
         const int tl = screen[i].second;
-        if (L.wt && L.splitk == 1 && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS) {
-          const float mt = time_layer(*m, L, *w, x, tl | PPS_TILE_B_TILED, 1, final_reps, st, t);
-          if (mt < best) { best = mt; L.tile = tl | PPS_TILE_B_TILED; }
+        if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS) {
+          for (int f : {PPS_TILE_B_TILED, PPS_TILE_COL_ORDER,
+                        PPS_TILE_B_TILED | PPS_TILE_COL_ORDER}) {
+            if ((f & PPS_TILE_B_TILED) && !L.wt) continue;
+            const float mt = time_layer(*m, L, *w, x, tl | f, 1, final_reps, st, t);
+            if (mt < best) { best = mt; L.tile = tl | f; }
+          }
         }
       }
       return best;

@@ -160,6 +160,8 @@ struct GemmParams {
   // bit 0 = A, bit 1 = B stored [rows / 16][K / 32][16][32] per plane, so a
   // 16-row DMA piece of one 32-wide K chunk is one contiguous KiB
   int tiled;
+  // conv tiles: enumerate output tiles column-major (PPS_TILE_COL_ORDER)
+  int colmajor;
   int tile;  // GemmTile; 0 = heuristic
   int splitk;           // >= 1; K slices enumerated with the batch on grid.y
   int64_t out_sstride;  // output stride between K slices (EPI_F_RAW)

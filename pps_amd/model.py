@@ -623,8 +623,9 @@ class PPSModel(object):
             res = bufs[L['residual']]
             ok = self.pps_tiles(L)
             if ok:
-                tb = tile & ~ops.TILE_B_TILED
-                t = (tb if tb in ok else ok[0]) | (tile & ops.TILE_B_TILED)
+                flags = tile & (ops.TILE_B_TILED | ops.TILE_COL_ORDER)
+                tb = tile & ~flags
+                t = (tb if tb in ok else ok[0]) | flags
                 ops.conv2d_bn_act_pps(bufs[L['input']], L['cin_eff'], w, L['kpad'], L['k'],
                                       L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                                       res, L['split_arr'], L['max_ave'], bufs[L['output']],

@@ -22,6 +22,7 @@ TILE_P_FIRST = 29  # first pipelined (gemm_x3p.hip) tile id, include/pps_abi.h
 TILE_P16_FIRST = 38  # pipelined tiles on 16x16x32 MFMA blocks (their own rounding)
 TILE_C16_FIRST = 56  # patch-staged 3x3 tiles (gemm_x3c.hip): K in (channel chunk, tap) order
 TILE_B_TILED = 0x100  # PPS_TILE_B_TILED: or-ed into a conv tile, the weights are chunk-tiled
+TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (same bits)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)
 
 

@@ -432,6 +432,12 @@ def test_conv_tiled_weights_bits(N, H, W, Cin, Cout, k, planes):
         ops.conv2d_bn_act_x3p(xin, Cin, w3t, kpad, k, 1, p, 1, sc, sh, None, True, yb,
                               tile=t | 0x100)
         assert torch.equal(ya, yb), 'tile %d' % t
+        # column-major tile order (PPS_TILE_COL_ORDER), either weight layout
+        for f, wl in ((0x200, w3), (0x300, w3t)):
+            yb.fill_(float('nan'))
+            ops.conv2d_bn_act_x3p(xin, Cin, wl, kpad, k, 1, p, 1, sc, sh, None, True, yb,
+                                  tile=t | f)
+            assert torch.equal(ya, yb), 'tile %d flags %#x' % (t, f)
     for t in (1, 28, 54):
         with pytest.raises(RuntimeError):
             ops.conv2d_bn_act_x3p(xin, Cin, w3t, kpad, k, 1, p, 1, sc, sh, None, True, yb,
