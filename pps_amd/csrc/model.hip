@@ -1170,7 +1170,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
     PPS_MCHECK(N > 0, "N must be positive");
     const hipStream_t st = as_stream(stream);
     PPS_MCHECK(!capturing(st), "autotune cannot run inside a graph capture");
-    const int reps = 3, finalists = 4, final_reps = 10;
+    const int reps = 3, finalists = 4, final_reps = 10, final_rounds = 3;
     Workspace* w = &workspace(*m, N, st, true);
     std::vector<float> scratch((size_t)N * m->plan.feat_dim);
     DevBuf feat(scratch.size() * sizeof(float));
@@ -1193,22 +1193,25 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       std::vector<std::pair<float, int>> screen;
       for (int tl : cands_of(L)) screen.emplace_back(time_layer(*m, L, *w, x, tl, L.splitk, reps, st, t), tl);
       std::sort(screen.begin(), screen.end());
-      float best = 1e30f;
+      // finalists, each also on the chunk-tiled weight copy and / or in
+      // column-major tile order; timed in interleaved rounds (min per
+      // variant), so a drifting clock does not favour whichever ran first
+      std::vector<int> var;
       for (int i = 0; i < (int)screen.size() && i < finalists; ++i) {
-        const float ms = time_layer(*m, L, *w, x, screen[i].second, L.splitk, final_reps, st, t);
-        if (ms < best) { best = ms; L.tile = screen[i].second; }
-        // the same tile on the chunk-tiled weight copy and / or in column-major
-        // tile order
         const int tl = screen[i].second;
-        if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS) {
+        var.push_back(tl);
+        if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS)
           for (int f : {PPS_TILE_B_TILED, PPS_TILE_COL_ORDER,
-                        PPS_TILE_B_TILED | PPS_TILE_COL_ORDER}) {
-            if ((f & PPS_TILE_B_TILED) && !L.wt) continue;
-            const float mt = time_layer(*m, L, *w, x, tl | f, 1, final_reps, st, t);
-            if (mt < best) { best = mt; L.tile = tl | f; }
-          }
-        }
+                        PPS_TILE_B_TILED | PPS_TILE_COL_ORDER})
+            if (!(f & PPS_TILE_B_TILED) || L.wt) var.push_back(tl | f);
       }
+      std::vector<float> tmin(var.size(), 1e30f);
+      for (int r = 0; r < final_rounds; ++r)
+        for (size_t v = 0; v < var.size(); ++v)
+          tmin[v] = std::min(tmin[v], time_layer(*m, L, *w, x, var[v], L.splitk, final_reps, st, t));
+      float best = 1e30f;
+      for (size_t v = 0; v < var.size(); ++v)
+        if (tmin[v] < best) { best = tmin[v]; L.tile = var[v]; }
       return best;
     };
     const bool tune_planes = (flags & PPS_AUTOTUNE_NO_PLANES) == 0 && m->act_planes;
