@@ -17,10 +17,16 @@ build/%.o: pps_amd/csrc/%.hip pps_amd/csrc/pps_internal.hpp pps_amd/csrc/gemm_co
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJS)
+# relink when a source file is added or removed (not only when one changes)
+build/srcs.list: FORCE
+	@mkdir -p build
+	@echo '$(SRCS)' | cmp -s - $@ || echo '$(SRCS)' > $@
+
+$(LIB): $(OBJS) build/srcs.list
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean
+.PHONY: all clean FORCE
+FORCE:
