@@ -473,3 +473,34 @@ def test_topk_long_rows_wave_kernel(G, k):
     ref = np.argsort(d, axis=1, kind='stable')[:, :k]
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
     np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, ref, axis=1))
+
+
+@pytest.mark.parametrize('case', ['market_small', 'full_dim'])
+def test_sharded_evaluator_tiled_query_planes(golden, case):
+    """The distance path bench.py tunes (queries and gallery as chunk-tiled
+    bf16x3 planes, pps_distmat_x3p_tiled) inside the evaluator equals the
+    default path: the same distance bits, the same mAP / CMC, and the mAP of
+    the reference's own evaluation."""
+    from pps_amd import distributed as pdist
+    g = golden(case)
+    if 'qid' not in g:
+        pytest.skip('no ids in this fixture')
+    qf, gf = _cuda(g['qf']), _cuda(g['gf'])
+    ev_ = pdist.ShardedEvaluator(g['qid'], g['qcam'], g['gid'], g['gcam'], 0, 1)
+    be = pdist.HipBackend
+    saved = (be.distmat_tile, be.distmat_qplanes)
+    outs = []
+    try:
+        for tile, qp in ((0, False), (52, True), (47, True)):
+            be.distmat_tile, be.distmat_qplanes = tile, qp
+            outs.append(ev_.run(qf, gf, keep_dist=True))
+    finally:
+        be.distmat_tile, be.distmat_qplanes = saved
+    if g['qf'].shape[1] % 32 == 0:
+        assert torch.equal(outs[1]['dist'], outs[2]['dist'])
+    for o in outs[1:]:
+        np.testing.assert_allclose(o['dist'].cpu().numpy(), outs[0]['dist'].cpu().numpy(),
+                                   rtol=0, atol=1e-5)
+        assert abs(o['mAP'] - outs[0]['mAP']) < 1e-9
+        np.testing.assert_array_equal(o['cmc'], outs[0]['cmc'])
+    assert abs(outs[1]['mAP'] - float(g['mAP'])) < 1e-6
