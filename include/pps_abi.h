@@ -392,6 +392,25 @@ int pps_conv2d_bn_act_x3p_splitk(const float* x, const uint16_t* x3, int64_t x_p
                                  uint16_t* y3, int64_t y_plane, int Ho, int Wo,
                                  int ldy, int splitk, float* part, int tile,
                                  void* stream);
+/* The same split-K in ONE launch (no summing pass): each slice parks its
+ * raw partial tile in part [splitk][N*Ho*Wo][Cout] and bumps a per-tile
+ * arrival counter; the last slice of a tile to arrive sums the partials in
+ * slice order and applies the epilogue -- the bits of
+ * pps_conv2d_bn_act_x3p_splitk.  counters: n_counters >= output tiles of
+ * the tile shape, all zero on entry, zero again on return (so a captured
+ * graph may replay it).  ReLU epilogues only (+ residual with f32 y, or
+ * y3 planes); tiles 45 / 47 / 48 / 49 / 50, PPS_TILE_B_TILED allowed.
+ * Same layer as pps_conv2d_bn_act_x3p: a bottleneck conv + AffineChannel
+ * [+ Sum] + Relu (ResNet.py:276-333). */
+int pps_conv2d_bn_act_x3p_splitk_fused(const float* x, const uint16_t* x3, int64_t x_plane,
+                                       int N, int H, int W, int Cin, int ldx,
+                                       const uint16_t* w3, int Cout, int Kpad, int KH,
+                                       int KW, int stride, int pad, int dil,
+                                       const float* scale, const float* shift,
+                                       const float* residual, int relu, float* y,
+                                       uint16_t* y3, int64_t y_plane, int Ho, int Wo,
+                                       int ldy, int splitk, float* part, int* counters,
+                                       int64_t n_counters, int tile, void* stream);
 int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin,
                               int ldx, int KH, int KW, int stride, int pad,
                               const float* x2, int H2, int W2, int Cin2,

@@ -82,6 +82,11 @@ SIGNATURES = {
                                      c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_i64, c_int,
                                      c_int, c_int, c_int, c_ptr, c_int, c_ptr],
+    'pps_conv2d_bn_act_x3p_splitk_fused': [c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int,
+                                           c_int, c_ptr, c_int, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr,
+                                           c_ptr, c_i64, c_int, c_int, c_int, c_int, c_ptr,
+                                           c_ptr, c_i64, c_int, c_ptr],
     'pps_conv2d_dual_bn_act_x3': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_ptr, c_int, c_int, c_int, c_int, c_int,
                                   c_ptr, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int,

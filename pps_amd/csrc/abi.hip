@@ -474,7 +474,8 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
                       int tile, void* stream, const uint16_t* x_pl = nullptr,
                       int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0,
-                      int splitk = 1, float* part = nullptr) {
+                      int splitk = 1, float* part = nullptr, int* fix_cnt = nullptr,
+                      int64_t n_cnt = 0) {
   PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
               "exactly one of x / x planes and one of y / y planes must be given");
   // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled;
@@ -483,7 +484,7 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
   tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (wtiled) {
-    PPS_ENFORCE(x3 && splitk == 1, "tiled weights: bf16x3 weights, no split-K");
+    PPS_ENFORCE(x3 && (splitk == 1 || fix_cnt), "tiled weights: bf16x3 weights, no two-pass split-K");
     PPS_ENFORCE(Kpad % 32 == 0 && Cin % 32 == 0, "tiled weights need Cin % 32 == 0");
     PPS_ENFORCE((tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_WS) ||
                     (tile > GEMM_TILE_WS && tile < GEMM_NUM_TILES),
@@ -546,6 +547,29 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     p.Kloop = Kpad / splitk; p.kb_valid = p.Kloop;
     p.b3 = static_cast<const uint16_t*>(w); p.b_plane = (int64_t)Cout * Kpad;
     p.b_bytes = (uint32_t)(p.b_plane * 2);
+    if (fix_cnt) {
+      // one launch: the last K slice of each tile to finish sums the parked
+      // partials (slice order) and runs BN [+ residual] + ReLU [-> planes]
+      PPS_ENFORCE(relu, "one-launch split-K: conv + BN + ReLU epilogues only");
+      PPS_ENFORCE(!(residual && y_pl), "one-launch split-K: residual with f32 output only");
+      const int t = tile ? tile : GEMM_TILE_P16_FIRST + 7;
+      const int bm = x3p_tile_rows(t, x_pl != nullptr), bn = x3p_tile_cols(t, x_pl != nullptr);
+      PPS_ENFORCE(bm > 0 && bn > 0, "one-launch split-K needs a pipelined tile");
+      const int64_t ntile = ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
+      PPS_ENFORCE(n_cnt >= ntile, "one-launch split-K: " + std::to_string(ntile) +
+                                      " tile counters needed, " + std::to_string(n_cnt) + " given");
+      if (wtiled) {
+        p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * Kpad;
+        p.tiled = 2;
+        p.b_bytes = (uint32_t)(p.b_plane * 2);
+      }
+      p.tile = t;
+      p.part = part; p.part_sstride = M * Cout; p.fix_cnt = fix_cnt;
+      p.out_sstride = 0;
+      if (y_pl) { p.out = nullptr; p.out3 = y_pl; p.out_plane = y_plane; }
+      return launch_gemm_x3(p, (y_pl ? EPI_CONV | EPI_F_PLANES : EPI_CONV) | EPI_F_FIX, 1,
+                            as_stream(stream));
+    }
     p.out = part; p.out3 = nullptr; p.ldo = Cout; p.out_sstride = M * Cout;
     p.residual = nullptr; p.relu = 0;
     p.tile = tile ? tile : GEMM_TILE_P_FIRST + 8;
@@ -597,6 +621,21 @@ int pps_conv2d_bn_act_x3p_splitk(const float* x, const uint16_t* x3, int64_t x_p
   return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
                    shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x3, x_plane, y3,
                    y_plane, splitk, part);
+}
+
+int pps_conv2d_bn_act_x3p_splitk_fused(const float* x, const uint16_t* x3, int64_t x_plane,
+                                       int N, int H, int W, int Cin, int ldx, const uint16_t* w3,
+                                       int Cout, int Kpad, int KH, int KW, int stride, int pad,
+                                       int dil, const float* scale, const float* shift,
+                                       const float* residual, int relu, float* y, uint16_t* y3,
+                                       int64_t y_plane, int Ho, int Wo, int ldy, int splitk,
+                                       float* part, int* counters, int64_t n_counters, int tile,
+                                       void* stream) {
+  PPS_ENFORCE(splitk >= 2 && splitk <= 16, "splitk must be in [2, 16]");
+  PPS_ENFORCE(counters != nullptr, "null tile counters");
+  return conv_impl(x, N, H, W, Cin, ldx, w3, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x3, x_plane, y3,
+                   y_plane, splitk, part, counters, n_counters);
 }
 
 int pps_conv2d_bn_act_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N, int H,

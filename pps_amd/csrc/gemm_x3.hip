@@ -269,8 +269,14 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
-  if ((p.tiled & 2) && (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST || p.splitk > 1)) {
+  if ((p.tiled & 2) && (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST ||
+                       (p.splitk > 1 && !p.ksplit_conv))) {
     set_error("chunk-tiled weights run on the pipelined / patch tiles only");
+    return PPS_ERR_INVALID_ARG;
+  }
+  if ((epi & EPI_F_FIX) && (!p.ksplit_conv || !p.fix_cnt || !p.part || p.tile < GEMM_TILE_P_FIRST ||
+                           p.tile == GEMM_TILE_WS || p.tile >= GEMM_TILE_C16_FIRST)) {
+    set_error("one-launch conv split-K needs a pipelined tile, partials and counters");
     return PPS_ERR_INVALID_ARG;
   }
   if (p.tile == GEMM_TILE_WS) {

@@ -247,7 +247,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // ---- B pieces: plane pl, piece q = wave*BPW + j covers tile columns
   // 16q..16q+15; lane l takes column 16q + (l >> 2) and fills physical chunk
   // l & 3 with logical chunk (l & 3) ^ ((col >> 2) & 3) = (l & 3) ^ ((l >> 4) & 3)
-  const uint16_t* b3 = p.b3 + batch * p.b_bstride + kofs0;
+  // (chunk-tiled B: a 32-wide K chunk is 512 elements of a 16-column block)
+  const uint16_t* b3 = p.b3 + batch * p.b_bstride + ((p.tiled & 2) ? kofs0 * 16 : kofs0);
   const rsrc_t rb0 = make_rsrc(b3, p.b_bytes);
   const rsrc_t rb1 = make_rsrc(b3 + p.b_plane, p.b_bytes);
   const rsrc_t rb2 = make_rsrc(b3 + 2 * p.b_plane, p.b_bytes);
@@ -504,6 +505,11 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
 #endif
 
+  if constexpr ((EPI & EPI_F_FIX) != 0) {
+    if (!fix_reduce<BM, BN, WM, WN, S>(p, acc, lds, kslice, blockIdx.x + gridDim.x * batch, m0,
+                                       n0, wm, wn, r32, h))
+      return;
+  }
   if constexpr (DISTLDS) {
     if (p.sym)
       dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
@@ -531,9 +537,38 @@ static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
 
 // NSF / NSP: LDS stages with f32 / bf16-plane A operands (NSP = 0: the tile
 // does not take plane activations)
-template <int BM, int BN, int WM, int WN, int NSF, int NSP, int S>
+// FX: also built with the one-launch split-K epilogues (EPI_F_FIX)
+template <int BM, int BN, int WM, int WN, int NSF, int NSP, int S, bool FX = false>
 static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
+  if (epi & EPI_F_FIX) {
+    if constexpr (FX && NSP != 0) {
+      constexpr int F = EPI_F_FIX;
+      const bool a3 = p.a3 != nullptr;
+      switch (epi) {
+        case C | RL | F:
+          if (a3) launch_one_p<BM, BN, WM, WN, NSP, C | RL | F, true, S>(p, batch, stream);
+          else launch_one_p<BM, BN, WM, WN, NSF, C | RL | F, false, S>(p, batch, stream);
+          break;
+        case C | RL | PL | F:
+          if (a3) launch_one_p<BM, BN, WM, WN, NSP, C | RL | PL | F, true, S>(p, batch, stream);
+          else launch_one_p<BM, BN, WM, WN, NSF, C | RL | PL | F, false, S>(p, batch, stream);
+          break;
+        case C | RS | RL | F:
+          if (a3) launch_one_p<BM, BN, WM, WN, NSP, C | RS | RL | F, true, S>(p, batch, stream);
+          else launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | F, false, S>(p, batch, stream);
+          break;
+        default:
+          set_error("one-launch split-K: conv + BN + ReLU [+ residual | planes] only");
+          return PPS_ERR_INVALID_ARG;
+      }
+      PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+      return PPS_OK;
+    } else {
+      set_error("tile not built for one-launch split-K");
+      return PPS_ERR_INVALID_ARG;
+    }
+  }
   if constexpr (NSP == 0) {
     if (p.a3) {
       set_error("tile not built for bf16-plane activations");
@@ -647,7 +682,7 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
     // 8-wave versions of 128x128 / 192x128 (two waves per SIMD in one
     // workgroup; 128x128 also two workgroups per CU): res3/res4 3x3 and
     // res4 2c run 6-10 % faster on them
-    case 7: return launch_tile_p<128, 128, 4, 2, 2, 2, S>(p, epi, batch, stream);
+    case 7: return launch_tile_p<128, 128, 4, 2, 2, 2, S, S == 16>(p, epi, batch, stream);
     case 8:  // plane A: 12 pieces of 16 rows over 8 waves (uneven, two stages)
       return launch_tile_p<192, 128, 2, 4, 2, 2, S>(p, epi, batch, stream);
     default:
@@ -705,15 +740,15 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
   // plane A on the 192-row 8-wave and 96-row tiles: 12 / 6 pieces of 16 rows
   // spread unevenly over the waves (two stages)
   if (variant == GEMM_TILE_P16_192x128W42 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<192, 128, 4, 2, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<192, 128, 4, 2, 2, 2, 16, true>(p, epi, batch, stream);
   if (variant == GEMM_TILE_P16_192x64W41 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<192, 64, 4, 1, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<192, 64, 4, 1, 2, 2, 16, true>(p, epi, batch, stream);
   if (variant == GEMM_TILE_P16_96x128W22 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<96, 128, 2, 2, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<96, 128, 2, 2, 2, 2, 16, true>(p, epi, batch, stream);
   // 96x128 with 8 waves as 2 x 4 (48 x 32 per wave): 256 tiles for
   // M = 12,288 x N = 256 at two waves per SIMD
   if (variant == GEMM_TILE_P16_96x128W24 - GEMM_TILE_P_FIRST)
-    return launch_tile_p<96, 128, 2, 4, 2, 2, 16>(p, epi, batch, stream);
+    return launch_tile_p<96, 128, 2, 4, 2, 2, 16, true>(p, epi, batch, stream);
   // three LDS stages (two chunks in flight behind the one being consumed) on
   // the 8-wave 128x128 / 192x128 tiles, for long-K GEMMs whose operands come
   // from the Infinity Cache rather than L2 (distance matrix, res5);

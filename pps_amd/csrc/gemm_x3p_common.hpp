@@ -143,6 +143,67 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   }
 }
 
+// One-launch conv split-K (EPI_F_FIX): park this K slice's raw accumulators
+// as a dense [M][Ncol] partial tile, count the slice in with an agent-scope
+// atomic after a release fence; the slice that arrives last (any slice) resets
+// the counter, acquires, and reloads acc as part[0] + part[1] + ... in slice
+// order -- the sums splitk_conv_epilogue_kernel forms, so the epilogue that
+// follows gives its bits.  No workgroup waits on another (no spin), so
+// residency does not matter.  Returns false in the slices that leave.
+template <int BM, int BN, int WM, int WN, int S>
+__device__ inline bool fix_reduce(const GemmParams& p,
+                                  typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                  unsigned char* lds, int kslice, int tile_id, int m0, int n0,
+                                  int wm, int wn, int r32, int h) {
+  constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
+  const int ld = p.Ncol;
+  const int mrem = p.M - m0, nrem = p.Ncol - n0;
+  float* base = p.part + (int64_t)m0 * ld + n0;
+  auto each = [&](auto&& fn) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rr = wm * (BM / WM) + i * S + r32;
+      if (rr >= mrem) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int cb = wn * (BN / WN) + j * S + 4 * h;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          if (cb + 8 * q < nrem) fn(i, j, q, (int64_t)rr * ld + cb + 8 * q);
+      }
+    }
+  };
+  float* mine = base + kslice * p.part_sstride;
+  each([&](int i, int j, int q, int64_t o) {
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+    *reinterpret_cast<f32x4*>(mine + o) = v;
+  });
+#ifndef X3P_FIX_FENCE
+#define X3P_FIX_FENCE 1  // probes only: 0 drops both fences (wrong results, fence cost)
+#endif
+  if (X3P_FIX_FENCE) __threadfence();  // release: this thread's partial stores before the count
+  __syncthreads();  // every wave parked (and is done with the LDS stages)
+  int* flag = reinterpret_cast<int*>(lds);
+  if (threadIdx.x == 0) {
+    const int old = atomicAdd(p.fix_cnt + tile_id, 1);
+    const int last = old == p.splitk - 1;
+    if (last) atomicExch(p.fix_cnt + tile_id, 0);  // zero for the next launch
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  if (X3P_FIX_FENCE) __threadfence();  // acquire: the other slices' partials
+  each([&](int i, int j, int q, int64_t o) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(base + o);
+    for (int s = 1; s < p.splitk; ++s) v += *reinterpret_cast<const f32x4*>(base + s * p.part_sstride + o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = v[e];
+  });
+  return true;
+}
+
 // The same conv epilogue staged through LDS: the waves park their
 // accumulators as a [BM][BN+4] f32 tile, then the workgroup walks it row by
 // row, so scale/shift, the residual and the output move as whole contiguous

@@ -342,6 +342,8 @@ struct Workspace {
   std::map<std::string, Buf> bufs;  // plane-capable tensors hold 6 B per element
   Buf part;                         // conv split-K partials
   size_t part_floats = 0;
+  Buf cnt;                          // one-launch split-K tile counters (zero between launches)
+  size_t cnt_ints = 0;
   Buf nhwc4;                        // input staging for pps_forward_nchw / _bgr
 };
 
@@ -594,6 +596,33 @@ size_t part_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) 
   return need;
 }
 
+// tiles built with the one-launch split-K epilogue (gemm_x3p.hip FX)
+bool fix_tile(int tile) {
+  const int t = tile & 0xff;
+  return t == GEMM_TILE_P16_FIRST + 7 ||
+         (t >= GEMM_TILE_P16_192x128W42 && t <= GEMM_TILE_P16_96x128W24);
+}
+
+// tile counters for the one-launch split-K: an upper bound on the output
+// tiles of any split conv (the smallest FIX tile is 96 x 128 / 192 x 64)
+size_t cnt_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) {
+  size_t need = 0;
+  for (const auto& L : m.layers)
+    if (L.op == Op::Conv && L.splitk > 1) {
+      const Shape& y = shapes.at(L.output);
+      const size_t M = (size_t)(y.d[0] * y.d[1] * y.d[2]);
+      need = std::max(need, ((M + 95) / 96) * (((size_t)L.cout + 63) / 64));
+    }
+  return need;
+}
+
+void grow_counters(Workspace& w, size_t need, hipStream_t st) {
+  if (need <= w.cnt_ints) return;
+  w.cnt = std::make_shared<DevBuf>(need * sizeof(int));
+  hip_check(hipMemsetAsync(w.cnt->p, 0, need * sizeof(int), st), "hipMemsetAsync");
+  w.cnt_ints = need;
+}
+
 bool capturing(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
@@ -610,6 +639,12 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
                  "split-K partials grew after pps_model_reserve: reserve again outside capture");
       w.part = std::make_shared<DevBuf>(need * sizeof(float));
       w.part_floats = need;
+    }
+    const size_t cneed = cnt_need(m, w.shapes);
+    if (cneed > w.cnt_ints) {
+      PPS_MCHECK(allow_alloc && !capturing(st),
+                 "split-K counters grew after pps_model_reserve: reserve again outside capture");
+      grow_counters(w, cneed, st);
     }
     return w;
   }
@@ -634,6 +669,7 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
   }
   w.part_floats = part_need(m, w.shapes);
   if (w.part_floats) w.part = std::make_shared<DevBuf>(w.part_floats * sizeof(float));
+  grow_counters(w, cnt_need(m, w.shapes), st);
   return m.ws.emplace(N, std::move(w)).first->second;
 }
 
@@ -665,6 +701,11 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     return a;
   };
   auto fbuf = [&](const std::string& name) { return w.bufs.at(name)->as<float>(); };
+  // split convs run in one launch on the FIX tiles (same bits as the
+  // two-pass split-K), else raw partials + the summing pass (plain weights)
+  const bool fused_sk = sk > 1 && L.op == Op::Conv && fix_tile(tile) && L.relu &&
+                        !(L.planes_out && !L.residual.empty());
+  if (sk > 1 && !fused_sk) tile &= ~PPS_TILE_B_TILED;
   // PPS_TILE_B_TILED in the tile: the chunk-tiled weight copy (plain convs)
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) && L.wt;
   if (L.op == Op::Heads) tile &= ~PPS_TILE_COL_ORDER;
@@ -686,7 +727,12 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
         float* yf = L.planes_out ? nullptr : fbuf(L.output);
         uint16_t* y3 = L.planes_out ? w.bufs.at(L.output)->as<uint16_t>() : nullptr;
         const int64_t ypl = L.planes_out ? ys.numel() : 0;
-        if (sk > 1)
+        if (fused_sk)
+          rc_check(pps_conv2d_bn_act_x3p_splitk_fused(
+              a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout, L.kpad, L.k, L.k, L.stride,
+              L.pad, L.dil, sc, sh, res, L.relu, yf, y3, ypl, Ho, Wo, L.cout, sk,
+              w.part->as<float>(), w.cnt->as<int>(), (int64_t)w.cnt_ints, t, st));
+        else if (sk > 1)
           rc_check(pps_conv2d_bn_act_x3p_splitk(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
                                                 L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil,
                                                 sc, sh, res, L.relu, yf, y3, ypl, Ho, Wo, L.cout,
@@ -1247,8 +1293,13 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
           L.splitk = sk;
           w = &workspace(*m, N, st, true);  // grow the partials buffer
           L.splitk = save;
-          for (int tl = GEMM_TILE_P_FIRST; tl < GEMM_TILE_C16_FIRST; ++tl)  // not 3x3-patch ids
-            screen.push_back({time_layer(*m, L, *w, x, tl, sk, reps, st, t), {tl, sk}});
+          // the one-launch split-K tiles, on plain and chunk-tiled weights
+          for (int tl = GEMM_TILE_P16_FIRST + 7; tl <= GEMM_TILE_P16_96x128W24; ++tl) {
+            if (!fix_tile(tl)) continue;
+            for (int f : {0, PPS_TILE_B_TILED})
+              if (!f || L.wt)
+                screen.push_back({time_layer(*m, L, *w, x, tl | f, sk, reps, st, t), {tl | f, sk}});
+          }
         }
         if (screen.empty()) continue;
         std::sort(screen.begin(), screen.end());

@@ -55,7 +55,9 @@ constexpr int64_t kMaxBufBytes = (int64_t)1 << 31;  // buffer-resource addressin
 enum Epi {
   EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16,
   EPI_F_PLANES = 32,  // gemm_x3p.hip: result written as three bf16 planes (out3)
-  EPI_F_PPS = 64      // gemm_x3p.hip: + strip pooling and part power set of each image
+  EPI_F_PPS = 64,     // gemm_x3p.hip: + strip pooling and part power set of each image
+  EPI_F_FIX = 128     // gemm_x3p.hip conv split-K: the last K slice of a tile to finish
+                      // sums the parked partials and runs the epilogue (no second pass)
 };
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
@@ -189,6 +191,13 @@ struct GemmParams {
   float* pps_out;
   int pps_S, pps_max_ave, pps_nimg, pps_write_y;
   int pps_h[10];
+  // EPI_F_FIX (conv split-K, one launch): each K slice parks its raw partial
+  // tile at part + slice * part_sstride ([M][Ncol] dense); a per-tile arrival
+  // counter fix_cnt[tile] (zero between launches, reset by the last arrival)
+  // picks the slice that sums all partials in slice order and finishes
+  float* part;
+  int64_t part_sstride;
+  int* fix_cnt;
 };
 constexpr int kPpsFuseMaxStrips = 10;
 constexpr int kPpsFuseMaxCols = 256;  // widest tile the fused pooling takes (two column passes)

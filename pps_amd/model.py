@@ -587,6 +587,12 @@ class PPSModel(object):
         tile = L.get('tile', 0) if tile is None else tile
         sk = L.get('splitk', 1) if splitk is None else splitk
         w = L.get('w')
+        # split convs run in one launch on the FIX tiles (same bits as the
+        # two-pass split-K, which takes plain weights only)
+        fused_sk = (op == 'conv' and sk > 1 and (tile & 0xff) in ops.FIX_TILES and L['relu']
+                    and not (L.get('planes_out') and L['residual']))
+        if sk > 1 and not fused_sk:
+            tile &= ~ops.TILE_B_TILED
         if op in ('conv', 'conv_dual', 'conv_pps') and tile > 0 and tile & ops.TILE_B_TILED:
             # the chunk-tiled weight copy (pps_model_autotune may pick it)
             if '_wt' not in L:
@@ -599,7 +605,9 @@ class PPSModel(object):
                                   L['stride'], L['pad'], L['dil'], L['scale'], L['shift'],
                                   res, L['relu'], bufs[L['output']], tile=tile, splitk=sk,
                                   part=self._part_for(sk * np.prod(self._shapes[L['output']]))
-                                  if sk > 1 else None)
+                                  if sk > 1 else None,
+                                  counters=self._cnt_for(np.prod(self._shapes[L['output']][:3]),
+                                                         L['cout']) if fused_sk else None)
         elif op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act(bufs[L['input']], L['cin_eff'], w, L['kpad'], L['k'],
@@ -780,6 +788,14 @@ class PPSModel(object):
         if self._part is None or self._part.numel() < n:
             self._part = torch.empty((int(n),), dtype=torch.float32, device=self.device)
         return self._part
+
+    def _cnt_for(self, M, cout):
+        """Zeroed tile counters of the one-launch split-K (>= the output tiles
+        of the smallest FIX tile; the kernel leaves them zero)."""
+        n = -(-int(M) // 96) * -(-int(cout) // 64)
+        if getattr(self, '_cnt', None) is None or self._cnt.numel() < n:
+            self._cnt = torch.zeros((n,), dtype=torch.int32, device=self.device)
+        return self._cnt
 
     def splitks(self):
         """{layer name: split-K factor} of the conv layers that use split-K."""

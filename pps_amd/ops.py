@@ -23,6 +23,8 @@ TILE_P16_FIRST = 38  # pipelined tiles on 16x16x32 MFMA blocks (their own roundi
 TILE_C16_FIRST = 56  # patch-staged 3x3 tiles (gemm_x3c.hip): K in (channel chunk, tap) order
 TILE_B_TILED = 0x100  # PPS_TILE_B_TILED: or-ed into a conv tile, the weights are chunk-tiled
 TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (same bits)
+# tiles built with the one-launch split-K epilogue (conv2d_bn_act_x3p(..., counters=))
+FIX_TILES = (45, 47, 48, 49, 50)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)
 
 
@@ -612,10 +614,13 @@ def _is_planes(t):
 
 
 def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, residual, relu,
-                      y, tile=0, splitk=1, part=None):
+                      y, tile=0, splitk=1, part=None, counters=None):
     """conv2d_bn_act on the pipelined bf16x3 GEMM where the input and/or the
     output are bf16x3 activation planes (act_planes) instead of f32 NHWC:
-    x / y may each be either.  Same bits as the f32-activation call."""
+    x / y may each be either.  Same bits as the f32-activation call.
+    splitk > 1: K slices with raw partials in `part`, summed in slice order by
+    a second pass -- or, with `counters` (int32, zero, >= output tiles), by
+    the last slice of each tile in the same launch (same bits)."""
     xs = x.shape[1:] if _is_planes(x) else x.shape
     ys = y.shape[1:] if _is_planes(y) else y.shape
     N, H, W, ldx = xs
@@ -641,6 +646,14 @@ def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, resid
         if part is None or part.numel() < splitk * M * Cout:
             raise RuntimeError('split-K needs a partials buffer of >= %d floats'
                                % (splitk * M * Cout))
+        if counters is not None:
+            call('pps_conv2d_bn_act_x3p_splitk_fused', xp, x3, xpl, N, H, W, cin, ldx,
+                 _dev(w3, 'w', torch.int16), Cout, kpad, k, k, stride, pad, dil,
+                 _dev(scale, 'scale'), _dev(shift, 'shift'), rp, int(bool(relu)), yp, y3, ypl,
+                 Ho, Wo, Cout, int(splitk), _dev(part, 'part'),
+                 _dev(counters, 'counters', torch.int32), counters.numel(), int(tile),
+                 _stream())
+            return y
         call('pps_conv2d_bn_act_x3p_splitk', xp, x3, xpl, N, H, W, cin, ldx,
              _dev(w3, 'w', torch.int16), Cout, kpad, k, k, stride, pad, dil,
              _dev(scale, 'scale'), _dev(shift, 'shift'), rp, int(bool(relu)), yp, y3, ypl, Ho,

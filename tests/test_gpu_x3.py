@@ -371,6 +371,63 @@ def test_conv_x3_splitk(N, H, W, Cin, Cout, k, s, p, splitk, mode):
         assert e_split <= X3_VS_F32 * e_one + ERR_FLOOR, (tile, e_split, e_one)
 
 
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (64, 24, 8, 256, 256, 3, 1, 1),    # res4 branch2b at the bench batch
+    (4, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
+    (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+])
+@pytest.mark.parametrize('splitk', [2, 3, 4])
+@pytest.mark.parametrize('mode', ['f32', 'planes_in', 'planes_out', 'residual', 'tiled_w'])
+def test_conv_x3_splitk_fused_bits(N, H, W, Cin, Cout, k, s, p, splitk, mode):
+    """One-launch split-K (last arriving K slice sums the parked partials)
+    gives the bits of the two-pass split-K on every FIX tile, for f32 / plane
+    inputs and outputs, a residual and chunk-tiled weights, and leaves the
+    tile counters zero (a replayed graph starts clean).  Repeated launches
+    give the same bits (the arrival order does not change the sum order)."""
+    from pps_amd import model, ops
+    Kpad = k * k * Cin
+    if Kpad % (32 * splitk):
+        pytest.skip('K does not split into whole 32-wide chunks')
+    rng = np.random.RandomState(Cin + Cout + splitk + 7)
+    xn = rng.randn(N, H, W, Cin).astype(np.float32)
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    sc = _cuda(rng.uniform(0.5, 1.5, Cout).astype(np.float32))
+    sh = _cuda((rng.randn(Cout) * 0.1).astype(np.float32))
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    shape = (N, Ho, Wo, Cout)
+    res = _cuda(rng.randn(*shape).astype(np.float32)) if mode == 'residual' else None
+    wp, kpad = model.pack_conv_weight(w)
+    w3 = ops.split_bf16x3(_cuda(wp))
+    x = _cuda(xn)
+    xin = _planes_of(x) if mode == 'planes_in' else x
+    part = torch.empty(splitk * N * Ho * Wo * Cout, device='cuda')
+    cnt = torch.zeros(4096, dtype=torch.int32, device='cuda')
+
+    def out():
+        if mode == 'planes_out':
+            return ops.act_planes(shape, 'cuda')
+        return torch.full(shape, float('nan'), device='cuda')
+
+    for tile in (45, 47, 48, 49, 50):
+        ref = out()
+        ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, s, p, 1, sc, sh, res, True, ref,
+                              tile=tile, splitk=splitk, part=part)
+        wf, tf = w3, tile
+        if mode == 'tiled_w':
+            wf, tf = ops.tile_planes(w3), tile | ops.TILE_B_TILED
+        for rep in range(2):
+            y = out()
+            ops.conv2d_bn_act_x3p(xin, Cin, wf, kpad, k, s, p, 1, sc, sh, res, True, y,
+                                  tile=tf, splitk=splitk, part=part, counters=cnt)
+            torch.cuda.synchronize()
+            assert torch.equal(y.view(torch.int32), ref.view(torch.int32)) if mode != 'planes_out' \
+                else torch.equal(y, ref), (tile, rep)
+            assert int(cnt.abs().sum()) == 0, (tile, rep)
+    with pytest.raises(RuntimeError):  # tile counters too few
+        ops.conv2d_bn_act_x3p(xin, Cin, w3, kpad, k, s, p, 1, sc, sh, res, True, out(),
+                              tile=45, splitk=splitk, part=part, counters=cnt[:0])
+
+
 def test_forward_splitk_layers():
     """The model with split-K on the res5 convs (and plane edges) gives the
     one-pass features within the f32 forward tolerance."""
