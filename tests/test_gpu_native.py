@@ -97,6 +97,46 @@ def test_native_bench_table_bit_identical():
     assert np.array_equal(b, d)
 
 
+def test_native_fused_splitk_layers():
+    """Split-K on FIX tiles (one launch, tile counters in the workspace,
+    plain and chunk-tiled weights, plane edges in and out) in the C plan
+    equals the Python orchestrator bit for bit, and a captured graph replays
+    it to the same bits (the counters come back to zero every launch)."""
+    from pps_amd import ops
+    _, pm, nm = _models()
+    _, x = _input(4, seed=3)
+    base = nm.forward(x).cpu().numpy()
+    tiles, sks = {}, {}
+    fix = [t for t in ops.FIX_TILES]
+    for i, L in enumerate(pm.layers):
+        if L['op'] == 'conv' and L['name'][:4] in ('res4', 'res5') and L['relu']:
+            sk = 2 if L['kpad'] % 64 == 0 else 1
+            if sk == 1:
+                continue
+            sks[L['name']] = sk
+            tiles[L['name']] = fix[i % len(fix)] | (ops.TILE_B_TILED if i % 2 else 0)
+    assert sks
+    pm.set_tiles(tiles)
+    pm.set_planes([n for n in ('res4_1_branch2a', 'res5_1_branch2a') if n in sks])
+    pm.set_splitks(sks)
+    nm.apply_table(pm)
+    assert nm.splitks() == sks
+    a = pm.forward(x).cpu().numpy()
+    b = nm.forward(x).cpu().numpy()
+    assert np.array_equal(a, b)
+    np.testing.assert_allclose(b, base, rtol=0, atol=2e-5)
+    nm.reserve(4)
+    out = torch.empty((4, nm.feat_dim), device='cuda')
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nm.forward(x, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), b)
+
+
 def test_native_graph_capture():
     """pps_forward is stream-ordered and capturable once N is reserved."""
     _, pm, nm = _models()
