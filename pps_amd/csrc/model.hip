@@ -1216,7 +1216,10 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
     PPS_MCHECK(N > 0, "N must be positive");
     const hipStream_t st = as_stream(stream);
     PPS_MCHECK(!capturing(st), "autotune cannot run inside a graph capture");
-    const int reps = 3, finalists = 4, final_reps = 10, final_rounds = 3;
+#ifndef PPS_TUNE_FINALISTS
+#define PPS_TUNE_FINALISTS 4  // probes: more screened tiles into the interleaved final rounds
+#endif
+    const int reps = 3, finalists = PPS_TUNE_FINALISTS, final_reps = 10, final_rounds = 3;
     Workspace* w = &workspace(*m, N, st, true);
     std::vector<float> scratch((size_t)N * m->plan.feat_dim);
     DevBuf feat(scratch.size() * sizeof(float));
