@@ -31,7 +31,7 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA
 PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # bf16 MFMA = 16x the f32 rate (~2.5 PF)
 # bf16x3 path: every f32 product costs 6 bf16 MFMA terms -> its own MFMA roof
 PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
-TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r03', 'pmc_traffic.json')
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r04', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -263,7 +263,7 @@ def rank_roofline(ev, dist, reps=20):
 
 def _pmc_traffic(key, math, batch):
     """HBM bytes per launch measured by rocprofv3 PMC passes of this bench
-    (scripts/pmc_traffic.py -> profiles/r03/pmc_traffic.json): FETCH_SIZE x 2
+    (scripts/pmc_traffic.py -> profiles/r04/pmc_traffic.json): FETCH_SIZE x 2
     (gfx950 reports half of wide streaming reads) + WRITE_SIZE, per launch.
     None unless the file was measured for the same math and batch."""
     try:
@@ -375,6 +375,114 @@ def usable_cores():
         pass
     use = aff if quota is None else max(1, min(aff, int(quota)))
     return use, aff, quota
+
+
+class ClockSampler(object):
+    """Shader clock of this rank's GPU during the timed loop (VERDICT r03:
+    tell box-to-box spread from a regression).  Reads the driver's current
+    sclk level (sysfs pp_dpm_sclk, the '*' line) from a host thread every
+    `period` s while the GPU replays the step; the host thread only waits on
+    the GPU meanwhile.  pp_dpm_sclk is the DPM level the SMU reports, up to
+    ~10 % above the in-kernel clock of MFMA-dense kernels
+    (MI355X_MICROARCH.md, DVFS give-back): a box-spread indicator, not the
+    effective clock (the PMC pass's GRBM_GUI_ACTIVE is that)."""
+
+    def __init__(self, device=0, period=0.02):
+        import threading
+        self.path = self._find(device)
+        self.period = period
+        self.samples = []
+        self._stop = threading.Event()
+        self._thread = None
+
+    @staticmethod
+    def _find(device):
+        import glob
+        try:
+            pr = torch.cuda.get_device_properties(device)
+            bdf = '%04x:%02x:%02x.0' % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        except Exception:
+            return None
+        cands = ['/sys/bus/pci/devices/%s/pp_dpm_sclk' % bdf]
+        for p in glob.glob('/sys/class/drm/card*/device/pp_dpm_sclk'):
+            if os.path.basename(os.path.realpath(os.path.dirname(p))) == bdf:
+                cands.append(p)
+        for p in cands:
+            if os.path.exists(p):
+                return p
+        return None
+
+    def read(self):
+        if not self.path:
+            return None
+        try:
+            with open(self.path) as f:
+                for line in f:
+                    if line.rstrip().endswith('*'):
+                        return float(line.split(':', 1)[1].strip().rstrip('*').strip()
+                                     .lower().replace('mhz', ''))
+        except (OSError, ValueError, IndexError):
+            return None
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            v = self.read()
+            if v is not None:
+                self.samples.append(v)
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        import threading
+        self.before = self.read()
+        if self.path:
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+        self.after = self.read()
+
+    def summary(self):
+        s = np.array(self.samples, np.float64)
+        if not self.path:
+            return dict(source=None, note='pp_dpm_sclk not readable on this host')
+        return dict(source=self.path, unit='MHz', before=self.before, after=self.after,
+                    samples=int(s.size),
+                    median=float(np.median(s)) if s.size else None,
+                    min=float(s.min()) if s.size else None,
+                    max=float(s.max()) if s.size else None,
+                    note='DPM level during the timed loop (host thread, %g s period); '
+                         'the in-kernel clock of MFMA-dense kernels reads up to ~10 %% '
+                         'lower' % self.period)
+
+
+def table_digest(nm):
+    """The tuning table behind `value`: a digest of (layer, tile, planes,
+    split-K) and the layer count per rounding group (tests/_tiles.py: the
+    32x32x16 group below tile 38, the 16x16x32 group 38-55 incl. the
+    weight-stationary 54, the patch-staged 3x3 group 56-59; the stem and the
+    head reduction are fixed kernels)."""
+    import hashlib
+    from pps_amd import ops
+    layers = nm.layers()
+    planes = set(nm.planes())
+    rows, groups = [], {}
+    for L in layers:
+        if L['op'] not in ('conv', 'conv_dual', 'heads', 'conv_pps'):
+            continue
+        t = L['tile']
+        rows.append('%s:%d:%d:%d' % (L['name'], t, int(L['name'] in planes), L['splitk']))
+        base = t & 0xff
+        g = ('auto' if base == 0 else 'x32' if base < ops.TILE_P16_FIRST else
+             'x16' if base < ops.TILE_C16_FIRST else 'patch')
+        groups[g] = groups.get(g, 0) + 1
+    return dict(sha1=hashlib.sha1('\n'.join(rows).encode()).hexdigest()[:16],
+                layers_per_rounding_group=groups, plane_edges=len(planes),
+                splitk_layers=sum(1 for L in layers if L['splitk'] > 1))
 
 
 def e2e_stage(nm, rank, world, n_images, batch, threads):
@@ -547,6 +655,34 @@ def dry_run(args, rank, world):
         dist.destroy_process_group()
 
 
+def build_bench_model(batch, rank=0, table=None, autotune=True, flags=0):
+    """The measured configuration: seeded weights of the PPS architecture,
+    the whole-network C handle, the rank's seeded uint8 Market-sized images,
+    their preprocessed NHWC4 batch, and the tuning table -- `table` (a saved
+    tiles file) or pps_model_autotune on this device at this batch.
+    tests/test_gpu_bench_table.py builds the same thing, so the table the
+    parity tests check is the one the timed loop runs."""
+    from pps_amd import model, native, ops
+    cfg = market_cfg()
+    plan = model.build_plan()
+    blobs = model.synthetic_weights(plan, seed=0)
+    # the product form: one handle behind the whole-network C ABI
+    # (pps_model_create / pps_forward_bgr)
+    nm = native.NativeModel(blobs)
+    H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
+    g = torch.Generator(device='cuda')
+    g.manual_seed(1234 + rank)
+    imgs = torch.randint(0, 256, (batch, 128, 64, 3), generator=g, device='cuda',
+                         dtype=torch.int64).to(torch.uint8)
+    xbuf = torch.empty((batch, H, W, 4), dtype=torch.float32, device='cuda')
+    ops.preprocess_bgr(imgs, cfg.PIXEL_MEANS.ravel(), (H, W), xbuf)
+    if table is not None:
+        nm.apply_table(table)
+    elif autotune:
+        nm.autotune(xbuf, flags)
+    return nm, blobs, imgs, xbuf
+
+
 def main():
     args = parse()
     env_world = os.environ.get('WORLD_SIZE')
@@ -579,35 +715,24 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
-    from pps_amd import model, native
+    from pps_amd import native
     from pps_amd import distributed as pdist
-    cfg = market_cfg()
-    plan = model.build_plan()
-    blobs = model.synthetic_weights(plan, seed=0)
-    # the product form: one handle behind the whole-network C ABI
-    # (pps_model_create / pps_forward_bgr), tuned by pps_model_autotune
-    nm = native.NativeModel(blobs)
     B = args.batch
-    H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
-    g = torch.Generator(device='cuda')
-    g.manual_seed(1234 + rank)
-    imgs = torch.randint(0, 256, (B, 128, 64, 3), generator=g, device='cuda',
-                         dtype=torch.int64).to(torch.uint8)
-    xbuf = torch.empty((B, H, W, 4), dtype=torch.float32, device='cuda')
-    feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')
-    from pps_amd import ops
-    ops.preprocess_bgr(imgs, cfg.PIXEL_MEANS.ravel(), (H, W), xbuf)
+    saved = None
     if args.tiles_file and os.path.exists(args.tiles_file):
         with open(args.tiles_file) as f:
             saved = json.load(f)
-        nm.apply_table(saved)
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
         pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
-    elif not args.no_autotune:
-        # per-layer tile / plane choice on this device, outside the timed
-        # region (PPS_AUTOTUNE_SPLITK=1: also try conv split-K)
-        nm.autotune(xbuf, native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1'
-                    else 0)
+    # per-layer tile / plane choice on this device, outside the timed region
+    # (PPS_AUTOTUNE_SPLITK=1: also try conv split-K)
+    nm, blobs, imgs, xbuf = build_bench_model(
+        B, rank, table=saved, autotune=not args.no_autotune,
+        flags=native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1' else 0)
+    cfg = market_cfg()
+    H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
+    feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')
+    from pps_amd import ops
     nm.reserve(B)
 
     def step():   # uint8 images -> preprocess -> forward, one C call
@@ -628,12 +753,13 @@ def main():
 
     pdist.barrier(world)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    pdist.barrier(world)
-    elapsed = time.perf_counter() - t0
+    with ClockSampler(local) as clk:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        pdist.barrier(world)
+        elapsed = time.perf_counter() - t0
     elapsed = pdist.max_over_ranks(elapsed, world)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * B * args.steps / elapsed
@@ -692,7 +818,9 @@ def main():
                    'global_batch': B * world, 'input_hw': [H, W], 'feat_dim': nm.feat_dim,
                    'parallelism': 'dp%d' % world, 'hipgraph': not args.no_graph,
                    'entry_point': 'pps_forward_bgr (whole-network C ABI)',
-                   'act_plane_edges': len(nm.planes()), 'splitk_layers': len(nm.splitks())},
+                   'act_plane_edges': len(nm.planes()), 'splitk_layers': len(nm.splitks()),
+                   'tuning_table': table_digest(nm)},
+        'gpu_clock': clk.summary(),
         'distmat_GBps': round(total_bytes / (dist_ms_max * 1e-3) / 1e9, 2),
         'distmat_ms': round(dist_ms_max, 3),
         'distmat_TFLOPs_per_gpu': round(dist_tflops, 2),

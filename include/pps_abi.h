@@ -135,10 +135,11 @@ int pps_distmat_x3p_tiled(const uint16_t* q3t, int64_t Q, const float* qsq,
                           int metric, float* out, int64_t ldo, int tile, void* stream);
 /* Self-distance of one feature set x [N][ld] (the reference's
  * compute_dist(g, g) / compute_dist(q, q) of re-ranking and multi-query,
- * reid_dataset_evaluator.py:169-175, 195-206): out [N][N] from the
- * upper-triangle tiles only, each strictly-upper tile also writing its
- * mirror (half the MFMA work).  x3 = pps_split_bf16x3(x) planes, xsq =
- * pps_row_sqnorm(x).  128x128 pipelined tiles (29, 36, 38, 45; 0 = 38);
+ * reid_dataset_evaluator.py:169-175, 195-206): out [N][N] from the tiles of
+ * the upper triangle only (enumerated by lcm(BM, BN) super-blocks), each
+ * writing its elements on or above the diagonal and mirroring the strictly-
+ * upper ones (half the MFMA work).  x3 = pps_split_bf16x3(x) planes, xsq =
+ * pps_row_sqnorm(x).  Any pipelined tile (29..53, 55; 0 = 43, 128 x 256);
  * D % 32 == 0.  Entry (i, j), i <= j, equals pps_distmat_x3's on the same
  * tile; the lower triangle holds exact copies (a symmetric matrix, unlike
  * the rounding-asymmetric full product). */
@@ -146,6 +147,12 @@ int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,
                         const uint16_t* x3, int D, int metric, float* out,
                         int64_t ldo, int tile, void* stream);
 
+/* pps_distmat_x3_self from chunk-tiled planes x3t [3][N16/16][D/32][16][32]
+ * (pps_split_bf16x3_sqnorm_tiled: planes + xsq in one pass): both operands
+ * staged by pure DMA, as pps_distmat_x3p_tiled.  Same bits as
+ * pps_distmat_x3_self on the same tile. */
+int pps_distmat_x3_self_tiled(const uint16_t* x3t, int64_t N, const float* xsq, int D,
+                              int metric, float* out, int64_t ldo, int tile, void* stream);
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
  * The diagonal is exactly 0 as in the reference's difference form. */
@@ -396,7 +403,8 @@ int pps_conv2d_bn_act_x3p_splitk(const float* x, const uint16_t* x3, int64_t x_p
  * raw partial tile in part [splitk][N*Ho*Wo][Cout] and bumps a per-tile
  * arrival counter; the last slice of a tile to arrive sums the partials in
  * slice order and applies the epilogue -- the bits of
- * pps_conv2d_bn_act_x3p_splitk.  counters: n_counters >= output tiles of
+ * pps_conv2d_bn_act_x3p_splitk at the same tile id (tile 0 means tile 45
+ * in both entries, so the defaults agree too).  counters: n_counters >= output tiles of
  * the tile shape, all zero on entry, zero again on return (so a captured
  * graph may replay it).  ReLU epilogues only (+ residual with f32 y, or
  * y3 planes); tiles 45 / 47 / 48 / 49 / 50, PPS_TILE_B_TILED allowed.
@@ -612,7 +620,12 @@ int pps_model_set_planes(PpsModel* model, const char* producer, int on);
 /* Time every tile per layer on this device (then plane edges, optionally
  * split-K) with x [N][H][W][4] as input; not capturable. */
 int pps_model_autotune(PpsModel* model, const float* x, int N, int flags, void* stream);
-/* Allocate (synchronously) the activation buffers for batch N. */
+/* Allocate (synchronously) the activation buffers for batch N and pin them:
+ * from here on they are never reallocated, so a hipGraph captured around
+ * pps_forward stays valid.  A later pps_model_set_splitk / set_tile /
+ * autotune that would need larger split-K buffers for batch N fails with
+ * PPS_ERR instead of freeing memory a captured graph still addresses:
+ * pps_model_release(N), pps_model_reserve(N) and recapture. */
 int pps_model_reserve(PpsModel* model, int N);
 int pps_model_release(PpsModel* model, int N);   /* N <= 0: all */
 /* An intermediate tensor of the last forward at batch N (debug / parity):

@@ -194,6 +194,90 @@ def re_ranking(q_g_dist, q_q_dist, g_g_dist, k1=20, k2=6, lambda_value=0.3):
     return final[:nq, nq:]
 
 
+def _row_topk_stable(a, k):
+    """Per row, the k smallest entries in (value, index) order: the first k
+    columns of a stable argsort, from argpartition + a (value, index) sort
+    of the k + ties candidates (whole-row argsort is O(N^2 log N) at
+    N ~ 16k)."""
+    n = a.shape[1]
+    kk = min(n, k)
+    part = np.argpartition(a, kk - 1, axis=1)[:, :kk]
+    out = np.empty((a.shape[0], kk), np.int64)
+    for i in range(a.shape[0]):
+        kth = a[i, part[i]].max()
+        cand = np.nonzero(a[i] <= kth)[0]          # every entry tied with the k-th too
+        order = np.lexsort((cand, a[i, cand]))      # value, then index
+        out[i] = cand[order[:kk]]
+    return out
+
+
+def re_ranking_sparse(q_g_dist, q_q_dist, g_g_dist, k1=20, k2=6, lambda_value=0.3):
+    """re_ranking above for N = Q + G in the tens of thousands, with the same
+    float32 values in the same operation order (sparse V / V_qe rows, the
+    inverted index as row lists) -- test infrastructure for the long-row GPU
+    check (tests/test_gpu_configs.py).  Ranks are the stable (value, index)
+    order, which equals np.argsort's wherever the first k1 + 1 values of a
+    row are distinct.  Pinned: equal to re_ranking on the golden fixture and
+    on random cases (tests/test_oracle_golden.py)."""
+    nq = q_g_dist.shape[0]
+    full = np.block([[q_q_dist, q_g_dist], [q_g_dist.T, g_g_dist]])
+    full = np.power(full, 2).astype(np.float32)
+    full = np.ascontiguousarray(np.transpose(1. * full / np.max(full, axis=0)))
+    n = full.shape[0]
+    half = int(np.around(k1 / 2.))
+    ranks = _row_topk_stable(full, max(k1 + 1, k2)).astype(np.int32)
+
+    def reciprocal(i, k):
+        fwd = ranks[i, :k + 1]
+        bwd = ranks[fwd, :k + 1]
+        return fwd[np.where(bwd == i)[0]]
+
+    V = [None] * n    # row i: (sorted columns, float32 weights)
+    for i in range(n):
+        core = reciprocal(i, k1)
+        expanded = core
+        for cand in core:
+            cand_set = reciprocal(cand, half)
+            if len(np.intersect1d(cand_set, core)) > 2. / 3 * len(cand_set):
+                expanded = np.append(expanded, cand_set)
+        expanded = np.unique(expanded)
+        w = np.exp(-full[i, expanded])
+        V[i] = (expanded, (1. * w / np.sum(w)).astype(np.float32))
+    if k2 != 1:
+        # np.mean(V[rows, :], axis=0): float32 sum down the k2 rows in row
+        # order (zeros of the other rows included), then / k2
+        Vqe = [None] * n
+        for i in range(n):
+            rows = [V[r] for r in ranks[i, :k2]]
+            cols = np.unique(np.concatenate([c for c, _ in rows]))
+            acc = np.zeros(len(cols), np.float32)
+            for c, v in rows:
+                dense = np.zeros(len(cols), np.float32)
+                dense[np.searchsorted(cols, c)] = v
+                acc = acc + dense
+            Vqe[i] = (cols, (acc / np.float32(k2)).astype(np.float32))
+        V = Vqe
+    inv = {}
+    for r in range(n):                     # V[:, j] != 0, rows ascending
+        c, v = V[r]
+        for j in c[v != 0]:
+            inv.setdefault(int(j), []).append(r)
+    vget = [dict(zip(c.tolist(), v.tolist())) for c, v in V]
+    jac = np.zeros((nq, n), np.float32)
+    for i in range(nq):
+        tmin = np.zeros(n, np.float32)
+        c, v = V[i]
+        for j, vij in zip(c, v):
+            if vij == 0:
+                continue
+            rows = np.asarray(inv[int(j)])
+            other = np.asarray([vget[r][int(j)] for r in rows], np.float32)
+            tmin[rows] = tmin[rows] + np.minimum(np.float32(vij), other)
+        jac[i] = 1 - tmin / (2. - tmin)
+    final = jac * (1 - lambda_value) + full[:nq] * lambda_value
+    return final[:nq, nq:]
+
+
 def parse_im_name(im_name, parse_type='id'):
     """reid_dataset_evaluator.py:224-231."""
     assert parse_type in ('id', 'cam')

@@ -270,6 +270,38 @@ int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,
   return launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
 }
 
+// The same from chunk-tiled planes (pps_split_bf16x3_sqnorm_tiled /
+// pps_tile_planes layout): both operands are the one tiled copy, staged by
+// pure DMA like pps_distmat_x3p_tiled.
+int pps_distmat_x3_self_tiled(const uint16_t* x3t, int64_t N, const float* xsq, int D,
+                              int metric, float* out, int64_t ldo, int tile, void* stream) {
+  PPS_ENFORCE(x3t && xsq && out, "null pointer");
+  PPS_ENFORCE(N >= 0 && D > 0 && D % 32 == 0, "D must be a positive multiple of 32");
+  PPS_ENFORCE(ldo >= N, "ldo < N");
+  PPS_ENFORCE(aligned16(x3t), "x3t must be 16-byte aligned");
+  PPS_ENFORCE(metric >= 0 && metric <= 2, "unknown metric");
+  const int64_t Np = (N + 15) / 16 * 16;
+  PPS_ENFORCE(Np * D * 2 < kMaxBufBytes, "planes over 2 GiB");
+  PPS_ENFORCE(N * ldo < (1ll << 31), "output larger than 2^31 elements");
+  PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P_FIRST && tile < GEMM_TILE_C16_FIRST &&
+                            tile != GEMM_TILE_WS),
+              "tiled self-distance needs a pipelined tile (0, 29..53 or 55)");
+  if (N == 0) return PPS_OK;
+  GemmParams p{};
+  p.splitk = 1;
+  p.tiled = 3;
+  p.a3 = x3t; p.a_plane = Np * D; p.a_bytes = (uint32_t)(Np * D * 2);
+  p.H = 1; p.W = (int)N; p.Cin = D; p.lda = D;
+  p.KH = p.KW = 1; p.stride = 1; p.pad = 0; p.dil = 1; p.Ho = 1; p.Wo = (int)N;
+  p.M = (int)N;
+  p.b3 = x3t; p.b_plane = Np * D; p.b_bytes = (uint32_t)(Np * D * 2);
+  p.ldb = D; p.kb_valid = D; p.Ncol = (int)N;
+  p.Kloop = D;
+  p.norm_a = xsq; p.norm_b = xsq;
+  p.out = out; p.ldo = ldo; p.metric = metric; p.sym = 1; p.tile = tile;
+  return launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
+}
+
 int pps_pairwise_distance(const float* X, int N, int D, float* Z, void* stream) {
   PPS_ENFORCE(X && Z, "null pointer");
   PPS_ENFORCE(N >= 0 && D > 0 && D % 4 == 0, "X must be 2-D [N][D] with D % 4 == 0");
@@ -572,7 +604,9 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     }
     p.out = part; p.out3 = nullptr; p.ldo = Cout; p.out_sstride = M * Cout;
     p.residual = nullptr; p.relu = 0;
-    p.tile = tile ? tile : GEMM_TILE_P_FIRST + 8;
+    // tile 0: tile 45, the one-launch entry's default (same rounding group,
+    // so both entries give the same bits at tile 0 as at any equal id)
+    p.tile = tile ? tile : GEMM_TILE_P16_FIRST + 7;
     const int rc = launch_gemm_x3(p, EPI_CONV | EPI_F_RAW, 1, as_stream(stream));
     if (rc != PPS_OK) return rc;
     return splitk_conv_epilogue(part, splitk, M, Cout, scale, shift, residual, relu,

@@ -345,6 +345,9 @@ struct Workspace {
   Buf cnt;                          // one-launch split-K tile counters (zero between launches)
   size_t cnt_ints = 0;
   Buf nhwc4;                        // input staging for pps_forward_nchw / _bgr
+  // set by pps_model_reserve: a graph captured afterwards may hold these
+  // buffers' addresses, so they are never reallocated until pps_model_release
+  bool pinned = false;
 };
 
 }  // namespace
@@ -634,7 +637,12 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
   if (it != m.ws.end()) {
     Workspace& w = it->second;
     const size_t need = part_need(m, w.shapes);
+    const std::string pinned_msg =
+        "the buffers of batch " + std::to_string(N) +
+        " are pinned by pps_model_reserve (a captured graph may hold them) and the tuning "
+        "table now needs larger split-K ";
     if (need > w.part_floats) {
+      PPS_MCHECK(!w.pinned, pinned_msg + "partials: pps_model_release, reserve again, recapture");
       PPS_MCHECK(allow_alloc && !capturing(st),
                  "split-K partials grew after pps_model_reserve: reserve again outside capture");
       w.part = std::make_shared<DevBuf>(need * sizeof(float));
@@ -642,6 +650,7 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
     }
     const size_t cneed = cnt_need(m, w.shapes);
     if (cneed > w.cnt_ints) {
+      PPS_MCHECK(!w.pinned, pinned_msg + "counters: pps_model_release, reserve again, recapture");
       PPS_MCHECK(allow_alloc && !capturing(st),
                  "split-K counters grew after pps_model_reserve: reserve again outside capture");
       grow_counters(w, cneed, st);
@@ -1136,6 +1145,7 @@ int pps_model_reserve(PpsModel* m, int N) {
     PPS_MCHECK(m && N > 0, "bad arguments");
     Workspace& w = workspace(*m, N, nullptr, true);
     nhwc4_buffer(*m, w, nullptr);
+    w.pinned = true;
   });
 }
 

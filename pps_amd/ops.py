@@ -152,7 +152,9 @@ class GalleryIndex(object):
         return self._tiled
 
 
-SELF_TILES = (0, TILE_P_FIRST, TILE_P_FIRST + 7, TILE_P16_FIRST, TILE_P16_FIRST + 7)
+# tiles the symmetric self-distance takes: every pipelined tile (the upper
+# triangle is enumerated by lcm(BM, BN) super-blocks); 0 = tile 43
+SELF_TILES = (0,) + tuple(range(TILE_P_FIRST, 54)) + (55,)
 
 
 def dist_buffer(Q, G, device):
@@ -189,24 +191,31 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
             torch.empty((Q, G), dtype=torch.float32, device=q.device)
     if tuple(out.shape) != (Q, G):
         raise RuntimeError('out must be [%d, %d], got %s' % (Q, G, tuple(out.shape)))
+    # the mark re_ranking reads: set on every return, so a reused buffer
+    # never carries a stale True from an earlier self-distance
+    out._pps_symmetric = False
     if math == 'f32':
         call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
              _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
     tiled = bool(q_planes) and D % 32 == 0 and (tile == 0 or tile >= TILE_P_FIRST)
-    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g, tiled=tiled and not (
-        symmetric or (symmetric is None and g.data_ptr() == q.data_ptr())))
+    f = g.feats if isinstance(g, GalleryIndex) else g
     if symmetric is None:
-        f = idx.feats
         symmetric = (f.data_ptr() == q.data_ptr() and tuple(f.shape) == tuple(q.shape) and
                      f.stride() == q.stride() and q.is_contiguous() and D % 32 == 0 and
                      tile in SELF_TILES)
     if symmetric:
-        call('pps_distmat_x3_self', _dev(q, 'x'), Q, D, _dev(idx.sqnorm, 'xsq'),
-             _dev(idx.planes, 'x3', torch.int16), D, METRICS[metric],
-             _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
+        # one read of x -> chunk-tiled planes + norms; both operands staged
+        # from that copy by DMA (pps_distmat_x3_self_tiled)
+        if isinstance(g, GalleryIndex) and g._tiled is not None:
+            x3t, xsq = g._tiled, g.sqnorm
+        else:
+            x3t, xsq = split_sqnorm_tiled(q)
+        call('pps_distmat_x3_self_tiled', _dev(x3t, 'x3t', torch.int16), Q, _dev(xsq, 'xsq'),
+             D, METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         out._pps_symmetric = True   # mirrored tiles: exactly symmetric (re_ranking uses it)
         return out
+    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g, tiled=tiled)
     if q_planes:
         if tiled and q.is_contiguous():  # both operands chunk-tiled, queries in one pass
             qt, qsq = split_sqnorm_tiled(q)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p $OUT
 STEPS=${STEPS:-20}
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -x ${PYTEST_ARGS} > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
 if [ $rc -gt 1 ]; then echo "pytest crashed/timed out; stopping"; exit $rc; fi

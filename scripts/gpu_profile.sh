@@ -10,7 +10,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out
-mkdir -p $OUT profiles/r03
+R=${ROUND_DIR:-profiles/r04}
+mkdir -p $OUT $R
 TILES=$OUT/tiles.json
 rm -f $TILES
 # TILES_IN=<committed table>: skip the tuning run, profile that table
@@ -29,7 +30,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o r
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
 python scripts/pmc_traffic.py $OUT/pmcb $MATH 64 50 > $OUT/pmc_traffic.json || exit 1
 cat $OUT/pmc_traffic.json
-cp $OUT/pmc_traffic.json profiles/r03/pmc_traffic.json   # bench-final reads it (box copy)
+cp $OUT/pmc_traffic.json $R/pmc_traffic.json   # bench-final reads it (box copy)
 step bench-final
 PPS_BENCH_LAYERS=$OUT/layers.json timeout -k 10 600 python bench.py --tiles-file $TILES > $OUT/bench_final.log 2>&1 || { tail -5 $OUT/bench_final.log; exit 1; }
 tail -1 $OUT/bench_final.log

@@ -214,6 +214,38 @@ def test_duke_rerank_vs_oracle_500x3000():
     assert 0.3 < r["mAP"] < 0.8   # non-trivial regime (plain mAP ~0.28, re-ranked ~0.50)
 
 
+def test_rerank_long_rows_vs_oracle():
+    """Q + G = 16500 >= 16384: the OD rows are long enough for the wave-
+    streaming top-k (topk_wave_kernel) inside pps_re_ranking (VERDICT r03
+    item 5).  Same float32 distances into both; the checker is the oracle's
+    sparse restatement (pinned equal to oracle.re_ranking,
+    tests/test_oracle_golden.py)."""
+    from pps_amd import ops
+    from pps_amd import reid_dataset_evaluator as gev
+    Q, G, D = 1000, 15500, 256
+    rng = np.random.RandomState(7)
+    qid = rng.randint(1, 700, Q)
+    gid = rng.randint(1, 700, G)
+    qcam = rng.randint(1, 9, Q)
+    gcam = rng.randint(1, 9, G)
+    cent = rng.randn(700, D).astype(np.float32)
+    f = cent[np.concatenate([qid, gid])] + 2.5 * rng.randn(Q + G, D).astype(np.float32)
+    f = (f / np.linalg.norm(f, axis=1, keepdims=True)).astype(np.float32)
+    qg = ev.compute_dist(f[:Q], f[Q:])
+    qq = ev.compute_dist(f[:Q], f[:Q])
+    gg = ev.compute_dist(f[Q:], f[Q:])
+    ref = ev.re_ranking_sparse(qg, qq, gg, k1=20, k2=6, lambda_value=0.3)
+    rr = ops.re_ranking(*(torch.from_numpy(np.ascontiguousarray(x)).cuda()
+                          for x in (qg, qq, gg)), 20, 6, 0.3)
+    rrn = rr.cpu().numpy()
+    err = float(np.abs(rrn - ref).max())
+    ap, valid, first = gev.rank_eval(rr, qid, gid, qcam, gcam)
+    r = check_rank_metrics(ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy(), ref,
+                           qid, gid, qcam, gcam, tie_eps(rrn, ref))
+    print('re-ranking 1000 x 15500 (long rows): max|err| %.3g, %s' % (err, r))
+    assert err < 1e-5, err
+
+
 def test_duke_full_size_cosine_rerank_properties():
     from pps_amd import ops
     from pps_amd import reid_dataset_evaluator as gev

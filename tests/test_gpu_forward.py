@@ -19,8 +19,6 @@ LAYER_RTOL = 1e-5   # intermediate stage outputs, relative to their max
 PRE_ATOL = 3e-3     # preprocess vs the float64 oracle, f32 separable passes: observed
                     # 9.7e-4 at Market size, 2.0e-3 on the ragged up-scales (values up
                     # to ~255: ~1e-5 of the range)
-BENCH_TILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                           'profiles', 'r03', 'tiles_v3.json')
 
 
 def _cuda(x):
@@ -288,46 +286,6 @@ def test_fpn_variant_forward_vs_oracle():
     out = model.PPSModel(blobs, plan=plan).forward(_cuda(xin)).cpu().numpy()
     err = float(np.abs(out - ref).max())
     print('FPN forward max|err| vs oracle %.3g' % err)
-    assert err <= FWD_ATOL
-
-
-def test_bench_configuration_vs_oracle():
-    """The configuration bench.py measures -- batch 64, the committed
-    autotune result (per-layer tiles from both rounding groups, bf16x3
-    activation-plane edges) -- against the CPU oracle on a few of the 64
-    images: forward -> normalised features."""
-    import json
-    import os
-    from oracle.forward import GraphForward
-    from oracle import preprocess as pre
-    from pps_amd import model, ops
-    tf = BENCH_TILES
-    if not os.path.exists(tf):
-        pytest.skip('no committed tiles file')
-    _market_cfg()
-    plan = model.build_plan()
-    blobs = model.synthetic_weights(plan, seed=0)
-    m = model.PPSModel(blobs, math='x3')
-    with open(tf) as f:
-        saved = json.load(f)
-    m.set_tiles(saved)
-    m.set_planes(saved.get('__planes__', []))
-    m.set_splitks(saved.get('__splitk__', {}))
-    assert len(m.planes()) > 0
-    # the run uses exactly the tile ids the autotune chose (incl. 50-53)
-    want = {v for k, v in saved.items() if not k.startswith('__')}
-    assert set(m.tiles().values()) == want, (sorted(want), sorted(set(m.tiles().values())))
-    rng = np.random.RandomState(64)
-    imgs = rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)
-    x = ops.preprocess_bgr(torch.from_numpy(imgs).cuda(), pre.PIXEL_MEANS, (384, 128))
-    feat = m.forward(x).cpu().numpy()
-    pick = [0, 17, 63]
-    # the oracle forward on the kernel's own preprocessed input (preprocess
-    # parity is test_preprocess_vs_oracle's)
-    xin = x[pick, :, :, :3].cpu().numpy().transpose(0, 3, 1, 2)
-    ref = GraphForward(blobs)(np.ascontiguousarray(xin, np.float32)).numpy()
-    err = float(np.abs(feat[pick] - ref).max())
-    print('bench configuration forward max|err| vs oracle %.3g' % err)
     assert err <= FWD_ATOL
 
 

@@ -2,7 +2,6 @@
 pps_abi.h) against the Python orchestrator (bit for bit, same tuning table)
 and the CPU oracle (tight bound): the forward a C/C++ caller gets through the
 ABI with no pps_amd/model.py orchestration."""
-import json
 import os
 
 import numpy as np
@@ -12,7 +11,6 @@ import torch
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TILES = os.path.join(ROOT, 'profiles', 'r03', 'tiles_v0.json')
 FWD_ATOL = 1e-6   # normalised features vs the oracle (observed ~6e-8)
 
 
@@ -66,35 +64,6 @@ def test_native_forward_bit_identical_and_vs_oracle(math):
     err = float(np.abs(b - ref).max())
     print('native forward (%s) max|err| vs oracle %.3g' % (math, err))
     assert err <= FWD_ATOL
-
-
-def test_native_bench_table_bit_identical():
-    """Batch 64 with the committed autotune table (tiles of both rounding
-    groups, plane edges): pps_forward == PPSModel.forward bit for bit, and
-    the uint8 / NCHW entry points equal preprocess + pps_forward."""
-    if not os.path.exists(TILES):
-        pytest.skip('no committed tiles file')
-    from oracle import preprocess as pre
-    from pps_amd import ops
-    _, pm, nm = _models()
-    with open(TILES) as f:
-        saved = json.load(f)
-    pm.set_tiles(saved)
-    pm.set_planes(saved.get('__planes__', []))
-    pm.set_splitks(saved.get('__splitk__', {}))
-    nm.apply_table(pm)
-    assert nm.tiles() == pm.tiles() and sorted(nm.planes()) == sorted(pm.planes())
-    rng = np.random.RandomState(64)
-    imgs = torch.from_numpy(rng.randint(0, 256, (64, 128, 64, 3)).astype(np.uint8)).cuda()
-    x = ops.preprocess_bgr(imgs, pre.PIXEL_MEANS, (384, 128))
-    a = pm.forward(x).cpu().numpy()
-    b = nm.forward(x).cpu().numpy()
-    assert np.array_equal(a, b)
-    c = nm.forward_bgr(imgs).cpu().numpy()
-    assert np.array_equal(b, c)
-    nchw = x[..., :3].permute(0, 3, 1, 2).contiguous()
-    d = nm.forward_nchw(nchw).cpu().numpy()
-    assert np.array_equal(b, d)
 
 
 def test_native_fused_splitk_layers():
@@ -224,3 +193,24 @@ def test_native_errors_are_enforce_style():
         native.call('pps_model_set_planes', nm.handle, b'res2_0_branch2c', 1)
     with pytest.raises(ValueError, match='not a plane-eligible producer'):
         nm.set_planes(['res2_0_branch2c'])
+
+
+def test_reserved_buffers_are_pinned():
+    """after pps_model_reserve(N) a tuning change that needs
+    larger split-K buffers must fail (a captured graph may still address the
+    old ones) instead of reallocating; release + reserve re-enables it."""
+    _, pm, nm = _models()
+    _, x = _input(2, seed=5)
+    nm.reserve(2)
+    nm.forward(x)
+    torch.cuda.synchronize()
+    L = next(L for L in nm.layers(N=2) if L['op'] == 'conv' and L['name'].startswith('res5')
+             and L['name'].endswith('branch2b'))
+    nm.set_splitks({L['name']: 2})
+    with pytest.raises(RuntimeError, match='pinned by pps_model_reserve'):
+        nm.forward(x)
+    nm.release(2)
+    nm.reserve(2)
+    out = nm.forward(x)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(out).all())

@@ -109,3 +109,24 @@ def test_oracle_cmc_all_modes_vs_reference(golden):
         np.testing.assert_allclose(ev.cmc(d, qid, gid, qcam, gcam, topk=5,
                                           separate_camera_set=True),
                                    g[tag + '_sep1_fmb0_top5'], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('k2', [6, 1])
+def test_rerank_sparse_restatement_equals_oracle(golden, k2):
+    """oracle.re_ranking_sparse (the long-row GPU test's checker) computes the
+    same float32 values as oracle.re_ranking, which the golden pins."""
+    g = golden('rerank')
+    a = ev.re_ranking(g['q_g'], g['q_q'], g['g_g'], k1=20, k2=k2, lambda_value=0.3)
+    b = ev.re_ranking_sparse(g['q_g'], g['q_q'], g['g_g'], k1=20, k2=k2, lambda_value=0.3)
+    np.testing.assert_array_equal(a, b)
+    rng = np.random.RandomState(5)
+    Q, G, D = 60, 340, 32
+    cent = rng.randn(40, D).astype(np.float32)
+    ids = rng.randint(0, 40, Q + G)
+    f = cent[ids] + 1.5 * rng.randn(Q + G, D).astype(np.float32)
+    qg = ev.compute_dist(f[:Q], f[Q:])
+    qq = ev.compute_dist(f[:Q], f[:Q])
+    gg = ev.compute_dist(f[Q:], f[Q:])
+    a = ev.re_ranking(qg, qq, gg, k1=20, k2=k2, lambda_value=0.3)
+    b = ev.re_ranking_sparse(qg, qq, gg, k1=20, k2=k2, lambda_value=0.3)
+    np.testing.assert_array_equal(a, b)
