@@ -301,6 +301,18 @@ int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t
 int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
                          int64_t G, int k1, int k2, double lambda_value, int flags,
                          void* workspace, int64_t ws_bytes, float* out, void* stream);
+/* The same with row strides (e.g. the 16-byte-aligned rows of padded
+ * distance buffers).  With PPS_RERANK_SYMMETRIC, N = Q + G >= 16384 and
+ * every block's rows 16-byte aligned (ld % 4 == 0; ld_qq >= Q rounded up to
+ * 4), the N x N normalised distance is never built: its top-k (the
+ * wave-streaming kernel), the V weights and the Jaccard blend read the
+ * blocks in place and compute M[i][j]^2 / colmax[i] on the fly (the same
+ * float32 operations); only q_g^T is materialised (in the workspace).
+ * Results equal the dense path's bit for bit. */
+int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t ld_qq,
+                      const float* g_g, int64_t ld_gg, int64_t Q, int64_t G, int k1, int k2,
+                      double lambda_value, int flags, void* workspace, int64_t ws_bytes,
+                      float* out, void* stream);
 
 /* ---- feature extractor ----------------------------------------------------
  * Implicit-GEMM convolution + test-mode SpatialBN + optional residual Sum +

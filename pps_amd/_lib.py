@@ -35,6 +35,8 @@ SIGNATURES = {
                               c_i64, c_int, c_ptr],
     'pps_distmat_x3_self': [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_i64,
                             c_int, c_ptr],
+    'pps_distmat_x3_self_tiled': [c_ptr, c_i64, c_ptr, c_int, c_int, c_ptr, c_i64, c_int,
+                                  c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
@@ -99,6 +101,8 @@ SIGNATURES = {
                        c_ptr, c_i64, c_ptr, c_ptr],
     'pps_re_ranking_flags': [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int, c_int, ctypes.c_double,
                              c_int, c_ptr, c_i64, c_ptr, c_ptr],
+    'pps_re_ranking_ld': [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_int, c_int,
+                          ctypes.c_double, c_int, c_ptr, c_i64, c_ptr, c_ptr],
     'pps_stem_conv_pool_x3': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
                               c_int, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,

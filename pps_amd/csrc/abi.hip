@@ -51,8 +51,8 @@ int rank_prepare(int, int64_t, int, const float*, const int32_t*, const int32_t*
 int rank_count_stream(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
                       const int32_t*, const int32_t*, const int32_t*, int, const float*,
                       const int32_t*, const int32_t*, int32_t*, int32_t*, hipStream_t);
-int rerank(const float*, const float*, const float*, int64_t, int64_t, int, int, double,
-           void*, size_t, float*, hipStream_t, int);
+int rerank(const float*, int64_t, const float*, int64_t, const float*, int64_t, int64_t, int64_t,
+           int, int, double, void*, size_t, float*, hipStream_t, int);
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
 int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
                             const float*, int, int, float*, hipStream_t);
@@ -472,11 +472,13 @@ int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   return (int64_t)rerank_workspace_bytes(Q, G, k1, k2);
 }
 
-int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
-                         int64_t G, int k1, int k2, double lambda_value, int flags,
-                         void* workspace, int64_t ws_bytes, float* out, void* stream) {
+int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t ld_qq,
+                      const float* g_g, int64_t ld_gg, int64_t Q, int64_t G, int k1, int k2,
+                      double lambda_value, int flags, void* workspace, int64_t ws_bytes,
+                      float* out, void* stream) {
   PPS_ENFORCE(q_g && q_q && g_g && workspace && out, "null pointer");
   PPS_ENFORCE(Q > 0 && G > 0, "bad shape");
+  PPS_ENFORCE(ld_qg >= G && ld_qq >= Q && ld_gg >= G, "leading dims smaller than the rows");
   PPS_ENFORCE(k1 >= 1 && k1 + 1 <= 64, "k1 + 1 must be <= 64");
   PPS_ENFORCE(k2 >= 1 && k2 <= k1 + 1, "k2 must be in [1, k1 + 1]");
   const int K1 = k1 + 1, Kh = (int)lrint(k1 / 2.0) + 1;
@@ -486,8 +488,15 @@ int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, i
   PPS_ENFORCE((Q + G) * 4 <= 160 * 1024, "Q + G must be <= 40960 (LDS accumulator)");
   PPS_ENFORCE((Q + G) >= K1, "need Q + G >= k1 + 1");
   PPS_ENFORCE((flags & ~PPS_RERANK_SYMMETRIC) == 0, "unknown re-ranking flags");
-  return rerank(q_g, q_q, g_g, Q, G, k1, k2, lambda_value, workspace, (size_t)ws_bytes, out,
-                as_stream(stream), flags);
+  return rerank(q_g, ld_qg, q_q, ld_qq, g_g, ld_gg, Q, G, k1, k2, lambda_value, workspace,
+                (size_t)ws_bytes, out, as_stream(stream), flags);
+}
+
+int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
+                         int64_t G, int k1, int k2, double lambda_value, int flags,
+                         void* workspace, int64_t ws_bytes, float* out, void* stream) {
+  return pps_re_ranking_ld(q_g, G, q_q, Q, g_g, G, Q, G, k1, k2, lambda_value, flags, workspace,
+                           ws_bytes, out, stream);
 }
 
 int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,

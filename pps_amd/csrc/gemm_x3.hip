@@ -300,17 +300,17 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     return PPS_ERR_INVALID_ARG;
   }
   if (p.sym) {
-    // self-distance: square pipelined tiles only (the triangle is by tile)
-    const int v = p.tile >= GEMM_TILE_P_FIRST ? p.tile - GEMM_TILE_P_FIRST : GEMM_TILE_P16_FIRST -
-                                                                                 GEMM_TILE_P_FIRST;
-    const int vb = v % (GEMM_TILE_P16_FIRST - GEMM_TILE_P_FIRST);
-    if (!(epi & EPI_DIST) || p.M != p.Ncol || !x3p_eligible(p, epi) || (vb != 0 && vb != 7) ||
-        p.tile >= GEMM_TILE_P16_192x128W42) {  // ids 47+ are not square
-      set_error("symmetric distance: needs EPI_DIST, M == Ncol and a 128x128 pipelined tile "
-                "(29, 36, 38 or 45)");
+    // self-distance: any pipelined tile (the upper triangle is enumerated by
+    // lcm(BM, BN) super-blocks, gemm_x3p.hip); tile 0 = tile 43 (128 x 256,
+    // the distance matrix's winner)
+    const int t = p.tile ? p.tile : GEMM_TILE_P16_FIRST + 5;
+    if (!(epi & EPI_DIST) || p.M != p.Ncol || !x3p_eligible(p, epi) || t < GEMM_TILE_P_FIRST ||
+        t >= GEMM_TILE_C16_FIRST || t == GEMM_TILE_WS) {
+      set_error("symmetric distance: needs EPI_DIST, M == Ncol and a pipelined tile "
+                "(29..53 or 55)");
       return PPS_ERR_INVALID_ARG;
     }
-    return launch_gemm_x3p(p, epi, batch, stream, v);
+    return launch_gemm_x3p(p, epi, batch, stream, t - GEMM_TILE_P_FIRST);
   }
   if (p.a3 || (epi & EPI_F_PLANES)) {
     // bf16-plane activations exist only in the pipelined family

@@ -123,14 +123,20 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const bool sym = (EPI & EPI_DIST) && p.sym;
   int tile_m, tile_n;
   if (sym) {
-    // self-distance: the grid enumerates only the upper-triangle tiles, so
-    // every XCD gets an equal, contiguous share of them.  Grouped like the
-    // distance order below: GM row panels (~32 MB) sweep their columns
-    // together (column-major inside the group), so each column block is
-    // streamed once per group instead of once per row panel.
-    const int n = tiles_n;
-    const int k = xcd_remap(blockIdx.x, n * (n + 1) / 2);
-    const int64_t panel = (int64_t)BM * p.Kloop * (A3 ? 6 : 4);
+    // self-distance: the grid enumerates the upper triangle of SB x SB
+    // super-blocks (SB = lcm(BM, BN), so non-square tiles tile them:
+    // TPM x TPN tiles each), so every XCD gets an equal, contiguous share.
+    // Grouped like the distance order below: GM super-block rows (~32 MB of
+    // row panels) sweep their columns together (column-major inside the
+    // group), so each column block is streamed once per group instead of
+    // once per row panel.  The tiles of a super-block are consecutive ids
+    // (one XCD after the remap).
+    constexpr int SB = sym_block<BM, BN>();
+    constexpr int TPM = SB / BM, TPN = SB / BN, TPS = TPM * TPN;
+    const int n = (p.Ncol + SB - 1) / SB;
+    const int kk = xcd_remap(blockIdx.x, TPS * (n * (n + 1) / 2));
+    const int k = kk / TPS, t = kk - k * TPS;
+    const int64_t panel = (int64_t)SB * p.Kloop * (A3 ? 6 : 4);
     const int64_t want = ((int64_t)X3P_GM_MB << 20) / (panel > 0 ? panel : 1);
     const int GM = (int)(want < 1 ? 1 : (want < n ? want : n));
     int g0 = 0, base = 0;
@@ -143,18 +149,25 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     }
     const int gm = n - g0 < GM ? n - g0 : GM;
     const int r = k - base;
-    const int t1 = gm * (gm + 1) / 2;  // the group's own triangle, column c has c+1 tiles
+    const int t1 = gm * (gm + 1) / 2;  // the group's own triangle, column c has c+1 blocks
+    int sbm, sbn;
     if (r < t1) {
       int c = (int)((sqrt(8.0 * r + 1.0) - 1.0) * 0.5);
       while (c > 0 && c * (c + 1) / 2 > r) --c;
       while ((c + 1) * (c + 2) / 2 <= r) ++c;
-      tile_m = g0 + (r - c * (c + 1) / 2);
-      tile_n = g0 + c;
+      sbm = g0 + (r - c * (c + 1) / 2);
+      sbn = g0 + c;
     } else {
       const int r2 = r - t1;
-      tile_n = g0 + gm + r2 / gm;
-      tile_m = g0 + r2 % gm;
+      sbn = g0 + gm + r2 / gm;
+      sbm = g0 + r2 % gm;
     }
+    tile_m = sbm * TPM + t / TPN;
+    tile_n = sbn * TPN + t % TPN;
+    // past the matrix (a partial last super-block), or strictly below the
+    // diagonal (its mirror is written by another tile of the super-block):
+    // the whole workgroup leaves before touching LDS or memory
+    if (tile_m * BM >= p.M || tile_n * BN >= p.Ncol || tile_m * BM >= tile_n * BN + BN) return;
   } else {
     const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
     if (EPI & EPI_DIST) {
@@ -512,7 +525,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   }
   if constexpr (DISTLDS) {
     if (p.sym)
-      dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
+      dist_epilogue_sym_lds<BM, BN, WM, WN, S>(p, acc, lds, m0, n0, wm, wn, r32, h);
     else
       dist_epilogue_lds<BM, BN, WM, WN, S>(p, acc, lds, m0, n0, wm, wn, r32, h);
   } else if constexpr ((EPI & EPI_DIST) != 0)
@@ -528,8 +541,11 @@ template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3, int S>
 static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
-  // self-distance (square tiles, M == Ncol): upper-triangle tiles only
-  const int nblk = ((EPI & EPI_DIST) && p.sym) ? tiles_n * (tiles_n + 1) / 2 : tiles_m * tiles_n;
+  // self-distance (M == Ncol): the tiles of the upper-triangle super-blocks
+  constexpr int SB = sym_block<BM, BN>();
+  const int nsb = (p.Ncol + SB - 1) / SB;
+  const int nblk = ((EPI & EPI_DIST) && p.sym) ? (SB / BM) * (SB / BN) * (nsb * (nsb + 1) / 2)
+                                               : tiles_m * tiles_n;
   hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, EPI, NS, A3, S>),
                      dim3(nblk, batch * p.splitk), dim3(64 * WM * WN), 0, stream, p, tiles_m,
                      tiles_n);

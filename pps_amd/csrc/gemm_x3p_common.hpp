@@ -60,6 +60,15 @@ __device__ inline f32x16 mfma_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
 #define X3P_GM_MB 32
 #endif
 
+// Self-distance super-block: the least common multiple of the tile sides, so
+// the upper triangle is enumerated by square blocks that whole tiles cover.
+template <int BM, int BN>
+constexpr int sym_block() {
+  int a = BM, b = BN;
+  while (b) { const int t = a % b; a = b; b = t; }
+  return BM / a * BN;
+}
+
 template <int S> struct AccT { typedef f32x16 type; };
 template <> struct AccT<16> { typedef f32x4 type; };
 
@@ -503,8 +512,112 @@ __device__ inline void dist_epilogue_lds(const GemmParams& p,
   }
 }
 
+// One distance from a dot product and the two squared norms (the formulas
+// of dist_epilogue / dist_epilogue_lds, factored out for the symmetric
+// epilogue: same operations in the same order).
+__device__ inline float dist_value(const GemmParams& p, float dot, float qn, float gn) {
+  float d;
+  if (p.metric == PPS_METRIC_COSINE) {
+    const float den = fmaxf(sqrtf(qn), 1e-12f) * fmaxf(sqrtf(gn), 1e-12f);
+    d = 1.f - dot / den;
+  } else {
+    d = fmaxf(__builtin_fmaf(-2.f, dot, qn) + gn, 0.f);
+    if (p.metric == PPS_METRIC_EUCLIDEAN) d = sqrtf(d);
+  }
+  return d;
+}
+
+// Self-distance epilogue through LDS: the tile's dot products are parked as
+// [BM][BN+4]; pass 1 writes the elements on or above the diagonal (global
+// row <= column) as whole row segments and leaves the finished distances in
+// LDS; pass 2 writes the strictly-upper ones a second time at the mirrored
+// position, walking the tile by columns so that each store is 16 bytes of
+// one output row (4 consecutive tile rows).  Elements below the diagonal are
+// the mirror of another tile of the same diagonal super-block.  The mirror
+// is a copy, so the matrix is exactly symmetric; the upper triangle has the
+// bits of the full (non-symmetric) product on the same tile.
+template <int BM, int BN, int WM, int WN, int S>
+__device__ inline void dist_epilogue_sym_lds(const GemmParams& p,
+                                             typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
+                                             unsigned char* lds, int m0, int n0, int wm, int wn,
+                                             int r32, int h) {
+  constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
+  constexpr int LD = BN + 4;
+  constexpr int NT = 64 * WM * WN;
+  float* t = reinterpret_cast<float*>(lds);
+  __syncthreads();  // every wave is done reading the last stage
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * (BM / WM) + i * S + r32;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cb = wn * (BN / WN) + j * S + 4 * h;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        *reinterpret_cast<f32x4*>(t + rr * LD + cb + 8 * q) = v;
+      }
+    }
+  }
+  __syncthreads();
+  float* __restrict__ out = p.out;
+  const int64_t ldo = p.ldo;
+  const int mrem = p.M - m0, nrem = p.Ncol - n0;
+  const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                   (m0 & 3) == 0 && (n0 & 3) == 0;
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+    const int row = idx / C4, col = 4 * (idx - row * C4);
+    if (row >= mrem || col >= nrem) continue;
+    const int gr = m0 + row, gc = n0 + col;
+    const float qn = p.norm_a[gr];
+    f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gn = col + e < nrem ? p.norm_b[gc + e] : 0.f;
+      float d = dist_value(p, a[e], qn, gn);
+      if (p.zero_diag && gr == gc + e) d = 0.f;
+      v[e] = d;
+    }
+    *reinterpret_cast<f32x4*>(t + row * LD + col) = v;  // for the mirror pass
+    float* o = out + (int64_t)gr * ldo + gc;
+    if (vec && col + 3 < nrem && gr <= gc) {
+      *reinterpret_cast<f32x4*>(o) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < nrem && gr <= gc + e) o[e] = v[e];
+    }
+  }
+  __syncthreads();
+  constexpr int R4 = BM / 4;
+  for (int idx = threadIdx.x; idx < BN * R4; idx += NT) {
+    const int col = idx / R4, row = 4 * (idx - col * R4);
+    if (col >= nrem || row >= mrem) continue;
+    const int gc = n0 + col, gr = m0 + row;
+    if (gr >= gc) continue;  // nothing strictly above the diagonal here
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = t[(row + e) * LD + col];
+    float* o = out + (int64_t)gc * ldo + gr;   // out[gc][gr .. gr + 3]
+    if (vec && row + 3 < mrem && gr + 3 < gc) {
+      *reinterpret_cast<f32x4*>(o) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (row + e < mrem && gr + e < gc) o[e] = v[e];
+    }
+  }
+}
+
 // Distance epilogue on transposed accumulators: same formulas as
 // dist_epilogue; 16-byte stores when the output rows are 16-byte aligned.
+// Self-distance tiles (p.sym) write the elements on or above the diagonal
+// and mirror the strictly-upper ones (per element where the tile crosses
+// the diagonal).
 template <int BM, int BN, int WM, int WN, int S = 32>
 __device__ inline void dist_epilogue_t(const GemmParams& p,
                                        typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
@@ -513,8 +626,12 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
   constexpr int TN = BN / WN / S;
   constexpr int NQ = S * S / 256;
   float* __restrict__ out = p.out + (int64_t)m0 * p.ldo + n0;
-  const bool mirror = p.sym && m0 < n0;  // strictly-upper tile of a self-distance
-  const bool diag = p.sym && m0 == n0;   // diagonal tile: its own upper half, mirrored
+  // strictly-upper tile of a self-distance: every element mirrored
+  const bool mirror = p.sym && m0 + BM <= n0;
+  // a tile crossing the diagonal: per element, global row <= column written,
+  // strictly above also mirrored
+  const bool diag = p.sym && !mirror;
+  const int dmn = m0 - n0;
   float* __restrict__ outT = p.out + (int64_t)n0 * p.ldo + m0;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;
@@ -561,13 +678,13 @@ __device__ inline void dist_epilogue_t(const GemmParams& p,
           v[e] = d;
         }
         float* o = out + rr * ldo + c;
-        if (diag) {  // diagonal tile of a self-distance: upper half, mirrored
+        if (diag) {  // a tile on the diagonal: its upper part, mirrored
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int cc = c + e;
-            if (cc < nrem && rr <= cc) {
+            if (cc < nrem && rr + dmn <= cc) {
               o[e] = v[e];
-              if (rr < cc) outT[cc * ldo + rr] = v[e];
+              if (rr + dmn < cc) outT[cc * ldo + rr] = v[e];
             }
           }
           continue;

@@ -240,4 +240,33 @@ int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
                const MergeOffsets& offs, int kout, float* out_vals, int32_t* out_idx,
                hipStream_t st);
 
+// ---- re-ranking (rerank.hip) -------------------------------------------------
+// The concatenated distance matrix M = [[q_q, q_g], [q_g^T, g_g]]
+// (reid_dataset_evaluator.py:447-452) read in place from its blocks (row
+// strides ld*; qgT = q_g transposed, [G][ldT]), and for a SYMMETRIC M (q_q,
+// g_g exactly symmetric) the normalised square of :452-454,
+// OD[i][j] = M[j][i]^2 / colmax[i] = M[i][j]^2 / colmax[i], computed on the fly
+// with the arithmetic of the OD-building kernels ((m * m) / colmax).
+struct RrMatrix {
+  const float* qg;
+  const float* qq;
+  const float* gg;
+  const float* qgT;
+  int64_t ldqg, ldqq, ldgg, ldT, Q, G;
+  const float* colmax;
+  __device__ float m(int64_t r, int64_t c) const {
+    if (r < Q) return c < Q ? qq[r * ldqq + c] : qg[r * ldqg + (c - Q)];
+    return c < Q ? qgT[(r - Q) * ldT + c] : gg[(r - Q) * ldgg + (c - Q)];
+  }
+  __device__ float od(int64_t i, int64_t j) const {
+    const float v = m(i, j);
+    return (v * v) / colmax[i];
+  }
+};
+// stable (value, index) top-k of every row of OD (symmetric M, rows of N =
+// Q + G >= 16384 entries, every block 16-byte aligned): the wave-streaming
+// top-k reading M's blocks in place (no N x N OD buffer)
+int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st);
+bool topk_rr_eligible(const RrMatrix& M, int k);
+
 }  // namespace pps

@@ -1215,28 +1215,54 @@ __device__ unsigned long long wave_cut(unsigned long long* buf, int& n, int k, i
   return T;
 }
 
-template <int KM>
+// RR (re-ranking, rerank.hip): row q is row q of OD for a symmetric M read
+// in place -- a virtual row of the M row's first block (Q entries, padded to
+// naq = Q rounded up to 4 with +inf, never selected) followed by its second
+// block (G entries), each entry transformed to (m * m) / colmax[q] before the
+// filter; packed indices are the global column (virtual index with the pad
+// taken out: a monotone map, so the order is the same).
+template <int KM, bool RR>
 __global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
 topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, int cap,
-                 float* __restrict__ vals, int32_t* __restrict__ idx) {
+                 float* __restrict__ vals, int32_t* __restrict__ idx, RrMatrix rr) {
   extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers
   // wave-uniform: segment bounds, buffer base and counts live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   unsigned long long* buf = tkw + wave * cap;
   const int64_t q = blockIdx.x;
-  const float* row = dist + q * ldd;
+  const float* row = RR ? nullptr : dist + q * ldd;
+  // RR: the two blocks of M's row q
+  const int64_t na = RR ? rr.Q : 0, naq = RR ? (rr.Q + 3) / 4 * 4 : 0;
+  const float* rowA = RR ? (q < rr.Q ? rr.qq + q * rr.ldqq : rr.qgT + (q - rr.Q) * rr.ldT) : nullptr;
+  const float* rowB = RR ? (q < rr.Q ? rr.qg + q * rr.ldqg : rr.gg + (q - rr.Q) * rr.ldgg) : nullptr;
+  const float cm = RR ? rr.colmax[q] : 1.f;
+  if (RR) G = naq + rr.G;  // virtual row length
+  // virtual index -> column of OD
+  auto col = [&](uint32_t i) -> uint32_t {
+    return RR ? (i < (uint32_t)naq ? i : i - (uint32_t)(naq - na)) : i;
+  };
+  // one loaded entry -> its OD value (RR) / itself
+  auto xf = [&](float m, int64_t i) -> float {
+    if (!RR) return m;
+    return (i >= na && i < naq) ? __builtin_huge_valf() : (m * m) / cm;
+  };
   // this wave's segment [s0, s1): whole float4s of the 16-byte-aligned row
   const int64_t GV = G & ~(int64_t)3;
   const int64_t per = ((GV / 4 + kTkwWaves - 1) / kTkwWaves) * 4;
   const int64_t s0 = min(GV, (int64_t)wave * per), s1 = min(GV, s0 + per);
-  const rsrc_t rrow = make_rsrc(row, (uint32_t)(GV * 4));  // past GV: reads zero (masked)
+  const rsrc_t rrow = make_rsrc(RR ? rowA : row, (uint32_t)(GV * 4));  // past GV: reads zero (masked)
   const unsigned long long below = (1ull << lane) - 1ull;
   auto load = [&](int64_t it, f32x4 (&dst)[kTkwU]) {
 #pragma unroll
     for (int u = 0; u < kTkwU; ++u) {
       const int64_t i = s0 + it * kTkwIter + 4 * (u * 64 + lane);
-      dst[u] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rrow, (int)(i < s1 ? i * 4 : GV * 4), 0, 0));
+      if (RR) {  // per-lane block select; past the segment a harmless in-row address
+        const float* a = i >= s1 ? rowA : (i < naq ? rowA + i : rowB + (i - naq));
+        dst[u] = *reinterpret_cast<const f32x4*>(a);
+      } else {
+        dst[u] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rrow, (int)(i < s1 ? i * 4 : GV * 4), 0, 0));
+      }
     }
   };
   const int64_t niter = (s1 - s0 + kTkwIter - 1) / kTkwIter;
@@ -1266,12 +1292,15 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
     asm volatile("" ::: "memory");
     load(it + PPS_TKW_D, nxt);
     unsigned long long m[kTkwU][4], any = 0ull;
+    float ev[kTkwU][4];
 #pragma unroll
     for (int u = 0; u < kTkwU; ++u) {
+      const int64_t iv = s0 + it * kTkwIter + 4 * (u * 64 + lane);
       const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        m[u][t] = __ballot(!(e[t] > thr_f));
+        ev[u][t] = xf(e[t], iv + t);
+        m[u][t] = __ballot(!(ev[u][t] > thr_f));
         any |= m[u][t];
       }
     }
@@ -1280,12 +1309,12 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
 #pragma unroll
       for (int u = 0; u < kTkwU; ++u) {
         const int64_t i0 = s0 + it * kTkwIter + 4 * (u * 64 + lane);
-        const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+        const float* e = ev[u];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (!m[u][t]) continue;
           const int64_t i = i0 + t;
-          const unsigned long long packed = ((unsigned long long)float_key(e[t]) << 32) | (uint32_t)i;
+          const unsigned long long packed = ((unsigned long long)float_key(e[t]) << 32) | col((uint32_t)i);
           const bool take = i < s1 && packed <= thr;
           const unsigned long long bal = __ballot(take);
           if (take) buf[n + __popcll(bal & below)] = packed;
@@ -1301,7 +1330,7 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
 #pragma unroll
     for (int u = 0; u < kTkwU; ++u) {
       const uint32_t i0 = (uint32_t)(s0 + it * kTkwIter) + 4u * (uint32_t)(u * 64 + lane);
-      const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+      const float* e = ev[u];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const unsigned long long mm = m[u][t];
@@ -1311,7 +1340,7 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
           const uint32_t key = ub ^ ((uint32_t)((int32_t)ub >> 31) | 0x80000000u);
           const int pos = n + (int)__builtin_amdgcn_mbcnt_hi(
                                   (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-          buf[pos] = ((unsigned long long)key << 32) | (i0 + (uint32_t)t);
+          buf[pos] = ((unsigned long long)key << 32) | col(i0 + (uint32_t)t);
         }
         n += __popcll(mm);
       }
@@ -1346,8 +1375,9 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
   if (wave == 0 && GV < G) {
     const int64_t i = GV + lane;
     const bool take = i < G;
+    const float e = RR ? (take ? xf(rowB[i - naq], i) : 0.f) : row[take ? i : 0];
     const unsigned long long packed =
-        take ? (((unsigned long long)float_key(row[take ? i : 0]) << 32) | (uint32_t)i) : ~0ull;
+        take ? (((unsigned long long)float_key(e) << 32) | col((uint32_t)i)) : ~0ull;
     const unsigned long long bal = __ballot(take);
     if (take) buf[n + __popcll(bal & below)] = packed;
     n += __popcll(bal);
@@ -1412,12 +1442,13 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
   if (v4 && G >= kTkwMinRow && k <= kTkwMaxK && topk_wave_enabled()) {
     const int cap = tkw_cap(k);
     const size_t lds = (size_t)kTkwWaves * cap * 8;
+    const RrMatrix none{};
     if (k <= 128)
-      hipLaunchKernelGGL(topk_wave_kernel<128>, dim3((unsigned)Q), dim3(kTopkThreads), lds, st,
-                         dist, G, ldd, k, cap, vals, idx);
+      hipLaunchKernelGGL((topk_wave_kernel<128, false>), dim3((unsigned)Q), dim3(kTopkThreads),
+                         lds, st, dist, G, ldd, k, cap, vals, idx, none);
     else
-      hipLaunchKernelGGL(topk_wave_kernel<kTkwMaxK>, dim3((unsigned)Q), dim3(kTopkThreads), lds,
-                         st, dist, G, ldd, k, cap, vals, idx);
+      hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, false>), dim3((unsigned)Q),
+                         dim3(kTopkThreads), lds, st, dist, G, ldd, k, cap, vals, idx, none);
   } else if (v4)
     hipLaunchKernelGGL(topk_kernel<true>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
                        ldd, k, vals, idx);
@@ -1425,6 +1456,31 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
     hipLaunchKernelGGL(topk_kernel<false>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist,
                        G, ldd, k, vals, idx);
   PPS_CHECK_LAUNCH("topk_kernel");
+  return PPS_OK;
+}
+
+bool topk_rr_eligible(const RrMatrix& M, int k) {
+  auto a16 = [](const float* p, int64_t ld) { return aligned16(p) && (ld & 3) == 0; };
+  return M.Q + M.G >= kTkwMinRow && k <= kTkwMaxK && topk_wave_enabled() &&
+         a16(M.qq, M.ldqq) && a16(M.qg, M.ldqg) && a16(M.gg, M.ldgg) && a16(M.qgT, M.ldT) &&
+         M.ldT >= (M.Q + 3) / 4 * 4 && M.ldqq >= (M.Q + 3) / 4 * 4 && M.Q + M.G < (1ll << 31);
+}
+
+int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st) {
+  const int64_t N = M.Q + M.G;
+  if (!topk_rr_eligible(M, k)) {
+    set_error("topk_rr: needs N >= 16384, k <= 256 and 16-byte aligned block rows");
+    return PPS_ERR_INVALID_ARG;
+  }
+  const int cap = tkw_cap(k);
+  const size_t lds = (size_t)kTkwWaves * cap * 8;
+  if (k <= 128)
+    hipLaunchKernelGGL((topk_wave_kernel<128, true>), dim3((unsigned)N), dim3(kTopkThreads), lds,
+                       st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M);
+  else
+    hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, true>), dim3((unsigned)N), dim3(kTopkThreads),
+                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M);
+  PPS_CHECK_LAUNCH("topk_wave_kernel<rr>");
   return PPS_OK;
 }
 

@@ -23,11 +23,23 @@
 
 namespace pps {
 
-// M[r][c] of the concatenated distance matrix (before squaring)
-__device__ inline float rr_m(const float* qg, const float* qq, const float* gg, int64_t Q,
-                             int64_t G, int64_t r, int64_t c) {
-  if (r < Q) return c < Q ? qq[r * Q + c] : qg[r * G + (c - Q)];
-  return c < Q ? qg[c * G + (r - Q)] : gg[(r - Q) * G + (c - Q)];
+// PPS_RERANK_INPLACE=0: keep the dense OD path (A/B runs)
+static bool getenv_flag_off(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '0';
+}
+
+// M[r][c] of the concatenated distance matrix (before squaring), blocks with
+// row strides (q_g^T read from q_g's columns)
+struct RrIn {
+  const float* qg;
+  const float* qq;
+  const float* gg;
+  int64_t ldqg, ldqq, ldgg;
+};
+__device__ inline float rr_m(const RrIn& in, int64_t Q, int64_t r, int64_t c) {
+  if (r < Q) return c < Q ? in.qq[r * in.ldqq + c] : in.qg[r * in.ldqg + (c - Q)];
+  return c < Q ? in.qg[c * in.ldqg + (r - Q)] : in.gg[(r - Q) * in.ldgg + (c - Q)];
 }
 
 // OD rows are padded to a multiple of 4 floats: 16-byte aligned rows let the
@@ -95,10 +107,8 @@ __global__ void rerank_rowmax_sq_kernel(const float* __restrict__ x, int64_t C, 
 #endif
 template <int T>
 __global__ void __launch_bounds__(256)
-rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
-                       const float* __restrict__ gg, int64_t Q, int64_t G,
-                       const float* __restrict__ colmax, float* __restrict__ od, int64_t ldo,
-                       int64_t i_min, int64_t j_max) {
+rerank_build_od_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ colmax,
+                       float* __restrict__ od, int64_t ldo, int64_t i_min, int64_t j_max) {
   // writes OD[i][j] for i >= i_min, j < j_max (tiles cover that window)
   constexpr int H = T / 64;
   __shared__ float tile[T][T + 1];
@@ -116,7 +126,7 @@ rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ q
       for (int h = 0; h < H; ++h) {
         const int64_t j = j0 + tx + 64 * h;
         if (j < N && j < j_max && i >= i_min) {
-          const float m = qg[i * G + (j - Q)];
+          const float m = in.qg[i * in.ldqg + (j - Q)];
           od[i * ldo + j] = (m * m) / cm;
         }
       }
@@ -130,7 +140,7 @@ rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ q
       const int64_t c = i0 + tx + 64 * h;
       float v = 0.f;
       if (r < N && c < N) {
-        const float m = rr_m(qg, qq, gg, Q, G, r, c);
+        const float m = rr_m(in, Q, r, c);
         v = m * m;
       }
       tile[k][tx + 64 * h] = v;
@@ -157,10 +167,8 @@ rerank_build_od_kernel(const float* __restrict__ qg, const float* __restrict__ q
 // thread; same arithmetic (m * m, then / colmax) as the transposing kernel.
 constexpr int kOdRowChunk = 2048;
 __global__ void __launch_bounds__(256)
-rerank_build_od_rows_kernel(const float* __restrict__ qg, const float* __restrict__ qq,
-                            const float* __restrict__ gg, int64_t Q, int64_t G,
-                            const float* __restrict__ colmax, float* __restrict__ od,
-                            int64_t ldo) {
+rerank_build_od_rows_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ colmax,
+                            float* __restrict__ od, int64_t ldo) {
   const int64_t N = Q + G;
   const int64_t i = blockIdx.y;
   // row i's sources: [0, Q) from qq (i < Q) -- none for i >= Q (qg^T, tiled
@@ -176,13 +184,40 @@ rerank_build_od_rows_kernel(const float* __restrict__ qg, const float* __restric
     const int64_t j = j0 + u * 256 + threadIdx.x;
     m[u] = 0.f;
     if (j < N)
-      m[u] = j < Q ? qq[i * Q + j] : (i < Q ? qg[i * G + (j - Q)] : gg[(i - Q) * G + (j - Q)]);
+      m[u] = j < Q ? in.qq[i * in.ldqq + j]
+                   : (i < Q ? in.qg[i * in.ldqg + (j - Q)] : in.gg[(i - Q) * in.ldgg + (j - Q)]);
   }
 #pragma unroll
   for (int u = 0; u < kOdRowChunk / 256; ++u) {
     const int64_t j = j0 + u * 256 + threadIdx.x;
     if (j < N) orow[j] = (m[u] * m[u]) / cm;
   }
+}
+
+// q_g^T [G][ldT] for the in-place path (the one block of M that is not a
+// row of an input): 64 x 64 tiles through LDS, 256-byte row pieces both ways
+__global__ void __launch_bounds__(256)
+rerank_transpose_kernel(const float* __restrict__ qg, int64_t ldqg, int64_t Q, int64_t G,
+                        float* __restrict__ qgT, int64_t ldT) {
+  __shared__ float tile[64][65];
+  const int64_t q0 = blockIdx.y * 64ll, g0 = blockIdx.x * 64ll;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int k = ty; k < 64; k += 4) {
+    const int64_t q = q0 + k, g = g0 + tx;
+    tile[k][tx] = (q < Q && g < G) ? qg[q * ldqg + g] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {
+    const int64_t g = g0 + k, q = q0 + tx;
+    if (g < G && q < Q) qgT[g * ldT + q] = tile[tx][k];
+  }
+}
+
+// OD[i][j]: the dense buffer, or (OTF) computed from M in place
+template <bool OTF>
+__device__ inline float od_at(const float* od, int64_t ldo, const RrMatrix& M, int64_t i,
+                              int64_t j) {
+  return OTF ? M.od(i, j) : od[i * ldo + j];
 }
 
 // ---- 3) V rows -----------------------------------------------------------------
@@ -196,10 +231,12 @@ __device__ inline bool in_row(const int32_t* rank, int K1, int row, int len, int
   return false;
 }
 
+template <bool OTF>
 __global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, int64_t ldo,
                                      const int32_t* __restrict__ rank, int K1, int Kh,
                                      int vcap, int32_t* __restrict__ v_idx,
-                                     float* __restrict__ v_val, int32_t* __restrict__ v_cnt) {
+                                     float* __restrict__ v_val, int32_t* __restrict__ v_cnt,
+                                     RrMatrix M) {
   __shared__ int32_t exp_[kVCap];
   __shared__ int32_t R[64];
   __shared__ int32_t s_n;
@@ -265,12 +302,12 @@ __global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, in
   float wsum = 0.f;
   if (lane == 0) {
     // weight = exp(-OD[i, idx]); V = weight / sum(weight) (float32, in index order)
-    for (int t = 0; t < u; ++t) wsum += expf(-od[i * ldo + exp_[t]]);
+    for (int t = 0; t < u; ++t) wsum += expf(-od_at<OTF>(od, ldo, M, i, exp_[t]));
   }
   wsum = __shfl(wsum, 0);
   const int cap = min(u, vcap);
   for (int t = lane; t < cap; t += 64) {
-    const float w = expf(-od[i * ldo + exp_[t]]);
+    const float w = expf(-od_at<OTF>(od, ldo, M, i, exp_[t]));
     v_idx[i * vcap + t] = exp_[t];
     v_val[i * vcap + t] = w / wsum;
   }
@@ -434,8 +471,9 @@ __global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_
 }
 
 // ---- 6) Jaccard + blend for the query rows ------------------------------------
+template <bool OTF>
 __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restrict__ od,
-                                      int64_t ldo,
+                                      int64_t ldo, RrMatrix M,
                                       const int32_t* __restrict__ q_idx,
                                       const float* __restrict__ q_val,
                                       const int32_t* __restrict__ q_cnt, int qcap,
@@ -461,24 +499,35 @@ __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restr
     const float t = tm[j];
     const float jac = 1.f - __fdiv_rn(t, 2.f - t);
     out[i * (N - Q) + (j - Q)] = __fadd_rn(__fmul_rn(jac, one_m_lam),
-                                           __fmul_rn(od[i * ldo + j], lam));
+                                           __fmul_rn(od_at<OTF>(od, ldo, M, i, j), lam));
   }
 }
 
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
 
-int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t G, int k1,
-           int k2, double lambda, void* ws, size_t ws_bytes, float* out, hipStream_t st,
-           int flags) {
+namespace {
+struct RrLayout {  // V-row capacities of a (k1, k2) configuration
+  int K1, Kh, vcap, qcap;
+  RrLayout(int k1, int k2) {
+    K1 = k1 + 1;
+    Kh = (int)lrint(k1 / 2.0) + 1;  // int(np.around(k1 / 2.)) + 1
+    const int vbound = K1 + K1 * Kh;
+    vcap = vbound <= 256 ? 256 : (vbound <= 512 ? 512 : 1024);
+    qcap = k2 * vcap;
+  }
+};
+}  // namespace
+
+int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const float* gg,
+           int64_t ldgg, int64_t Q, int64_t G, int k1, int k2, double lambda, void* ws,
+           size_t ws_bytes, float* out, hipStream_t st, int flags) {
   // NumPy (NEP 50) casts the Python-float factors to float32: lambda and 1-lambda
   const float lam = (float)lambda, one_m_lam = (float)(1.0 - lambda);
   const int64_t N = Q + G;
   const int64_t ldo = od_stride(N);
-  const int K1 = k1 + 1;
-  const int Kh = (int)lrint(k1 / 2.0) + 1;  // int(np.around(k1 / 2.)) + 1
-  const int vbound = K1 + K1 * Kh;
-  const int vcap = vbound <= 256 ? 256 : (vbound <= 512 ? 512 : 1024);
-  const int qcap = k2 * vcap;
+  const RrLayout L(k1, k2);
+  const int K1 = L.K1, Kh = L.Kh, vcap = L.vcap, qcap = L.qcap;
+  const int64_t ldT = (Q + 3) / 4 * 4;
   // workspace carve-up (all 256-B aligned)
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t bytes) {
@@ -506,40 +555,56 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
               std::to_string((size_t)(p - reinterpret_cast<char*>(ws))) + " bytes");
     return PPS_ERR_CAPACITY;
   }
+  const RrIn in{qg, qq, gg, ldqg, ldqq, ldgg};
+  // In place (symmetric M, long rows, 16-byte rows): no N x N OD buffer --
+  // its top-k, the V weights and the Jaccard blend read M's blocks and
+  // compute (m * m) / colmax on the fly; q_g^T (the block that is nobody's
+  // row) goes where OD would start.
+  RrMatrix M{qg, qq, gg, od, ldqg, ldqq, ldgg, ldT, Q, G, colmax};
+  const bool inplace = (flags & PPS_RERANK_SYMMETRIC) && topk_rr_eligible(M, K1) &&
+                       getenv_flag_off("PPS_RERANK_INPLACE") == false;
   // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M
   unsigned* cm = reinterpret_cast<unsigned*>(colmax);
   (void)hipMemsetAsync(cm, 0, sizeof(unsigned) * N, st);
-  auto colmax_sq = [&](const float* x, int64_t R, int64_t C, unsigned* out) {
+  auto colmax_sq = [&](const float* x, int64_t R, int64_t C, int64_t ld, unsigned* o) {
     if (R <= 0 || C <= 0) return;
     hipLaunchKernelGGL(rerank_colmax_sq_kernel,
                        dim3((unsigned)((C + 255) / 256), (unsigned)((R + kCmRows - 1) / kCmRows)),
-                       dim3(256), 0, st, x, R, C, C, out);
+                       dim3(256), 0, st, x, R, C, ld, o);
   };
-  colmax_sq(qq, Q, Q, cm);      // columns c < Q: rows r < Q
-  colmax_sq(qg, Q, G, cm + Q);  // columns c >= Q: rows r < Q
-  colmax_sq(gg, G, G, cm + Q);  // columns c >= Q: rows r >= Q
-  hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, G,
+  colmax_sq(qq, Q, Q, ldqq, cm);      // columns c < Q: rows r < Q
+  colmax_sq(qg, Q, G, ldqg, cm + Q);  // columns c >= Q: rows r < Q
+  colmax_sq(gg, G, G, ldgg, cm + Q);  // columns c >= Q: rows r >= Q
+  hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, ldqg,
                      cm);       // columns c < Q: rows r >= Q (qg^T)
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
   constexpr int T = PPS_OD_TILE;
-  if (flags & PPS_RERANK_SYMMETRIC) {
-    // rows streamed from M's rows; only the qg^T block (i >= Q, j < Q) is
-    // transposed
-    hipLaunchKernelGGL(rerank_build_od_rows_kernel,
-                       dim3((unsigned)((N + kOdRowChunk - 1) / kOdRowChunk), (unsigned)N),
-                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo);
-    PPS_CHECK_LAUNCH_S("rerank_build_od_rows_kernel", st);
-    const int64_t ti = (N + T - 1) / T - Q / T;   // row tiles covering [Q, N)
-    hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((Q + T - 1) / T), (unsigned)ti),
-                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo, Q, Q);
+  if (inplace) {
+    hipLaunchKernelGGL(rerank_transpose_kernel, dim3((unsigned)((G + 63) / 64), (unsigned)((Q + 63) / 64)),
+                       dim3(256), 0, st, qg, ldqg, Q, G, od, ldT);
+    PPS_CHECK_LAUNCH_S("rerank_transpose_kernel", st);
+    const int rc = topk_rr(M, K1, topv, rank, st);
+    if (rc != PPS_OK) return rc;
   } else {
-    hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((N + T - 1) / T),
-                                                       (unsigned)((N + T - 1) / T)),
-                       dim3(256), 0, st, qg, qq, gg, Q, G, colmax, od, ldo, (int64_t)0, N);
+    if (flags & PPS_RERANK_SYMMETRIC) {
+      // rows streamed from M's rows; only the qg^T block (i >= Q, j < Q) is
+      // transposed
+      hipLaunchKernelGGL(rerank_build_od_rows_kernel,
+                         dim3((unsigned)((N + kOdRowChunk - 1) / kOdRowChunk), (unsigned)N),
+                         dim3(256), 0, st, in, Q, G, colmax, od, ldo);
+      PPS_CHECK_LAUNCH_S("rerank_build_od_rows_kernel", st);
+      const int64_t ti = (N + T - 1) / T - Q / T;   // row tiles covering [Q, N)
+      hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((Q + T - 1) / T), (unsigned)ti),
+                         dim3(256), 0, st, in, Q, G, colmax, od, ldo, Q, Q);
+    } else {
+      hipLaunchKernelGGL(rerank_build_od_kernel<T>, dim3((unsigned)((N + T - 1) / T),
+                                                         (unsigned)((N + T - 1) / T)),
+                         dim3(256), 0, st, in, Q, G, colmax, od, ldo, (int64_t)0, N);
+    }
+    PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
+    const int rc = topk(od, N, N, ldo, K1, topv, rank, st);
+    if (rc != PPS_OK) return rc;
   }
-  PPS_CHECK_LAUNCH_S("rerank_build_od_kernel", st);
-  int rc = topk(od, N, N, ldo, K1, topv, rank, st);
-  if (rc != PPS_OK) return rc;
   PPS_CHECK_LAUNCH_S("rerank topk", st);
   if (debug_sync()) {  // every neighbour index must address a row of OD
     std::vector<int32_t> h((size_t)(N * K1));
@@ -551,8 +616,12 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
         return PPS_ERR_LAUNCH;
       }
   }
-  hipLaunchKernelGGL(rerank_v_rows_kernel, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo, rank,
-                     K1, Kh, vcap, v_idx, v_val, v_cnt);
+  if (inplace)
+    hipLaunchKernelGGL(rerank_v_rows_kernel<true>, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo,
+                       rank, K1, Kh, vcap, v_idx, v_val, v_cnt, M);
+  else
+    hipLaunchKernelGGL(rerank_v_rows_kernel<false>, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo,
+                       rank, K1, Kh, vcap, v_idx, v_val, v_cnt, M);
   PPS_CHECK_LAUNCH_S("rerank_v_rows_kernel", st);
   if (k2 != 1) {
     hipLaunchKernelGGL(rerank_vqe_kernel, dim3((unsigned)N), dim3(256), 0, st, N, rank, K1, k2,
@@ -574,22 +643,25 @@ int rerank(const float* qg, const float* qq, const float* gg, int64_t Q, int64_t
   hipLaunchKernelGGL(rerank_csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
                      q_val, q_cnt, qc, start, fill, csc_row, csc_val);
   PPS_CHECK_LAUNCH_S("rerank_csc_fill_kernel", st);
-  hipLaunchKernelGGL(rerank_jaccard_kernel, dim3((unsigned)Q), dim3(256), sizeof(float) * N, st,
-                     Q, N, od, ldo, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam, one_m_lam,
-                     out);
+  if (inplace)
+    hipLaunchKernelGGL(rerank_jaccard_kernel<true>, dim3((unsigned)Q), dim3(256), sizeof(float) * N,
+                       st, Q, N, od, ldo, M, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam,
+                       one_m_lam, out);
+  else
+    hipLaunchKernelGGL(rerank_jaccard_kernel<false>, dim3((unsigned)Q), dim3(256), sizeof(float) * N,
+                       st, Q, N, od, ldo, M, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam,
+                       one_m_lam, out);
   PPS_CHECK_LAUNCH_S("rerank_jaccard_kernel", st);
   return PPS_OK;
 }
 
 size_t rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   const int64_t N = Q + G;
-  const int K1 = k1 + 1;
-  const int Kh = (int)lrint(k1 / 2.0) + 1;
-  const int vbound = K1 + K1 * Kh;
-  const int vcap = vbound <= 256 ? 256 : (vbound <= 512 ? 512 : 1024);
-  const int64_t qcap = (int64_t)k2 * vcap;
+  const RrLayout L(k1, k2);
+  const int64_t K1 = L.K1, vcap = L.vcap, qcap = L.qcap;
   auto r = [](size_t b) { return (b + 255) / 256 * 256; };
   size_t s = 0;
+  // the OD buffer also holds q_g^T ([G][Q rounded up to 4] <= N x od_stride)
   s += r(4 * N * od_stride(N)) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
   s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
   return s;

@@ -188,11 +188,12 @@ class HipBackend(object):
 
     @staticmethod
     def self_dist(x, metric):
-        return ops.compute_dist(x, x, metric=metric)
+        return ops.compute_dist(x, x, metric=metric, pad_rows=True)
 
     @staticmethod
     def re_ranking(q_g, q_q, g_g):
-        return ops.re_ranking(q_g.contiguous(), q_q.contiguous(), g_g.contiguous())
+        # strided blocks go in as they are (a copy would drop the symmetric mark)
+        return ops.re_ranking(q_g, q_q, g_g)
 
     @staticmethod
     def rank_eval(dist, qid, gid, qcam, gcam):

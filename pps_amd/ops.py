@@ -489,10 +489,12 @@ def ap_finalize(sorted_d, pos_total, hist, before):
 
 def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None):
     """k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519) -> [Q, G].
-    symmetric: q_q and g_g are exactly symmetric (PPS_RERANK_SYMMETRIC: the
-    N x N matrix is built from rows, only q_g^T is transposed); None = both
-    came from compute_dist's mirrored self-distance (tagged
-    `_pps_symmetric`).  Same result either way on symmetric inputs."""
+    symmetric: q_q and g_g are exactly symmetric (PPS_RERANK_SYMMETRIC: with
+    16-byte rows and N >= 16384 the N x N normalised distance is never built,
+    pps_re_ranking_ld; else it is built from rows, only q_g^T transposed);
+    None = both came from compute_dist's mirrored self-distance (tagged
+    `_pps_symmetric`).  Same result either way on symmetric inputs.  Inputs
+    may be row-padded views (dist_buffer / compute_dist(pad_rows=True))."""
     Q, G = q_g.shape
     assert tuple(q_q.shape) == (Q, Q) and tuple(g_g.shape) == (G, G)
     if symmetric is None:
@@ -503,9 +505,10 @@ def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None):
         raise RuntimeError('bad re-ranking arguments')
     ws = torch.empty((int(nbytes),), dtype=torch.uint8, device=q_g.device)
     out = torch.empty((Q, G), dtype=torch.float32, device=q_g.device)
-    call('pps_re_ranking_flags', _dev(q_g, 'q_g'), _dev(q_q, 'q_q'), _dev(g_g, 'g_g'), Q, G,
-         k1, k2, float(lambda_value), RERANK_SYMMETRIC if symmetric else 0, ws.data_ptr(),
-         int(nbytes), out.data_ptr(), _stream())
+    call('pps_re_ranking_ld', _dev_rows(q_g, 'q_g'), _ld(q_g), _dev_rows(q_q, 'q_q'), _ld(q_q),
+         _dev_rows(g_g, 'g_g'), _ld(g_g), Q, G, k1, k2, float(lambda_value),
+         RERANK_SYMMETRIC if symmetric else 0, ws.data_ptr(), int(nbytes), out.data_ptr(),
+         _stream())
     return out
 
 

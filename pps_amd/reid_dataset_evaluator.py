@@ -218,9 +218,10 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
     if cfg.REID.RERANK:
         # :161-207 -- re-ranked scores overwrite the plain ones
         with measure_time('Re-ranking distance...', verbose):
-            q_q = ops.compute_dist(qf, qf, metric=metric)
-            g_g = ops.compute_dist(gf, gf, metric=metric)
-            rr = ops.re_ranking(q_g.contiguous(), q_q, g_g)
+            # 16-byte rows: re-ranking reads the blocks in place (no N x N copy)
+            q_q = ops.compute_dist(qf, qf, metric=metric, pad_rows=True)
+            g_g = ops.compute_dist(gf, gf, metric=metric, pad_rows=True)
+            rr = ops.re_ranking(q_g, q_q, g_g)
         with measure_time('Computing scores for re-ranked distance...', verbose):
             mAP, cmc_scores = compute_score(rr, ids[q_inds], ids[g_inds], cams[q_inds],
                                             cams[g_inds])
@@ -229,8 +230,8 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
             print_scores(mAP, cmc_scores)
         if mq_inds.any():
             with measure_time('Multi Query, Re-ranking distance...', verbose):
-                mq_mq = ops.compute_dist(pooled, pooled, metric=metric)
-                rr_mq = ops.re_ranking(mq_g.contiguous(), mq_mq, g_g)
+                mq_mq = ops.compute_dist(pooled, pooled, metric=metric, pad_rows=True)
+                rr_mq = ops.re_ranking(mq_g, mq_mq, g_g)
             with measure_time('Multi Query, Computing scores for re-ranked distance...',
                               verbose):
                 mq_mAP, mq_cmc = compute_score(rr_mq, keys[:, 0], ids[g_inds], keys[:, 1],

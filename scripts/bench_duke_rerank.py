@@ -52,12 +52,12 @@ def main():
     for rep in range(a.reps + 1):
         e = [ev() for _ in range(5)]
         e[0].record()
-        q_g = ops.compute_dist(qf, gf, metric='cosine')
+        q_g = ops.compute_dist(qf, gf, metric='cosine', pad_rows=True)
         e[1].record()
         mark('q_g')
-        q_q = ops.compute_dist(qf, qf, metric='cosine')
+        q_q = ops.compute_dist(qf, qf, metric='cosine', pad_rows=True)
         mark('q_q')
-        g_g = ops.compute_dist(gf, gf, metric='cosine')
+        g_g = ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
         mark('g_g')
         e[2].record()
         rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)   # q_q, g_g mirrored: symmetric path

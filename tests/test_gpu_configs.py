@@ -232,11 +232,17 @@ def test_rerank_long_rows_vs_oracle():
     f = cent[np.concatenate([qid, gid])] + 2.5 * rng.randn(Q + G, D).astype(np.float32)
     f = (f / np.linalg.norm(f, axis=1, keepdims=True)).astype(np.float32)
     qg = ev.compute_dist(f[:Q], f[Q:])
-    qq = ev.compute_dist(f[:Q], f[:Q])
-    gg = ev.compute_dist(f[Q:], f[Q:])
+    # exactly symmetric self-distances (upper triangle mirrored, as the GPU's
+    # self-distance GEMM returns them), so the in-place path runs: N >= 16384,
+    # 16-byte rows (Q, G % 4 == 0), PPS_RERANK_SYMMETRIC
+    sym = lambda d: np.triu(d) + np.triu(d, 1).T
+    qq = sym(ev.compute_dist(f[:Q], f[:Q]))
+    gg = sym(ev.compute_dist(f[Q:], f[Q:]))
     ref = ev.re_ranking_sparse(qg, qq, gg, k1=20, k2=6, lambda_value=0.3)
-    rr = ops.re_ranking(*(torch.from_numpy(np.ascontiguousarray(x)).cuda()
-                          for x in (qg, qq, gg)), 20, 6, 0.3)
+    dev = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (qg, qq, gg)]
+    rr = ops.re_ranking(*dev, k1=20, k2=6, lambda_value=0.3, symmetric=True)
+    dense = ops.re_ranking(*dev, k1=20, k2=6, lambda_value=0.3, symmetric=False)
+    assert torch.equal(rr, dense)   # in place == the dense N x N path, bit for bit
     rrn = rr.cpu().numpy()
     err = float(np.abs(rrn - ref).max())
     ap, valid, first = gev.rank_eval(rr, qid, gid, qcam, gcam)
@@ -244,6 +250,30 @@ def test_rerank_long_rows_vs_oracle():
                            qid, gid, qcam, gcam, tie_eps(rrn, ref))
     print('re-ranking 1000 x 15500 (long rows): max|err| %.3g, %s' % (err, r))
     assert err < 1e-5, err
+
+
+def test_rerank_inplace_equals_dense_duke_shape():
+    """Duke shape (2228 + 17661, odd G): the padded blocks from
+    compute_dist(pad_rows=True) take the in-place path (no N x N buffer); the
+    same blocks copied dense take the dense OD path -- identical bits, also
+    against the non-symmetric (transposing) OD path."""
+    from pps_amd import ops
+    Q, G, D = 2228, 17661, 256
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(3)
+    rng = np.random.RandomState(3)
+    x = _feats(300, rng.randint(1, 301, Q + G), D, gen, noise=2.5)
+    qf, gf = x[:Q].contiguous(), x[Q:].contiguous()
+    q_g = ops.compute_dist(qf, gf, metric='cosine', pad_rows=True)
+    q_q = ops.compute_dist(qf, qf, metric='cosine', pad_rows=True)
+    g_g = ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
+    assert q_g.stride(0) % 4 == 0 and g_g.stride(0) % 4 == 0
+    a = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+    b = ops.re_ranking(q_g.contiguous(), q_q.contiguous(), g_g.contiguous(), 20, 6, 0.3,
+                       symmetric=True)
+    c = ops.re_ranking(q_g.contiguous(), q_q.contiguous(), g_g.contiguous(), 20, 6, 0.3,
+                       symmetric=False)
+    assert torch.equal(a, b) and torch.equal(a, c)
 
 
 def test_duke_full_size_cosine_rerank_properties():
