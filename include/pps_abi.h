@@ -215,10 +215,11 @@ int pps_ap_finalize(int64_t Q, int Ptot, const float* sorted_d,
  *    (distance, global index) -> sorted_d / sorted_idx [Q][R*Pmax] (padding
  *    +inf / -1), pos_total [Q], and the query's bin-lookup cells
  *    [Q][pps_rank_cells()] (int32, 16-byte aligned) that c) reads.
- *    Capacity: R*Pmax <= 8192 merged positives per query (the merge sort
- *    holds 16 B per positive in LDS: 128 KiB of gfx950's 160 KiB), else
- *    PPS_ERR_CAPACITY -- i.e. one identity may have at most 8192 / R
- *    same-id gallery entries per shard (Market: 72).
+ *    Up to R*Pmax = 8192 merged positives per query the merge sort runs in
+ *    LDS (16 B per positive, 128 KiB of gfx950's 160 KiB); beyond, the
+ *    query's lists are sorted in place in its sorted_d / sorted_idx row in
+ *    global memory (same order; slower, for identities with thousands of
+ *    gallery entries per shard).  No capacity limit (R*Pmax < 2^30).
  * c) pps_rank_count_stream: for this shard's rows, hist[q][p] += #entries
  *    with p = first positive d_p >= d, before[q] += #entries ordered before
  *    the first positive, over all entries of the row minus this shard's junk

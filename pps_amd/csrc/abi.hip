@@ -374,11 +374,9 @@ int pps_rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32
   PPS_ENFORCE(((uintptr_t)cells & 15) == 0, "cells must be 16-byte aligned");
   PPS_ENFORCE(R >= 1 && R <= kMergeMaxLists, "R must be in [1, 64]");
   PPS_ENFORCE(Q >= 0 && Pmax > 0, "bad shape");
-  if ((int64_t)R * Pmax > kRankMergeCap) {
-    set_error("merged positive capacity R*Pmax=" + std::to_string((int64_t)R * Pmax) +
-              " exceeds " + std::to_string(kRankMergeCap) + " (LDS of the merge sort)");
-    return PPS_ERR_CAPACITY;
-  }
+  // beyond kRankMergeCap merged positives the lists are sorted in place in
+  // global memory (rank_prepare_global_kernel): no capacity limit
+  PPS_ENFORCE((int64_t)R * Pmax < (1ll << 30), "R * Pmax must be < 2^30");
   return rank_prepare(R, Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total,
                       cells, as_stream(stream));
 }

@@ -443,10 +443,104 @@ __global__ void rank_prepare_kernel(int R, int64_t Q, int Pmax, const float* __r
   }
 }
 
+// b') rank_prepare for merged lists longer than the LDS merge holds (R*Pmax
+// > kRankMergeCap: an identity with thousands of gallery entries per shard).
+// The query's lists are copied into its output row (sorted_d / sorted_idx,
+// padding +inf / -1 past P) and sorted there in place by the block: a
+// bitonic network for any length -- the first compare of each merge step
+// mirrors inside the block (i <-> block end - 1 - i), the rest are half-
+// cleaners, every compare puts the smaller (distance, index) key first and
+// partners at or past P are skipped (they act as +inf at the end) -- over
+// the L2-resident row, one block barrier per stage.  Keys are unique
+// (global indices), so the order is the LDS path's.  Then the bin-lookup
+// cells from the sorted row (the positive's cell computed on the fly).
+__global__ void rank_prepare_global_kernel(int R, int64_t Q, int Pmax,
+                                           const float* __restrict__ pos_d,
+                                           const int32_t* __restrict__ pos_idx,
+                                           const int32_t* __restrict__ pos_cnt,
+                                           float* __restrict__ sorted_d,
+                                           int32_t* __restrict__ sorted_idx,
+                                           int32_t* __restrict__ pos_total,
+                                           int32_t* __restrict__ cells) {
+  const int64_t q = blockIdx.x;
+  const int64_t Ptot = (int64_t)R * Pmax;
+  __shared__ int offs[kMergeMaxLists + 1];
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int r = 0; r < R; ++r) {
+      offs[r] = o;
+      const int c = pos_cnt[(int64_t)r * Q + q];
+      o += c < Pmax ? c : Pmax;
+    }
+    offs[R] = o;
+  }
+  __syncthreads();
+  const int P = offs[R];
+  float* gd = sorted_d + q * Ptot;
+  int32_t* gi = sorted_idx + q * Ptot;
+  for (int r = 0; r < R; ++r) {
+    const int n = offs[r + 1] - offs[r];
+    for (int p = threadIdx.x; p < n; p += blockDim.x) {
+      gd[offs[r] + p] = pos_d[((int64_t)r * Q + q) * Pmax + p];
+      gi[offs[r] + p] = pos_idx[((int64_t)r * Q + q) * Pmax + p];
+    }
+  }
+  for (int64_t p = P + threadIdx.x; p < Ptot; p += blockDim.x) {
+    gd[p] = INFINITY;
+    gi[p] = -1;
+  }
+  if (threadIdx.x == 0) pos_total[q] = P;
+  if (P == 0) return;  // uniform
+  __syncthreads();
+  auto cas = [&](int i, int j) {  // i < j: the smaller key to i
+    const float di = gd[i], dj = gd[j];
+    const int ii = gi[i], ij = gi[j];
+    if (key_less(dj, ij, di, ii)) {
+      gd[i] = dj; gi[i] = ij;
+      gd[j] = di; gi[j] = ii;
+    }
+  };
+  int n2 = 1;
+  while (n2 < P) n2 <<= 1;
+  for (int size = 2; size <= n2; size <<= 1) {
+    const int half = size >> 1;
+    for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {  // mirror step
+      const int b = t / half, o = t - b * half;
+      const int i = b * size + o, j = b * size + size - 1 - o;
+      if (j < P) cas(i, j);
+    }
+    __syncthreads();
+    for (int stride = half >> 1; stride > 0; stride >>= 1) {  // half-cleaners
+      for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
+        const int b = t / stride, o = t - b * stride;
+        const int i = 2 * b * stride + o, j = i + stride;
+        if (j < P) cas(i, j);
+      }
+      __syncthreads();
+    }
+  }
+  const float df = gd[0], inv = cell_scale(df, gd[P - 1]);
+  for (int c = threadIdx.x; c < kStreamCells; c += blockDim.x) {
+    int lo = 0, hi = P;  // first positive whose cell is >= c (non-decreasing in p)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cell_of(gd[mid], df, inv) < c) lo = mid + 1; else hi = mid;
+    }
+    cells[q * kStreamCells + c] = lo | ((lo < P && cell_of(gd[lo], df, inv) == c) ? kCellDirty : 0);
+  }
+}
+
 int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* pos_idx,
                  const int32_t* pos_cnt, float* sorted_d, int32_t* sorted_idx,
                  int32_t* pos_total, int32_t* cells, hipStream_t st) {
   if (Q <= 0) return PPS_OK;
+  if ((int64_t)R * Pmax > kRankMergeCap) {
+    hipLaunchKernelGGL(rank_prepare_global_kernel, dim3((unsigned)Q), dim3(kEvalThreads), 0, st,
+                       R, Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total,
+                       cells);
+    PPS_CHECK_LAUNCH("rank_prepare_global_kernel");
+    return PPS_OK;
+  }
   const size_t lds = (size_t)4 * R * Pmax * sizeof(int);
   hipLaunchKernelGGL(rank_prepare_kernel, dim3((unsigned)Q), dim3(kEvalThreads), lds, st, R,
                      Q, Pmax, pos_d, pos_idx, pos_cnt, sorted_d, sorted_idx, pos_total, cells);

@@ -62,9 +62,9 @@ def rank_eval(distmat, query_ids, gallery_ids, query_cams, gallery_cams, index=N
     true matches listed from a per-identity gallery index (ops.MatchIndex,
     built from the ids unless given), then one streaming count pass over the
     distance rows (pps_collect_matches / pps_rank_prepare /
-    pps_rank_count_stream / pps_ap_finalize).  Capacity: a query's identity
-    may have at most 8192 same-id gallery entries (pps_rank_prepare's LDS
-    merge; RuntimeError with PPS_ERR_CAPACITY beyond)."""
+    pps_rank_count_stream / pps_ap_finalize).  No capacity limit on a
+    query's true matches (pps_rank_prepare sorts lists beyond its LDS merge
+    in global memory)."""
     d = distmat if isinstance(distmat, torch.Tensor) and distmat.is_cuda and \
         distmat.dtype == torch.float32 and distmat.dim() == 2 and \
         (distmat.shape[0] < 2 or distmat.stride(1) == 1) else _to_dev(distmat)

@@ -504,3 +504,63 @@ def test_sharded_evaluator_tiled_query_planes(golden, case):
         assert abs(o['mAP'] - outs[0]['mAP']) < 1e-9
         np.testing.assert_array_equal(o['cmc'], outs[0]['cmc'])
     assert abs(outs[1]['mAP'] - float(g['mAP'])) < 1e-6
+
+
+def test_rank_prepare_beyond_lds_merge_cap():
+    """four gallery shards, one identity with 3000 entries
+    in every shard -- R * Pmax = 12000 merged positives, past the LDS merge
+    (8192): pps_rank_prepare sorts in global memory.  AP, validity and the
+    first-match rank of every query equal the oracle's mean_ap / the stable
+    argsort on the same float32 distances (reid_dataset_evaluator.py:366-439),
+    sharded and unsharded alike."""
+    from pps_amd import ops
+    R, Gs, big, D = 4, 4000, 3000, 32
+    rng = np.random.RandomState(11)
+    gid = np.concatenate([np.concatenate([np.full(big, 7), rng.randint(100, 600, Gs - big)])
+                          for _ in range(R)])
+    gcam = rng.randint(1, 7, R * Gs)
+    Q = 48
+    qid = np.concatenate([np.full(12, 7), rng.randint(100, 600, Q - 12)])
+    qcam = rng.randint(1, 7, Q)
+    f = rng.randn(Q + R * Gs, D).astype(np.float32)
+    d = ev.compute_dist(f[:Q], f[Q:])
+    dd = _cuda(d)
+    ref_ap, ref_valid = ev.mean_ap(d, qid, gid, qcam, gcam, average=False)
+    for shards in (1, R):
+        cuts = [r * (R * Gs) // shards for r in range(shards + 1)]
+        lists, parts = [], []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            ds = dd[:, a:b].contiguous()
+            idx = ops.MatchIndex(qid, qcam, gid[a:b], gcam[a:b])
+            p = ops.collect_matches(ds, idx, a, big * R // shards + 16)
+            lists.append(p[:3])
+            parts.append((ds, a, p[3]))
+        sp = ops.rank_prepare(torch.stack([l[0] for l in lists]),
+                              torch.stack([l[1] for l in lists]),
+                              torch.stack([l[2] for l in lists]))
+        assert sp.sorted_d.shape[1] > 8192
+        hist = before = None
+        for ds, a, junk in parts:
+            hist, before = ops.rank_count_stream(ds, a, sp, junk, hist, before)
+        ap, valid, first = ops.ap_finalize(sp.sorted_d, sp.pos_total, hist, before)
+        ap, valid, first = ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy()
+        np.testing.assert_array_equal(valid.astype(bool), ref_valid)
+        np.testing.assert_allclose(ap[ref_valid], ref_ap, rtol=0, atol=1e-12)
+        # first match: valid entries (not same id + same camera) before the
+        # first true match in the stable (distance, index) order
+        for q in range(Q):
+            order = np.lexsort((np.arange(d.shape[1]), d[q]))
+            junk = (gid[order] == qid[q]) & (gcam[order] == qcam[q])
+            o = order[~junk]
+            hit = np.nonzero(gid[o] == qid[q])[0]
+            assert first[q] == (hit[0] if len(hit) else -1), q
+        # the merged rows are the positives in (distance, index) order
+        q = 0
+        P = int(sp.pos_total[q])
+        assert P > 8192
+        sd = sp.sorted_d[q, :P].cpu().numpy()
+        si = sp.sorted_idx[q, :P].cpu().numpy()
+        pos = np.nonzero((gid == qid[q]) & (gcam != qcam[q]))[0]
+        want = pos[np.lexsort((pos, d[q, pos]))]
+        np.testing.assert_array_equal(si, want)
+        np.testing.assert_array_equal(sd, d[q, want])
