@@ -264,6 +264,16 @@ int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_
                      int topk, int first_match_break, double* ret, int32_t* valid,
                      void* stream);
 
+/* The whole rank list: idx [Q][ldi] int32, row q = every gallery column in
+ * (distance, index) order -- np.argsort(distmat, axis=1, kind='stable'), the
+ * reference's `indices = np.argsort(distmat, axis=1)`
+ * (reid_dataset_evaluator.py:319,420) with ties in index order; vals
+ * (optional, [Q][ldv]) the sorted distances.  One row per workgroup in LDS
+ * (bucket map of the row's own range + in-bucket ranks): G <=
+ * pps_argsort_rows_cap() (18368), else PPS_ERR_INVALID_ARG. */
+int pps_argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32_t* idx,
+                     int64_t ldi, float* vals, int64_t ldv, void* stream);
+int pps_argsort_rows_cap(void);
 /* Stable per-row top-k (k <= 1024) of a distance matrix, ascending, ties by
  * gallery index.  Replaces the `np.argsort(distmat, axis=1)[:, :k]` rank
  * list (reid_dataset_evaluator.py:319,420). */

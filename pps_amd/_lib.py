@@ -52,6 +52,7 @@ SIGNATURES = {
     'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                         c_ptr],
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_argsort_rows': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
     'pps_cmc_counts': [c_ptr, c_i64, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_cmc_finalize': [c_i64, c_int, c_ptr, c_ptr, c_int, c_int, c_ptr, c_ptr, c_ptr],
@@ -140,6 +141,7 @@ EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
     'pps_gemm_num_tiles': ([], ctypes.c_int),
     'pps_rank_cells': ([], ctypes.c_int),
+    'pps_argsort_rows_cap': ([], ctypes.c_int),
     'pps_stem_k': ([], ctypes.c_int),
     'pps_stem_variant': ([ctypes.c_int], ctypes.c_int),
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),

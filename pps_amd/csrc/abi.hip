@@ -38,6 +38,9 @@ int rank_counts(const float*, int64_t, int64_t, int64_t, const int32_t*, const i
 int ap_finalize(int64_t, int, const float*, const int32_t*, const int32_t*,
                 const int32_t*, double*, int32_t*, int32_t*, hipStream_t);
 int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStream_t);
+int argsort_rows(const float*, int64_t, int64_t, int64_t, int32_t*, int64_t, float*, int64_t,
+                 hipStream_t);
+int argsort_rows_cap();
 int cmc_counts(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
                const int32_t*, const int32_t*, const int32_t*, const int32_t*, int,
                const float*, const int32_t*, const int32_t*, int32_t*, hipStream_t);
@@ -445,6 +448,17 @@ int pps_topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float*
   PPS_ENFORCE(G < (1ll << 31), "G must fit int32");
   return topk(dist, Q, G, ldd, k, vals, idx, as_stream(stream));
 }
+
+int pps_argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32_t* idx,
+                     int64_t ldi, float* vals, int64_t ldv, void* stream) {
+  PPS_ENFORCE(dist && idx, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldd >= G && ldi >= G && (!vals || ldv >= G), "bad shape");
+  PPS_ENFORCE(G <= argsort_rows_cap(), "rows longer than " + std::to_string(argsort_rows_cap()) +
+                                           " entries (pps_argsort_rows_cap): use pps_topk");
+  return argsort_rows(dist, Q, G, ldd, idx, ldi, vals, ldv, as_stream(stream));
+}
+
+int pps_argsort_rows_cap(void) { return argsort_rows_cap(); }
 
 int pps_topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int k_in,
                    const int64_t* list_offsets, int k_out, float* out_vals,

@@ -283,6 +283,19 @@ def pairwise_distance(X):
     return Z
 
 
+def argsort_rows(dist, with_values=False):
+    """Every row's columns in stable (distance, index) order -> idx [Q, G]
+    int32 (and the sorted distances): np.argsort(dist, axis=1,
+    kind='stable') -- the reference's full rank list
+    (reid_dataset_evaluator.py:319,420).  G <= pps_argsort_rows_cap()."""
+    Q, G = dist.shape
+    idx = torch.empty((Q, G), dtype=torch.int32, device=dist.device)
+    vals = torch.empty((Q, G), dtype=torch.float32, device=dist.device) if with_values else None
+    call('pps_argsort_rows', _dev_rows(dist, 'dist'), Q, G, _ld(dist), idx.data_ptr(), G,
+         vals.data_ptr() if vals is not None else None, G, _stream())
+    return (idx, vals) if with_values else idx
+
+
 def topk(dist, k):
     """Stable ascending top-k per row -> (vals [Q,k] f32, idx [Q,k] i32)."""
     Q, G = dist.shape

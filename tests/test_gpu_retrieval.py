@@ -564,3 +564,45 @@ def test_rank_prepare_beyond_lds_merge_cap():
         want = pos[np.lexsort((pos, d[q, pos]))]
         np.testing.assert_array_equal(si, want)
         np.testing.assert_array_equal(sd, d[q, want])
+
+
+@pytest.mark.parametrize('Q,G,kind', [(3368, 15913, 'market'), (64, 17661, 'ties'),
+                                      (37, 1, 'plain'), (5, 4099, 'degenerate'),
+                                      (40, 18368, 'plain')])
+def test_argsort_rows_equals_stable_argsort(Q, G, kind):
+    """pps_argsort_rows == np.argsort(kind='stable') on every row (VERDICT
+    r03 item 8): Market-sized rows of L2 distances (the reference's full rank
+    list, reid_dataset_evaluator.py:319,420), rows with heavy ties and
+    negative zeros, all-equal and two-valued rows (one bucket: the wave
+    bitonic path), the maximum row length."""
+    from pps_amd import ops
+    rng = np.random.RandomState(G + Q)
+    if kind == 'market':
+        d = np.sqrt(rng.chisquare(50, size=(Q, G)).astype(np.float32) / 25)
+    elif kind == 'ties':
+        d = (rng.randint(0, 300, (Q, G)) / 16).astype(np.float32)
+        d[1] = -0.0
+        d[2, ::3] = 0.0
+        d[3] = np.float32(np.inf)
+        d[3, 7] = 1.0
+    elif kind == 'degenerate':
+        d = np.ones((Q, G), np.float32)
+        d[1, ::2] = 2.0
+        d[2] = rng.rand(G).astype(np.float32) * 1e-30
+        d[3] = np.float32(3.0) + np.arange(G, dtype=np.float32) * 1e-7
+    else:
+        d = rng.randn(Q, G).astype(np.float32)
+    buf = ops.dist_buffer(Q, G, 'cuda')
+    buf.copy_(torch.from_numpy(d))
+    idx, vals = ops.argsort_rows(buf, with_values=True)
+    want = np.argsort(d, axis=1, kind='stable')
+    got = idx.cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(d, want, 1))
+
+
+def test_argsort_rows_capacity_error():
+    from pps_amd import ops
+    cap = ops._lib.lib().pps_argsort_rows_cap()
+    with pytest.raises(RuntimeError, match='pps_topk'):
+        ops.argsort_rows(torch.zeros((2, cap + 1), device='cuda'))
