@@ -442,6 +442,19 @@ int pps_conv2d_bn_act_x3p_splitk_fused(const float* x, const uint16_t* x3, int64
                                        uint16_t* y3, int64_t y_plane, int Ho, int Wo,
                                        int ldy, int splitk, float* part, int* counters,
                                        int64_t n_counters, int tile, void* stream);
+/* The bottleneck seam (ResNet.py:276-333): branch2c of an identity block and
+ * branch2a of the next block in one launch, for the 1x1 stride-1 shapes of
+ * res2 / res3, (K1, N1, N2) = (64, 256, 64) or (128, 512, 128):
+ *   trunk [M][N1] = relu(x [M][K1] . w2c^T * scale2c + shift2c + residual)
+ *   y     [M][N2] = relu(trunk . w2a^T * scale2a + shift2a)
+ * w2c / w2a: bf16x3 planes [3][N1][K1] / [3][N2][N1] (pps_split_bf16x3 of
+ * the packed weights).  trunk is written (the next block's shortcut) but
+ * not read back.  Both outputs equal two pps_conv2d_bn_act_x3p calls on a
+ * 16x16x32-block tile (ids 38-55) bit for bit. */
+int pps_conv1x1_seam_x3(const float* x, int64_t M, int K1, const uint16_t* w2c, int N1,
+                        const float* scale2c, const float* shift2c, const float* residual,
+                        float* trunk, const uint16_t* w2a, int N2, const float* scale2a,
+                        const float* shift2a, float* y, void* stream);
 int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin,
                               int ldx, int KH, int KW, int stride, int pad,
                               const float* x2, int H2, int W2, int Cin2,

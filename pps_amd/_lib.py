@@ -52,6 +52,8 @@ SIGNATURES = {
     'pps_ap_finalize': [c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                         c_ptr],
     'pps_topk': [c_ptr, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr],
+    'pps_conv1x1_seam_x3': [c_ptr, c_i64, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
+                            c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_argsort_rows': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
     'pps_cmc_counts': [c_ptr, c_i64, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],

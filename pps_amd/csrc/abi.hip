@@ -518,6 +518,25 @@ int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t
                               ws_bytes, out, stream);
 }
 
+int pps_conv1x1_seam_x3(const float* x, int64_t M, int K1, const uint16_t* w2c, int N1,
+                        const float* scale2c, const float* shift2c, const float* residual,
+                        float* trunk, const uint16_t* w2a, int N2, const float* scale2a,
+                        const float* shift2a, float* y, void* stream) {
+  PPS_ENFORCE(x && w2c && scale2c && shift2c && residual && trunk && w2a && scale2a && shift2a &&
+                  y,
+              "null pointer");
+  PPS_ENFORCE(M >= 0 && M * N1 * 4 < kMaxBufBytes, "bad M");
+  PPS_ENFORCE(seam_supported(K1, N1, N2),
+              "bottleneck seam: (K1, N1, N2) must be (64, 256, 64) or (128, 512, 128), got (" +
+                  std::to_string(K1) + ", " + std::to_string(N1) + ", " + std::to_string(N2) + ")");
+  PPS_ENFORCE(aligned16(x) && aligned16(w2c) && aligned16(residual) && aligned16(trunk) &&
+                  aligned16(w2a) && aligned16(y) && aligned16(scale2c) && aligned16(shift2c) &&
+                  aligned16(scale2a) && aligned16(shift2a),
+              "seam operands must be 16-byte aligned");
+  SeamParams p{x, residual, w2c, scale2c, shift2c, trunk, w2a, scale2a, shift2a, y, (int)M};
+  return launch_seam_x3(p, K1, N1, N2, as_stream(stream));
+}
+
 // weights either f32 [Cout][Kpad] (x3 = 0) or bf16x3 planes [3][Cout][Kpad]
 // x3p: bf16x3 activation planes (x_pl / y_pl, plane strides in elements)
 // instead of f32 x / y -- gemm_x3p.hip tiles only

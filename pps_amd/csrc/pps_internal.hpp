@@ -222,6 +222,23 @@ int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
 int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
 int x3c_tile_cols(int tile);
 
+// ---- bottleneck seam (gemm_seam.hip): branch2c of block i + branch2a of block i+1
+struct SeamParams {
+  const float* a;        // [M][K1] branch2c input (f32 NHWC rows)
+  const float* res;      // [M][N1] the block's shortcut (its input trunk)
+  const uint16_t* w2c;   // [3][N1][K1] bf16x3 planes, plane stride N1 * K1
+  const float* s2c;
+  const float* t2c;
+  float* t;              // [M][N1] trunk out
+  const uint16_t* w2a;   // [3][N2][N1] planes, plane stride N2 * N1
+  const float* s2a;
+  const float* t2a;
+  float* y;              // [M][N2] next branch2a out
+  int M;
+};
+bool seam_supported(int K1, int N1, int N2);
+int launch_seam_x3(const SeamParams& p, int K1, int N1, int N2, hipStream_t st);
+
 // ---- retrieval (rank.hip) ---------------------------------------------------
 constexpr int kMergeMaxLists = 64;
 // rank_count_stream / cmc_counts: gallery entries per workgroup (grid.y =

@@ -690,6 +690,26 @@ def conv2d_bn_act_x3p(x, cin, w3, kpad, k, stride, pad, dil, scale, shift, resid
     return y
 
 
+def conv1x1_seam(x, w2c3, scale2c, shift2c, residual, trunk, w2a3, scale2a, shift2a, y):
+    """branch2c of an identity bottleneck + branch2a of the next one in one
+    launch (pps_conv1x1_seam_x3): trunk = relu(x . w2c * s + t + residual),
+    y = relu(trunk . w2a * s + t); x [..., K1], trunk / residual [..., N1],
+    y [..., N2] NHWC f32, (K1, N1, N2) = (64, 256, 64) or (128, 512, 128);
+    w2c3 / w2a3 bf16x3 planes of the packed [Cout][Kpad] weights.  Same bits
+    as the two convolutions on a 16x16x32-block tile."""
+    K1, N1, N2 = x.shape[-1], trunk.shape[-1], y.shape[-1]
+    M = x.numel() // K1
+    if residual.shape != trunk.shape or y.numel() // N2 != M or trunk.numel() // N1 != M:
+        raise RuntimeError('seam shapes: x %s, residual %s, trunk %s, y %s'
+                           % (tuple(x.shape), tuple(residual.shape), tuple(trunk.shape),
+                              tuple(y.shape)))
+    call('pps_conv1x1_seam_x3', _dev(x, 'x'), M, K1, _dev(w2c3, 'w2c', torch.int16), N1,
+         _dev(scale2c, 'scale2c'), _dev(shift2c, 'shift2c'), _dev(residual, 'residual'),
+         _dev(trunk, 'trunk'), _dev(w2a3, 'w2a', torch.int16), N2, _dev(scale2a, 'scale2a'),
+         _dev(shift2a, 'shift2a'), _dev(y, 'y'), _stream())
+    return trunk, y
+
+
 def conv2d_dual_bn_act(x, cin, k, stride, pad, x2, stride2, w, kpad1, shift, relu, y,
                        tile=0):
     """relu?(conv_k(x) + conv_1x1/stride2(x2) + shift), BN scales folded in w."""
