@@ -301,7 +301,8 @@ int pps_distmat_x3_self_tiled(const uint16_t* x3t, int64_t N, const float* xsq, 
   p.ldb = D; p.kb_valid = D; p.Ncol = (int)N;
   p.Kloop = D;
   p.norm_a = xsq; p.norm_b = xsq;
-  p.out = out; p.ldo = ldo; p.metric = metric; p.sym = 1; p.tile = tile;
+  p.out = out; p.ldo = ldo; p.metric = metric; p.sym = 1;
+  p.tile = tile ? tile : GEMM_TILE_P16_FIRST + 5;  // 128 x 256 (the distance matrix's)
   return launch_gemm_x3(p, EPI_DIST, 1, as_stream(stream));
 }
 

@@ -25,6 +25,8 @@
 // order then fma(acc, scale, shift) + residual, ReLU; 2a the same on T's
 // exact bf16x3 split with its K chunks in increasing order -- the sequence of
 // the S = 16 tiles (38-55): both outputs equal the unfused layers' bits.
+#include <cstdlib>
+
 #include "gemm_x3_common.hpp"
 
 namespace pps {
@@ -32,11 +34,10 @@ namespace pps {
 
 namespace {
 
-constexpr int kSeamWaves = 8;
-constexpr int kSeamRows = 16 * kSeamWaves;
-
-template <int K1, int N1, int N2, int CG>
+template <int K1, int N1, int N2, int CG, int W>
 struct SeamCfg {
+  static constexpr int NW = W;                 // waves = 16-row blocks per tile
+  static constexpr int ROWS = 16 * W;
   static constexpr int NCG = N1 / CG;          // stages per tile
   static constexpr int KC1 = K1 / 32;          // 2c K chunks
   static constexpr int JC = CG / 16;           // 2c column blocks per stage
@@ -45,28 +46,35 @@ struct SeamCfg {
   static constexpr int W2C = CG * K1 * 6;      // W2c slab bytes
   static constexpr int W2A = N2 * CG * 6;      // W2a slab bytes
   static constexpr int STAGE = W2C + W2A;
-  static constexpr int PPT = STAGE / 16 / (64 * kSeamWaves);  // 16-B pieces per thread
+  static constexpr int PPT = STAGE / 16 / (64 * W);  // 16-B pieces per thread
   static constexpr int LDT = CG + 4;           // scratch row (floats)
   static constexpr int SCR = 16 * LDT * 4;     // scratch bytes per wave
   static constexpr int C4 = CG / 4;            // lanes per scratch row (row layout)
   static constexpr int RPI = 64 / C4;          // rows per row-layout instruction
   static constexpr int NIT = 16 / RPI;         // row-layout instructions per 16 rows
   static constexpr int SSH = (2 * N1 + 2 * N2) * 4;
-  static constexpr int LDS = 2 * STAGE + kSeamWaves * SCR + SSH;
+  static constexpr int LDS = 2 * STAGE + W * SCR + SSH;
   // the next tile's A rows requested two stages ahead (K1 = 128: 32 more
   // live registers than the 256 of a two-wave-per-SIMD kernel allow)
   static constexpr bool PREA = K1 <= 64;
+  // residual blocks requested PD stages ahead (an HBM-bound kernel needs
+  // ~64 KB in flight per CU: two stages of 32 KB at CG = 64); PD = 2 runs
+  // the NCG stages of a tile unrolled, the ring slot of a stage = its index
+  static constexpr int PD = (K1 <= 64 && NCG <= 4) ? 2 : 1;
   static_assert(N1 % CG == 0 && CG % 32 == 0 && K1 % 32 == 0 && N2 % 16 == 0, "seam shape");
-  static_assert(PPT * 16 * 64 * kSeamWaves == STAGE, "slab does not split into pieces");
+  static_assert(PPT * 16 * 64 * W == STAGE && PPT % 2 == 0 && W2C == W2A,
+                "slab does not split into two equal halves of pieces");
   static_assert(RPI * C4 == 64 && NIT * RPI == 16, "scratch row layout");
   static_assert(N2 % CG == 0 && NCG % 2 == 0 && NCG >= 2, "2a epilogue in CG-column groups; stage pairs");
   static_assert(LDS <= 160 * 1024, "seam LDS");
 };
 
-template <int K1, int N1, int N2, int CG>
-__global__ void __launch_bounds__(64 * kSeamWaves)
+template <int K1, int N1, int N2, int CG, int W>
+__global__ void __launch_bounds__(64 * W)
 seam_kernel(SeamParams p, int ntiles) {
-  using C = SeamCfg<K1, N1, N2, CG>;
+  using C = SeamCfg<K1, N1, N2, CG, W>;
+  constexpr int kSeamWaves = W;
+  constexpr int kSeamRows = C::ROWS;
   __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -110,19 +118,24 @@ seam_kernel(SeamParams p, int ntiles) {
     loff = C::W2C + (pk * N2 + n) * 64 + ((slot ^ ((n >> 2) & 3)) << 4);
     return p.w2a;
   };
-  auto wload = [&](int cg, u32x4 (&wr)[C::PPT]) {
+  // the slab in two halves of PPT / 2 pieces: the W2c half (read by 2c) and
+  // the W2a half (read by 2a), so the staging registers hold one half at a
+  // time: the next stage's W2c half is requested at the top of a stage and
+  // stored after 2c, its W2a half requested then and stored after 2a
+  constexpr int HP = C::PPT / 2;
+  auto wload = [&](int cg, int half, u32x4 (&wr)[HP]) {
 #pragma unroll
-    for (int i = 0; i < C::PPT; ++i) {
+    for (int i = 0; i < HP; ++i) {
       int g, l;
-      const uint16_t* base = piece(i, cg, g, l);
+      const uint16_t* base = piece(half * HP + i, cg, g, l);
       wr[i] = *reinterpret_cast<const u32x4*>(base + g);
     }
   };
-  auto wstore = [&](int buf, const u32x4 (&wr)[C::PPT]) {
+  auto wstore = [&](int buf, int half, const u32x4 (&wr)[HP]) {
 #pragma unroll
-    for (int i = 0; i < C::PPT; ++i) {
+    for (int i = 0; i < HP; ++i) {
       int g, l;
-      (void)piece(i, 0, g, l);
+      (void)piece(half * HP + i, 0, g, l);
       *reinterpret_cast<u32x4*>(lds + buf * C::STAGE + l) = wr[i];
     }
   };
@@ -150,11 +163,19 @@ seam_kernel(SeamParams p, int ntiles) {
   const int t0 = blockIdx.x;
   f32x4 av[C::KC1][2];
   f32x4 rv0[C::NIT], rv1[C::NIT];
-  u32x4 wr[C::PPT];
+  f32x4 rvr[C::PD == 2 ? C::NCG : 1][C::NIT];
+  u32x4 wr[HP];
   aload(t0, av);
   rload(t0, 0, rv0);
-  wload(0, wr);
-  wstore(0, wr);
+  if constexpr (C::PD == 2) {
+#pragma unroll
+    for (int it = 0; it < C::NIT; ++it) rvr[0][it] = rv0[it];
+    rload(t0, 1, rvr[1]);
+  }
+  wload(0, 0, wr);
+  wstore(0, 0, wr);
+  wload(0, 1, wr);
+  wstore(0, 1, wr);
   __syncthreads();
 
   for (int tile = t0; tile < ntiles; tile += gridDim.x) {
@@ -168,13 +189,15 @@ seam_kernel(SeamParams p, int ntiles) {
     const int mbase = tile * kSeamRows + wave * 16;
     // one stage: rcur = its residual block (requested a stage ago), rnxt
     // receives the next stage's
-    auto stage = [&](int cg, f32x4 (&rcur)[C::NIT], f32x4 (&rnxt)[C::NIT], bool next_a) {
+    auto stage = [&](int cg, f32x4 (&rcur)[C::NIT], f32x4 (&rnxt)[C::NIT], bool next_a,
+                     int rl_tile, int rl_cg) {
       const int buf = cg & 1;   // NCG is even: stage parity repeats every tile
       // next stage's weights and residual (stage 0 of the next tile at the
       // end); the next tile's A rows two stages before they are split
       const bool last = cg + 1 == C::NCG;
-      wload(last ? 0 : cg + 1, wr);
-      rload(last ? tnext : tile, last ? 0 : cg + 1, rnxt);
+      const int cgn = last ? 0 : cg + 1;
+      wload(cgn, 0, wr);
+      rload(rl_tile, rl_cg, rnxt);
       if (next_a) aload(tnext, av);
       const unsigned char* sl = lds + buf * C::STAGE;
       // 2c: this wave's 16 x CG block
@@ -214,6 +237,8 @@ seam_kernel(SeamParams p, int ntiles) {
         *reinterpret_cast<f32x4*>(scr + row * C::LDT + col) = v;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wstore(buf ^ 1, 0, wr);
+      wload(cgn, 1, wr);
       // 2a: the finished block as K chunks cg KC2 .. of the next layer
 #pragma unroll
       for (int c = 0; c < C::KC2; ++c) {
@@ -235,19 +260,27 @@ seam_kernel(SeamParams p, int ntiles) {
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done
-      wstore(buf ^ 1, wr);
+      wstore(buf ^ 1, 1, wr);
       __syncthreads();
     };
     // two stages per trip (the residual ring's buffers keep static names);
     // the last two stages outside the loop, where the next tile's A rows are
     // requested (a load inside the loop would keep them live all along)
-    for (int cg = 0; cg < C::NCG - 2; cg += 2) {
-      stage(cg, rv0, rv1, false);
-      stage(cg + 1, rv1, rv0, false);
+    if constexpr (C::PD == 2) {
+#pragma unroll
+      for (int cg = 0; cg < C::NCG; ++cg) {
+        const int nx = cg + 2;
+        stage(cg, rvr[cg], rvr[nx % C::NCG], cg == C::NCG - 2, nx < C::NCG ? tile : tnext,
+              nx % C::NCG);
+      }
+    } else {
+      for (int cg = 0; cg < C::NCG - 2; cg += 2) {
+        stage(cg, rv0, rv1, false, tile, cg + 1);
+        stage(cg + 1, rv1, rv0, false, tile, cg + 2);
+      }
+      stage(C::NCG - 2, rv0, rv1, C::PREA, tile, C::NCG - 1);
+      stage(C::NCG - 1, rv1, rv0, false, tnext, 0);
     }
-    stage(C::NCG - 2, rv0, rv1, C::PREA);
-    stage(C::NCG - 1, rv1, rv0, false);
-    if (!C::PREA) aload(tnext, av);   // (res3: the prefetch would spill)
     // 2a epilogue in CG-column groups through the scratch: Y = relu(acc s + t)
 #pragma unroll
     for (int g = 0; g < N2 / CG; ++g) {
@@ -270,18 +303,20 @@ seam_kernel(SeamParams p, int ntiles) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (!C::PREA) aload(tnext, av);   // (res3: requested earlier it would spill)
   }
 }
 
-template <int K1, int N1, int N2, int CG>
+template <int K1, int N1, int N2, int CG, int W>
 int launch_seam(const SeamParams& p, hipStream_t st) {
+  constexpr int kSeamRows = 16 * W;
   const int ntiles = (p.M + kSeamRows - 1) / kSeamRows;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = ntiles < cus ? ntiles : cus;
-  hipLaunchKernelGGL((seam_kernel<K1, N1, N2, CG>), dim3((unsigned)grid), dim3(64 * kSeamWaves), 0,
-                     st, p, ntiles);
+  hipLaunchKernelGGL((seam_kernel<K1, N1, N2, CG, W>), dim3((unsigned)grid), dim3(64 * W), 0, st,
+                     p, ntiles);
   PPS_CHECK_LAUNCH("seam_kernel");
   return PPS_OK;
 }
@@ -294,8 +329,19 @@ bool seam_supported(int K1, int N1, int N2) {
 
 int launch_seam_x3(const SeamParams& p, int K1, int N1, int N2, hipStream_t st) {
   if (p.M <= 0) return PPS_OK;
-  if (K1 == 64 && N1 == 256 && N2 == 64) return launch_seam<64, 256, 64, 64>(p, st);
-  if (K1 == 128 && N1 == 512 && N2 == 128) return launch_seam<128, 512, 128, 32>(p, st);
+  // res2 (M = 196,608 at batch 64): 128-row tiles, 6 per CU; res3 (M =
+  // 49,152): 128-row tiles leave half the CUs one tile behind (384 tiles);
+  // 96-row tiles (6 waves) spill
+  if (K1 == 64 && N1 == 256 && N2 == 64) return launch_seam<64, 256, 64, 64, 8>(p, st);
+  if (K1 == 128 && N1 == 512 && N2 == 128) {
+    // PPS_SEAM_W3 (probes): 4 = 64-row tiles, one wave per SIMD, 3 per CU
+    static const int w3 = [] {
+      const char* e = getenv("PPS_SEAM_W3");
+      return e ? atoi(e) : 8;
+    }();
+    if (w3 == 4) return launch_seam<128, 512, 128, 32, 4>(p, st);
+    return launch_seam<128, 512, 128, 32, 8>(p, st);
+  }
   set_error("bottleneck seam: shapes (K1, N1, N2) = (64, 256, 64) or (128, 512, 128) only");
   return PPS_ERR_INVALID_ARG;
 }

@@ -263,7 +263,13 @@ int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
 // strides ld*; qgT = q_g transposed, [G][ldT]), and for a SYMMETRIC M (q_q,
 // g_g exactly symmetric) the normalised square of :452-454,
 // OD[i][j] = M[j][i]^2 / colmax[i] = M[i][j]^2 / colmax[i], computed on the fly
-// with the arithmetic of the OD-building kernels ((m * m) / colmax).
+// with the arithmetic of the OD-building kernels (rr_od).
+// OD's arithmetic, float32 as NumPy does it (np.power(M, 2) then / colmax):
+// a rounded square and an IEEE (correctly rounded) division -- spelled with
+// the _rn intrinsics so that every kernel computing it gives the same bits
+// (a plain `/` may be lowered to a reciprocal-based approximation)
+__device__ inline float rr_od(float m, float cm) { return __fdiv_rn(__fmul_rn(m, m), cm); }
+
 struct RrMatrix {
   const float* qg;
   const float* qq;
@@ -276,8 +282,7 @@ struct RrMatrix {
     return c < Q ? qgT[(r - Q) * ldT + c] : gg[(r - Q) * ldgg + (c - Q)];
   }
   __device__ float od(int64_t i, int64_t j) const {
-    const float v = m(i, j);
-    return (v * v) / colmax[i];
+    return rr_od(m(i, j), colmax[i]);
   }
 };
 // stable (value, index) top-k of every row of OD (symmetric M, rows of N =

@@ -1312,7 +1312,7 @@ __device__ unsigned long long wave_cut(unsigned long long* buf, int& n, int k, i
 // RR (re-ranking, rerank.hip): row q is row q of OD for a symmetric M read
 // in place -- a virtual row of the M row's first block (Q entries, padded to
 // naq = Q rounded up to 4 with +inf, never selected) followed by its second
-// block (G entries), each entry transformed to (m * m) / colmax[q] before the
+// block (G entries), each entry transformed to rr_od(m, colmax[q]) before the
 // filter; packed indices are the global column (virtual index with the pad
 // taken out: a monotone map, so the order is the same).
 template <int KM, bool RR>
@@ -1338,7 +1338,7 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
   // one loaded entry -> its OD value (RR) / itself
   auto xf = [&](float m, int64_t i) -> float {
     if (!RR) return m;
-    return (i >= na && i < naq) ? __builtin_huge_valf() : (m * m) / cm;
+    return (i >= na && i < naq) ? __builtin_huge_valf() : rr_od(m, cm);
   };
   // this wave's segment [s0, s1): whole float4s of the 16-byte-aligned row
   const int64_t GV = G & ~(int64_t)3;

@@ -127,7 +127,7 @@ rerank_build_od_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ 
         const int64_t j = j0 + tx + 64 * h;
         if (j < N && j < j_max && i >= i_min) {
           const float m = in.qg[i * in.ldqg + (j - Q)];
-          od[i * ldo + j] = (m * m) / cm;
+          od[i * ldo + j] = rr_od(m, cm);
         }
       }
     }
@@ -141,7 +141,7 @@ rerank_build_od_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ 
       float v = 0.f;
       if (r < N && c < N) {
         const float m = rr_m(in, Q, r, c);
-        v = m * m;
+        v = m;
       }
       tile[k][tx + 64 * h] = v;
     }
@@ -154,7 +154,7 @@ rerank_build_od_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ 
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const int64_t j = j0 + tx + 64 * h;
-      if (j < N && j < j_max) od[i * ldo + j] = tile[tx + 64 * h][k] / cm;
+      if (j < N && j < j_max) od[i * ldo + j] = rr_od(tile[tx + 64 * h][k], cm);
     }
   }
 }
@@ -164,7 +164,7 @@ rerank_build_od_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ 
 // M[i][j]^2 / colmax[i] is a row-major scaled copy of M's rows -- except the
 // block i >= Q, j < Q, which is qg^T and keeps the tiled transpose above.
 // One block streams kOdRowChunk entries of one OD row, 8 loads in flight per
-// thread; same arithmetic (m * m, then / colmax) as the transposing kernel.
+// thread; same arithmetic (rr_od) as the transposing kernel.
 constexpr int kOdRowChunk = 2048;
 __global__ void __launch_bounds__(256)
 rerank_build_od_rows_kernel(RrIn in, int64_t Q, int64_t G, const float* __restrict__ colmax,
@@ -190,7 +190,7 @@ rerank_build_od_rows_kernel(RrIn in, int64_t Q, int64_t G, const float* __restri
 #pragma unroll
   for (int u = 0; u < kOdRowChunk / 256; ++u) {
     const int64_t j = j0 + u * 256 + threadIdx.x;
-    if (j < N) orow[j] = (m[u] * m[u]) / cm;
+    if (j < N) orow[j] = rr_od(m[u], cm);
   }
 }
 

@@ -26,6 +26,8 @@ def timeit(fn, n=20):
 
 def main():
     for name, H, W, K1, t2c, t2a in (('res2', 96, 32, 64, 54, 54), ('res3', 48, 16, 128, 54, 47)):
+        if os.environ.get('ONLY') and os.environ['ONLY'] != name:
+            continue
         N = 64
         N1, N2 = 4 * K1, K1
         rng = np.random.RandomState(0)
