@@ -268,7 +268,8 @@ int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
 // a rounded square and an IEEE (correctly rounded) division -- spelled with
 // the _rn intrinsics so that every kernel computing it gives the same bits
 // (a plain `/` may be lowered to a reciprocal-based approximation)
-__device__ inline float rr_od(float m, float cm) { return __fdiv_rn(__fmul_rn(m, m), cm); }
+// (m * m) / cm, both rounded (a product feeding a division cannot fuse)
+__device__ inline float rr_od(float m, float cm) { return (m * m) / cm; }
 
 struct RrMatrix {
   const float* qg;

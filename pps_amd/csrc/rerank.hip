@@ -21,6 +21,15 @@
 
 #include "pps_internal.hpp"
 
+// NumPy rounds every float32 product and sum on its own; hipcc's default
+// fp-contract=fast would fuse e.g. the final blend jac * (1 - l) + od * l
+// into an FMA (one rounding fewer), differently in each instantiation --
+// off for the whole file (re-ranking is memory-bound; no FMA is needed).
+// The pragma governs operators written in this file only: the __fmul_rn /
+// __fadd_rn header helpers are plain operators compiled under the default
+// contract setting and DO fuse after inlining, so they are not used here.
+#pragma clang fp contract(off)
+
 namespace pps {
 
 // PPS_RERANK_INPLACE=0: keep the dense OD path (A/B runs)
@@ -497,9 +506,10 @@ __global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restr
   }
   for (int64_t j = Q + threadIdx.x; j < N; j += blockDim.x) {
     const float t = tm[j];
-    const float jac = 1.f - __fdiv_rn(t, 2.f - t);
-    out[i * (N - Q) + (j - Q)] = __fadd_rn(__fmul_rn(jac, one_m_lam),
-                                           __fmul_rn(od_at<OTF>(od, ldo, M, i, j), lam));
+    const float jac = 1.f - t / (2.f - t);
+    const float wj = jac * one_m_lam;                          // rounded
+    const float wo = od_at<OTF>(od, ldo, M, i, j) * lam;       // rounded
+    out[i * (N - Q) + (j - Q)] = wj + wo;
   }
 }
 

@@ -26,11 +26,12 @@ def main():
     N = Q + G
     nbytes = _lib.lib().pps_rerank_workspace_bytes(Q, G, k1, k2)
     outs, wss = [], []
-    for flags in (1, 0):
+    lam = float(os.environ.get('LAM', '0.3'))
+    for flags in (1, 0, 1):
         ws = torch.zeros((int(nbytes),), dtype=torch.uint8, device='cuda')
         out = torch.empty((Q, G), device='cuda')
         call('pps_re_ranking_ld', dev[0].data_ptr(), G, dev[1].data_ptr(), Q, dev[2].data_ptr(), G,
-             Q, G, k1, k2, 0.3, flags, ws.data_ptr(), int(nbytes), out.data_ptr(),
+             Q, G, k1, k2, lam, flags, ws.data_ptr(), int(nbytes), out.data_ptr(),
              torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         outs.append(out.cpu().numpy())
@@ -42,7 +43,9 @@ def main():
     regions = []
     for name, nb, dt in (('colmax', 4 * N, np.float32), ('topv', 4 * N * K1, np.float32),
                          ('rank', 4 * N * K1, np.int32), ('v_idx', 4 * N * 256, np.int32),
-                         ('v_val', 4 * N * 256, np.float32), ('v_cnt', 4 * N, np.int32)):
+                         ('v_val', 4 * N * 256, np.float32), ('v_cnt', 4 * N, np.int32),
+                         ('q_idx', 4 * N * 1536, np.int32), ('q_val', 4 * N * 1536, np.float32),
+                         ('q_cnt', 4 * N, np.int32)):
         regions.append((name, off, nb, dt))
         off += r(nb)
     for name, o, nb, dt in regions:
@@ -59,7 +62,13 @@ def main():
         i = rows[0]
         print('row', i, 'inplace', rank_a[i], '\ndense  ', rank_b[i])
     d = np.abs(outs[0] - outs[1])
-    print('out max diff', d.max(), 'count', int((d > 0).sum()))
+    print('lambda', lam, 'out max diff', d.max(), 'count', int((d > 0).sum()))
+    d2 = np.abs(outs[0] - outs[2])
+    print('in-place run to run: max diff', d2.max(), 'count', int((d2 > 0).sum()))
+    ref = ev.re_ranking_sparse(qg, qq, gg, k1=k1, k2=k2, lambda_value=lam)
+    for nm, o in (('inplace', outs[0]), ('dense', outs[1])):
+        e = np.abs(o - ref)
+        print(nm, 'vs oracle max', e.max(), 'exact', int((e == 0).sum()), 'of', e.size)
 
 
 if __name__ == '__main__':

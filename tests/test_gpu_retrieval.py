@@ -526,6 +526,7 @@ def test_rank_prepare_beyond_lds_merge_cap():
     d = ev.compute_dist(f[:Q], f[Q:])
     dd = _cuda(d)
     ref_ap, ref_valid = ev.mean_ap(d, qid, gid, qcam, gcam, average=False)
+    ref_valid = np.asarray(ref_valid).astype(bool)
     for shards in (1, R):
         cuts = [r * (R * Gs) // shards for r in range(shards + 1)]
         lists, parts = [], []
@@ -545,7 +546,7 @@ def test_rank_prepare_beyond_lds_merge_cap():
         ap, valid, first = ops.ap_finalize(sp.sorted_d, sp.pos_total, hist, before)
         ap, valid, first = ap.cpu().numpy(), valid.cpu().numpy(), first.cpu().numpy()
         np.testing.assert_array_equal(valid.astype(bool), ref_valid)
-        np.testing.assert_allclose(ap[ref_valid], ref_ap, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(ap[ref_valid], np.asarray(ref_ap)[ref_valid], rtol=0, atol=1e-12)
         # first match: valid entries (not same id + same camera) before the
         # first true match in the stable (distance, index) order
         for q in range(Q):
