@@ -298,7 +298,7 @@ int pps_topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int 
  * the stable (distance, index) order.  q_g [Q][G], q_q [Q][Q], g_g [G][G]
  * (euclidean distances, as compute_dist returns them).  Workspace: a caller
  * device buffer of pps_rerank_workspace_bytes(Q, G, k1, k2) bytes
- * (dominated by the dense N x N normalised distance, N = Q + G <= 40960). */
+ * (dominated by the dense N x N normalised distance, N = Q + G; G <= 38400). */
 int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2);
 int pps_re_ranking(const float* q_g, const float* q_q, const float* g_g, int64_t Q,
                    int64_t G, int k1, int k2, double lambda_value, void* workspace,

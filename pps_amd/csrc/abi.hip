@@ -498,7 +498,8 @@ int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t
   PPS_ENFORCE(K1 + K1 * Kh <= 1024, "expansion bound (k1+1)(round(k1/2)+2) must be <= 1024");
   PPS_ENFORCE(k2 * (K1 + K1 * Kh <= 256 ? 256 : (K1 + K1 * Kh <= 512 ? 512 : 1024)) <= 4096,
               "k2 * V row capacity must be <= 4096");
-  PPS_ENFORCE((Q + G) * 4 <= 160 * 1024, "Q + G must be <= 40960 (LDS accumulator)");
+  PPS_ENFORCE(jaccard_lds_bytes(G) + 2048 <= 160 * 1024,
+              "G must be <= 38400 (the Jaccard pass keeps a gallery row in LDS)");
   PPS_ENFORCE((Q + G) >= K1, "need Q + G >= k1 + 1");
   PPS_ENFORCE((flags & ~PPS_RERANK_SYMMETRIC) == 0, "unknown re-ranking flags");
   return rerank(q_g, ld_qg, q_q, ld_qq, g_g, ld_gg, Q, G, k1, k2, lambda_value, workspace,

@@ -269,6 +269,9 @@ int topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int kin,
 // the _rn intrinsics so that every kernel computing it gives the same bits
 // (a plain `/` may be lowered to a reciprocal-based approximation)
 // (m * m) / cm, both rounded (a product feeding a division cannot fuse)
+// dynamic LDS of the Jaccard pass for a gallery of G (rerank.hip)
+size_t jaccard_lds_bytes(int64_t G);
+
 __device__ inline float rr_od(float m, float cm) { return (m * m) / cm; }
 
 struct RrMatrix {

@@ -1315,15 +1315,26 @@ __device__ unsigned long long wave_cut(unsigned long long* buf, int& n, int k, i
 // block (G entries), each entry transformed to rr_od(m, colmax[q]) before the
 // filter; packed indices are the global column (virtual index with the pad
 // taken out: a monotone map, so the order is the same).
-template <int KM, bool RR>
+//
+// WPR (waves per row) 1: every wave streams a whole row of its own (a block
+// holds four rows) -- for many rows of moderate length (re-ranking's N rows
+// of N), where four waves per row would each cut their short segment three or
+// four times and then merge: one wave per row cuts ~log(row / 512) times in
+// all and sorts its own k, no block barrier.
+template <int KM, bool RR, int WPR = kTkwWaves>
 __global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
 topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, int cap,
-                 float* __restrict__ vals, int32_t* __restrict__ idx, RrMatrix rr) {
+                 float* __restrict__ vals, int32_t* __restrict__ idx, RrMatrix rr,
+                 int64_t nrows) {
+  static_assert(WPR == 1 || WPR == kTkwWaves, "one wave or the whole block per row");
   extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers
   // wave-uniform: segment bounds, buffer base and counts live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   unsigned long long* buf = tkw + wave * cap;
-  const int64_t q = blockIdx.x;
+  constexpr int RPB = kTkwWaves / WPR;   // rows per block
+  const int wseg = wave % WPR;           // this wave's segment of its row
+  const int64_t q = (int64_t)blockIdx.x * RPB + wave / WPR;
+  if (WPR == 1 && q >= nrows) return;   // (WPR = 1 has no block barrier)
   const float* row = RR ? nullptr : dist + q * ldd;
   // RR: the two blocks of M's row q
   const int64_t na = RR ? rr.Q : 0, naq = RR ? (rr.Q + 3) / 4 * 4 : 0;
@@ -1342,8 +1353,8 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
   };
   // this wave's segment [s0, s1): whole float4s of the 16-byte-aligned row
   const int64_t GV = G & ~(int64_t)3;
-  const int64_t per = ((GV / 4 + kTkwWaves - 1) / kTkwWaves) * 4;
-  const int64_t s0 = min(GV, (int64_t)wave * per), s1 = min(GV, s0 + per);
+  const int64_t per = ((GV / 4 + WPR - 1) / WPR) * 4;
+  const int64_t s0 = min(GV, (int64_t)wseg * per), s1 = min(GV, s0 + per);
   const rsrc_t rrow = make_rsrc(RR ? rowA : row, (uint32_t)(GV * 4));  // past GV: reads zero (masked)
   const unsigned long long below = (1ull << lane) - 1ull;
   auto load = [&](int64_t it, f32x4 (&dst)[kTkwU]) {
@@ -1465,8 +1476,8 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
   }
 #endif
   if (n > k) wave_cut<tkw_j<KM>()>(buf, n, k, 0);
-  // the < 4 entries past the last float4: wave 0 takes them (scalar loads)
-  if (wave == 0 && GV < G) {
+  // the < 4 entries past the last float4: segment 0 takes them (scalar loads)
+  if (wseg == 0 && GV < G) {
     const int64_t i = GV + lane;
     const bool take = i < G;
     const float e = RR ? (take ? xf(rowB[i - naq], i) : 0.f) : row[take ? i : 0];
@@ -1475,6 +1486,29 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
     const unsigned long long bal = __ballot(take);
     if (take) buf[n + __popcll(bal & below)] = packed;
     n += __popcll(bal);
+  }
+  if (WPR == 1) {   // the wave's own list is the row's: exact k, then sorted
+    if (n > k) wave_cut<tkw_j<KM>()>(buf, n, k, 0);
+    int n2 = 1;
+    while (n2 < k) n2 <<= 1;
+    for (int i = n + lane; i < n2; i += 64) buf[i] = ~0ull;
+    wave_lds_sync();
+    for (int size = 2; size <= n2; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = lane; t < n2 / 2; t += 64) {
+          const int i = 2 * stride * (t / stride) + (t % stride), j = i + stride;
+          const bool up = (i & size) == 0;
+          const unsigned long long a = buf[i], b = buf[j];
+          if ((a > b) == up) { buf[i] = b; buf[j] = a; }
+        }
+        wave_lds_sync();
+      }
+    for (int i = lane; i < k; i += 64) {
+      const unsigned long long v = buf[i];
+      vals[q * k + i] = key_float((uint32_t)(v >> 32));
+      idx[q * k + i] = (int32_t)(v & 0xffffffffu);
+    }
+    return;
   }
   // merge: wave 0 reads the four lists (<= k + 3 entries each) and keeps the
   // row's k best at the front of the LDS; the block sorts them
@@ -1539,10 +1573,10 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
     const RrMatrix none{};
     if (k <= 128)
       hipLaunchKernelGGL((topk_wave_kernel<128, false>), dim3((unsigned)Q), dim3(kTopkThreads),
-                         lds, st, dist, G, ldd, k, cap, vals, idx, none);
+                         lds, st, dist, G, ldd, k, cap, vals, idx, none, Q);
     else
       hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, false>), dim3((unsigned)Q),
-                         dim3(kTopkThreads), lds, st, dist, G, ldd, k, cap, vals, idx, none);
+                         dim3(kTopkThreads), lds, st, dist, G, ldd, k, cap, vals, idx, none, Q);
   } else if (v4)
     hipLaunchKernelGGL(topk_kernel<true>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
                        ldd, k, vals, idx);
@@ -1568,12 +1602,25 @@ int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st)
   }
   const int cap = tkw_cap(k);
   const size_t lds = (size_t)kTkwWaves * cap * 8;
-  if (k <= 128)
+  // one wave per row (PPS_TOPK_RR_WPR=4: the block per row, A/B runs)
+  static const bool wpr4 = [] {
+    const char* e = getenv("PPS_TOPK_RR_WPR");
+    return e && e[0] == '4';
+  }();
+  const unsigned rows_grid = (unsigned)((N + kTkwWaves - 1) / kTkwWaves);
+  if (wpr4 && k <= 128)
     hipLaunchKernelGGL((topk_wave_kernel<128, true>), dim3((unsigned)N), dim3(kTopkThreads), lds,
-                       st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M);
-  else
+                       st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+  else if (wpr4)
     hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, true>), dim3((unsigned)N), dim3(kTopkThreads),
-                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M);
+                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+  else if (k <= 128)
+    hipLaunchKernelGGL((topk_wave_kernel<128, true, 1>), dim3(rows_grid), dim3(kTopkThreads),
+                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+  else
+    hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, true, 1>), dim3(rows_grid),
+                       dim3(kTopkThreads), lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap,
+                       vals, idx, M, N);
   PPS_CHECK_LAUNCH("topk_wave_kernel<rr>");
   return PPS_OK;
 }

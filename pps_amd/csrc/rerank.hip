@@ -231,59 +231,123 @@ __device__ inline float od_at(const float* od, int64_t ldo, const RrMatrix& M, i
 
 // ---- 3) V rows -----------------------------------------------------------------
 // One 64-lane wave per row i.  rank: [N][K1] (K1 = k1 + 1 <= 64), rank[i][0..K1).
-constexpr int kVCap = 1024;  // max expansion entries per row (bound checked on host)
 
+// true if x is among rank[row][0, len): every load issued before the first
+// compare (indices clamped to len - 1, a repeat of an entry inside the
+// list), so a check costs one memory latency per 16 entries, not one per entry
 __device__ inline bool in_row(const int32_t* rank, int K1, int row, int len, int x) {
   const int32_t* r = rank + (int64_t)row * K1;
-  for (int t = 0; t < len; ++t)
-    if (r[t] == x) return true;
-  return false;
+  bool f = false;
+  for (int t0 = 0; t0 < len; t0 += 16) {
+    int32_t v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = r[min(t0 + u, len - 1)];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) f |= v[u] == x;
+  }
+  return f;
 }
 
+// NumPy's float32 np.sum of a contiguous vector (pairwise_sum, PW_BLOCKSIZE
+// 128: eight strided accumulators per block of <= 128, halves split at a
+// multiple of 8) -- the same rounding sequence as the reference's
+// np.sum(weight) (reid_dataset_evaluator.py:487).  D bounds the recursion.
+template <int D>
+__device__ float np_pairwise_sum(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int t = 0; t < n; ++t) r = r + a[t];
+    return r;
+  }
+  if (n <= 128 || D == 0) {
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int t = 8;
+    for (; t < n - (n % 8); t += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + a[t + j];
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; t < n; ++t) res = res + a[t];
+    return res;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a, n2) +
+         np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a + n2, n - n2);
+}
+
+// Dynamic LDS (ints) of the V-row kernel: the expansion list (E2 = the
+// expansion bound K1 + K1 * Kh rounded up to a power of two, the bitonic
+// length), then the candidate table [K1][Kh] aliased afterwards by the unique
+// list and its weights (2 * E2).  ~3 KB at k1 = 20: many rows per CU in flight.
+struct VRowsLds {
+  int E2, tab;
+  VRowsLds(int K1, int Kh) {
+    E2 = 1;
+    while (E2 < K1 + K1 * Kh) E2 <<= 1;
+    tab = K1 * Kh > 2 * E2 ? K1 * Kh : 2 * E2;
+  }
+  size_t bytes() const { return sizeof(int32_t) * (size_t)(E2 + tab); }
+};
+
 template <bool OTF>
-__global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, int64_t ldo,
-                                     const int32_t* __restrict__ rank, int K1, int Kh,
-                                     int vcap, int32_t* __restrict__ v_idx,
-                                     float* __restrict__ v_val, int32_t* __restrict__ v_cnt,
-                                     RrMatrix M) {
-  __shared__ int32_t exp_[kVCap];
+__global__ void __launch_bounds__(64)
+rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, int64_t ldo,
+                     const int32_t* __restrict__ rank, int K1, int Kh, int vcap, int E2,
+                     int32_t* __restrict__ v_idx, float* __restrict__ v_val,
+                     int32_t* __restrict__ v_cnt, RrMatrix M) {
+  extern __shared__ int32_t vr_lds[];
+  int32_t* exp_ = vr_lds;   // [E2] expansion list
+  // candidate table [nR][Kh]: the candidate's forward neighbour, or -1 when
+  // that neighbour does not list the candidate back; afterwards the unique
+  // expansion entries and their weights
+  int32_t* tab = vr_lds + E2;
   __shared__ int32_t R[64];
-  __shared__ int32_t s_n;
+  int32_t* uq = tab;
+  float* wv = reinterpret_cast<float*>(tab + E2);
   const int64_t i = blockIdx.x;
   const int lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1ull;
   // k-reciprocal neighbours of i: forward k1+1 list, kept if i is in their list
-  int f = lane < K1 ? rank[i * K1 + lane] : -1;
-  bool rec = lane < K1 && in_row(rank, K1, f, K1, (int)i);
-  unsigned long long bal = __ballot(rec);
+  const int f = lane < K1 ? rank[i * K1 + lane] : -1;
+  const bool rec = lane < K1 && in_row(rank, K1, f, K1, (int)i);
+  const unsigned long long bal = __ballot(rec);
   const int nR = __popcll(bal);
-  const int pos = __popcll(bal & ((1ull << lane) - 1ull));
   if (rec) {
-    R[pos] = f;
-    exp_[pos] = f;
+    R[__popcll(bal & below)] = f;
+    exp_[__popcll(bal & below)] = f;
   }
-  if (lane == 0) s_n = nR;
   __syncthreads();
-  // expansion: candidates' own k-reciprocal sets over round(k1/2)+1 neighbours
-  for (int jc = 0; jc < nR; ++jc) {
+  // every candidate's reciprocal test at once (all loads in flight together)
+  const int nc = nR * Kh;
+  for (int e = lane; e < nc; e += 64) {
+    const int jc = e / Kh, t = e - jc * Kh;
     const int cand = R[jc];
-    int cf = lane < Kh ? rank[(int64_t)cand * K1 + lane] : -1;
-    bool crec = lane < Kh && in_row(rank, K1, cf, Kh, cand);
-    unsigned long long cb = __ballot(crec);
+    const int cf = rank[(int64_t)cand * K1 + t];
+    tab[e] = in_row(rank, K1, cf, Kh, cand) ? cf : -1;
+  }
+  __syncthreads();
+  // expansion, candidate by candidate (the reference's order): a candidate's
+  // set joins if more than 2/3 of it lies in R
+  int s_n = nR;
+  for (int jc = 0; jc < nR; ++jc) {
+    const int cf = lane < Kh ? tab[jc * Kh + lane] : -1;
+    const bool crec = cf >= 0;
+    const unsigned long long cb = __ballot(crec);
     const int ncr = __popcll(cb);
     bool inR = false;
     if (crec)
       for (int t = 0; t < nR; ++t) inR |= (R[t] == cf);
     const int inter = __popcll(__ballot(crec && inR));
     if (3 * inter > 2 * ncr) {  // len(intersect) > 2/3 * len(candidate set)
-      const int base = s_n;
-      const int p = __popcll(cb & ((1ull << lane) - 1ull));
-      if (crec && base + p < kVCap) exp_[base + p] = cf;
-      __syncthreads();
-      if (lane == 0) s_n = base + ncr;
+      const int p = s_n + __popcll(cb & below);
+      if (crec && p < E2) exp_[p] = cf;
+      s_n += ncr;
     }
-    __syncthreads();
   }
-  const int n = min(s_n, kVCap);
+  __syncthreads();
+  const int n = min(s_n, E2);   // s_n <= K1 + K1 * Kh <= E2
   // np.unique: sort (bitonic over the next power of two) and drop repeats
   int n2 = 1;
   while (n2 < n) n2 <<= 1;
@@ -299,32 +363,119 @@ __global__ void rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, in
       }
       __syncthreads();
     }
-  // compact unique entries (lane 0, n <= 1024: cheap) and weight them
-  if (lane == 0) {
-    int u = 0;
-    for (int t = 0; t < n; ++t)
-      if (t == 0 || exp_[t] != exp_[t - 1]) exp_[u++] = exp_[t];
-    s_n = u;
+  // compact the unique entries (a ballot per 64) and weight them in parallel
+  int u = 0;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int t = b0 + lane;
+    const int x = t < n ? exp_[t] : 0;
+    const bool first = t < n && (t == 0 || exp_[t - 1] != x);
+    const unsigned long long fb = __ballot(first);
+    if (first) uq[u + __popcll(fb & below)] = x;
+    u += __popcll(fb);
   }
   __syncthreads();
-  const int u = s_n;
-  float wsum = 0.f;
-  if (lane == 0) {
-    // weight = exp(-OD[i, idx]); V = weight / sum(weight) (float32, in index order)
-    for (int t = 0; t < u; ++t) wsum += expf(-od_at<OTF>(od, ldo, M, i, exp_[t]));
-  }
+  // weight = exp(-OD[i, idx]); V = weight / np.sum(weight) (float32, index order)
+  for (int t = lane; t < u; t += 64) wv[t] = expf(-od_at<OTF>(od, ldo, M, i, uq[t]));
+  __syncthreads();
+  float wsum = lane == 0 ? np_pairwise_sum<4>(wv, u) : 0.f;
   wsum = __shfl(wsum, 0);
   const int cap = min(u, vcap);
   for (int t = lane; t < cap; t += 64) {
-    const float w = expf(-od_at<OTF>(od, ldo, M, i, exp_[t]));
-    v_idx[i * vcap + t] = exp_[t];
-    v_val[i * vcap + t] = w / wsum;
+    v_idx[i * vcap + t] = uq[t];
+    v_val[i * vcap + t] = wv[t] / wsum;
   }
   if (lane == 0) v_cnt[i] = u;
 }
 
 // ---- 4) V_qe rows: mean of k2 sparse rows (row order = initial_rank order) ----
 constexpr int kQeCap = 4096;
+constexpr int kQeSmall = 640;   // rows with <= this many concatenated entries: one wave
+
+// One wave per row whose k2 V rows hold <= kQeSmall entries together (the
+// common case; 10 KB of LDS, so many rows per CU are in flight).  Same merge
+// and the same column sums in row order t as rerank_vqe_kernel below, which
+// takes the longer rows.
+__global__ void __launch_bounds__(64)
+rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int k2,
+                       const int32_t* __restrict__ v_idx, const float* __restrict__ v_val,
+                       const int32_t* __restrict__ v_cnt, int vcap, int qcap,
+                       int32_t* __restrict__ q_idx, float* __restrict__ q_val,
+                       int32_t* __restrict__ q_cnt) {
+  __shared__ unsigned long long key[kQeSmall];  // (column << 32) | (t << 16) | slot
+  __shared__ float val[kQeSmall];
+  __shared__ int32_t lc[kQeSmall];
+  __shared__ int s_off[65], s_row[64];
+  const int64_t i = blockIdx.x;
+  const int lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  // row offsets: a wave prefix sum over the k2 (<= 64) rows
+  const int r = lane < k2 ? rank[i * K1 + lane] : 0;
+  const int len = lane < k2 ? min(v_cnt[r], vcap) : 0;
+  int incl = len;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  const int n = __shfl(incl, 63);
+  if (n > kQeSmall) return;   // rerank_vqe_kernel's row
+  if (lane < k2) {
+    s_row[lane] = r;
+    s_off[lane] = incl - len;
+  }
+  if (lane == 0) s_off[k2] = n;
+  __syncthreads();
+  auto list_of = [&](int e) {
+    int t = 0;
+    while (t + 1 < k2 && s_off[t + 1] <= e) ++t;
+    return t;
+  };
+  for (int e = lane; e < n; e += 64) {
+    const int t = list_of(e);
+    lc[e] = v_idx[(int64_t)s_row[t] * vcap + (e - s_off[t])];
+  }
+  __syncthreads();
+  for (int e = lane; e < n; e += 64) {
+    const int t = list_of(e);
+    const int32_t c = lc[e];
+    int pos = e - s_off[t];
+    for (int t2 = 0; t2 < k2; ++t2) {
+      if (t2 == t) continue;
+      int lo = s_off[t2], hi = s_off[t2 + 1];
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = t2 < t ? lc[mid] <= c : lc[mid] < c;
+        if (before) lo = mid + 1; else hi = mid;
+      }
+      pos += lo - s_off[t2];
+    }
+    key[pos] = ((unsigned long long)(uint32_t)c << 32) | ((unsigned long long)t << 16) |
+               (unsigned)pos;
+    val[pos] = v_val[(int64_t)s_row[t] * vcap + (e - s_off[t])];
+  }
+  __syncthreads();
+  // a column's entries are consecutive in key order; the lane at a segment's
+  // first entry sums it left to right (row order t) and writes output slot =
+  // the number of segment starts before it
+  int u = 0;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int e = b0 + lane;
+    const uint32_t col = e < n ? (uint32_t)(key[e] >> 32) : 0u;
+    const bool st = e < n && (e == 0 || (uint32_t)(key[e - 1] >> 32) != col);
+    const unsigned long long sb = __ballot(st);
+    if (st) {
+      float sum = val[key[e] & 0xffff];
+      for (int f = e + 1; f < n && (uint32_t)(key[f] >> 32) == col; ++f)
+        sum += val[key[f] & 0xffff];
+      const int slot = u + __popcll(sb & below);
+      if (slot < qcap) {
+        q_idx[i * qcap + slot] = (int32_t)col;
+        q_val[i * qcap + slot] = sum / (float)k2;
+      }
+    }
+    u += __popcll(sb);
+  }
+  if (lane == 0) q_cnt[i] = u;
+}
 
 __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int k2,
                                   const int32_t* __restrict__ v_idx,
@@ -349,6 +500,7 @@ __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, i
     s_off[k2] = o;
   }
   __syncthreads();
+  if (s_off[k2] <= kQeSmall) return;   // rerank_vqe_wave_kernel's row
   const int n = min(s_off[k2], kQeCap);
   auto list_of = [&](int e) {   // the row t holding concatenated entry e
     int t = 0;
@@ -480,32 +632,114 @@ __global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_
 }
 
 // ---- 6) Jaccard + blend for the query rows ------------------------------------
+// One block per query row i: temp_min over the gallery rows j >= Q (the only
+// columns the result keeps, :518) accumulates min(V_qe[i][col], V_qe[j][col])
+// column by column in increasing column order -- the reference's loop order
+// (:503-510), so every tm[j] sums in the same sequence.  The inverted index's
+// entries are staged into LDS kJacStage at a time (all loads of a stage in
+// flight together); the per-column pass then only touches LDS, one barrier
+// per column.
+constexpr int kJacThreads = 256;
+constexpr int kJacCols = 128;    // column metadata loaded per batch
+constexpr int kJacStage = 1024;  // staged (row, value) entries
+size_t jaccard_lds_bytes(int64_t G) {
+  return sizeof(float) * (size_t)G + (sizeof(int32_t) + sizeof(float)) * kJacStage;
+}
 template <bool OTF>
-__global__ void rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restrict__ od,
-                                      int64_t ldo, RrMatrix M,
-                                      const int32_t* __restrict__ q_idx,
-                                      const float* __restrict__ q_val,
-                                      const int32_t* __restrict__ q_cnt, int qcap,
-                                      const int32_t* __restrict__ start,
-                                      const int32_t* __restrict__ csc_row,
-                                      const float* __restrict__ csc_val, float lam,
-                                      float one_m_lam, float* __restrict__ out) {
-  extern __shared__ float tm[];  // [N] temp_min accumulator
+__global__ void __launch_bounds__(kJacThreads)
+rerank_jaccard_kernel(int64_t Q, int64_t N, const float* __restrict__ od, int64_t ldo,
+                      RrMatrix M, const int32_t* __restrict__ q_idx,
+                      const float* __restrict__ q_val, const int32_t* __restrict__ q_cnt,
+                      int qcap, const int32_t* __restrict__ start,
+                      const int32_t* __restrict__ csc_row, const float* __restrict__ csc_val,
+                      float lam, float one_m_lam, float* __restrict__ out) {
+  extern __shared__ float tm[];  // [G] temp_min of the gallery rows, then the stage
+  const int64_t G = N - Q;
+  int32_t* srow = reinterpret_cast<int32_t*>(tm + G);
+  float* sval = reinterpret_cast<float*>(srow + kJacStage);
+  __shared__ int m_off[kJacCols + 1], m_s0[kJacCols];
+  __shared__ float m_a[kJacCols];
+  __shared__ int s_wtot;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t i = blockIdx.x;
-  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) tm[j] = 0.f;
-  __syncthreads();
+  for (int64_t j = tid; j < G; j += kJacThreads) tm[j] = 0.f;
   const int c = min(q_cnt[i], qcap);
-  for (int e = 0; e < c; ++e) {  // nonzero columns of V_qe[i] in increasing order
-    const float a = q_val[i * qcap + e];
-    if (a == 0.f) continue;
-    const int col = q_idx[i * qcap + e];
-    const int s0 = start[col], s1 = start[col + 1];
-    for (int s = s0 + threadIdx.x; s < s1; s += blockDim.x)
-      tm[csc_row[s]] = tm[csc_row[s]] + fminf(a, csc_val[s]);  // one row per column entry
+  for (int e0 = 0; e0 < c; e0 += kJacCols) {
+    const int nb = min(kJacCols, c - e0);
+    // batch metadata: value, first entry and entry count of each column
+    // (zero-valued columns contribute nothing: count 0), offsets by a scan
+    int len = 0;
+    if (tid < kJacCols) {
+      float av = 0.f;
+      int s0 = 0;
+      if (tid < nb) {
+        av = q_val[i * qcap + e0 + tid];
+        if (av != 0.f) {
+          const int col = q_idx[i * qcap + e0 + tid];
+          s0 = start[col];
+          len = start[col + 1] - s0;
+        }
+      }
+      m_a[tid] = av;
+      m_s0[tid] = s0;
+      int incl = len;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (wave == 0 && lane == 63) s_wtot = incl;
+      m_off[tid + 1] = incl;   // wave 1 adds wave 0's total below
+    }
     __syncthreads();
+    if (tid >= 64 && tid < kJacCols) m_off[tid + 1] += s_wtot;
+    if (tid == 0) m_off[0] = 0;
+    __syncthreads();
+    int ca = 0;
+    while (ca < nb) {
+      // the longest run of columns [ca, cb) whose entries fit the stage
+      int lo = ca, hi = nb;   // largest cb with m_off[cb] - m_off[ca] <= kJacStage
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (m_off[mid] - m_off[ca] <= kJacStage) lo = mid; else hi = mid - 1;
+      }
+      const int cb = lo;
+      if (cb == ca) {   // one column longer than the stage: straight from memory
+        const float av = m_a[ca];
+        const int s0 = m_s0[ca], s1 = s0 + (m_off[ca + 1] - m_off[ca]);
+        for (int s = s0 + tid; s < s1; s += kJacThreads) {
+          const int64_t r = csc_row[s] - Q;
+          if (r >= 0) tm[r] = tm[r] + fminf(av, csc_val[s]);
+        }
+        __syncthreads();
+        ++ca;
+        continue;
+      }
+      const int base = m_off[ca], tot = m_off[cb] - base;
+      for (int f = tid; f < tot; f += kJacThreads) {
+        int l2 = ca, h2 = cb - 1;   // column holding staged entry f: last m_off <= base + f
+        while (l2 < h2) {
+          const int mid = (l2 + h2 + 1) >> 1;
+          if (m_off[mid] <= base + f) l2 = mid; else h2 = mid - 1;
+        }
+        const int s = m_s0[l2] + (base + f - m_off[l2]);
+        srow[f] = csc_row[s];
+        sval[f] = csc_val[s];
+      }
+      __syncthreads();
+      for (int k = ca; k < cb; ++k) {   // column order
+        const float av = m_a[k];
+        for (int f = m_off[k] - base + tid; f < m_off[k + 1] - base; f += kJacThreads) {
+          const int64_t r = srow[f] - Q;
+          if (r >= 0) tm[r] = tm[r] + fminf(av, sval[f]);   // one row per column entry
+        }
+        __syncthreads();
+      }
+      ca = cb;
+    }
   }
-  for (int64_t j = Q + threadIdx.x; j < N; j += blockDim.x) {
-    const float t = tm[j];
+  __syncthreads();
+  for (int64_t j = Q + tid; j < N; j += kJacThreads) {
+    const float t = tm[j - Q];
     const float jac = 1.f - t / (2.f - t);
     const float wj = jac * one_m_lam;                          // rounded
     const float wo = od_at<OTF>(od, ldo, M, i, j) * lam;       // rounded
@@ -626,14 +860,18 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
         return PPS_ERR_LAUNCH;
       }
   }
+  const VRowsLds vl(K1, Kh);
   if (inplace)
-    hipLaunchKernelGGL(rerank_v_rows_kernel<true>, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo,
-                       rank, K1, Kh, vcap, v_idx, v_val, v_cnt, M);
+    hipLaunchKernelGGL(rerank_v_rows_kernel<true>, dim3((unsigned)N), dim3(64), vl.bytes(), st, od,
+                       N, ldo, rank, K1, Kh, vcap, vl.E2, v_idx, v_val, v_cnt, M);
   else
-    hipLaunchKernelGGL(rerank_v_rows_kernel<false>, dim3((unsigned)N), dim3(64), 0, st, od, N, ldo,
-                       rank, K1, Kh, vcap, v_idx, v_val, v_cnt, M);
+    hipLaunchKernelGGL(rerank_v_rows_kernel<false>, dim3((unsigned)N), dim3(64), vl.bytes(), st,
+                       od, N, ldo, rank, K1, Kh, vcap, vl.E2, v_idx, v_val, v_cnt, M);
   PPS_CHECK_LAUNCH_S("rerank_v_rows_kernel", st);
   if (k2 != 1) {
+    hipLaunchKernelGGL(rerank_vqe_wave_kernel, dim3((unsigned)N), dim3(64), 0, st, N, rank, K1,
+                       k2, v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
+    PPS_CHECK_LAUNCH_S("rerank_vqe_wave_kernel", st);
     hipLaunchKernelGGL(rerank_vqe_kernel, dim3((unsigned)N), dim3(256), 0, st, N, rank, K1, k2,
                        v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
     PPS_CHECK_LAUNCH_S("rerank_vqe_kernel", st);
@@ -653,12 +891,13 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   hipLaunchKernelGGL(rerank_csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
                      q_val, q_cnt, qc, start, fill, csc_row, csc_val);
   PPS_CHECK_LAUNCH_S("rerank_csc_fill_kernel", st);
+  const size_t jac_lds = jaccard_lds_bytes(G);
   if (inplace)
-    hipLaunchKernelGGL(rerank_jaccard_kernel<true>, dim3((unsigned)Q), dim3(256), sizeof(float) * N,
+    hipLaunchKernelGGL(rerank_jaccard_kernel<true>, dim3((unsigned)Q), dim3(kJacThreads), jac_lds,
                        st, Q, N, od, ldo, M, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam,
                        one_m_lam, out);
   else
-    hipLaunchKernelGGL(rerank_jaccard_kernel<false>, dim3((unsigned)Q), dim3(256), sizeof(float) * N,
+    hipLaunchKernelGGL(rerank_jaccard_kernel<false>, dim3((unsigned)Q), dim3(kJacThreads), jac_lds,
                        st, Q, N, od, ldo, M, q_idx, q_val, q_cnt, qc, start, csc_row, csc_val, lam,
                        one_m_lam, out);
   PPS_CHECK_LAUNCH_S("rerank_jaccard_kernel", st);

@@ -88,6 +88,25 @@ def main():
                    unit='GB/s', frac=round(rr_bytes / rr_us / 1e3 / 8000.0, 4), traffic=None,
                    kernel='pps_re_ranking (OD build, top-%d, V / V_qe, Jaccard)' % 21,
                    avg_call_us=round(rr_us, 1), algorithmic_bytes_per_call=rr_bytes)
+    # gallery self-distance (g_g) alone: upper-triangle super-blocks on the
+    # chunk-tiled planes, mirrored in the epilogue.  Algorithmic flops = the
+    # triangle the kernel must compute, G (G + 1) / 2 pairs x 2 D (the full
+    # G x G product would be twice that); priced against the bf16x3 roof.
+    e0, e1 = ev(), ev()
+    e0.record()
+    for _ in range(5):
+        ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
+    e1.record()
+    e1.synchronize()
+    sd_us = e0.elapsed_time(e1) * 200.0
+    sd_flops = G * (G + 1) / 2 * 2.0 * D
+    x3 = ops.default_math() == 'x3'
+    sd_peak = 2517.0 / 6 if x3 else 157.3
+    roof_sd = dict(bound='mfma', achieved=round(sd_flops / sd_us / 1e6, 1), peak=round(sd_peak, 1),
+                   unit='TFLOP/s', frac=round(sd_flops / sd_us / 1e6 / sd_peak, 4), traffic=None,
+                   kernel='pps_distmat_x3_self_tiled (norms + plane split + triangle GEMM)',
+                   avg_call_us=round(sd_us, 1), algorithmic_flops_per_call=sd_flops,
+                   full_matrix_equivalent_TFLOPs=round(2 * G * G * D / sd_us / 1e6, 1))
     mAP, cmc = gev.scores_from_ranks(*res)
     mAP0, cmc0 = gev.scores_from_ranks(*gev.rank_eval(q_g, qid, gid, qcam, gcam))
     out = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
@@ -95,7 +114,7 @@ def main():
                       'synthetic features' % (Q, G, D),
                math=ops.default_math(), mAP_plain=round(mAP0, 6), cmc1_plain=round(float(cmc0[0]), 6),
                mAP_reranked=round(mAP, 6), cmc1_reranked=round(float(cmc[0]), 6),
-               gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr,
+               gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr, roofline_selfdist=roof_sd,
                rerank_symmetric=bool(getattr(g_g, '_pps_symmetric', False)))
     print(json.dumps(out), flush=True)
 
