@@ -293,6 +293,12 @@ struct RrMatrix {
 // Q + G >= 16384 entries, every block 16-byte aligned): the wave-streaming
 // top-k reading M's blocks in place (no N x N OD buffer)
 int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st);
+// symmetric M with colmax not yet known: rowmax[q] = max of row q's squares
+// (= column q's), and the top-k by (OD, index) through a top-(k+8) on m * m
+// (rank.hip); scratch of topk_rr_sq_scratch_bytes(N, k)
+int topk_rr_sq(const RrMatrix& M, int k, float* rowmax, void* scratch, size_t scratch_bytes,
+               float* vals, int32_t* idx, hipStream_t st);
+size_t topk_rr_sq_scratch_bytes(int64_t N, int k);
 bool topk_rr_eligible(const RrMatrix& M, int k);
 
 }  // namespace pps

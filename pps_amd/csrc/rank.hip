@@ -1321,11 +1321,14 @@ __device__ unsigned long long wave_cut(unsigned long long* buf, int& n, int k, i
 // of N), where four waves per row would each cut their short segment three or
 // four times and then merge: one wave per row cuts ~log(row / 512) times in
 // all and sorts its own k, no block barrier.
+//
+// rows (WPR 1): the rows to process are rows[0, *rows_n) (a device list).
 template <int KM, bool RR, int WPR = kTkwWaves>
 __global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
 topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, int cap,
                  float* __restrict__ vals, int32_t* __restrict__ idx, RrMatrix rr,
-                 int64_t nrows) {
+                 int64_t nrows, const int32_t* __restrict__ rows = nullptr,
+                 const int32_t* __restrict__ rows_n = nullptr) {
   static_assert(WPR == 1 || WPR == kTkwWaves, "one wave or the whole block per row");
   extern __shared__ unsigned long long tkw[];  // [waves][cap] buffers
   // wave-uniform: segment bounds, buffer base and counts live in SGPRs
@@ -1333,7 +1336,11 @@ topk_wave_kernel(const float* __restrict__ dist, int64_t G, int64_t ldd, int k, 
   unsigned long long* buf = tkw + wave * cap;
   constexpr int RPB = kTkwWaves / WPR;   // rows per block
   const int wseg = wave % WPR;           // this wave's segment of its row
-  const int64_t q = (int64_t)blockIdx.x * RPB + wave / WPR;
+  int64_t q = (int64_t)blockIdx.x * RPB + wave / WPR;
+  if (WPR == 1 && rows) {
+    if (q >= *rows_n) return;
+    q = rows[q];
+  }
   if (WPR == 1 && q >= nrows) return;   // (WPR = 1 has no block barrier)
   const float* row = RR ? nullptr : dist + q * ldd;
   // RR: the two blocks of M's row q
@@ -1573,10 +1580,12 @@ int topk(const float* dist, int64_t Q, int64_t G, int64_t ldd, int k, float* val
     const RrMatrix none{};
     if (k <= 128)
       hipLaunchKernelGGL((topk_wave_kernel<128, false>), dim3((unsigned)Q), dim3(kTopkThreads),
-                         lds, st, dist, G, ldd, k, cap, vals, idx, none, Q);
+                         lds, st, dist, G, ldd, k, cap, vals, idx, none, Q, nullptr,
+                         nullptr);
     else
       hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, false>), dim3((unsigned)Q),
-                         dim3(kTopkThreads), lds, st, dist, G, ldd, k, cap, vals, idx, none, Q);
+                         dim3(kTopkThreads), lds, st, dist, G, ldd, k, cap, vals, idx, none, Q, nullptr,
+                         nullptr);
   } else if (v4)
     hipLaunchKernelGGL(topk_kernel<true>, dim3((unsigned)Q), dim3(kTopkThreads), 0, st, dist, G,
                        ldd, k, vals, idx);
@@ -1610,19 +1619,234 @@ int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st)
   const unsigned rows_grid = (unsigned)((N + kTkwWaves - 1) / kTkwWaves);
   if (wpr4 && k <= 128)
     hipLaunchKernelGGL((topk_wave_kernel<128, true>), dim3((unsigned)N), dim3(kTopkThreads), lds,
-                       st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+                       st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N, nullptr, nullptr);
   else if (wpr4)
     hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, true>), dim3((unsigned)N), dim3(kTopkThreads),
-                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N, nullptr, nullptr);
   else if (k <= 128)
     hipLaunchKernelGGL((topk_wave_kernel<128, true, 1>), dim3(rows_grid), dim3(kTopkThreads),
-                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N);
+                       lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap, vals, idx, M, N, nullptr, nullptr);
   else
     hipLaunchKernelGGL((topk_wave_kernel<kTkwMaxK, true, 1>), dim3(rows_grid),
                        dim3(kTopkThreads), lds, st, nullptr, (int64_t)0, (int64_t)0, k, cap,
-                       vals, idx, M, N);
+                       vals, idx, M, N, nullptr, nullptr);
   PPS_CHECK_LAUNCH("topk_wave_kernel<rr>");
   return PPS_OK;
+}
+
+// Re-ranking's first pass over a symmetric M (rerank.hip, in place): per row
+// q the top-k' by (m * m, index) over M's row -- its first block (qq or
+// q_g^T, Q entries) then its second (q_g or g_g, G entries), column = Q +
+// position in the second -- and rowmax[q] = the max of the row's squares,
+// which for a symmetric M is colmax[q] (:453).  OD = (m * m) / colmax is a
+// monotone map of m * m, so rerank_rank_fix_kernel gets the top-k by (OD,
+// index) from this list.  One wave per row (four rows per block) streams the
+// two blocks as two segments through the same candidate buffer and threshold
+// (topk_wave_kernel's filter / cut / select); per entry one product, one
+// compare and one max, 32-bit offsets into buffer descriptors.
+template <int KM>
+__global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
+topk_rr_sq_kernel(RrMatrix rr, int k, int cap, float* __restrict__ vals,
+                  int32_t* __restrict__ idx, float* __restrict__ rowmax) {
+  extern __shared__ unsigned long long tkw[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  unsigned long long* buf = tkw + wave * cap;
+  const int64_t q = (int64_t)blockIdx.x * kTkwWaves + wave;
+  if (q >= rr.Q + rr.G) return;
+  const float* rowA = q < rr.Q ? rr.qq + q * rr.ldqq : rr.qgT + (q - rr.Q) * rr.ldT;
+  const float* rowB = q < rr.Q ? rr.qg + q * rr.ldqg : rr.gg + (q - rr.Q) * rr.ldgg;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int n = 0, cuts = 0;
+  unsigned long long thr = ~0ull;
+  float thr_f = key_float((uint32_t)(thr >> 32));   // NaN: everything passes
+  float mx = 0.f;
+  auto cut = [&]() {
+    thr = wave_cut<tkw_j<KM>()>(buf, n, k, kTkwSlack);
+    thr_f = key_float((uint32_t)(thr >> 32));
+    ++cuts;
+  };
+  auto segment = [&](const float* base, uint32_t L, uint32_t col0) {
+    const uint32_t V = L & ~3u;
+    const rsrc_t rs = make_rsrc(base, V * 4u);
+    const uint32_t niter = (V + kTkwIter - 1) / kTkwIter;
+    auto load = [&](uint32_t it, f32x4 (&dst)[kTkwU]) {
+#pragma unroll
+      for (int u = 0; u < kTkwU; ++u)
+        dst[u] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       rs, (int)((it * kTkwIter + 4u * (uint32_t)(u * 64 + lane)) * 4u), 0, 0));
+    };
+    auto step = [&](uint32_t it, const f32x4 (&cur)[kTkwU], f32x4 (&nxt)[kTkwU]) {
+      if (n + kTkwIter > cap || (cuts == 0 && n > k + kTkwSlack)) cut();
+      asm volatile("" ::: "memory");
+      load(it + PPS_TKW_D, nxt);
+      const uint32_t i0 = it * kTkwIter;
+      const bool last = i0 + kTkwIter > V;   // wave-uniform: the only partial iteration
+      float sq[kTkwU][4];
+      unsigned long long m[kTkwU][4], any = 0ull;
+#pragma unroll
+      for (int u = 0; u < kTkwU; ++u) {
+        const float e[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+        const uint32_t iv = i0 + 4u * (uint32_t)(u * 64 + lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          sq[u][t] = e[t] * e[t];
+          const bool valid = !last || iv + t < V;
+          mx = valid ? fmaxf(mx, sq[u][t]) : mx;
+          m[u][t] = __ballot(valid && !(sq[u][t] > thr_f));
+          any |= m[u][t];
+        }
+      }
+      if (!any) return;
+#pragma unroll
+      for (int u = 0; u < kTkwU; ++u) {
+        const uint32_t iv = i0 + 4u * (uint32_t)(u * 64 + lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const unsigned long long mm = m[u][t];
+          if (!mm) continue;
+          if ((mm >> lane) & 1ull) {
+            const uint32_t ub = __float_as_uint(sq[u][t]);
+            const uint32_t key = ub ^ ((uint32_t)((int32_t)ub >> 31) | 0x80000000u);
+            const int pos = n + (int)__builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+            buf[pos] = ((unsigned long long)key << 32) | (col0 + iv + (uint32_t)t);
+          }
+          n += __popcll(mm);
+        }
+      }
+    };
+    f32x4 a[kTkwU], b[kTkwU], c[kTkwU];
+    load(0, a);
+    asm volatile("" ::: "memory");
+    load(1, b);
+    for (uint32_t it = 0; it < niter; it += 3) {
+      step(it, a, c);
+      if (it + 1 < niter) step(it + 1, b, a);
+      if (it + 2 < niter) step(it + 2, c, b);
+    }
+    // the < 4 entries past the last float4
+    if (V < L) {
+      if (n + 4 > cap) cut();
+      const bool take = lane < (int)(L - V);
+      const float e = take ? base[V + lane] : 0.f;
+      const float s2 = e * e;
+      if (take) mx = fmaxf(mx, s2);
+      const unsigned long long packed =
+          ((unsigned long long)float_key(s2) << 32) | (col0 + V + (uint32_t)lane);
+      const bool keep = take && packed <= thr;
+      const unsigned long long bal = __ballot(keep);
+      if (keep) buf[n + __popcll(bal & below)] = packed;
+      n += __popcll(bal);
+    }
+    wave_lds_sync();
+  };
+  segment(rowA, (uint32_t)rr.Q, 0u);
+  segment(rowB, (uint32_t)rr.G, (uint32_t)rr.Q);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) rowmax[q] = mx;
+  if (n > k) wave_cut<tkw_j<KM>()>(buf, n, k, 0);
+  int n2 = 1;
+  while (n2 < k) n2 <<= 1;
+  for (int i = n + lane; i < n2; i += 64) buf[i] = ~0ull;
+  wave_lds_sync();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = lane; t < n2 / 2; t += 64) {
+        const int i = 2 * stride * (t / stride) + (t % stride), j = i + stride;
+        const bool up = (i & size) == 0;
+        const unsigned long long x = buf[i], y = buf[j];
+        if ((x > y) == up) { buf[i] = y; buf[j] = x; }
+      }
+      wave_lds_sync();
+    }
+  for (int i = lane; i < k; i += 64) {
+    const unsigned long long v = buf[i];
+    vals[q * k + i] = key_float((uint32_t)(v >> 32));
+    idx[q * k + i] = (int32_t)(v & 0xffffffffu);
+  }
+}
+
+// Top-k' by (m * m, index) -> the top-k by (OD, index), OD = (m * m) /
+// rowmax[q] (rr_od's arithmetic on the stored square).  One wave per row;
+// k' <= 64 entries, one per lane.  Exact whenever the k'-th entry's OD is
+// above the k-th's: every entry outside the list then has OD above the k-th
+// too.  Other rows (equal-OD runs longer than the slack) go to the list
+// fb_rows for the exact OD pass.
+__global__ void __launch_bounds__(256)
+rerank_rank_fix_kernel(int64_t N, int k, int kp, const float* __restrict__ sqv,
+                       const int32_t* __restrict__ sqi, const float* __restrict__ rowmax,
+                       float* __restrict__ topv, int32_t* __restrict__ rank,
+                       int32_t* __restrict__ fb_rows, int32_t* __restrict__ fb_n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= N) return;
+  const float cm = rowmax[q];
+  const float sq = lane < kp ? sqv[q * kp + lane] : 0.f;
+  const int32_t j = lane < kp ? sqi[q * kp + lane] : 0;
+  const float od = sq / cm;
+  const float vk = __shfl(od, k - 1), vl = __shfl(od, kp - 1);
+  if (!(vl > vk)) {
+    if (lane == 0) fb_rows[atomicAdd(fb_n, 1)] = (int32_t)q;
+    return;
+  }
+  const unsigned long long packed =
+      lane < kp ? (((unsigned long long)float_key(od) << 32) | (uint32_t)j) : ~0ull;
+  int pos = 0;
+  for (int t = 0; t < 64; ++t) pos += __shfl(packed, t) < packed ? 1 : 0;
+  if (lane < kp && pos < k) {
+    rank[q * k + pos] = j;
+    topv[q * k + pos] = od;
+  }
+}
+
+int topk_rr_sq(const RrMatrix& M, int k, float* rowmax, void* scratch, size_t scratch_bytes,
+               float* vals, int32_t* idx, hipStream_t st) {
+  const int64_t N = M.Q + M.G;
+  const int kp = k + 8 < 64 ? k + 8 : 64;
+  if (!topk_rr_eligible(M, kp)) {
+    set_error("topk_rr_sq: needs N >= 16384, k <= 256 and 16-byte aligned block rows");
+    return PPS_ERR_INVALID_ARG;
+  }
+  char* p = reinterpret_cast<char*>(scratch);
+  auto take = [&](size_t b) { char* r = p; p += (b + 255) / 256 * 256; return r; };
+  float* sqv = reinterpret_cast<float*>(take(sizeof(float) * N * kp));
+  int32_t* sqi = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * kp));
+  int32_t* fb_rows = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N));
+  int32_t* fb_n = reinterpret_cast<int32_t*>(take(sizeof(int32_t)));
+  if ((size_t)(p - reinterpret_cast<char*>(scratch)) > scratch_bytes) {
+    set_error("topk_rr_sq: scratch too small");
+    return PPS_ERR_CAPACITY;
+  }
+  (void)hipMemsetAsync(fb_n, 0, sizeof(int32_t), st);
+  const unsigned grid = (unsigned)((N + kTkwWaves - 1) / kTkwWaves);
+  {
+    const int cap = tkw_cap(kp);
+    hipLaunchKernelGGL(topk_rr_sq_kernel<128>, dim3(grid), dim3(kTopkThreads),
+                       (size_t)kTkwWaves * cap * 8, st, M, kp, cap, sqv, sqi, rowmax);
+    PPS_CHECK_LAUNCH("topk_rr_sq_kernel");
+  }
+  hipLaunchKernelGGL(rerank_rank_fix_kernel, dim3(grid), dim3(256), 0, st, N, k, kp, sqv, sqi,
+                     rowmax, vals, idx, fb_rows, fb_n);
+  PPS_CHECK_LAUNCH("rerank_rank_fix_kernel");
+  // the exact OD pass over the rows the fix-up could not settle (grid for
+  // all rows; waves past *fb_n return at once)
+  RrMatrix Mc = M;
+  Mc.colmax = rowmax;
+  const int cap = tkw_cap(k);
+  hipLaunchKernelGGL((topk_wave_kernel<128, true, 1>), dim3(grid), dim3(kTopkThreads),
+                     (size_t)kTkwWaves * cap * 8, st, nullptr, (int64_t)0, (int64_t)0, k, cap,
+                     vals, idx, Mc, N, fb_rows, fb_n);
+  PPS_CHECK_LAUNCH("topk_wave_kernel<rr, rows>");
+  return PPS_OK;
+}
+
+size_t topk_rr_sq_scratch_bytes(int64_t N, int k) {
+  const int kp = k + 8 < 64 ? k + 8 : 64;
+  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+  return r(sizeof(float) * N * kp) + r(sizeof(int32_t) * N * kp) + r(sizeof(int32_t) * N) +
+         r(sizeof(int32_t));
 }
 
 // ---- k-way merge of per-shard top-k lists ------------------------

@@ -807,11 +807,12 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   RrMatrix M{qg, qq, gg, od, ldqg, ldqq, ldgg, ldT, Q, G, colmax};
   const bool inplace = (flags & PPS_RERANK_SYMMETRIC) && topk_rr_eligible(M, K1) &&
                        getenv_flag_off("PPS_RERANK_INPLACE") == false;
-  // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M
+  // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M (in place:
+  // the top-k pass computes it, = the row maxima of the symmetric M)
   unsigned* cm = reinterpret_cast<unsigned*>(colmax);
-  (void)hipMemsetAsync(cm, 0, sizeof(unsigned) * N, st);
+  if (!inplace) (void)hipMemsetAsync(cm, 0, sizeof(unsigned) * N, st);
   auto colmax_sq = [&](const float* x, int64_t R, int64_t C, int64_t ld, unsigned* o) {
-    if (R <= 0 || C <= 0) return;
+    if (R <= 0 || C <= 0 || inplace) return;
     hipLaunchKernelGGL(rerank_colmax_sq_kernel,
                        dim3((unsigned)((C + 255) / 256), (unsigned)((R + kCmRows - 1) / kCmRows)),
                        dim3(256), 0, st, x, R, C, ld, o);
@@ -819,15 +820,24 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   colmax_sq(qq, Q, Q, ldqq, cm);      // columns c < Q: rows r < Q
   colmax_sq(qg, Q, G, ldqg, cm + Q);  // columns c >= Q: rows r < Q
   colmax_sq(gg, G, G, ldgg, cm + Q);  // columns c >= Q: rows r >= Q
-  hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, ldqg,
-                     cm);       // columns c < Q: rows r >= Q (qg^T)
+  if (!inplace)
+    hipLaunchKernelGGL(rerank_rowmax_sq_kernel, dim3((unsigned)Q), dim3(256), 0, st, qg, G, ldqg,
+                       cm);       // columns c < Q: rows r >= Q (qg^T)
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
   constexpr int T = PPS_OD_TILE;
   if (inplace) {
     hipLaunchKernelGGL(rerank_transpose_kernel, dim3((unsigned)((G + 63) / 64), (unsigned)((Q + 63) / 64)),
                        dim3(256), 0, st, qg, ldqg, Q, G, od, ldT);
     PPS_CHECK_LAUNCH_S("rerank_transpose_kernel", st);
-    const int rc = topk_rr(M, K1, topv, rank, st);
+    // scratch for the squared top-k: the OD region past q_g^T
+    const size_t tb = (sizeof(float) * (size_t)(G * ldT) + 255) / 256 * 256;
+    const size_t odb = sizeof(float) * (size_t)(N * ldo);
+    if (tb + topk_rr_sq_scratch_bytes(N, K1) > odb) {
+      set_error("rerank: OD region too small for the in-place top-k scratch");
+      return PPS_ERR_CAPACITY;
+    }
+    const int rc = topk_rr_sq(M, K1, colmax, reinterpret_cast<char*>(od) + tb, odb - tb, topv,
+                              rank, st);
     if (rc != PPS_OK) return rc;
   } else {
     if (flags & PPS_RERANK_SYMMETRIC) {

@@ -276,6 +276,28 @@ def test_rerank_inplace_equals_dense_duke_shape():
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
+def test_rerank_inplace_tied_rows_take_exact_pass():
+    """Gallery features repeated 24 times: every row's k1+1 = 21st and
+    (k1+9)-th neighbours lie in one run of equal distances, so the in-place
+    top-k on m * m cannot settle the (OD, index) order from its k+8 list and
+    hands the rows to the exact OD pass -- same bits as the dense path."""
+    from pps_amd import ops
+    Q, reps, U, D = 1000, 24, 700, 64
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(5)
+    rng = np.random.RandomState(5)
+    base = _feats(200, rng.randint(1, 201, Q + U), D, gen, noise=2.5)
+    qf = base[:Q].contiguous()
+    gf = base[Q:].repeat_interleave(reps, dim=0).contiguous()   # G = 16800
+    q_g = ops.compute_dist(qf, gf, metric='cosine', pad_rows=True)
+    q_q = ops.compute_dist(qf, qf, metric='cosine', pad_rows=True)
+    g_g = ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
+    a = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+    c = ops.re_ranking(q_g.contiguous(), q_q.contiguous(), g_g.contiguous(), 20, 6, 0.3,
+                       symmetric=False)
+    assert torch.equal(a, c)
+
+
 def test_duke_full_size_cosine_rerank_properties():
     from pps_amd import ops
     from pps_amd import reid_dataset_evaluator as gev
