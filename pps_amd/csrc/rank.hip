@@ -1644,10 +1644,18 @@ int topk_rr(const RrMatrix& M, int k, float* vals, int32_t* idx, hipStream_t st)
 // two blocks as two segments through the same candidate buffer and threshold
 // (topk_wave_kernel's filter / cut / select); per entry one product, one
 // compare and one max, 32-bit offsets into buffer descriptors.
+//
+// The list's fix-up runs in the same wave once the row max is known: OD of
+// each of the k' = kp entries, and when the kp-th entry's OD is above the
+// k-th's (so every entry outside the list has OD above the k-th too) the
+// top-k by (OD, index) is the list's k smallest (OD, index) pairs -- written
+// to vals (OD) / idx.  Otherwise (an equal-OD run longer than the slack) the
+// row goes to fb_rows for the exact OD pass.
 template <int KM>
 __global__ void __launch_bounds__(kTopkThreads) __attribute__((amdgpu_waves_per_eu(6)))
-topk_rr_sq_kernel(RrMatrix rr, int k, int cap, float* __restrict__ vals,
-                  int32_t* __restrict__ idx, float* __restrict__ rowmax) {
+topk_rr_sq_kernel(RrMatrix rr, int k, int kp, int cap, float* __restrict__ vals,
+                  int32_t* __restrict__ idx, float* __restrict__ rowmax,
+                  int32_t* __restrict__ fb_rows, int32_t* __restrict__ fb_n) {
   extern __shared__ unsigned long long tkw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   unsigned long long* buf = tkw + wave * cap;
@@ -1661,7 +1669,7 @@ topk_rr_sq_kernel(RrMatrix rr, int k, int cap, float* __restrict__ vals,
   float thr_f = key_float((uint32_t)(thr >> 32));   // NaN: everything passes
   float mx = 0.f;
   auto cut = [&]() {
-    thr = wave_cut<tkw_j<KM>()>(buf, n, k, kTkwSlack);
+    thr = wave_cut<tkw_j<KM>()>(buf, n, kp, kTkwSlack);
     thr_f = key_float((uint32_t)(thr >> 32));
     ++cuts;
   };
@@ -1677,7 +1685,7 @@ topk_rr_sq_kernel(RrMatrix rr, int k, int cap, float* __restrict__ vals,
                        rs, (int)((it * kTkwIter + 4u * (uint32_t)(u * 64 + lane)) * 4u), 0, 0));
     };
     auto step = [&](uint32_t it, const f32x4 (&cur)[kTkwU], f32x4 (&nxt)[kTkwU]) {
-      if (n + kTkwIter > cap || (cuts == 0 && n > k + kTkwSlack)) cut();
+      if (n + kTkwIter > cap || (cuts == 0 && n > kp + kTkwSlack)) cut();
       asm volatile("" ::: "memory");
       load(it + PPS_TKW_D, nxt);
       const uint32_t i0 = it * kTkwIter;
@@ -1746,58 +1754,26 @@ topk_rr_sq_kernel(RrMatrix rr, int k, int cap, float* __restrict__ vals,
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
   if (lane == 0) rowmax[q] = mx;
-  if (n > k) wave_cut<tkw_j<KM>()>(buf, n, k, 0);
-  int n2 = 1;
-  while (n2 < k) n2 <<= 1;
-  for (int i = n + lane; i < n2; i += 64) buf[i] = ~0ull;
-  wave_lds_sync();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = lane; t < n2 / 2; t += 64) {
-        const int i = 2 * stride * (t / stride) + (t % stride), j = i + stride;
-        const bool up = (i & size) == 0;
-        const unsigned long long x = buf[i], y = buf[j];
-        if ((x > y) == up) { buf[i] = y; buf[j] = x; }
-      }
-      wave_lds_sync();
-    }
-  for (int i = lane; i < k; i += 64) {
-    const unsigned long long v = buf[i];
-    vals[q * k + i] = key_float((uint32_t)(v >> 32));
-    idx[q * k + i] = (int32_t)(v & 0xffffffffu);
-  }
-}
-
-// Top-k' by (m * m, index) -> the top-k by (OD, index), OD = (m * m) /
-// rowmax[q] (rr_od's arithmetic on the stored square).  One wave per row;
-// k' <= 64 entries, one per lane.  Exact whenever the k'-th entry's OD is
-// above the k-th's: every entry outside the list then has OD above the k-th
-// too.  Other rows (equal-OD runs longer than the slack) go to the list
-// fb_rows for the exact OD pass.
-__global__ void __launch_bounds__(256)
-rerank_rank_fix_kernel(int64_t N, int k, int kp, const float* __restrict__ sqv,
-                       const int32_t* __restrict__ sqi, const float* __restrict__ rowmax,
-                       float* __restrict__ topv, int32_t* __restrict__ rank,
-                       int32_t* __restrict__ fb_rows, int32_t* __restrict__ fb_n) {
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= N) return;
-  const float cm = rowmax[q];
-  const float sq = lane < kp ? sqv[q * kp + lane] : 0.f;
-  const int32_t j = lane < kp ? sqi[q * kp + lane] : 0;
-  const float od = sq / cm;
-  const float vk = __shfl(od, k - 1), vl = __shfl(od, kp - 1);
+  if (n > kp) wave_cut<tkw_j<KM>()>(buf, n, kp, 0);   // exactly the kp best (row >= kp)
+  // fix-up: one list entry per lane (kp <= 64)
+  const unsigned long long v = lane < kp ? buf[lane] : ~0ull;
+  const float od = key_float((uint32_t)(v >> 32)) / mx;   // rr_od's (m * m) / colmax
+  int ps = 0;   // position in (m * m, index) order
+  for (int t = 0; t < kp; ++t) ps += __shfl(v, t) < v ? 1 : 0;
+  const unsigned long long at_k = __ballot(lane < kp && ps == k - 1);
+  const unsigned long long at_l = __ballot(lane < kp && ps == kp - 1);
+  const float vk = __shfl(od, (int)__builtin_ctzll(at_k)), vl = __shfl(od, (int)__builtin_ctzll(at_l));
   if (!(vl > vk)) {
     if (lane == 0) fb_rows[atomicAdd(fb_n, 1)] = (int32_t)q;
     return;
   }
   const unsigned long long packed =
-      lane < kp ? (((unsigned long long)float_key(od) << 32) | (uint32_t)j) : ~0ull;
+      lane < kp ? (((unsigned long long)float_key(od) << 32) | (v & 0xffffffffu)) : ~0ull;
   int pos = 0;
-  for (int t = 0; t < 64; ++t) pos += __shfl(packed, t) < packed ? 1 : 0;
+  for (int t = 0; t < kp; ++t) pos += __shfl(packed, t) < packed ? 1 : 0;
   if (lane < kp && pos < k) {
-    rank[q * k + pos] = j;
-    topv[q * k + pos] = od;
+    vals[q * k + pos] = od;
+    idx[q * k + pos] = (int32_t)(v & 0xffffffffu);
   }
 }
 
@@ -1809,29 +1785,21 @@ int topk_rr_sq(const RrMatrix& M, int k, float* rowmax, void* scratch, size_t sc
     set_error("topk_rr_sq: needs N >= 16384, k <= 256 and 16-byte aligned block rows");
     return PPS_ERR_INVALID_ARG;
   }
-  char* p = reinterpret_cast<char*>(scratch);
-  auto take = [&](size_t b) { char* r = p; p += (b + 255) / 256 * 256; return r; };
-  float* sqv = reinterpret_cast<float*>(take(sizeof(float) * N * kp));
-  int32_t* sqi = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * kp));
-  int32_t* fb_rows = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N));
-  int32_t* fb_n = reinterpret_cast<int32_t*>(take(sizeof(int32_t)));
-  if ((size_t)(p - reinterpret_cast<char*>(scratch)) > scratch_bytes) {
+  if (scratch_bytes < topk_rr_sq_scratch_bytes(N, k)) {
     set_error("topk_rr_sq: scratch too small");
     return PPS_ERR_CAPACITY;
   }
+  int32_t* fb_n = reinterpret_cast<int32_t*>(scratch);
+  int32_t* fb_rows = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(scratch) + 256);
   (void)hipMemsetAsync(fb_n, 0, sizeof(int32_t), st);
   const unsigned grid = (unsigned)((N + kTkwWaves - 1) / kTkwWaves);
-  {
-    const int cap = tkw_cap(kp);
-    hipLaunchKernelGGL(topk_rr_sq_kernel<128>, dim3(grid), dim3(kTopkThreads),
-                       (size_t)kTkwWaves * cap * 8, st, M, kp, cap, sqv, sqi, rowmax);
-    PPS_CHECK_LAUNCH("topk_rr_sq_kernel");
-  }
-  hipLaunchKernelGGL(rerank_rank_fix_kernel, dim3(grid), dim3(256), 0, st, N, k, kp, sqv, sqi,
-                     rowmax, vals, idx, fb_rows, fb_n);
-  PPS_CHECK_LAUNCH("rerank_rank_fix_kernel");
-  // the exact OD pass over the rows the fix-up could not settle (grid for
-  // all rows; waves past *fb_n return at once)
+  const int capp = tkw_cap(kp);
+  hipLaunchKernelGGL(topk_rr_sq_kernel<128>, dim3(grid), dim3(kTopkThreads),
+                     (size_t)kTkwWaves * capp * 8, st, M, k, kp, capp, vals, idx, rowmax, fb_rows,
+                     fb_n);
+  PPS_CHECK_LAUNCH("topk_rr_sq_kernel");
+  // the exact OD pass over the rows the list could not settle (grid for all
+  // rows; waves past *fb_n return at once)
   RrMatrix Mc = M;
   Mc.colmax = rowmax;
   const int cap = tkw_cap(k);
@@ -1842,11 +1810,8 @@ int topk_rr_sq(const RrMatrix& M, int k, float* rowmax, void* scratch, size_t sc
   return PPS_OK;
 }
 
-size_t topk_rr_sq_scratch_bytes(int64_t N, int k) {
-  const int kp = k + 8 < 64 ? k + 8 : 64;
-  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
-  return r(sizeof(float) * N * kp) + r(sizeof(int32_t) * N * kp) + r(sizeof(int32_t) * N) +
-         r(sizeof(int32_t));
+size_t topk_rr_sq_scratch_bytes(int64_t N, int) {
+  return 256 + (sizeof(int32_t) * N + 255) / 256 * 256;
 }
 
 // ---- k-way merge of per-shard top-k lists ------------------------

@@ -400,7 +400,8 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
                        const int32_t* __restrict__ v_idx, const float* __restrict__ v_val,
                        const int32_t* __restrict__ v_cnt, int vcap, int qcap,
                        int32_t* __restrict__ q_idx, float* __restrict__ q_val,
-                       int32_t* __restrict__ q_cnt) {
+                       int32_t* __restrict__ q_cnt, int32_t* __restrict__ col_cnt,
+                       int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_n) {
   __shared__ unsigned long long key[kQeSmall];  // (column << 32) | (t << 16) | slot
   __shared__ float val[kQeSmall];
   __shared__ int32_t lc[kQeSmall];
@@ -417,7 +418,10 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
     if (lane >= o) incl += y;
   }
   const int n = __shfl(incl, 63);
-  if (n > kQeSmall) return;   // rerank_vqe_kernel's row
+  if (n > kQeSmall) {   // rerank_vqe_kernel's row
+    if (lane == 0) ovf_rows[atomicAdd(ovf_n, 1)] = (int32_t)i;
+    return;
+  }
   if (lane < k2) {
     s_row[lane] = r;
     s_off[lane] = incl - len;
@@ -468,8 +472,10 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
         sum += val[key[f] & 0xffff];
       const int slot = u + __popcll(sb & below);
       if (slot < qcap) {
+        const float qv = sum / (float)k2;
         q_idx[i * qcap + slot] = (int32_t)col;
-        q_val[i * qcap + slot] = sum / (float)k2;
+        q_val[i * qcap + slot] = qv;
+        if (qv != 0.f) atomicAdd(&col_cnt[col], 1);   // the inverted index's column sizes
       }
     }
     u += __popcll(sb);
@@ -477,17 +483,39 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
   if (lane == 0) q_cnt[i] = u;
 }
 
+__device__ void vqe_row_long(int64_t i, const int32_t* __restrict__ rank, int K1, int k2,
+                             const int32_t* __restrict__ v_idx,
+                             const float* __restrict__ v_val,
+                             const int32_t* __restrict__ v_cnt, int vcap, int qcap,
+                             int32_t* __restrict__ q_idx, float* __restrict__ q_val,
+                             int32_t* __restrict__ q_cnt, int32_t* __restrict__ col_cnt);
+
 __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int k2,
                                   const int32_t* __restrict__ v_idx,
                                   const float* __restrict__ v_val,
                                   const int32_t* __restrict__ v_cnt, int vcap, int qcap,
                                   int32_t* __restrict__ q_idx, float* __restrict__ q_val,
-                                  int32_t* __restrict__ q_cnt) {
+                                  int32_t* __restrict__ q_cnt, int32_t* __restrict__ col_cnt,
+                                  const int32_t* __restrict__ ovf_rows,
+                                  const int32_t* __restrict__ ovf_n) {
+  // the rows rerank_vqe_wave_kernel left: ovf_rows[0, *ovf_n), a block each
+  for (int r = blockIdx.x; r < *ovf_n; r += gridDim.x) {
+    __syncthreads();   // LDS reuse across rows
+    vqe_row_long(ovf_rows[r], rank, K1, k2, v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val,
+                 q_cnt, col_cnt);
+  }
+}
+
+__device__ void vqe_row_long(int64_t i, const int32_t* __restrict__ rank, int K1, int k2,
+                             const int32_t* __restrict__ v_idx,
+                             const float* __restrict__ v_val,
+                             const int32_t* __restrict__ v_cnt, int vcap, int qcap,
+                             int32_t* __restrict__ q_idx, float* __restrict__ q_val,
+                             int32_t* __restrict__ q_cnt, int32_t* __restrict__ col_cnt) {
   __shared__ unsigned long long key[kQeCap];  // (column << 32) | (t << 16) | slot
   __shared__ float val[kQeCap];
   __shared__ int32_t lc[kQeCap];              // the k2 rows' columns, concatenated
   __shared__ int s_off[65], s_row[64];
-  const int64_t i = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   if (tid == 0) {
     int o = 0;
@@ -500,7 +528,6 @@ __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, i
     s_off[k2] = o;
   }
   __syncthreads();
-  if (s_off[k2] <= kQeSmall) return;   // rerank_vqe_wave_kernel's row
   const int n = min(s_off[k2], kQeCap);
   auto list_of = [&](int e) {   // the row t holding concatenated entry e
     int t = 0;
@@ -567,8 +594,10 @@ __global__ void rerank_vqe_kernel(int64_t N, const int32_t* __restrict__ rank, i
     for (int f = e + 1; f < n && (uint32_t)(key[f] >> 32) == col; ++f)
       sum += val[key[f] & 0xffff];
     if (u < qcap) {
+      const float qv = sum / (float)k2;
       q_idx[i * qcap + u] = (int32_t)col;
-      q_val[i * qcap + u] = sum / (float)k2;
+      q_val[i * qcap + u] = qv;
+      if (qv != 0.f) atomicAdd(&col_cnt[col], 1);
     }
     ++u;
   }
@@ -585,27 +614,26 @@ __global__ void rerank_csc_count_kernel(int64_t N, const int32_t* __restrict__ q
     if (q_val[i * qcap + e] != 0.f) atomicAdd(&col_cnt[q_idx[i * qcap + e]], 1);
 }
 
-__global__ void rerank_scan_kernel(int64_t N, const int32_t* __restrict__ cnt,
-                                   int32_t* __restrict__ start) {
-  // single block exclusive scan (N <= ~100k: cheap next to the rest)
-  __shared__ int32_t part[1024];
-  const int tid = threadIdx.x;
+__global__ void __launch_bounds__(1024)
+rerank_scan_kernel(int64_t N, const int32_t* __restrict__ cnt, int32_t* __restrict__ start) {
+  // single block exclusive scan: a run of `per` counts per thread, the 1024
+  // run totals scanned by wave shuffles (16 waves) and a scan of the wave totals
+  __shared__ int32_t wtot[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t per = (N + 1023) / 1024;
   const int64_t a = tid * per, b = min(N, a + per);
   int32_t s = 0;
   for (int64_t e = a; e < b; ++e) s += cnt[e];
-  part[tid] = s;
-  __syncthreads();
-  if (tid == 0) {
-    int32_t run = 0;
-    for (int t = 0; t < 1024; ++t) {
-      const int32_t v = part[t];
-      part[t] = run;
-      run += v;
-    }
+  int32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
   }
+  if (lane == 63) wtot[wave] = incl;
   __syncthreads();
-  int32_t run = part[tid];
+  int32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wtot[w];
+  int32_t run = base + incl - s;
   for (int64_t e = a; e < b; ++e) {
     start[e] = run;
     run += cnt[e];
@@ -794,6 +822,8 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   int32_t* fill = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (N + 1)));
   int32_t* csc_row = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * qcap));
   float* csc_val = reinterpret_cast<float*>(take(sizeof(float) * N * qcap));
+  int32_t* ovf_rows = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N));
+  int32_t* ovf_n = reinterpret_cast<int32_t*>(take(sizeof(int32_t)));
   if ((size_t)(p - reinterpret_cast<char*>(ws)) > ws_bytes) {
     set_error("rerank workspace too small: need " +
               std::to_string((size_t)(p - reinterpret_cast<char*>(ws))) + " bytes");
@@ -878,12 +908,16 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
     hipLaunchKernelGGL(rerank_v_rows_kernel<false>, dim3((unsigned)N), dim3(64), vl.bytes(), st,
                        od, N, ldo, rank, K1, Kh, vcap, vl.E2, v_idx, v_val, v_cnt, M);
   PPS_CHECK_LAUNCH_S("rerank_v_rows_kernel", st);
+  // the V_qe kernels also count the inverted index's column sizes
+  (void)hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * (N + 1), st);
   if (k2 != 1) {
+    (void)hipMemsetAsync(ovf_n, 0, sizeof(int32_t), st);
     hipLaunchKernelGGL(rerank_vqe_wave_kernel, dim3((unsigned)N), dim3(64), 0, st, N, rank, K1,
-                       k2, v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
+                       k2, v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt, col_cnt,
+                       ovf_rows, ovf_n);
     PPS_CHECK_LAUNCH_S("rerank_vqe_wave_kernel", st);
-    hipLaunchKernelGGL(rerank_vqe_kernel, dim3((unsigned)N), dim3(256), 0, st, N, rank, K1, k2,
-                       v_idx, v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt);
+    hipLaunchKernelGGL(rerank_vqe_kernel, dim3(256), dim3(256), 0, st, N, rank, K1, k2, v_idx,
+                       v_val, v_cnt, vcap, qcap, q_idx, q_val, q_cnt, col_cnt, ovf_rows, ovf_n);
     PPS_CHECK_LAUNCH_S("rerank_vqe_kernel", st);
   } else {
     (void)hipMemcpyAsync(q_idx, v_idx, sizeof(int32_t) * N * vcap, hipMemcpyDeviceToDevice, st);
@@ -891,11 +925,12 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
     (void)hipMemcpyAsync(q_cnt, v_cnt, sizeof(int32_t) * N, hipMemcpyDeviceToDevice, st);
   }
   const int qc = k2 != 1 ? qcap : vcap;
-  (void)hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * (N + 1), st);
   (void)hipMemsetAsync(fill, 0, sizeof(int32_t) * (N + 1), st);
-  hipLaunchKernelGGL(rerank_csc_count_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
-                     q_val, q_cnt, qc, col_cnt);
-  PPS_CHECK_LAUNCH_S("rerank_csc_count_kernel", st);
+  if (k2 == 1) {   // V_qe = V: count here
+    hipLaunchKernelGGL(rerank_csc_count_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
+                       q_val, q_cnt, qc, col_cnt);
+    PPS_CHECK_LAUNCH_S("rerank_csc_count_kernel", st);
+  }
   hipLaunchKernelGGL(rerank_scan_kernel, dim3(1), dim3(1024), 0, st, N, col_cnt, start);
   PPS_CHECK_LAUNCH_S("rerank_scan_kernel", st);
   hipLaunchKernelGGL(rerank_csc_fill_kernel, dim3((unsigned)N), dim3(256), 0, st, N, q_idx,
@@ -923,6 +958,7 @@ size_t rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   // the OD buffer also holds q_g^T ([G][Q rounded up to 4] <= N x od_stride)
   s += r(4 * N * od_stride(N)) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
   s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
+  s += r(4 * N) + r(4);   // V_qe overflow rows + count
   return s;
 }
 

@@ -290,7 +290,7 @@ def test_re_ranking_vs_golden(golden):
     assert abs(m - float(g['mAP'])) < 1e-6
 
 
-@pytest.mark.parametrize('k1,k2', [(20, 6), (10, 1), (6, 3)])
+@pytest.mark.parametrize('k1,k2', [(20, 6), (10, 1), (6, 3), (24, 8)])
 def test_re_ranking_vs_oracle_params(k1, k2):
     from pps_amd import reid_dataset_evaluator as gev
     rng = np.random.RandomState(k1 + k2)
