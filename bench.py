@@ -301,6 +301,7 @@ def conv_roofline(nm, x, reps=20):
     split is rescaled to the graph-replay total (ROCm does not allow event
     nodes inside a captured graph, which would time launches in the replay
     directly)."""
+    from pps_amd import ops
     N = int(x.shape[0])
     layers = nm.layers(N)
     out = torch.empty((N, nm.feat_dim), dtype=torch.float32, device='cuda')
@@ -318,24 +319,43 @@ def conv_roofline(nm, x, reps=20):
     e1.record()
     e1.synchronize()
     fwd_ms = e0.elapsed_time(e1) / reps
+    # launch units: a PPS_TILE_SEAM layer and the next branch2a it computes
+    # are one launch (timed as forward_layers(i, i + 2))
+    units, i = [], 0
+    while i < len(layers):
+        n = 2 if (layers[i]['tile'] & ops.TILE_SEAM) and i + 1 < len(layers) else 1
+        units.append((i, n))
+        i += n
     splits = []
     for _ in range(5):   # per-launch medians of five eager passes
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(layers) + 1)]
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(units) + 1)]
         evs[0].record()
-        for i in range(len(layers)):
-            nm.forward_layers(x, i, i + 1, out=out)
-            evs[i + 1].record()
+        for u, (i, n) in enumerate(units):
+            nm.forward_layers(x, i, i + n, out=out)
+            evs[u + 1].record()
         torch.cuda.synchronize()
-        splits.append([evs[i].elapsed_time(evs[i + 1]) for i in range(len(layers))])
+        splits.append([evs[u].elapsed_time(evs[u + 1]) for u in range(len(units))])
     eager = [float(v) for v in np.median(np.array(splits), axis=0)]
     scale = fwd_ms / sum(eager)
-    conv_ms = scale * sum(t for L, t in zip(layers, eager) if L['gemm'])
-    conv_flops = sum(L['flops'] for L in layers if L['gemm'])
-    conv_bytes = sum(L['bytes'] for L in layers if L['gemm'])
-    n_launch = sum(1 for L in layers if L['gemm'])
-    per = {L['name']: dict(op=L['op'], flops=L['flops'], ms=t * scale, ms_eager=t,
-                           bytes=L['bytes'], tile=L['tile'], planes_out=L['planes_out'])
-           for L, t in zip(layers, eager)}
+    per = {}
+    for (i, n), t in zip(units, eager):
+        L = layers[i]
+        if n == 1:
+            per[L['name']] = dict(op=L['op'], flops=L['flops'], ms=t * scale, ms_eager=t,
+                                  bytes=L['bytes'], tile=L['tile'], planes_out=L['planes_out'],
+                                  gemm=L['gemm'])
+        else:   # the seam: both layers' FLOPs; the trunk is not re-read by branch2a
+            X = layers[i + 1]
+            trunk = 4.0 * float(np.prod(L['out_shape']))
+            per[L['name'] + '+' + X['name']] = dict(
+                op='seam', flops=L['flops'] + X['flops'], ms=t * scale, ms_eager=t,
+                bytes=L['bytes'] + X['bytes'] - trunk, tile=L['tile'], planes_out=False,
+                gemm=True)
+    conv = [v for v in per.values() if v['gemm']]
+    conv_ms = sum(v['ms'] for v in conv)
+    conv_flops = sum(v['flops'] for v in conv)
+    conv_bytes = sum(v['bytes'] for v in conv)
+    n_launch = len(conv)
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     if nm.math == 'x3':
         peak, kernel = PEAK_X3_TFLOPS, ('implicit-GEMM conv: gemm_x3p_kernel<*> (LDS-DMA pipelined), gemm_x3c_kernel<*> (3x3 '
@@ -482,7 +502,8 @@ def table_digest(nm):
         groups[g] = groups.get(g, 0) + 1
     return dict(sha1=hashlib.sha1('\n'.join(rows).encode()).hexdigest()[:16],
                 layers_per_rounding_group=groups, plane_edges=len(planes),
-                splitk_layers=sum(1 for L in layers if L['splitk'] > 1))
+                splitk_layers=sum(1 for L in layers if L['splitk'] > 1),
+                seam_pairs=sum(1 for L in layers if L['tile'] & ops.TILE_SEAM))
 
 
 def e2e_stage(nm, rank, world, n_images, batch, threads):

@@ -81,6 +81,15 @@ int pps_gemm_num_tiles(void);
  * block (consecutive workgroups -- one XCD -- share a weight block instead
  * of an activation panel).  Same bits. */
 #define PPS_TILE_COL_ORDER 0x200
+/* Whole-network plan only (pps_model_set_tile / autotune), on a bottleneck's
+ * branch2c (1x1 + BN + identity residual + ReLU) whose output feeds the next
+ * block's branch2a (1x1 + BN + ReLU): one launch of the bottleneck seam kernel
+ * (pps_conv1x1_seam_x3) computes both -- the trunk is written for the next
+ * block's residual and never re-read for its branch2a; the branch2a layer's
+ * own tile is then not launched.  Base tile 54 (the same 16x16x32 rounding
+ * group: same bits).  (Cin, Cout, next Cout) = (64, 256, 64) or (128, 512,
+ * 128), f32 activations at both ends, no split-K. */
+#define PPS_TILE_SEAM 0x400
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
@@ -598,6 +607,7 @@ int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets
 #define PPS_MATH_F32 1  /* exact f32 MFMA (v_mfma_f32_32x32x2_f32)         */
 #define PPS_AUTOTUNE_NO_PLANES 1  /* keep the plane edges as they are     */
 #define PPS_AUTOTUNE_SPLITK 2     /* also try conv split-K 2..4           */
+#define PPS_AUTOTUNE_NO_SEAM 4    /* do not try PPS_TILE_SEAM pairs       */
 
 typedef struct PpsBlob {     /* one Detectron blob, HOST float32 memory   */
   const char* name;          /* e.g. "res2_0_branch2a_w", "pps01_bn_riv"  */

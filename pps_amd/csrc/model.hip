@@ -329,6 +329,7 @@ struct Layer {
   int nsub = 0, dim = 0, dim_inner = 0;
   int tile = 0, splitk = 1;
   bool planes_in = false, planes_out = false;
+  int seam_next = -1;   // the next layer a PPS_TILE_SEAM launch also computes
 };
 
 struct Shape {
@@ -600,6 +601,25 @@ size_t part_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) 
 }
 
 // tiles built with the one-launch split-K epilogue (gemm_x3p.hip FX)
+// A branch2c -> next branch2a pair the seam kernel covers (structure only;
+// seam_ok adds the table's conditions)
+bool seam_pair(const PpsModel& m, size_t i) {
+  if (!m.x3 || i + 1 >= m.layers.size()) return false;
+  const Layer& L = m.layers[i];
+  const Layer& X = m.layers[i + 1];
+  auto plain1x1 = [](const Layer& A) {
+    return A.op == Op::Conv && A.k == 1 && A.stride == 1 && A.pad == 0 && A.relu &&
+           A.kpad == A.cin_eff && A.w;
+  };
+  return plain1x1(L) && plain1x1(X) && !L.residual.empty() && X.residual.empty() &&
+         X.input == L.output && X.cin_eff == L.cout && seam_supported(L.cin_eff, L.cout, X.cout);
+}
+bool seam_ok(const PpsModel& m, const Layer& L) {
+  if (L.seam_next < 0) return false;
+  const Layer& X = m.layers[L.seam_next];
+  return !L.planes_in && !L.planes_out && !X.planes_out && L.splitk == 1 && X.splitk == 1;
+}
+
 bool fix_tile(int tile) {
   const int t = tile & 0xff;
   return t == GEMM_TILE_P16_FIRST + 7 ||
@@ -724,6 +744,18 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
   const float* sc = L.scale ? L.scale->as<float>() : nullptr;
   const float* sh = L.shift ? L.shift->as<float>() : nullptr;
   const int N = w.N;
+  if (L.op == Op::Conv && (tile & PPS_TILE_SEAM)) {
+    PPS_MCHECK(seam_ok(m, L), "layer '" + L.name + "': PPS_TILE_SEAM needs f32 activations "
+                              "at both ends and no split-K");
+    const Layer& X = m.layers[L.seam_next];
+    const Act a = act(L.input, false);
+    const int64_t M = a.s.d[0] * a.s.d[1] * a.s.d[2];
+    rc_check(pps_conv1x1_seam_x3(a.f, M, L.cin_eff, L.w->as<uint16_t>(), L.cout, sc, sh,
+                                 fbuf(L.residual), fbuf(L.output), X.w->as<uint16_t>(), X.cout,
+                                 X.scale->as<float>(), X.shift->as<float>(), fbuf(X.output),
+                                 st));
+    return;
+  }
   switch (L.op) {
     case Op::Conv: {
       const Act a = act(L.input, L.planes_in);
@@ -854,7 +886,11 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
   Workspace& w = workspace(m, N, st, true);
   for (int i = first; i < last; ++i) {
     const Layer& L = m.layers[i];
-    run_layer(m, L, w, x, feat, i + 1 == (int)m.layers.size(), L.tile, L.splitk, st);
+    // computed by the previous layer's seam launch (when that ran here too)
+    if (i > first && (m.layers[i - 1].tile & PPS_TILE_SEAM) && m.layers[i - 1].seam_next == i)
+      continue;
+    run_layer(m, L, w, x, feat, i + 1 == (int)m.layers.size(), L.tile & ~(i + 1 == last ? PPS_TILE_SEAM : 0),
+              L.splitk, st);
   }
 }
 
@@ -1048,6 +1084,8 @@ int pps_model_create(const PpsBlob* blobs, int nblobs, const PpsModelConfig* cfg
     }
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     (void)hipStreamDestroy(st);
+    for (size_t i = 0; i < m->layers.size(); ++i)
+      if (seam_pair(*m, i)) m->layers[i].seam_next = (int)i + 1;
     *out = m.release();
   });
 }
@@ -1089,8 +1127,13 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
-    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
+    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM);
     PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
+    PPS_MCHECK(!(tile & PPS_TILE_SEAM) ||
+                   (L->seam_next >= 0 && base == GEMM_TILE_WS &&
+                    !(tile & (PPS_TILE_B_TILED | PPS_TILE_COL_ORDER))),
+               std::string("PPS_TILE_SEAM: '") + layer +
+                   "' is not a branch2c feeding a seam-capable branch2a (base tile 54)");
     PPS_MCHECK(!(tile & PPS_TILE_B_TILED) ||
                    (L->wt && base >= GEMM_TILE_P_FIRST && base != GEMM_TILE_WS),
                "PPS_TILE_B_TILED: x3 conv with Cin % 32 == 0 on a pipelined tile only");
@@ -1325,6 +1368,27 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         }
         if (best < 0.98f * cost[i]) {
           L.tile = pick.first; L.splitk = pick.second; cost[i] = best;
+        }
+      }
+    }
+    if (!(flags & PPS_AUTOTUNE_NO_SEAM)) {
+      // bottleneck seams: branch2c + the next branch2a in one launch, kept
+      // if > 2 % faster than the two tuned launches
+      for (size_t i = 0; i < m->layers.size(); ++i) {
+        Layer& L = m->layers[i];
+        if (!seam_ok(*m, L)) continue;
+        const int save = L.tile;
+        float ts = 1e30f;
+        for (int r = 0; r < final_rounds; ++r)
+          ts = std::min(ts, time_layer(*m, L, *w, x, GEMM_TILE_WS | PPS_TILE_SEAM, 1, final_reps,
+                                       st, t));
+        const float sep = cost[i] + cost[L.seam_next];
+        if (ts < 0.98f * sep) {
+          L.tile = GEMM_TILE_WS | PPS_TILE_SEAM;
+          cost[i] = ts;
+          cost[L.seam_next] = 0.f;
+        } else {
+          L.tile = save;
         }
       }
     }

@@ -585,6 +585,7 @@ class PPSModel(object):
     def _run(self, L, bufs, out=None, tile=None, splitk=None):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
+        tile &= ~ops.TILE_SEAM   # one layer alone (forward() runs the seam pairs)
         sk = L.get('splitk', 1) if splitk is None else splitk
         w = L.get('w')
         # split convs run in one launch on the FIX tiles (same bits as the
@@ -669,12 +670,23 @@ class PPSModel(object):
             self._alloc(N, H, W)
         bufs = dict(self._bufs)
         bufs['data'] = x
-        for L in self.layers:
+        fused = None   # the branch2a the previous seam launch computed
+        for i, L in enumerate(self.layers):
+            if L is fused:
+                continue
             if timer is not None:
                 ev0 = torch.cuda.Event(enable_timing=True, external=timer_external)
                 ev1 = torch.cuda.Event(enable_timing=True, external=timer_external)
                 ev0.record()
-            self._run(L, bufs, out)
+            if L['op'] == 'conv' and L.get('tile', 0) & ops.TILE_SEAM:
+                # PPS_TILE_SEAM (set by the C autotune): this branch2c and the
+                # next block's branch2a in one launch, as the C plan runs them
+                fused = self.layers[i + 1]
+                ops.conv1x1_seam(bufs[L['input']], L['w'], L['scale'], L['shift'],
+                                 bufs[L['residual']], bufs[L['output']], fused['w'],
+                                 fused['scale'], fused['shift'], bufs[fused['output']])
+            else:
+                self._run(L, bufs, out)
             if timer is not None:
                 ev1.record()
                 timer.append((L.get('name', L['output']), L['op'], L['flops'], ev0, ev1))

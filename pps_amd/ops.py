@@ -23,6 +23,7 @@ TILE_P16_FIRST = 38  # pipelined tiles on 16x16x32 MFMA blocks (their own roundi
 TILE_C16_FIRST = 56  # patch-staged 3x3 tiles (gemm_x3c.hip): K in (channel chunk, tap) order
 TILE_B_TILED = 0x100  # PPS_TILE_B_TILED: or-ed into a conv tile, the weights are chunk-tiled
 TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (same bits)
+TILE_SEAM = 0x400  # PPS_TILE_SEAM (whole-network plan): branch2c + next branch2a in one launch
 # tiles built with the one-launch split-K epilogue (conv2d_bn_act_x3p(..., counters=))
 FIX_TILES = (45, 47, 48, 49, 50)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)

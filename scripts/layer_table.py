@@ -21,7 +21,7 @@ PEAK_X3 = 2516.8 / 6  # bf16 dense MFMA peak / 6 product terms (bench.py)
 
 def is_mfma(nm):
     return ('gemm_x3_kernel<' in nm or 'gemm_x3p_kernel<' in nm or 'gemm_x3c_kernel<' in nm or
-            'gemm_ws_kernel<' in nm or
+            'gemm_ws_kernel<' in nm or 'seam_kernel<' in nm or
             ('stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)) and epi_of(nm) != 1
 
 
@@ -29,7 +29,7 @@ def main():
     layers = json.load(open(sys.argv[1]))
     d = sys.argv[2]
     gemm = [(k, v) for k, v in layers.items() if v['op'] in
-            ('conv', 'conv_dual', 'heads', 'stem_pool', 'conv_pps')]
+            ('conv', 'conv_dual', 'heads', 'stem_pool', 'conv_pps', 'seam')]
     n = len(gemm)
     f = [v for nm, v in load(glob.glob(os.path.join(d, 'p1', '*counter_collection.csv'))[0],
                              'FETCH_SIZE') if is_mfma(nm)][-n:]

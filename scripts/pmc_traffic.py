@@ -40,7 +40,7 @@ def load_all(path):
 
 
 def epi_of(name):
-    if '<' not in name:
+    if '<' not in name or 'seam_kernel<' in name:
         return 0   # the fused stem: a conv epilogue
     args = name.split('<', 1)[1].split('>', 1)[0].split(',')
     if 'gemm_ws_kernel' in name:   # <NCH, BN2, EPI, W>
@@ -57,7 +57,8 @@ def main():
         else ('gemm_f32_kernel',)
 
     def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
-        return any(k + '<' in nm for k in knames) or ('stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)
+        return any(k + '<' in nm for k in knames + ('seam_kernel',)) or (
+            'stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)
     out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
                       'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
     for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):

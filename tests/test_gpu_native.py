@@ -214,3 +214,39 @@ def test_reserved_buffers_are_pinned():
     out = nm.forward(x)
     torch.cuda.synchronize()
     assert bool(torch.isfinite(out).all())
+
+
+def test_bottleneck_seam_in_the_plan():
+    """PPS_TILE_SEAM on res2_1 / res3_1 branch2c: one launch computes it and
+    the next block's branch2a -- the same bits as the two layers on the
+    16x16x32 group tiles (54 and 38), in the C plan and the Python twin; the
+    flag is refused on a layer that is not such a pair, and eager ranges
+    that split a pair still compute both layers."""
+    from pps_amd import ops
+    _, pm, nm = _models()
+    _, x = _input(2)
+    base = dict(nm.tiles())
+    base.update({'res2_1_branch2c': 54, 'res2_2_branch2a': 38,
+                 'res3_1_branch2c': 54, 'res3_2_branch2a': 38})
+    nm.set_tiles(base)
+    pm.set_tiles(base)
+    ref = nm.forward(x).cpu().numpy()
+    seam = dict(base)
+    for k in ('res2_1_branch2c', 'res3_1_branch2c'):
+        seam[k] = 54 | ops.TILE_SEAM
+    nm.set_tiles(seam)
+    pm.set_tiles(seam)
+    assert nm.tiles()['res2_1_branch2c'] == 54 | ops.TILE_SEAM
+    assert np.array_equal(nm.forward(x).cpu().numpy(), ref)
+    assert np.array_equal(pm.forward(x).cpu().numpy(), ref)
+    # a range ending at the seam layer, then one starting at its branch2a
+    names = [L['name'] for L in nm.layers(2)]
+    i = names.index('res2_1_branch2c')
+    out = torch.empty((2, nm.feat_dim), dtype=torch.float32, device='cuda')
+    nm.forward_layers(x, 0, i + 1, out=out)
+    nm.forward_layers(x, i + 1, len(names), out=out)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    with pytest.raises(RuntimeError, match='PPS_TILE_SEAM'):
+        nm.set_tiles({'res2_0_branch2c': 54 | ops.TILE_SEAM})   # projection block (dual)
+    with pytest.raises(RuntimeError, match='PPS_TILE_SEAM'):
+        nm.set_tiles({'res4_1_branch2c': 54 | ops.TILE_SEAM})   # (256, 1024, 256): no kernel
