@@ -279,7 +279,7 @@ int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_
  * (reid_dataset_evaluator.py:319,420) with ties in index order; vals
  * (optional, [Q][ldv]) the sorted distances.  One row per workgroup in LDS
  * (bucket map of the row's own range + in-bucket ranks): G <=
- * pps_argsort_rows_cap() (18368), else PPS_ERR_INVALID_ARG. */
+ * pps_argsort_rows_cap() (18240), else PPS_ERR_INVALID_ARG. */
 int pps_argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32_t* idx,
                      int64_t ldi, float* vals, int64_t ldv, void* stream);
 int pps_argsort_rows_cap(void);
@@ -329,6 +329,12 @@ int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, i
  * blocks in place and compute M[i][j]^2 / colmax[i] on the fly (the same
  * float32 operations); only q_g^T is materialised (in the workspace).
  * Results equal the dense path's bit for bit. */
+/* PPS_RERANK_WHOLE (with PPS_RERANK_SYMMETRIC, pps_re_ranking_ld): the three
+ * blocks are views of ONE exactly symmetric N x N matrix [[q_q, q_g],
+ * [q_g^T, g_g]] with one row stride (q_g = q_q + Q, g_g = q_q + Q * ld + Q;
+ * e.g. the mirrored self-distance of the concatenated [queries; gallery]
+ * features): q_g^T is read from its lower-left block, not transposed. */
+#define PPS_RERANK_WHOLE 2
 int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t ld_qq,
                       const float* g_g, int64_t ld_gg, int64_t Q, int64_t G, int k1, int k2,
                       double lambda_value, int flags, void* workspace, int64_t ws_bytes,

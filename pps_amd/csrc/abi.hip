@@ -501,7 +501,13 @@ int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t
   PPS_ENFORCE(jaccard_lds_bytes(G) + 2048 <= 160 * 1024,
               "G must be <= 38400 (the Jaccard pass keeps a gallery row in LDS)");
   PPS_ENFORCE((Q + G) >= K1, "need Q + G >= k1 + 1");
-  PPS_ENFORCE((flags & ~PPS_RERANK_SYMMETRIC) == 0, "unknown re-ranking flags");
+  PPS_ENFORCE((flags & ~(PPS_RERANK_SYMMETRIC | PPS_RERANK_WHOLE)) == 0,
+              "unknown re-ranking flags");
+  PPS_ENFORCE(!(flags & PPS_RERANK_WHOLE) ||
+                  ((flags & PPS_RERANK_SYMMETRIC) && ld_qg == ld_qq && ld_gg == ld_qq &&
+                   q_g == q_q + Q && g_g == q_q + Q * ld_qq + Q),
+              "PPS_RERANK_WHOLE: q_q, q_g and g_g must be the blocks of one symmetric matrix "
+              "(one row stride, q_g = q_q + Q, g_g = q_q + Q * ld + Q) and PPS_RERANK_SYMMETRIC set");
   return rerank(q_g, ld_qg, q_q, ld_qq, g_g, ld_gg, Q, G, k1, k2, lambda_value, workspace,
                 (size_t)ws_bytes, out, as_stream(stream), flags);
 }

@@ -834,7 +834,10 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   // its top-k, the V weights and the Jaccard blend read M's blocks and
   // compute (m * m) / colmax on the fly; q_g^T (the block that is nobody's
   // row) goes where OD would start.
-  RrMatrix M{qg, qq, gg, od, ldqg, ldqq, ldgg, ldT, Q, G, colmax};
+  // PPS_RERANK_WHOLE: q_g^T is the matrix's own lower-left block
+  const bool whole = (flags & PPS_RERANK_WHOLE) != 0;
+  RrMatrix M{qg, qq, gg, whole ? qq + Q * ldqq : od, ldqg, ldqq, ldgg, whole ? ldqq : ldT,
+             Q, G, colmax};
   const bool inplace = (flags & PPS_RERANK_SYMMETRIC) && topk_rr_eligible(M, K1) &&
                        getenv_flag_off("PPS_RERANK_INPLACE") == false;
   // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M (in place:
@@ -856,9 +859,12 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   PPS_CHECK_LAUNCH_S("rerank_colmax_sq_kernel", st);
   constexpr int T = PPS_OD_TILE;
   if (inplace) {
-    hipLaunchKernelGGL(rerank_transpose_kernel, dim3((unsigned)((G + 63) / 64), (unsigned)((Q + 63) / 64)),
-                       dim3(256), 0, st, qg, ldqg, Q, G, od, ldT);
-    PPS_CHECK_LAUNCH_S("rerank_transpose_kernel", st);
+    if (!whole) {
+      hipLaunchKernelGGL(rerank_transpose_kernel,
+                         dim3((unsigned)((G + 63) / 64), (unsigned)((Q + 63) / 64)), dim3(256), 0,
+                         st, qg, ldqg, Q, G, od, ldT);
+      PPS_CHECK_LAUNCH_S("rerank_transpose_kernel", st);
+    }
     // scratch for the squared top-k: the OD region past q_g^T
     const size_t tb = (sizeof(float) * (size_t)(G * ldT) + 255) / 256 * 256;
     const size_t odb = sizeof(float) * (size_t)(N * ldo);

@@ -30,8 +30,10 @@ namespace {
 constexpr int kSortThreads = 512;
 constexpr int kSortBuckets = 4096;
 constexpr int kSortSmall = 64;   // larger buckets: one wave's bitonic sort
-// LDS: packed row (8 B per entry) + bucket offsets, within 160 KiB
-constexpr int kSortCap = (160 * 1024 - 4 * kSortBuckets - 256) / 8 / 64 * 64;  // 18400
+constexpr int kSortBigMax = 18432 / kSortSmall;   // buckets that can exceed kSortSmall
+// LDS: packed row (8 B per entry) + bucket offsets + the large-bucket list,
+// within 160 KiB
+constexpr int kSortCap = (160 * 1024 - 4 * kSortBuckets - 4 * kSortBigMax - 256) / 8 / 64 * 64;
 constexpr int kSortU = (kSortCap + kSortThreads - 1) / kSortThreads;            // entries per thread
 
 // -0.0 is keyed as +0.0 (they compare equal, so NumPy's stable sort keeps
@@ -52,6 +54,8 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
   __shared__ unsigned long long pk[kSortCap];
   __shared__ unsigned off[kSortBuckets];
   __shared__ uint32_t red_min[kSortThreads / 64], red_max[kSortThreads / 64];
+  __shared__ int big[kSortBigMax];   // buckets over kSortSmall entries
+  __shared__ int s_nbig;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   constexpr int NW = kSortThreads / 64;
   float cur[kSortU], nxt[kSortU];
@@ -136,25 +140,45 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       }
     }
     __syncthreads();
-    // 3) rank inside small buckets, straight to the output row
-    int32_t* orow = idx + q * ldi;
-    float* vrow = vals ? vals + q * ldv : nullptr;
-    for (int p = t; p < G; p += kSortThreads) {
-      const unsigned long long v = pk[p];
-      const int b = bucket((uint32_t)(v >> 32));
+    // 3) the buckets holding more than kSortSmall entries (ties, degenerate
+    // rows): a list in LDS, found by every thread over its own buckets
+    if (t == 0) s_nbig = 0;
+    __syncthreads();
+    for (int b = t; b < kSortBuckets; b += kSortThreads) {
       const int s = b ? (int)off[b - 1] : 0, e = (int)off[b];
-      if (e - s > kSortSmall) continue;
-      int r = 0;
-      for (int j = s; j < e; ++j) r += pk[j] < v ? 1 : 0;
-      orow[s + r] = (int32_t)(uint32_t)v;
-      if (vrow) vrow[s + r] = sort_key_float((uint32_t)(v >> 32));
+      if (e - s > kSortSmall) big[atomicAdd(&s_nbig, 1)] = b;
     }
+    // 4) small buckets: every entry's rank among its bucket's packed keys,
+    // then (after the barrier: the ranks read the unsorted bucket) written
+    // to its final slot -- pk ends up sorted
+    unsigned long long sv[kSortU];
+    int sp[kSortU];
+#pragma unroll
+    for (int u = 0; u < kSortU; ++u) {
+      const int p = t + u * kSortThreads;
+      sp[u] = -1;
+      if (p < G) {
+        const unsigned long long v = pk[p];
+        const int b = bucket((uint32_t)(v >> 32));
+        const int s = b ? (int)off[b - 1] : 0, e = (int)off[b];
+        if (e - s <= kSortSmall) {
+          int r = 0;
+          for (int j = s; j < e; ++j) r += pk[j] < v ? 1 : 0;
+          sv[u] = v;
+          sp[u] = s + r;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kSortU; ++u)
+      if (sp[u] >= 0) pk[sp[u]] = sv[u];
     // large buckets: one wave each, bitonic network for any length in place
     // (mirror step, then half-cleaners; partners past the end are skipped)
-    for (int b = wave; b < kSortBuckets; b += NW) {
+    for (int bi = wave; bi < s_nbig; bi += NW) {
+      const int b = big[bi];
       const int s = b ? (int)off[b - 1] : 0, e = (int)off[b];
       const int n = e - s;
-      if (n <= kSortSmall) continue;   // wave-uniform
       unsigned long long* a = pk + s;
       int n2 = 1;
       while (n2 < n) n2 <<= 1;
@@ -181,10 +205,15 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
       }
-      for (int x = lane; x < n; x += 64) {
-        orow[s + x] = (int32_t)(uint32_t)a[x];
-        if (vrow) vrow[s + x] = sort_key_float((uint32_t)(a[x] >> 32));
-      }
+    }
+    __syncthreads();
+    // 5) the sorted row out, coalesced
+    int32_t* orow = idx + q * ldi;
+    float* vrow = vals ? vals + q * ldv : nullptr;
+    for (int p = t; p < G; p += kSortThreads) {
+      const unsigned long long v = pk[p];
+      orow[p] = (int32_t)(uint32_t)v;
+      if (vrow) vrow[p] = sort_key_float((uint32_t)(v >> 32));
     }
     __syncthreads();   // pk / off are rebuilt for the next row
 #pragma unroll

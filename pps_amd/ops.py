@@ -501,14 +501,16 @@ def ap_finalize(sorted_d, pos_total, hist, before):
     return ap, valid, first
 
 
-def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None):
+def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None, whole=False):
     """k-reciprocal re-ranking (reid_dataset_evaluator.py:442-519) -> [Q, G].
     symmetric: q_q and g_g are exactly symmetric (PPS_RERANK_SYMMETRIC: with
     16-byte rows and N >= 16384 the N x N normalised distance is never built,
     pps_re_ranking_ld; else it is built from rows, only q_g^T transposed);
     None = both came from compute_dist's mirrored self-distance (tagged
     `_pps_symmetric`).  Same result either way on symmetric inputs.  Inputs
-    may be row-padded views (dist_buffer / compute_dist(pad_rows=True))."""
+    may be row-padded views (dist_buffer / compute_dist(pad_rows=True)).
+    whole: the three are the blocks of one symmetric [N, N] self-distance
+    (self_distance_blocks) -- q_g^T is read in place (PPS_RERANK_WHOLE)."""
     Q, G = q_g.shape
     assert tuple(q_q.shape) == (Q, Q) and tuple(g_g.shape) == (G, G)
     if symmetric is None:
@@ -521,12 +523,25 @@ def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None):
     out = torch.empty((Q, G), dtype=torch.float32, device=q_g.device)
     call('pps_re_ranking_ld', _dev_rows(q_g, 'q_g'), _ld(q_g), _dev_rows(q_q, 'q_q'), _ld(q_q),
          _dev_rows(g_g, 'g_g'), _ld(g_g), Q, G, k1, k2, float(lambda_value),
-         RERANK_SYMMETRIC if symmetric else 0, ws.data_ptr(), int(nbytes), out.data_ptr(),
-         _stream())
+         (RERANK_SYMMETRIC if symmetric else 0) | (RERANK_WHOLE if whole else 0),
+         ws.data_ptr(), int(nbytes), out.data_ptr(), _stream())
     return out
 
 
 RERANK_SYMMETRIC = 1   # pps_abi.h PPS_RERANK_SYMMETRIC
+RERANK_WHOLE = 2       # pps_abi.h PPS_RERANK_WHOLE
+
+
+def self_distance_blocks(x, Q, metric='euclidean'):
+    """Re-ranking's three distance blocks from ONE mirrored self-distance of
+    x = [queries; gallery] ([N, D], the first Q rows the queries): -> (M,
+    q_g, q_q, g_g), the blocks row-padded views of the exactly symmetric
+    [N, N] M (compute_dist(x, x), upper triangle + mirror, one bf16x3 split of
+    x).  Pass them to re_ranking(..., whole=True); q_g serves the plain
+    ranking as well.  Same values as the three separate compute_dist calls
+    on the same tile group."""
+    M = compute_dist(x, x, metric=metric, pad_rows=True, symmetric=True)
+    return M, M[:Q, Q:], M[:Q, :Q], M[Q:, Q:]
 
 
 def max_positives(qid, qcam, gid, gcam):

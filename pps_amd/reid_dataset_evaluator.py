@@ -185,12 +185,27 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         ap, valid, first = rank_eval(dist, q_ids, g_ids, q_cams, g_cams)
         return scores_from_ranks(ap, valid, first, topk=10)
 
-    qf = feat.index_select(0, qi).contiguous()
-    gf = feat.index_select(0, gi).contiguous()
+    tiled = ops.default_math() == 'x3' and feat.shape[1] % 32 == 0
+    # re-ranking on the x3 path: ONE mirrored self-distance of [queries;
+    # gallery] gives q_g, q_q and g_g as blocks of one exactly symmetric
+    # matrix (re-ranking then reads q_g^T in place, PPS_RERANK_WHOLE)
+    whole = bool(cfg.REID.RERANK) and tiled
+    if whole:
+        x = feat.index_select(0, torch.cat([qi, gi])).contiguous()
+        qf, gf = x[:len(qi)], x[len(qi):]
+    else:
+        qf = feat.index_select(0, qi).contiguous()
+        gf = feat.index_select(0, gi).contiguous()
     with measure_time('Computing distance...', verbose):
         if verbose:
             print('Array size: ', tuple(qf.shape), tuple(gf.shape))
-        q_g = ops.compute_dist(qf, gf, metric=metric, pad_rows=True)
+        # the gallery split into chunk-tiled bf16x3 planes once: q_g and the
+        # multi-query mq_g read it
+        gsrc = ops.GalleryIndex(gf, tiled=True) if tiled else gf
+        if whole:
+            _, q_g, q_q, g_g = ops.self_distance_blocks(x, len(qi), metric=metric)
+        else:
+            q_g = ops.compute_dist(qf, gsrc, metric=metric, pad_rows=True, q_planes=tiled)
     with measure_time('Computing scores...', verbose):
         mAP, cmc_scores = compute_score(q_g, ids[q_inds], ids[g_inds], cams[q_inds],
                                         cams[g_inds])
@@ -207,7 +222,8 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         pooled = ops.group_mean(feat, [mq_rows[v] for v in groups.values()])
         keys = np.array(list(groups.keys()))
         with measure_time('Multi Query, Computing distance...', verbose):
-            mq_g = ops.compute_dist(pooled, gf, metric=metric, pad_rows=True)
+            mq_g = ops.compute_dist(pooled, gsrc, metric=metric, pad_rows=True,
+                                    q_planes=tiled)
         with measure_time('Multi Query, Computing scores...', verbose):
             mq_mAP, mq_cmc = compute_score(mq_g, keys[:, 0], ids[g_inds], keys[:, 1],
                                            cams[g_inds])
@@ -219,9 +235,12 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         # :161-207 -- re-ranked scores overwrite the plain ones
         with measure_time('Re-ranking distance...', verbose):
             # 16-byte rows: re-ranking reads the blocks in place (no N x N copy)
-            q_q = ops.compute_dist(qf, qf, metric=metric, pad_rows=True)
-            g_g = ops.compute_dist(gf, gf, metric=metric, pad_rows=True)
-            rr = ops.re_ranking(q_g, q_q, g_g)
+            if whole:
+                rr = ops.re_ranking(q_g, q_q, g_g, symmetric=True, whole=True)
+            else:
+                q_q = ops.compute_dist(qf, qf, metric=metric, pad_rows=True)
+                g_g = ops.compute_dist(gf, gsrc, metric=metric, pad_rows=True)
+                rr = ops.re_ranking(q_g, q_q, g_g)
         with measure_time('Computing scores for re-ranked distance...', verbose):
             mAP, cmc_scores = compute_score(rr, ids[q_inds], ids[g_inds], cams[q_inds],
                                             cams[g_inds])
@@ -231,7 +250,9 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         if mq_inds.any():
             with measure_time('Multi Query, Re-ranking distance...', verbose):
                 mq_mq = ops.compute_dist(pooled, pooled, metric=metric, pad_rows=True)
-                rr_mq = ops.re_ranking(mq_g, mq_mq, g_g)
+                # g_g a block of the whole matrix: exactly symmetric, untagged
+                sym = True if whole and getattr(mq_mq, '_pps_symmetric', False) else None
+                rr_mq = ops.re_ranking(mq_g, mq_mq, g_g, symmetric=sym)
             with measure_time('Multi Query, Computing scores for re-ranked distance...',
                               verbose):
                 mq_mAP, mq_cmc = compute_score(rr_mq, keys[:, 0], ids[g_inds], keys[:, 1],

@@ -49,36 +49,34 @@ def main():
             print('ok:', what, flush=True)
 
     times = {}
+    x = torch.cat([qf, gf]).contiguous()   # the evaluator's [queries; gallery] rows
     for rep in range(a.reps + 1):
-        e = [ev() for _ in range(5)]
+        e = [ev() for _ in range(4)]
         e[0].record()
-        q_g = ops.compute_dist(qf, gf, metric='cosine', pad_rows=True)
+        # as reid_dataset_evaluator.evaluate runs it with REID.RERANK: one
+        # mirrored self-distance of [queries; gallery] -> q_g, q_q, g_g blocks
+        _, q_g, q_q, g_g = ops.self_distance_blocks(x, Q, metric='cosine')
         e[1].record()
-        mark('q_g')
-        q_q = ops.compute_dist(qf, qf, metric='cosine', pad_rows=True)
-        mark('q_q')
-        g_g = ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
-        mark('g_g')
+        mark('self-distance')
+        rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3, symmetric=True, whole=True)
         e[2].record()
-        rr = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)   # q_q, g_g mirrored: symmetric path
-        e[3].record()
         mark('re_ranking')
         res = gev.rank_eval(rr, qid, gid, qcam, gcam)
-        e[4].record()
+        e[3].record()
         torch.cuda.synchronize()
         if rep:
-            for k, (s, t) in dict(q_g_ms=(0, 1), q_q_g_g_ms=(1, 2), rerank_ms=(2, 3),
-                                  rank_eval_ms=(3, 4), total_ms=(0, 4)).items():
+            for k, (s, t) in dict(dist_ms=(0, 1), rerank_ms=(1, 2), rank_eval_ms=(2, 3),
+                                  total_ms=(0, 3)).items():
                 times.setdefault(k, []).append(e[s].elapsed_time(e[t]))
     # re-ranking alone, 5 launches between HIP events: its HBM roofline with
     # algorithmic bytes = the three input blocks read once (N^2 floats) +
     # the [Q, G] result written (its passes over OD are the kernel's choice)
     for _ in range(1):
-        ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+        ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3, symmetric=True, whole=True)
     e0, e1 = ev(), ev()
     e0.record()
     for _ in range(5):
-        ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3)
+        ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3, symmetric=True, whole=True)
     e1.record()
     e1.synchronize()
     rr_us = e0.elapsed_time(e1) * 200.0
@@ -88,34 +86,36 @@ def main():
                    unit='GB/s', frac=round(rr_bytes / rr_us / 1e3 / 8000.0, 4), traffic=None,
                    kernel='pps_re_ranking (OD build, top-%d, V / V_qe, Jaccard)' % 21,
                    avg_call_us=round(rr_us, 1), algorithmic_bytes_per_call=rr_bytes)
-    # gallery self-distance (g_g) alone: upper-triangle super-blocks on the
+    # the [N, N] self-distance alone: upper-triangle super-blocks on the
     # chunk-tiled planes, mirrored in the epilogue.  Algorithmic flops = the
-    # triangle the kernel must compute, G (G + 1) / 2 pairs x 2 D (the full
-    # G x G product would be twice that); priced against the bf16x3 roof.
+    # triangle the kernel must compute, N (N + 1) / 2 pairs x 2 D (the full
+    # N x N product would be twice that); priced against the bf16x3 roof.
     e0, e1 = ev(), ev()
     e0.record()
     for _ in range(5):
-        ops.compute_dist(gf, gf, metric='cosine', pad_rows=True)
+        ops.self_distance_blocks(x, Q, metric='cosine')   # split included
     e1.record()
     e1.synchronize()
     sd_us = e0.elapsed_time(e1) * 200.0
-    sd_flops = G * (G + 1) / 2 * 2.0 * D
+    sd_flops = N * (N + 1) / 2 * 2.0 * D
     x3 = ops.default_math() == 'x3'
     sd_peak = 2517.0 / 6 if x3 else 157.3
     roof_sd = dict(bound='mfma', achieved=round(sd_flops / sd_us / 1e6, 1), peak=round(sd_peak, 1),
                    unit='TFLOP/s', frac=round(sd_flops / sd_us / 1e6 / sd_peak, 4), traffic=None,
-                   kernel='pps_distmat_x3_self_tiled (norms + plane split + triangle GEMM)',
+                   kernel='pps_distmat_x3_self_tiled over [queries; gallery] (norms + plane '
+                          'split + triangle GEMM)',
                    avg_call_us=round(sd_us, 1), algorithmic_flops_per_call=sd_flops,
-                   full_matrix_equivalent_TFLOPs=round(2 * G * G * D / sd_us / 1e6, 1))
+                   full_matrix_equivalent_TFLOPs=round(2 * N * N * D / sd_us / 1e6, 1))
     mAP, cmc = gev.scores_from_ranks(*res)
     mAP0, cmc0 = gev.scores_from_ranks(*gev.rank_eval(q_g, qid, gid, qcam, gcam))
+    del x
     out = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
     out.update(config='Duke sizes Q=%d G=%d D=%d cosine + re-ranking (k1=20,k2=6,l=0.3), '
                       'synthetic features' % (Q, G, D),
                math=ops.default_math(), mAP_plain=round(mAP0, 6), cmc1_plain=round(float(cmc0[0]), 6),
                mAP_reranked=round(mAP, 6), cmc1_reranked=round(float(cmc[0]), 6),
                gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr, roofline_selfdist=roof_sd,
-               rerank_symmetric=bool(getattr(g_g, '_pps_symmetric', False)))
+               rerank_inputs='blocks of one mirrored [N, N] self-distance (PPS_RERANK_WHOLE)')
     print(json.dumps(out), flush=True)
 
 

@@ -335,3 +335,29 @@ def test_duke_full_size_cosine_rerank_properties():
                            qid, gid, qcam, gcam, 0.0)
     assert r['ap_differs'] == 0 and r['first_differs'] == 0, r
     print('Duke full size: re-ranked %s' % r)
+
+
+def test_rerank_whole_matrix_blocks():
+    """re-ranking inputs as the blocks of ONE mirrored self-distance of
+    [queries; gallery] (ops.self_distance_blocks, PPS_RERANK_WHOLE: q_g^T read
+    from the matrix's lower-left block, no transpose): the blocks equal the
+    three separate compute_dist calls bit for bit, and so does the re-ranked
+    result (in place, N >= 16384); the flag is refused on separate buffers."""
+    from pps_amd import ops
+    Q, G, D = 1000, 15500, 64
+    gen = torch.Generator(device='cuda')
+    gen.manual_seed(11)
+    rng = np.random.RandomState(11)
+    x = _feats(300, rng.randint(1, 301, Q + G), D, gen, noise=2.5)
+    qf, gf = x[:Q], x[Q:]
+    M, q_g, q_q, g_g = ops.self_distance_blocks(x, Q, metric='cosine')
+    assert torch.equal(M[Q:, :Q], M[:Q, Q:].t())   # the mirror: q_g^T in place
+    sq_g = ops.compute_dist(qf, gf, metric='cosine', pad_rows=True)
+    sq_q = ops.compute_dist(qf.contiguous(), qf.contiguous(), metric='cosine', pad_rows=True)
+    sg_g = ops.compute_dist(gf.contiguous(), gf.contiguous(), metric='cosine', pad_rows=True)
+    assert torch.equal(q_g, sq_g) and torch.equal(q_q, sq_q) and torch.equal(g_g, sg_g)
+    a = ops.re_ranking(q_g, q_q, g_g, 20, 6, 0.3, symmetric=True, whole=True)
+    b = ops.re_ranking(sq_g, sq_q, sg_g, 20, 6, 0.3)
+    assert torch.equal(a, b)
+    with pytest.raises(RuntimeError, match='PPS_RERANK_WHOLE'):
+        ops.re_ranking(sq_g, sq_q, sg_g, 20, 6, 0.3, symmetric=True, whole=True)
