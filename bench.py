@@ -178,9 +178,10 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         t_rank.append(res['t_rank_ms'])
         t_total.append(res['t_total_ms'])
     rank_roof = rank_roofline(ev, res['dist'])
+    argsort_roof = argsort_roofline(res['dist'])
     dist_roof = distmat_roofline(q_local, g_local, world)
     del res['dist']
-    out = dict(rank_roofline=rank_roof, dist_roofline=dist_roof,
+    out = dict(rank_roofline=rank_roof, dist_roofline=dist_roof, argsort_roofline=argsort_roof,
                distmat_tile=pdist.HipBackend.distmat_tile,
                distmat_qplanes=pdist.HipBackend.distmat_qplanes,
                distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
@@ -259,6 +260,34 @@ def rank_roofline(ev, dist, reps=20):
                        'binary search + LDS histogram against the sorted positives)',
                 avg_launch_us=round(us, 2), algorithmic_bytes_per_launch=byt,
                 rows=Q, cols=G, row_stride=dist.stride(0))
+
+
+def argsort_roofline(dist, reps=10):
+    """The full stable rank list of the same distance block (the reference's
+    np.argsort(distmat, axis=1), reid_dataset_evaluator.py:319,420) by
+    pps_argsort_rows, timed with HIP events on its stream: algorithmic bytes
+    = Q * G * 4 read + Q * G * 4 indices written per launch.  Reported beside
+    the evaluator's path (which needs only the ranks of the positives)."""
+    from pps_amd import ops
+    Q, G = dist.shape
+    if G > ops._lib.lib().pps_argsort_rows_cap():
+        return None
+    idx = ops.argsort_rows(dist)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.argsort_rows(dist)
+    e1.record()
+    e1.synchronize()
+    del idx
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    byt = 2 * Q * G * 4
+    return dict(bound='hbm', achieved=round(byt / (us * 1e-6) / 1e9, 1), peak=PEAK_HBM_GBPS,
+                unit='GB/s', frac=round(byt / (us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4),
+                kernel='argsort_rows_kernel (row in LDS: bucket histogram / scatter, in-bucket '
+                       'ranks, sorted row streamed out)',
+                avg_launch_us=round(us, 2), algorithmic_bytes_per_launch=byt, rows=Q, cols=G)
 
 
 def _pmc_traffic(key, math, batch):
@@ -852,6 +881,7 @@ def main():
         'mAP_synthetic': round(ret['mAP'], 6), 'cmc1_synthetic': round(ret['cmc1'], 6),
         'roofline': roof,
         'roofline_rank': ret['rank_roofline'],
+        'roofline_argsort': ret['argsort_roofline'],
         'roofline_distmat': dict(
             bound='mfma',
             achieved=(ret['dist_roofline'] or {}).get('achieved', round(dist_tflops, 2)),

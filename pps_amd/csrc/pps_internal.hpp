@@ -243,7 +243,10 @@ int launch_seam_x3(const SeamParams& p, int K1, int N1, int N2, hipStream_t st);
 constexpr int kMergeMaxLists = 64;
 // rank_count_stream / cmc_counts: gallery entries per workgroup (grid.y =
 // chunks of a row, <= 65535)
-constexpr int kRankStreamChunk = 8192;
+#ifndef RANK_STREAM_U
+#define RANK_STREAM_U 8   // float4 per thread in flight in the rank streams
+#endif
+constexpr int kRankStreamChunk = 256 * 4 * RANK_STREAM_U;
 // rank_prepare merges R*Pmax positives in dynamic LDS (4 int arrays):
 // 16 B per merged positive, 128 KiB at the cap -- within gfx950's 160 KiB
 // LDS per workgroup (this library is built for gfx950 only)

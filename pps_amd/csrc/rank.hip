@@ -560,9 +560,6 @@ int rank_prepare(int R, int64_t Q, int Pmax, const float* pos_d, const int32_t* 
 #define RANK_STREAM_VARIANT 0  // probes only (scripts/rank_probe.py): 1 = stream + compare,
                                // 2 = + binary search, no histogram atomics
 #endif
-#ifndef RANK_STREAM_U
-#define RANK_STREAM_U 8
-#endif
 constexpr int kStreamThreads = 256;
 constexpr int kStreamU = RANK_STREAM_U;                      // float4 per thread in flight
 constexpr int kStreamChunk = kStreamThreads * kStreamU * 4;  // 8192 entries per block

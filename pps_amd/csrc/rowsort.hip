@@ -162,8 +162,17 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
         const int b = bucket((uint32_t)(v >> 32));
         const int s = b ? (int)off[b - 1] : 0, e = (int)off[b];
         if (e - s <= kSortSmall) {
+          // the bucket's first 8 entries in one batch of loads (the bucket
+          // holds this entry, so s + min(k, n - 1) is in it), the rest after:
+          // one LDS latency per entry instead of one per compare
+          const int n = e - s;
+          unsigned long long w[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = pk[s + (k < n ? k : n - 1)];
           int r = 0;
-          for (int j = s; j < e; ++j) r += pk[j] < v ? 1 : 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) r += (k < n && w[k] < v) ? 1 : 0;
+          for (int j = s + 8; j < e; ++j) r += pk[j] < v ? 1 : 0;
           sv[u] = v;
           sp[u] = s + r;
         }
