@@ -138,7 +138,7 @@ int pps_split_bf16x3_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t l
                                   uint16_t* out3t, float* sqnorm, void* stream);
 /* pps_distmat_x3p on tiled query and gallery planes (pps_tile_planes): each
  * 16-row DMA piece of a 32-wide K chunk is one contiguous KiB.  Same bits as
- * pps_distmat_x3p on the same tile; pipelined tiles 29..53 (0 = 42). */
+ * pps_distmat_x3p on the same tile; pipelined tiles 29..53 (0 = 43, 128 x 256). */
 int pps_distmat_x3p_tiled(const uint16_t* q3t, int64_t Q, const float* qsq,
                           const uint16_t* g3t, const float* gsq, int64_t G, int D,
                           int metric, float* out, int64_t ldo, int tile, void* stream);

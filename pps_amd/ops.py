@@ -245,7 +245,7 @@ def tile_planes(planes):
 
 def _tiled_tile(tile):
     """The tile a tiled-plane distance GEMM runs: pipelined ids 29-53 as
-    given; ids 54+ (which a distance matrix runs as tile 38) -> 0 (tile 42,
+    given; ids 54+ (which a distance matrix runs as tile 38) -> 0 (tile 43,
     the same 16x16x32 rounding group)."""
     return int(tile) if TILE_P_FIRST <= tile < 54 else 0
 
