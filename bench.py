@@ -157,10 +157,16 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
             e1.synchronize()
             return e0.elapsed_time(e1) / n
 
-        # one launch each to screen, then the 4 best re-timed over 3 launches
-        # (single launches left the pick to +-3 % noise between close tiles)
+        # one launch each to screen, then the 4 best re-timed in three
+        # interleaved rounds of 5 launches, min per tile (single launches left
+        # the pick to +-3 % noise between close tiles; interleaving keeps a
+        # drifting clock from favouring whichever ran first)
         screen = {c: time_dist(c[0], c[1], 1) for c in cands}
-        final = {c: time_dist(c[0], c[1], 3) for c in sorted(screen, key=screen.get)[:4]}
+        fin = sorted(screen, key=screen.get)[:4]
+        final = {c: 1e30 for c in fin}
+        for _ in range(3):
+            for c in fin:
+                final[c] = min(final[c], time_dist(c[0], c[1], 5))
         best = min(final, key=final.get)
         pdist.HipBackend.distmat_tile = best[0]
         pdist.HipBackend.distmat_qplanes = best[1]
