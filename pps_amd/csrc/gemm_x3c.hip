@@ -24,6 +24,10 @@
 // f32-level error, tests/test_gpu_x3.py).
 #include "gemm_x3p_common.hpp"
 
+#ifndef X3P_PRIO
+#define X3P_PRIO 0  // probes: s_setprio(1) around every MFMA cluster
+#endif
+
 namespace pps {
 
 constexpr int kX3cTaps = 9;  // 3x3
@@ -239,11 +243,13 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
     }
   };
   auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TNH][3], int half) {
+    if (X3P_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int jj = 0; jj < TNH; ++jj)
         acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
+    if (X3P_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: patch 0 whole (older than every counted issue), then NS - 1
