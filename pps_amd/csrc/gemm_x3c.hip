@@ -73,6 +73,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (X3P_PRIO == 2 && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);  // probes
   const int wm = wave / WN;
   const int wn = wave - wm * WN;
   const int r32 = lane & (S - 1);
@@ -243,13 +244,13 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
     }
   };
   auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TNH][3], int half) {
-    if (X3P_PRIO) __builtin_amdgcn_s_setprio(1);
+    if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int jj = 0; jj < TNH; ++jj)
         acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
-    if (X3P_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: patch 0 whole (older than every counted issue), then NS - 1

@@ -38,7 +38,7 @@ namespace pps {
 // chunk) or 16 (v_mfma_f32_16x16x32_bf16, one group per chunk; the wave's
 // column blocks are processed in two halves to keep the same pipeline).
 #ifndef X3P_PRIO
-#define X3P_PRIO 0  // probes: s_setprio(1) around every MFMA cluster
+#define X3P_PRIO 0  // probes: 1 = s_setprio(1) around every MFMA cluster, 2 = younger half raised
 #endif
 #ifndef X3P_CLK
 #define X3P_CLK 0  // diagnostic builds: per-workgroup shader clocks / 100 MHz ticks
@@ -118,6 +118,10 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // probes: the younger half of an 8-wave workgroup at raised priority for
+  // the whole kernel (two waves per SIMD: the second-dispatched half loses
+  // arbitration to the first at every segment start otherwise)
+  if (X3P_PRIO == 2 && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int wm = wave / WN;
   const int wn = wave - wm * WN;
   const int r32 = lane & (S - 1);  // lane's row within an MFMA block
@@ -411,12 +415,12 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       }
     };
     auto mfmas = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TN][3]) {
-      if (X3P_PRIO) __builtin_amdgcn_s_setprio(1);
+      if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma_x3t(fa[i], fb[j], acc[i][j]);
-      if (X3P_PRIO) __builtin_amdgcn_s_setprio(0);
+      if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     };
     // Software pipeline over 16-wide K groups (two per chunk): the reads and
     // the split of group q+1 are issued in the same basic block as the MFMAs
@@ -471,13 +475,13 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       }
     };
     auto mfmas16 = [&](const bf16x8 (&fa)[TM][3], const bf16x8 (&fb)[TNH][3], int half) {
-      if (X3P_PRIO) __builtin_amdgcn_s_setprio(1);
+      if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int jj = 0; jj < TNH; ++jj)
           acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
-      if (X3P_PRIO) __builtin_amdgcn_s_setprio(0);
+      if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     };
     bf16x8 fa0[TM][3], fa1[TM][3], fb0[TNH][3], fb1[TNH][3];
     readA16(lds, fa0);
