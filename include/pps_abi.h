@@ -273,6 +273,36 @@ int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_
                      int topk, int first_match_break, double* ret, int32_t* valid,
                      void* stream);
 
+/* CMC with single_gallery_shot=True (reid_dataset_evaluator.py:334-346,
+ * `_unique_sample` :275-280).  Identities are dense (gid in [0, U); qid in
+ * [0, U) or -1 when absent from the gallery).  The random draws stay with the
+ * caller's NumPy RNG; these three steps do the rest on the device:
+ *  - pps_sgs_keys: keys [Q][G] = gid of the p-th entry of order (the stable
+ *    rank list of pps_argsort_rows, [Q][ldo]) when it is valid for the query
+ *    (different identity or camera; with separate_camera_set also a different
+ *    camera), else U;
+ *  - pps_argsort_rows(keys, .., perm, vals=sorted keys): the caller's;
+ *  - pps_sgs_groups: per query the identities' groups of perm in the order
+ *    the reference's `ids_dict` meets them (by first ranked position):
+ *    gstart / glen [Q][U] (entries t < nids[q]), nids [Q], qt [Q] = the
+ *    query identity's group (-1: no valid entry of it, the query is skipped);
+ *  - (caller) draws [nr][repeat][ldd], draws[i][r][t] in [0, glen[q][t]) for
+ *    the listed queries rows[i] -- np.random.randint(0, tile(glen, repeat))
+ *    is the reference's np.random.choice stream, call for call;
+ *  - pps_sgs_ranks: k [nr][repeat] = the number of drawn entries ranked
+ *    before the query identity's draw (the reference's one hit per repeat).
+ * G <= pps_argsort_rows_cap(), U <= 16384. */
+int pps_sgs_keys(const int32_t* order, int64_t Q, int64_t G, int64_t ldo, const int32_t* gid,
+                 const int32_t* gcam, const int32_t* qid, const int32_t* qcam,
+                 int separate_camera_set, int U, float* keys, void* stream);
+int pps_sgs_groups(const float* sorted_keys, const int32_t* perm, int64_t Q, int64_t G, int U,
+                   const int32_t* qid, int32_t* gstart, int32_t* glen, int32_t* nids,
+                   int32_t* qt, void* stream);
+int pps_sgs_ranks(const int32_t* perm, int64_t Q, int64_t G, const int32_t* rows, int64_t nr,
+                  const int32_t* gstart, const int32_t* glen, const int32_t* nids,
+                  const int32_t* qt, int U, int repeat, const int32_t* draws, int64_t ldd,
+                  int32_t* k, void* stream);
+
 /* The whole rank list: idx [Q][ldi] int32, row q = every gallery column in
  * (distance, index) order -- np.argsort(distmat, axis=1, kind='stable'), the
  * reference's `indices = np.argsort(distmat, axis=1)`

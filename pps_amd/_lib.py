@@ -55,6 +55,12 @@ SIGNATURES = {
     'pps_conv1x1_seam_x3': [c_ptr, c_i64, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
                             c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_argsort_rows': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
+    'pps_sgs_keys': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_ptr,
+                     c_ptr],
+    'pps_sgs_groups': [c_ptr, c_ptr, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                       c_ptr],
+    'pps_sgs_ranks': [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int,
+                      c_ptr, c_i64, c_ptr, c_ptr],
     'pps_cmc_counts': [c_ptr, c_i64, c_i64, c_i64, c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_cmc_finalize': [c_i64, c_int, c_ptr, c_ptr, c_int, c_int, c_ptr, c_ptr, c_ptr],

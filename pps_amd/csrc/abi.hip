@@ -41,6 +41,14 @@ int topk(const float*, int64_t, int64_t, int64_t, int, float*, int32_t*, hipStre
 int argsort_rows(const float*, int64_t, int64_t, int64_t, int32_t*, int64_t, float*, int64_t,
                  hipStream_t);
 int argsort_rows_cap();
+int sgs_keys(const int32_t*, int64_t, int64_t, int64_t, const int32_t*, const int32_t*,
+             const int32_t*, const int32_t*, int, int, float*, hipStream_t);
+int sgs_groups(const float*, const int32_t*, int64_t, int64_t, int, const int32_t*, int32_t*,
+               int32_t*, int32_t*, int32_t*, hipStream_t);
+int sgs_ranks(const int32_t*, int64_t, const int32_t*, int64_t, const int32_t*, const int32_t*,
+              const int32_t*, const int32_t*, int, int, const int32_t*, int64_t, int32_t*,
+              hipStream_t);
+size_t sgs_groups_lds_bytes(int64_t, int);
 int cmc_counts(const float*, int64_t, int64_t, int64_t, int64_t, int, const float*,
                const int32_t*, const int32_t*, const int32_t*, const int32_t*, int,
                const float*, const int32_t*, const int32_t*, int32_t*, hipStream_t);
@@ -462,6 +470,40 @@ int pps_argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32
 }
 
 int pps_argsort_rows_cap(void) { return argsort_rows_cap(); }
+
+int pps_sgs_keys(const int32_t* order, int64_t Q, int64_t G, int64_t ldo, const int32_t* gid,
+                 const int32_t* gcam, const int32_t* qid, const int32_t* qcam,
+                 int separate_camera_set, int U, float* keys, void* stream) {
+  PPS_ENFORCE(order && gid && gcam && qid && qcam && keys, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 0 && ldo >= G, "bad shape");
+  PPS_ENFORCE(U >= 1 && U <= 16384, "U (distinct gallery identities) must be in [1, 16384]");
+  return sgs_keys(order, Q, G, ldo, gid, gcam, qid, qcam, separate_camera_set ? 1 : 0, U, keys,
+                  as_stream(stream));
+}
+
+int pps_sgs_groups(const float* sorted_keys, const int32_t* perm, int64_t Q, int64_t G, int U,
+                   const int32_t* qid, int32_t* gstart, int32_t* glen, int32_t* nids,
+                   int32_t* qt, void* stream) {
+  PPS_ENFORCE(sorted_keys && perm && qid && gstart && glen && nids && qt, "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 1 && G <= argsort_rows_cap(), "G must be in [1, " +
+                                                               std::to_string(argsort_rows_cap()) +
+                                                               "]");
+  PPS_ENFORCE(U >= 1 && U <= 16384, "U (distinct gallery identities) must be in [1, 16384]");
+  PPS_ENFORCE(sgs_groups_lds_bytes(G, U) <= 160 * 1024, "groups do not fit in LDS");
+  return sgs_groups(sorted_keys, perm, Q, G, U, qid, gstart, glen, nids, qt, as_stream(stream));
+}
+
+int pps_sgs_ranks(const int32_t* perm, int64_t Q, int64_t G, const int32_t* rows, int64_t nr,
+                  const int32_t* gstart, const int32_t* glen, const int32_t* nids,
+                  const int32_t* qt, int U, int repeat, const int32_t* draws, int64_t ldd,
+                  int32_t* k, void* stream) {
+  PPS_ENFORCE(perm && gstart && glen && nids && qt && k && (nr == 0 || (rows && draws)),
+              "null pointer");
+  PPS_ENFORCE(Q >= 0 && G >= 1 && nr >= 0 && repeat >= 1 && ldd >= 1, "bad shape");
+  PPS_ENFORCE(U >= 1 && U <= 16384 && ldd <= U, "ldd must be in [1, U]");
+  return sgs_ranks(perm, G, rows, nr, gstart, glen, nids, qt, U, repeat, draws, ldd, k,
+                   as_stream(stream));
+}
 
 int pps_topk_merge(const float* vals, const int32_t* idx, int R, int64_t Q, int k_in,
                    const int64_t* list_offsets, int k_out, float* out_vals,

@@ -297,6 +297,39 @@ def argsort_rows(dist, with_values=False):
     return (idx, vals) if with_values else idx
 
 
+def sgs_groups(order, gid, gcam, qid, qcam, U, separate_camera_set):
+    """Steps 1-3 of CMC single_gallery_shot (pps_sgs_keys, pps_argsort_rows,
+    pps_sgs_groups) from the stable rank list `order` [Q, G] and dense
+    identities (device int32).  Returns (perm, gstart, glen, nids, qt)."""
+    Q, G = order.shape
+    dev = order.device
+    keys = torch.empty((Q, G), dtype=torch.float32, device=dev)
+    call('pps_sgs_keys', _dev_rows(order, 'order', torch.int32), Q, G, _ld(order),
+         _dev(gid, 'gid', torch.int32), _dev(gcam, 'gcam', torch.int32),
+         _dev(qid, 'qid', torch.int32), _dev(qcam, 'qcam', torch.int32),
+         1 if separate_camera_set else 0, U, keys.data_ptr(), _stream())
+    perm, skeys = argsort_rows(keys, with_values=True)
+    del keys
+    i32 = lambda *s: torch.empty(s, dtype=torch.int32, device=dev)
+    gstart, glen, nids, qt = i32(Q, U), i32(Q, U), i32(Q), i32(Q)
+    call('pps_sgs_groups', skeys.data_ptr(), perm.data_ptr(), Q, G, U, _dev(qid, 'qid', torch.int32),
+         gstart.data_ptr(), glen.data_ptr(), nids.data_ptr(), qt.data_ptr(), _stream())
+    return perm, gstart, glen, nids, qt
+
+
+def sgs_ranks(perm, gstart, glen, nids, qt, rows, draws):
+    """Step 5 of CMC single_gallery_shot (pps_sgs_ranks): draws [nr, repeat,
+    ldd] int32 for the query rows `rows` [nr] -> k [nr, repeat] int32."""
+    Q, G = perm.shape
+    U = gstart.shape[1]
+    nr, repeat, ldd = draws.shape
+    k = torch.empty((nr, repeat), dtype=torch.int32, device=perm.device)
+    call('pps_sgs_ranks', perm.data_ptr(), Q, G, _dev(rows, 'rows', torch.int32), nr,
+         gstart.data_ptr(), glen.data_ptr(), nids.data_ptr(), qt.data_ptr(), U, repeat,
+         _dev(draws, 'draws', torch.int32), ldd, k.data_ptr(), _stream())
+    return k
+
+
 def topk(dist, k):
     """Stable ascending top-k per row -> (vals [Q,k] f32, idx [Q,k] i32)."""
     Q, G = dist.shape

@@ -105,17 +105,25 @@ def mean_ap(distmat, query_ids=None, gallery_ids=None, query_cams=None,
 
 def cmc(distmat, query_ids=None, gallery_ids=None, query_cams=None, gallery_cams=None,
         topk=100, separate_camera_set=False, single_gallery_shot=False,
-        first_match_break=False, average=True):
+        first_match_break=False, average=True, rng=None):
     """reid_dataset_evaluator.py:283-363 with the same defaults and outputs:
     the fractional CMC (first_match_break=False), the first-match CMC, and
     separate_camera_set, from per-positive counts on the device
     (pps_cmc_counts / pps_cmc_finalize; the Market protocol evaluate() uses
     takes the mAP pass's first-match ranks instead).  The ranking is the
-    stable (distance, index) order.  single_gallery_shot draws random gallery
-    samples 100 times per query (:334-346) and is not built."""
+    stable (distance, index) order.  single_gallery_shot (:334-346) draws one
+    valid gallery entry per identity 100 times per valid query with `rng`
+    (default: the global np.random, as the reference's np.random.choice):
+    the same draws in the same order, so a seeded call equals the
+    reference's; the grouping and ranking run on the device (_cmc_sgs)."""
     if single_gallery_shot:
-        raise NotImplementedError('single_gallery_shot (random per-identity sampling, '
-                                  'reid_dataset_evaluator.py:334-346) is not built')
+        ret, valid = _cmc_sgs(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk,
+                              separate_camera_set, first_match_break, rng)
+        if not valid.any():
+            raise RuntimeError('No valid query')
+        if average:
+            return np.sum(ret, axis=0) / valid.sum()
+        return ret, valid.astype(np.float64)
     d = distmat if isinstance(distmat, torch.Tensor) and distmat.is_cuda and \
         distmat.dtype == torch.float32 and distmat.dim() == 2 and \
         (distmat.shape[0] < 2 or distmat.stride(1) == 1) else _to_dev(distmat)
@@ -139,6 +147,53 @@ def cmc(distmat, query_ids=None, gallery_ids=None, query_cams=None, gallery_cams
     if average:
         return np.sum(ret, axis=0) / valid.sum()
     return ret, valid.astype(np.float64)
+
+
+def _cmc_sgs(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk,
+             separate_camera_set, first_match_break, rng, repeat=100):
+    """CMC single_gallery_shot (reid_dataset_evaluator.py:321-363 with
+    :334-346): stable rank list (pps_argsort_rows), per-query identity groups
+    in `ids_dict` order (pps_sgs_keys / pps_sgs_groups), the reference's
+    draws (`_unique_sample` :275-280: one np.random.choice per identity and
+    repeat, reproduced call for call by one randint per query), and the
+    query identity's rank among the draws (pps_sgs_ranks)."""
+    rng = rng or np.random
+    d = _to_dev(distmat)
+    Q, G = d.shape
+    gid = np.asarray(gallery_ids).astype(np.int64)
+    qid = np.asarray(query_ids).astype(np.int64)
+    uniq = np.unique(gid)
+    U = len(uniq)
+    gdense = np.searchsorted(uniq, gid)
+    qpos = np.minimum(np.searchsorted(uniq, qid), U - 1)
+    qdense = np.where(uniq[qpos] == qid, qpos, -1)
+    dev = d.device
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32)).to(dev)
+    order = ops.argsort_rows(d)
+    perm, gstart, glen, nids, qt = ops.sgs_groups(order, i32(gdense), i32(gallery_cams),
+                                                  i32(qdense), i32(query_cams), U,
+                                                  separate_camera_set)
+    del order
+    glen_h, nids_h, qt_h = _np(glen), _np(nids), _np(qt)
+    valid = qt_h >= 0
+    rows = np.nonzero(valid)[0]
+    ret = np.zeros((Q, topk))
+    delta = 1. if first_match_break else 1. / (1 * repeat)   # one hit per repeat (:347-356)
+    if len(rows):
+        ldd = int(nids_h[rows].max())
+        chunk = max(1, (64 << 20) // (repeat * ldd * 4))
+        for c0 in range(0, len(rows), chunk):
+            rs = rows[c0:c0 + chunk]
+            draws = np.zeros((len(rs), repeat, ldd), dtype=np.int32)
+            for i, q in enumerate(rs):   # query order, as the reference draws
+                n = int(nids_h[q])
+                draws[i, :, :n] = rng.randint(0, np.tile(glen_h[q, :n], repeat)).reshape(repeat, n)
+            k = _np(ops.sgs_ranks(perm, gstart, glen, nids, qt, i32(rs), i32(draws)))
+            qq = np.repeat(rs, repeat)
+            kk = k.reshape(-1)
+            keep = kk < topk
+            np.add.at(ret, (qq[keep], kk[keep]), delta)
+    return ret.cumsum(axis=1), valid
 
 
 def parse_im_name(im_name, parse_type='id'):

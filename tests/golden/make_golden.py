@@ -178,6 +178,40 @@ def case_cmc_modes(ev):
     return dict(name='cmc_modes', keys=len(out))
 
 
+def case_sgs(ev):
+    """The reference `cmc(single_gallery_shot=True)` (:334-346): 100 repeats
+    per valid query, one gallery entry drawn per identity with the global
+    np.random (`_unique_sample`, :275-280), seeded here before each call.
+    The distances are given as float32 values with no tie inside a row, so
+    the reference's quicksort argsort is the stable order."""
+    out = {}
+    for fseed in range(31, 64):   # the first feature seed without a tie in any row
+        x, ids, cams = synth_features(40, 6, 64, 1.8, fseed, 40)
+        (qf, qid, qcam), (gf, gid, gcam) = split_qg(x, ids, cams, 0.15, fseed)
+        dist, _ = quiet(ev.compute_dist, qf, gf, type='euclidean')
+        dist = dist.astype(np.float32)
+        s = np.sort(dist, axis=1)
+        if not np.any(s[:, 1:] == s[:, :-1]):
+            break
+    else:
+        raise AssertionError('tied distances in every candidate')
+    out.update(qid=qid, gid=gid, qcam=qcam, gcam=gcam, dist=dist)
+    for seed, sep, fmb, topk in ((0, False, False, 100), (1, True, False, 100),
+                                 (2, False, True, 20), (3, True, True, 10)):
+        key = 'seed%d_sep%d_fmb%d_top%d' % (seed, sep, fmb, topk)
+        np.random.seed(seed)
+        out[key + '_all'], out[key + '_valid'] = ev.cmc(
+            dist.astype(np.float64), qid, gid, qcam, gcam, topk=topk, separate_camera_set=sep,
+            single_gallery_shot=True, first_match_break=fmb, average=False)
+        np.random.seed(seed)
+        out[key] = ev.cmc(dist.astype(np.float64), qid, gid, qcam, gcam, topk=topk,
+                          separate_camera_set=sep, single_gallery_shot=True,
+                          first_match_break=fmb)
+        out[key + '_next_draw'] = np.random.randint(1 << 30)   # the RNG state left behind
+    np.savez_compressed(os.path.join(HERE, 'cmc_sgs.npz'), **out)
+    return dict(name='cmc_sgs', Q=len(qid), G=len(gid), keys=len(out))
+
+
 class _FakeJsonDataset(object):
     def __init__(self, entries):
         self.entries = entries
@@ -226,6 +260,7 @@ def main():
     meta.append(case_rerank(ev))
     meta.append(case_evaluate(ev))
     meta.append(case_cmc_modes(ev))
+    meta.append(case_sgs(ev))
     import sklearn
     meta = dict(cases=meta, numpy=np.__version__, sklearn=sklearn.__version__,
                 python=sys.version.split()[0],

@@ -416,8 +416,61 @@ def test_cmc_all_modes_vs_reference_golden(golden, tag):
     np.testing.assert_array_equal(gev.cmc(d, qid, gid, qcam, gcam, topk=5,
                                           separate_camera_set=True),
                                   g[tag + '_sep1_fmb0_top5'])
-    with pytest.raises(NotImplementedError, match='single_gallery_shot'):
-        gev.cmc(d, qid, gid, qcam, gcam, single_gallery_shot=True)
+
+
+SGS_CASES = ((0, False, False, 100), (1, True, False, 100), (2, False, True, 20),
+             (3, True, True, 10))
+
+
+def test_cmc_single_gallery_shot_vs_reference_golden(golden):
+    """cmc(single_gallery_shot=True) against the reference's own output
+    (cmc_sgs.npz: the reference cmc run after np.random.seed(s)): the same
+    global-RNG draws in the same order -> per-query rows and averages
+    bit-exact, and the RNG left in the same state."""
+    from pps_amd import reid_dataset_evaluator as gev
+    g = golden('cmc_sgs')
+    d, qid, gid, qcam, gcam = g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam']
+    for seed, sep, fmb, topk in SGS_CASES:
+        key = 'seed%d_sep%d_fmb%d_top%d' % (seed, sep, fmb, topk)
+        kw = dict(topk=topk, separate_camera_set=sep, single_gallery_shot=True,
+                  first_match_break=fmb)
+        np.random.seed(seed)
+        ret, valid = gev.cmc(d, qid, gid, qcam, gcam, average=False, **kw)
+        np.testing.assert_array_equal(valid, g[key + '_valid'], err_msg=key)
+        np.testing.assert_array_equal(ret, g[key + '_all'], err_msg=key)
+        np.random.seed(seed)
+        np.testing.assert_array_equal(gev.cmc(d, qid, gid, qcam, gcam, **kw), g[key],
+                                      err_msg=key)
+        assert np.random.randint(1 << 30) == g[key + '_next_draw'], key
+
+
+@pytest.mark.parametrize('Q,G,n_ids,seed', [(40, 3000, 100, 0), (25, 700, 12, 1),
+                                            (7, 1, 1, 2), (30, 18240, 40, 3)])
+def test_cmc_single_gallery_shot_vs_oracle(Q, G, n_ids, seed):
+    """Larger / ragged cases vs the oracle (the reference's loop with a
+    RandomState): many identities, few identities with long groups, a
+    one-entry gallery, and the argsort cap; query identities missing from the
+    gallery (skipped, no draws), junk ids, repeated cameras."""
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(seed)
+    d = rng.rand(Q, G).astype(np.float32)
+    gid = rng.randint(-1, n_ids, size=G)
+    qid = rng.randint(0, n_ids + 3, size=Q)
+    qcam = rng.randint(1, 4, size=Q)
+    gcam = rng.randint(1, 4, size=G)
+    for sep in (False, True):
+        for fmb in (False, True):
+            kw = dict(topk=50, separate_camera_set=sep, single_gallery_shot=True,
+                      first_match_break=fmb, average=False)
+            try:
+                want = ev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(seed + 10), **kw)
+            except RuntimeError:   # no valid query
+                with pytest.raises(RuntimeError, match='No valid query'):
+                    gev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(seed + 10), **kw)
+                continue
+            got = gev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(seed + 10), **kw)
+            np.testing.assert_array_equal(got[1], want[1])
+            np.testing.assert_array_equal(got[0], want[0])
 
 
 def test_cmc_counts_sharded_equal_unsharded(golden):

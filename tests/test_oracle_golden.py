@@ -111,6 +111,39 @@ def test_oracle_cmc_all_modes_vs_reference(golden):
                                    g[tag + '_sep1_fmb0_top5'], rtol=0, atol=1e-12)
 
 
+def test_oracle_cmc_single_gallery_shot_vs_reference_golden(golden):
+    """The oracle cmc(single_gallery_shot=True) draws what the reference draws
+    (cmc_sgs.npz, the reference run after np.random.seed(s)): identical
+    per-query rows, averages and RNG state left behind."""
+    g = golden('cmc_sgs')
+    d, qid, gid, qcam, gcam = g['dist'], g['qid'], g['gid'], g['qcam'], g['gcam']
+    for seed, sep, fmb, topk in ((0, 0, 0, 100), (1, 1, 0, 100), (2, 0, 1, 20), (3, 1, 1, 10)):
+        key = 'seed%d_sep%d_fmb%d_top%d' % (seed, sep, fmb, topk)
+        kw = dict(topk=topk, separate_camera_set=bool(sep), single_gallery_shot=True,
+                  first_match_break=bool(fmb))
+        np.random.seed(seed)
+        ret, valid = ev.cmc(d, qid, gid, qcam, gcam, average=False, **kw)
+        np.testing.assert_array_equal(ret, g[key + '_all'], err_msg=key)
+        np.testing.assert_array_equal(valid, g[key + '_valid'])
+        assert np.random.randint(1 << 30) == g[key + '_next_draw']
+        np.testing.assert_array_equal(
+            ev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(seed), **kw), g[key])
+
+
+def test_sgs_draws_are_the_reference_choice_stream():
+    """The product path draws one randint(0, tile(lens, repeat)) per query;
+    NumPy's legacy RandomState gives exactly the values (and state) of the
+    reference's per-identity np.random.choice calls, one-entry lists
+    consuming nothing."""
+    rs = np.random.RandomState(0)
+    lens = rs.randint(1, 40, size=500)
+    lens[::7] = 1
+    a, b = np.random.RandomState(5), np.random.RandomState(5)
+    seq = [a.choice(list(range(n))) for _ in range(3) for n in lens]
+    np.testing.assert_array_equal(seq, b.randint(0, np.tile(lens.astype(np.int32), 3)))
+    assert a.randint(1 << 30) == b.randint(1 << 30)
+
+
 @pytest.mark.parametrize('k2', [6, 1])
 def test_rerank_sparse_restatement_equals_oracle(golden, k2):
     """oracle.re_ranking_sparse (the long-row GPU test's checker) computes the
