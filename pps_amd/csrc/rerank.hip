@@ -667,7 +667,10 @@ __global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_
 // entries are staged into LDS kJacStage at a time (all loads of a stage in
 // flight together); the per-column pass then only touches LDS, one barrier
 // per column.
-constexpr int kJacThreads = 256;
+// 16 waves per block (two blocks per CU, the LDS row): the per-column pass
+// and the blend are latency chains, so more waves in flight is what helps --
+// Duke re-ranking 906 -> 845 (512 threads) -> 818 us (1024) vs 256 threads
+constexpr int kJacThreads = 1024;
 constexpr int kJacCols = 128;    // column metadata loaded per batch
 constexpr int kJacStage = 1024;  // staged (row, value) entries
 size_t jaccard_lds_bytes(int64_t G) {
