@@ -614,31 +614,47 @@ __global__ void rerank_csc_count_kernel(int64_t N, const int32_t* __restrict__ q
     if (q_val[i * qcap + e] != 0.f) atomicAdd(&col_cnt[q_idx[i * qcap + e]], 1);
 }
 
+// single-block exclusive scan over tiles of 1024 x kScanU counts: a thread's
+// kScanU consecutive counts are loaded together (one memory latency per tile,
+// not one per count), summed, and the 1024 sums scanned by wave shuffles and
+// the 16 wave totals; the tile total carries into the next tile
+constexpr int kScanU = 8;
 __global__ void __launch_bounds__(1024)
 rerank_scan_kernel(int64_t N, const int32_t* __restrict__ cnt, int32_t* __restrict__ start) {
-  // single block exclusive scan: a run of `per` counts per thread, the 1024
-  // run totals scanned by wave shuffles (16 waves) and a scan of the wave totals
   __shared__ int32_t wtot[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t per = (N + 1023) / 1024;
-  const int64_t a = tid * per, b = min(N, a + per);
-  int32_t s = 0;
-  for (int64_t e = a; e < b; ++e) s += cnt[e];
-  int32_t incl = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
+  int32_t carry = 0;
+  for (int64_t base = 0; base < N; base += 1024 * kScanU) {
+    const int64_t e0 = base + (int64_t)tid * kScanU;
+    int32_t v[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) v[u] = e0 + u < N ? cnt[e0 + u] : 0;
+    int32_t s = 0;
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) s += v[u];
+    int32_t incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int32_t wb = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      const int32_t x = wtot[w];
+      if (w < wave) wb += x;
+      tot += x;
+    }
+    int32_t run = carry + wb + incl - s;
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      if (e0 + u < N) start[e0 + u] = run;
+      run += v[u];
+    }
+    carry += tot;
+    __syncthreads();   // wtot is rewritten by the next tile
   }
-  if (lane == 63) wtot[wave] = incl;
-  __syncthreads();
-  int32_t base = 0;
-  for (int w = 0; w < wave; ++w) base += wtot[w];
-  int32_t run = base + incl - s;
-  for (int64_t e = a; e < b; ++e) {
-    start[e] = run;
-    run += cnt[e];
-  }
-  if (tid == 1023) start[N] = run;
+  if (tid == 0) start[N] = carry;
 }
 
 __global__ void rerank_csc_fill_kernel(int64_t N, const int32_t* __restrict__ q_idx,
