@@ -46,6 +46,8 @@ def parse():
     p.add_argument('--batch', type=int, default=64)
     p.add_argument('--no-graph', action='store_true', help='eager launches (no hipGraph)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-duke', action='store_true',
+                   help='skip the Duke configuration leg (configs[2], rank 0 at N = 1)')
     p.add_argument('--no-e2e', action='store_true',
                    help='skip the end-to-end JPEG-files stage (e2e block of the line)')
     p.add_argument('--e2e-images', type=int, default=Q_MARKET + G_MARKET)
@@ -910,6 +912,15 @@ def main():
                                         '(pps_distmat_x3p_tiled)'
                                         if ret['distmat_qplanes'] else '')),
     }
+    if rank == 0 and world == 1 and not args.no_duke:
+        # BASELINE configs[2] (Duke sizes, cosine + k-reciprocal re-ranking),
+        # timed after the headline workload: distance / re-ranking / rank
+        # stages and their rooflines (scripts/bench_duke_rerank.py)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), 'scripts'))
+        from bench_duke_rerank import run_duke
+        torch.cuda.empty_cache()
+        out['config_duke'] = run_duke(reps=3)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(blobs)
     if rank == 0:

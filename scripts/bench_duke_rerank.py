@@ -19,10 +19,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 Q, G, D = 2228, 17661, 3968
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--reps', type=int, default=3)
-    a = ap.parse_args()
+def run_duke(reps=3):
+    """The Duke configuration's timings and rooflines as one dict (bench.py
+    adds it to its line as `config_duke`)."""
     from pps_amd import ops
     from pps_amd import reid_dataset_evaluator as gev
     rng = np.random.RandomState(0)
@@ -50,7 +49,7 @@ def main():
 
     times = {}
     x = torch.cat([qf, gf]).contiguous()   # the evaluator's [queries; gallery] rows
-    for rep in range(a.reps + 1):
+    for rep in range(reps + 1):
         e = [ev() for _ in range(4)]
         e[0].record()
         # as reid_dataset_evaluator.evaluate runs it with REID.RERANK: one
@@ -116,7 +115,14 @@ def main():
                mAP_reranked=round(mAP, 6), cmc1_reranked=round(float(cmc[0]), 6),
                gallery_pairs_GB=round((Q + G) ** 2 * 4 / 1e9, 2), roofline_rerank=roof_rr, roofline_selfdist=roof_sd,
                rerank_inputs='blocks of one mirrored [N, N] self-distance (PPS_RERANK_WHOLE)')
-    print(json.dumps(out), flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reps', type=int, default=3)
+    a = ap.parse_args()
+    print(json.dumps(run_duke(a.reps)), flush=True)
 
 
 if __name__ == '__main__':
