@@ -473,6 +473,24 @@ def test_cmc_single_gallery_shot_vs_oracle(Q, G, n_ids, seed):
             np.testing.assert_array_equal(got[0], want[0])
 
 
+def test_cmc_single_gallery_shot_many_identities():
+    """Thousands of gallery identities (the groups kernel's LDS holds two
+    ints per identity: ~80 KB here) vs the oracle, one mode."""
+    from pps_amd import reid_dataset_evaluator as gev
+    rng = np.random.RandomState(7)
+    Q, G, n_ids = 3, 12000, 5000
+    d = rng.rand(Q, G).astype(np.float32)
+    gid = rng.randint(0, n_ids, size=G)
+    qid = gid[rng.randint(0, G, size=Q)]
+    qcam = rng.randint(1, 4, size=Q)
+    gcam = rng.randint(1, 4, size=G)
+    kw = dict(topk=100, single_gallery_shot=True, average=False)
+    want = ev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(3), **kw)
+    got = gev.cmc(d, qid, gid, qcam, gcam, rng=np.random.RandomState(3), **kw)
+    np.testing.assert_array_equal(got[1], want[1])
+    np.testing.assert_array_equal(got[0], want[0])
+
+
 def test_cmc_counts_sharded_equal_unsharded(golden):
     """pps_cmc_counts is additive over gallery shards (global indices)."""
     from pps_amd import ops
