@@ -402,7 +402,10 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
                        int32_t* __restrict__ q_idx, float* __restrict__ q_val,
                        int32_t* __restrict__ q_cnt, int32_t* __restrict__ col_cnt,
                        int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_n) {
-  __shared__ unsigned long long key[kQeSmall];  // (column << 32) | (t << 16) | slot
+  // the merged row: kcol[pos] / val[pos] at each entry's final position
+  // (column, then row order t); 4-byte columns keep the block at ~8 KB of
+  // LDS, so ~19 rows per CU are in flight
+  __shared__ int32_t kcol[kQeSmall];
   __shared__ float val[kQeSmall];
   __shared__ int32_t lc[kQeSmall];
   __shared__ int s_off[65], s_row[64];
@@ -452,24 +455,22 @@ rerank_vqe_wave_kernel(int64_t N, const int32_t* __restrict__ rank, int K1, int 
       }
       pos += lo - s_off[t2];
     }
-    key[pos] = ((unsigned long long)(uint32_t)c << 32) | ((unsigned long long)t << 16) |
-               (unsigned)pos;
+    kcol[pos] = c;
     val[pos] = v_val[(int64_t)s_row[t] * vcap + (e - s_off[t])];
   }
   __syncthreads();
-  // a column's entries are consecutive in key order; the lane at a segment's
+  // a column's entries are consecutive in merged order; the lane at a segment's
   // first entry sums it left to right (row order t) and writes output slot =
   // the number of segment starts before it
   int u = 0;
   for (int b0 = 0; b0 < n; b0 += 64) {
     const int e = b0 + lane;
-    const uint32_t col = e < n ? (uint32_t)(key[e] >> 32) : 0u;
-    const bool st = e < n && (e == 0 || (uint32_t)(key[e - 1] >> 32) != col);
+    const int32_t col = e < n ? kcol[e] : 0;
+    const bool st = e < n && (e == 0 || kcol[e - 1] != col);
     const unsigned long long sb = __ballot(st);
     if (st) {
-      float sum = val[key[e] & 0xffff];
-      for (int f = e + 1; f < n && (uint32_t)(key[f] >> 32) == col; ++f)
-        sum += val[key[f] & 0xffff];
+      float sum = val[e];
+      for (int f = e + 1; f < n && kcol[f] == col; ++f) sum += val[f];
       const int slot = u + __popcll(sb & below);
       if (slot < qcap) {
         const float qv = sum / (float)k2;
