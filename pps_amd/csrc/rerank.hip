@@ -389,7 +389,7 @@ rerank_v_rows_kernel(const float* __restrict__ od, int64_t N, int64_t ldo,
 
 // ---- 4) V_qe rows: mean of k2 sparse rows (row order = initial_rank order) ----
 constexpr int kQeCap = 4096;
-constexpr int kQeSmall = 640;   // rows with <= this many concatenated entries: one wave
+constexpr int kQeSmall = 512;   // rows with <= this many concatenated entries: one wave
 
 // One wave per row whose k2 V rows hold <= kQeSmall entries together (the
 // common case; 10 KB of LDS, so many rows per CU are in flight).  Same merge
