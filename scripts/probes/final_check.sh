@@ -12,3 +12,5 @@ timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.
 tail -1 $OUT/bench.log | cut -c1-300
 timeout -k 10 300 python scripts/bench_duke_rerank.py > $OUT/duke.log 2>&1 || { tail -5 $OUT/duke.log; exit 1; }
 tail -1 $OUT/duke.log | cut -c1-200
+bash scripts/probes/bench_n2_rehearsal.sh > $OUT/n2.log 2>&1 || { tail -5 $OUT/n2.log; exit 1; }
+tail -1 $OUT/bench_n2_gloo.log | cut -c1-200
