@@ -450,20 +450,34 @@ __global__ void split_sqnorm_kernel(const float* __restrict__ x, int64_t rows, i
   unsigned short* o = TILED ? out3 + (row >> 4) * 16 * (int64_t)D + (row & 15) * 32
                             : out3 + row * (int64_t)D;
   float s = 0.f;
-  for (int k = lane * 4; k < D; k += 256) {
-    const f32x4 v = real ? *reinterpret_cast<const f32x4*>(r + k) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    s = __builtin_fmaf(v[0], v[0], s);
-    s = __builtin_fmaf(v[1], v[1], s);
-    s = __builtin_fmaf(v[2], v[2], s);
-    s = __builtin_fmaf(v[3], v[3], s);
-    u32x2 hi, mid, lo;
-    unsigned a, m, l;
-    split2(v[0], v[1], a, m, l); hi[0] = a; mid[0] = m; lo[0] = l;
-    split2(v[2], v[3], a, m, l); hi[1] = a; mid[1] = m; lo[1] = l;
-    const int64_t ko = TILED ? (int64_t)(k >> 5) * 512 + (k & 31) : k;
-    *reinterpret_cast<u32x2*>(o + ko) = hi;
-    *reinterpret_cast<u32x2*>(o + plane + ko) = mid;
-    *reinterpret_cast<u32x2*>(o + 2 * plane + ko) = lo;
+  // kSplitU row segments of 256 per trip: their loads issue together (one
+  // memory latency per trip, not per segment); the norm still accumulates
+  // segment after segment, row_sqnorm_kernel's order
+  constexpr int kSplitU = 4;
+  for (int k0 = lane * 4; k0 < D; k0 += 256 * kSplitU) {
+    f32x4 v[kSplitU];
+#pragma unroll
+    for (int u = 0; u < kSplitU; ++u) {
+      const int k = k0 + 256 * u;
+      v[u] = real && k < D ? *reinterpret_cast<const f32x4*>(r + k) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kSplitU; ++u) {
+      const int k = k0 + 256 * u;
+      if (k >= D) break;
+      s = __builtin_fmaf(v[u][0], v[u][0], s);
+      s = __builtin_fmaf(v[u][1], v[u][1], s);
+      s = __builtin_fmaf(v[u][2], v[u][2], s);
+      s = __builtin_fmaf(v[u][3], v[u][3], s);
+      u32x2 hi, mid, lo;
+      unsigned a, m, l;
+      split2(v[u][0], v[u][1], a, m, l); hi[0] = a; mid[0] = m; lo[0] = l;
+      split2(v[u][2], v[u][3], a, m, l); hi[1] = a; mid[1] = m; lo[1] = l;
+      const int64_t ko = TILED ? (int64_t)(k >> 5) * 512 + (k & 31) : k;
+      *reinterpret_cast<u32x2*>(o + ko) = hi;
+      *reinterpret_cast<u32x2*>(o + plane + ko) = mid;
+      *reinterpret_cast<u32x2*>(o + 2 * plane + ko) = lo;
+    }
   }
 #pragma unroll
   for (int o2 = 32; o2 >= 1; o2 >>= 1) s += __shfl_xor(s, o2);
