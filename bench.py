@@ -31,9 +31,17 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA
 PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # bf16 MFMA = 16x the f32 rate (~2.5 PF)
 # bf16x3 path: every f32 product costs 6 bf16 MFMA terms -> its own MFMA roof
 PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+# f16x2 distance path (csrc/gemm_h2.hip): 3 f16 MFMA terms per f32-level
+# product (f16 MFMA: the bf16 rate) -> its roof in f32-equivalent TFLOP/s
+PEAK_H2_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
 TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r04', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
+
+
+def ops_dist_math():
+    from pps_amd import ops
+    return ops.dist_math()
 
 
 def parse():
@@ -134,16 +142,25 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
         # gallery index and query planes prepared once: the tiles compete on the
         # GEMM alone (what roofline_distmat times)
-        gidx = ops.GalleryIndex(g_local, tiled=D_FEAT % 32 == 0)
-        qt, qsq = ops.split_sqnorm_tiled(qa) if D_FEAT % 32 == 0 else (None, None)
+        h2 = ops.dist_math() == 'h2' and D_FEAT % 32 == 0
+        if h2:   # f16x2 split of both operands; the h2 tiles compete
+            gidx = ops.GalleryIndex(g_local, math='h2')
+            q2, qrs, qsq = ops.split_h2_tiled(qa)
+            qt = None
+            cands = [(t, False) for t in range(1, ops.h2_num_tiles())]
+        else:
+            gidx = ops.GalleryIndex(g_local, tiled=D_FEAT % 32 == 0, math='x3')
+            qt, qsq = ops.split_sqnorm_tiled(qa) if D_FEAT % 32 == 0 else (None, None)
+            # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
+            cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
+            if ops.dist_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
+                cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)]
         dout = ops.dist_buffer(Q_MARKET, g_local.shape[0], 'cuda')
-        # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
-        cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
-        if ops.default_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
-            cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)]
 
         def launch_dist(t, qp):
-            if qp:
+            if h2:
+                ops.distmat_h2(q2, qrs, qsq, gidx, dout, tile=t)
+            elif qp:
                 ops.distmat_planes(None, qsq, gidx, dout, tile=t, q_tiled=qt, Q=Q_MARKET,
                                    D=D_FEAT)
             else:
@@ -200,21 +217,28 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
 
 
 def distmat_roofline(q_local, g_local, world, reps=10):
-    """The distance GEMM launch alone (gemm_x3p_kernel EPI_DIST on the bench's
-    tile), the way a gallery index is used: gallery planes + norms prepared
-    once (GalleryIndex), queries split once; `reps` launches between HIP
-    events on the kernel's stream.  Algorithmic work 2 Q G_r D FLOP."""
+    """The distance GEMM launch alone (gemm_h2_kernel, or gemm_x3p_kernel
+    EPI_DIST, on the bench's tile), the way a gallery index is used: gallery
+    split + norms prepared once (GalleryIndex), queries split once; `reps`
+    launches between HIP events on the kernel's stream.  Algorithmic work
+    2 Q G_r D FLOP, priced against the MFMA roof of the arithmetic the kernel
+    runs (h2: 3 f16 terms per product; x3: 6 bf16 terms)."""
     from pps_amd import ops
     from pps_amd import distributed as pdist
     be = pdist.HipBackend
-    if ops.default_math() != 'x3':
+    dm = ops.dist_math()
+    if dm == 'f32':
         return None
     q_all = pdist.all_gather_rows(q_local, [q_local.shape[0]] * world) if world > 1 else q_local
-    idx = ops.GalleryIndex(g_local)
     Q, D = q_all.shape
+    h2 = dm == 'h2' and D % 32 == 0
+    idx = ops.GalleryIndex(g_local, math='h2' if h2 else 'x3')
     out = ops.dist_buffer(Q, g_local.shape[0], q_all.device)
     qp = bool(be.distmat_qplanes)
-    if qp:
+    if h2:
+        q2, qrs, qsq = ops.split_h2_tiled(q_all)
+        launch = lambda: ops.distmat_h2(q2, qrs, qsq, idx, out, tile=be.distmat_tile)
+    elif qp:
         q3, qsq = ops.split_sqnorm(q_all)
         q3t = ops.tile_planes(q3) if D % 32 == 0 else None
         launch = lambda: ops.distmat_planes(q3, qsq, idx, out, tile=be.distmat_tile, q_tiled=q3t)
@@ -231,12 +255,16 @@ def distmat_roofline(q_local, g_local, world, reps=10):
     us = e0.elapsed_time(e1) * 1e3 / reps
     G = g_local.shape[0]
     flops = 2.0 * Q * G * D
-    byt = (Q + G) * D * 6 + Q * G * 4   # the bf16x3 operand planes read once + the matrix
+    # the operand planes read once + the matrix written once
+    byt = (Q + G) * D * (4 if h2 else 6) + Q * G * 4
     tf = flops / (us * 1e-6) / 1e12
-    return dict(achieved=round(tf, 2), frac=round(tf / PEAK_X3_TFLOPS, 4),
+    peak = PEAK_H2_TFLOPS if h2 else PEAK_X3_TFLOPS
+    return dict(achieved=round(tf, 2), peak=round(peak, 1), frac=round(tf / peak, 4),
+                frac_of_x3_roof=round(tf / PEAK_X3_TFLOPS, 4),
+                math='h2' if h2 else 'x3',
                 avg_launch_us=round(us, 2), flops_per_launch=flops,
-                operand_and_output_bytes_per_launch=byt, queries_as_planes=bool(qp),
-                timing='%d launches between HIP events, gallery index and query planes '
+                operand_and_output_bytes_per_launch=byt, queries_as_planes=bool(qp or h2),
+                timing='%d launches between HIP events, gallery index and query split '
                        'prepared once' % reps)
 
 
@@ -782,6 +810,9 @@ def main():
             saved = json.load(f)
         pdist.HipBackend.distmat_tile = int(saved.get('__distmat__', 0))
         pdist.HipBackend.distmat_qplanes = bool(saved.get('__distmat_qplanes__', False))
+        # a table tuned for another distance arithmetic: its tile id means nothing here
+        if saved.get('__distmat_math__', 'x3') != ops_dist_math():
+            pdist.HipBackend.distmat_tile, pdist.HipBackend.distmat_qplanes = 0, False
     # per-layer tile / plane choice on this device, outside the timed region
     # (PPS_AUTOTUNE_SPLITK=1: also try conv split-K)
     nm, blobs, imgs, xbuf = build_bench_model(
@@ -854,6 +885,7 @@ def main():
         with open(args.tiles_file, 'w') as f:
             json.dump(dict(nm.tiles(), __distmat__=ret['distmat_tile'],
                            __distmat_qplanes__=ret['distmat_qplanes'],
+                           __distmat_math__=ops_dist_math(),
                            __planes__=nm.planes(), __splitk__=nm.splitks()), f, indent=0)
     e2e = None
     if not args.no_e2e:
@@ -861,7 +893,9 @@ def main():
     dist_bytes = (Q_MARKET + ret['G_local']) * D_FEAT * 4 + Q_MARKET * ret['G_local'] * 4
     dist_flops = 2.0 * Q_MARKET * ret['G_local'] * D_FEAT
     dist_tflops = dist_flops / (ret['distmat_ms'] * 1e-3) / 1e12
-    dist_math = ops.default_math()
+    dist_math = ops.dist_math()
+    dist_peak = {'h2': PEAK_H2_TFLOPS, 'x3': PEAK_X3_TFLOPS}.get(dist_math, PEAK_FP32_MFMA_TFLOPS)
+    droof = ret['dist_roofline'] or {}
     # whole-job distmat GB/s: all ranks' shards / the slowest rank's time
     dist_ms_max = pdist.max_over_ranks(ret['distmat_ms'], world)
     total_bytes = (Q_MARKET + G_MARKET) * D_FEAT * 4 + Q_MARKET * G_MARKET * 4
@@ -892,25 +926,29 @@ def main():
         'roofline_argsort': ret['argsort_roofline'],
         'roofline_distmat': dict(
             bound='mfma',
-            achieved=(ret['dist_roofline'] or {}).get('achieved', round(dist_tflops, 2)),
-            peak=round(PEAK_X3_TFLOPS if dist_math == 'x3' else PEAK_FP32_MFMA_TFLOPS, 1),
+            achieved=droof.get('achieved', round(dist_tflops, 2)),
+            peak=droof.get('peak', round(dist_peak, 1)),
             unit='TFLOP/s',
-            frac=(ret['dist_roofline'] or {}).get(
-                'frac', round(dist_tflops / (PEAK_X3_TFLOPS if dist_math == 'x3'
-                                             else PEAK_FP32_MFMA_TFLOPS), 4)),
-            avg_launch_us=(ret['dist_roofline'] or {}).get('avg_launch_us'),
+            frac=droof.get('frac', round(dist_tflops / dist_peak, 4)),
+            frac_of_x3_roof=droof.get('frac_of_x3_roof'),
+            math=dist_math,
+            peak_note=('f32-equivalent TFLOP/s: dense f16 MFMA rate / 3 terms per product '
+                       '(h2); / 6 bf16 terms (x3); exact f32 MFMA rate (f32)'),
+            avg_launch_us=droof.get('avg_launch_us'),
             with_index_prep=dict(ms=round(ret['distmat_ms'], 3), TFLOPs=round(dist_tflops, 2),
                                  note='gallery shard split + norms + query gather + GEMM, '
                                       'as retrieval_ms runs it'),
             hbm_GBps=round(dist_bytes / (ret['distmat_ms'] * 1e-3) / 1e9, 2),
             traffic=_pmc_traffic('distmat', dist_math, Q_MARKET),
             algorithmic_bytes_per_launch=dist_bytes,
-            timing=(ret['dist_roofline'] or {}).get('timing'),
-            kernel='%s EPI_DIST, tile %d' % (
-                'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
-                ret['distmat_tile']) + (', queries and gallery as chunk-tiled bf16x3 planes '
-                                        '(pps_distmat_x3p_tiled)'
-                                        if ret['distmat_qplanes'] else '')),
+            timing=droof.get('timing'),
+            kernel=('gemm_h2_kernel (f16x2, pps_distmat_h2_tiled), tile %d' % ret['distmat_tile']
+                    if dist_math == 'h2' else
+                    '%s EPI_DIST, tile %d' % (
+                        'gemm_x3p_kernel' if dist_math == 'x3' else 'gemm_f32_kernel',
+                        ret['distmat_tile']) + (
+                        ', queries and gallery as chunk-tiled bf16x3 planes '
+                        '(pps_distmat_x3p_tiled)' if ret['distmat_qplanes'] else ''))),
     }
     if rank == 0 and world == 1 and not args.no_duke:
         # BASELINE configs[2] (Duke sizes, cosine + k-reciprocal re-ranking),

@@ -162,6 +162,35 @@ int pps_distmat_x3_self(const float* x, int64_t N, int64_t ld, const float* xsq,
  * pps_distmat_x3_self on the same tile. */
 int pps_distmat_x3_self_tiled(const uint16_t* x3t, int64_t N, const float* xsq, int D,
                               int metric, float* out, int64_t ldo, int tile, void* stream);
+
+/* ---- f16x2 distance GEMM ("h2", round 5) -----------------------------------
+ * The same distances as pps_distmat_x3p_tiled / pps_distmat_x3_self_tiled in
+ * THREE f16 MFMA terms per product instead of six bf16 ones.  Each row x is
+ * scaled by a power of two 2^s (per row: max|x 2^s| in [2^14, 2^15)) and
+ * split x 2^s = h0 + h1 + r, h0 = f16(x 2^s), h1 = f16(x 2^s - h0),
+ * |r| <= 2^-22 |x 2^s|; q.g = 2^-(s_q + s_g) (h0.h0' + h0.h1' + h1.h0') with
+ * f32 accumulation (csrc/gemm_h2.hip states the error bound).  Same metric
+ * formulas and squared norms as the x3 path.
+ *
+ * pps_split_f16x2_sqnorm_tiled: one read of x [rows][ld] -> out2t, the two
+ * f16 planes chunk-tiled [2][rows16/16][D/32][16][32] (rows16 = rows rounded
+ * up to 16, padding rows zero; 2 * rows16 * D f16), rscale[r] = 2^-s_r and
+ * sqnorm[r] = pps_row_sqnorm's value (same bits).  D % 32 == 0. */
+int pps_split_f16x2_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld,
+                                 uint16_t* out2t, float* rscale, float* sqnorm, void* stream);
+/* Query x gallery distances from two such splits.  tile: 0 = default
+ * (256 x 256, 8 waves), 1..pps_h2_num_tiles()-1 the alternatives listed in
+ * csrc/gemm_h2.hip (speed only: every tile gives the same bits). */
+int pps_distmat_h2_tiled(const uint16_t* q2t, int64_t Q, const float* qsq, const float* qrs,
+                         const uint16_t* g2t, const float* gsq, const float* grs, int64_t G,
+                         int D, int metric, float* out, int64_t ldo, int tile, void* stream);
+/* Self-distance of one split (upper-triangle tiles + mirror: an exactly
+ * symmetric matrix whose upper triangle has the bits of pps_distmat_h2_tiled
+ * on the same operands). */
+int pps_distmat_h2_self_tiled(const uint16_t* x2t, int64_t N, const float* xsq, const float* xrs,
+                              int D, int metric, float* out, int64_t ldo, int tile,
+                              void* stream);
+int pps_h2_num_tiles(void);
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
  * The diagonal is exactly 0 as in the reference's difference form. */

@@ -37,6 +37,11 @@ SIGNATURES = {
                             c_int, c_ptr],
     'pps_distmat_x3_self_tiled': [c_ptr, c_i64, c_ptr, c_int, c_int, c_ptr, c_i64, c_int,
                                   c_ptr],
+    'pps_split_f16x2_sqnorm_tiled': [c_ptr, c_i64, c_int, c_i64, c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_distmat_h2_tiled': [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_int,
+                             c_int, c_ptr, c_i64, c_int, c_ptr],
+    'pps_distmat_h2_self_tiled': [c_ptr, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_i64, c_int,
+                                  c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
@@ -148,6 +153,7 @@ SIGNATURES = {
 EXTRA = {
     'pps_abi_version': ([], ctypes.c_int),
     'pps_gemm_num_tiles': ([], ctypes.c_int),
+    'pps_h2_num_tiles': ([], ctypes.c_int),
     'pps_rank_cells': ([], ctypes.c_int),
     'pps_argsort_rows_cap': ([], ctypes.c_int),
     'pps_stem_k': ([], ctypes.c_int),

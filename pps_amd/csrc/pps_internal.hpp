@@ -198,6 +198,10 @@ struct GemmParams {
   float* part;
   int64_t part_sstride;
   int* fix_cnt;
+  // f16x2 distance GEMM (gemm_h2.hip): per-row power-of-two inverse scales of
+  // the A / B rows (the split stores x * 2^s, the dot product is scaled back)
+  const float* rs_a;
+  const float* rs_b;
 };
 constexpr int kPpsFuseMaxStrips = 10;
 constexpr int kPpsFuseMaxCols = 256;  // widest tile the fused pooling takes (two column passes)
@@ -221,6 +225,12 @@ bool x3c_eligible(const GemmParams& p, int epi, int batch, int tile);
 int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
 int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
 int x3c_tile_cols(int tile);
+
+// ---- f16x2 distance GEMM (gemm_h2.hip) ---------------------------------------
+constexpr int kH2NumTiles = 6;
+int launch_gemm_h2(const GemmParams& p, hipStream_t stream, int tile);
+int split_h2_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out2t,
+                          float* rscale, float* sqnorm, hipStream_t stream);
 
 // ---- bottleneck seam (gemm_seam.hip): branch2c of block i + branch2a of block i+1
 struct SeamParams {

@@ -144,13 +144,15 @@ def broadcast_object(obj, world, src=0):
 class HipBackend(object):
     """libpps_hip.so kernels (the product path)."""
     device = 'cuda'
-    distmat_tile = 0   # GEMM tile for the distance matrix (0 = heuristic; bench tunes it)
-    distmat_qplanes = False  # queries pre-split into bf16x3 planes (ops.compute_dist)
+    distmat_math = None   # distance arithmetic (None = ops.dist_math(): 'h2' by default)
+    distmat_tile = 0   # GEMM tile of that arithmetic (0 = default; bench tunes it)
+    distmat_qplanes = False  # x3: queries pre-split into bf16x3 planes (ops.compute_dist)
 
     @classmethod
     def distmat(cls, q, g, metric):
         return ops.compute_dist(q, g, metric=metric, tile=cls.distmat_tile,
-                                q_planes=cls.distmat_qplanes, pad_rows=True)
+                                q_planes=cls.distmat_qplanes, pad_rows=True,
+                                math=cls.distmat_math)
 
     @staticmethod
     def prepare(ev):

@@ -83,6 +83,38 @@ def default_math():
     return m
 
 
+def dist_math():
+    """Arithmetic of the distance GEMMs (compute_dist and everything built on
+    it): 'h2' (default: f16x2, three f16 MFMA terms per product, f32-level
+    error -- csrc/gemm_h2.hip), 'x3' (six bf16 terms) or 'f32' (exact f32
+    MFMA), from PPS_DIST_MATH; PPS_MATH=f32 (exact f32 everywhere) also
+    selects 'f32' here."""
+    m = os.environ.get('PPS_DIST_MATH')
+    if m is None:
+        return 'f32' if default_math() == 'f32' else 'h2'
+    if m not in ('h2', 'x3', 'f32'):
+        raise ValueError('PPS_DIST_MATH must be h2, x3 or f32, got %r' % m)
+    return m
+
+
+def h2_num_tiles():
+    return int(_lib.lib().pps_h2_num_tiles())
+
+
+def split_h2_tiled(x):
+    """f16x2 split of a [R, D] tensor (D % 32 == 0) for the h2 distance GEMM,
+    one read of x: -> (planes, rscale, sqnorm) with planes the two f16 planes
+    chunk-tiled as an int16 [2, R16, D] tensor, rscale [R] the per-row
+    power-of-two inverse scales, sqnorm [R] = row_sqnorm(x) (same bits)."""
+    R, D = x.shape
+    r16 = (R + 15) // 16 * 16
+    planes = torch.empty((2, r16, D), dtype=torch.int16, device=x.device)
+    rs = torch.empty((R,), dtype=torch.float32, device=x.device)
+    sq = torch.empty((R,), dtype=torch.float32, device=x.device)
+    call('pps_split_f16x2_sqnorm_tiled', _dev(x, 'x'), R, D, D, _dev(planes, 'out2t', torch.int16), _dev(rs, 'rscale'), _dev(sq, 'sqnorm'), _stream())
+    return planes, rs, sq
+
+
 def row_sqnorm(x):
     """Squared L2 norm of every row of a [R, D] tensor (fixed summation order)."""
     R, D = x.shape
@@ -115,18 +147,29 @@ def split_sqnorm_tiled(x):
 
 
 class GalleryIndex(object):
-    """A gallery prepared once for the bf16x3 distance GEMM: features split
-    into three bf16 planes + squared norms; score any number of query
-    batches against it with compute_dist(q, index).  tiled=True prepares the
-    planes in the chunk-tiled layout the query-planes GEMM streams (one pass;
-    the row-major planes are then split on first use)."""
+    """A gallery prepared once for the distance GEMM; score any number of
+    query batches against it with compute_dist(q, index).  math 'h2' (the
+    dist_math() default when D % 32 == 0): the f16x2 split (split_h2_tiled:
+    two chunk-tiled f16 planes, per-row scales, squared norms); 'x3': the
+    features split into three bf16 planes + squared norms, tiled=True in the
+    chunk-tiled layout the query-planes GEMM streams (one pass; the row-major
+    planes are then split on first use)."""
 
-    def __init__(self, g, tiled=False):
+    def __init__(self, g, tiled=False, math=None):
         if g.dim() != 2:
             raise RuntimeError('gallery must be [G, D], got %s' % (tuple(g.shape),))
         self.feats = g
-        self._planes = self._tiled = None
-        if tiled and g.is_contiguous() and g.shape[1] % 32 == 0:
+        self._planes = self._tiled = self.h2 = None
+        math = math or dist_math()
+        if math == 'f32':
+            math = 'x3'   # an index is a split; f32 distances take the features as they are
+        if math == 'h2' and not (g.is_contiguous() and g.shape[1] % 32 == 0):
+            math = 'x3'   # the f16x2 kernel needs D % 32 == 0 (chunk-tiled planes)
+        self.math = math
+        if math == 'h2':
+            self.h2 = split_h2_tiled(g)   # (planes, rscale, sqnorm)
+            self.sqnorm = self.h2[2]
+        elif tiled and g.is_contiguous() and g.shape[1] % 32 == 0:
             self._tiled, self.sqnorm = split_sqnorm_tiled(g)
         elif g.is_contiguous() and g.shape[1] % 4 == 0:
             self._planes, self.sqnorm = split_sqnorm(g)
@@ -169,7 +212,10 @@ def dist_buffer(Q, G, device):
 def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes=None,
                  symmetric=None, pad_rows=False):
     """[Q,D] x [G,D] -> [Q,G] distance matrix (reid_dataset_evaluator.py:244).
-    g may be a GalleryIndex (then the x3 kernel runs on its prepared planes).
+    math: 'h2' / 'x3' / 'f32' (None = dist_math(), or the GalleryIndex's own).
+    g may be a GalleryIndex (then the GEMM runs on its prepared split).
+    h2: queries split by split_h2_tiled, pps_distmat_h2_tiled (tile = h2 tile
+    id, 0 = default); D % 32 != 0 runs x3.
     q_planes (x3): also split the queries into bf16x3 planes first so the
     pipelined GEMM stages both operands by DMA (pps_distmat_x3p; pipelined
     tiles only).  Same bits either way; measured at the Market shape it is
@@ -177,11 +223,14 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     so None = off.
     pad_rows: return a [Q, G] view of a buffer with 16-byte-aligned rows
     (dist_buffer) instead of a dense matrix.
-    symmetric (x3): a self-distance (q and g the same rows, e.g.
+    symmetric (h2, x3): a self-distance (q and g the same rows, e.g.
     compute_dist(g, g) of re-ranking) computed from the upper-triangle tiles
-    and mirrored (pps_distmat_x3_self, half the work); None = whenever q IS
-    g's data, D % 32 == 0 and the tile is a square one (SELF_TILES)."""
-    math = 'x3' if isinstance(g, GalleryIndex) else (math or default_math())
+    and mirrored (pps_distmat_h2_self_tiled / pps_distmat_x3_self, half the
+    work); None = whenever q IS g's data, D % 32 == 0 and (x3) the tile is a
+    square one (SELF_TILES)."""
+    if isinstance(g, GalleryIndex):
+        math = g.math
+    math = math or dist_math()
     if q.dim() != 2 or len(g.shape) != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
                            % (tuple(q.shape), tuple(g.shape)))
@@ -196,15 +245,33 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     # never carries a stale True from an earlier self-distance
     out._pps_symmetric = False
     if math == 'f32':
-        call('pps_distmat', _dev(q, 'q'), Q, D, _dev(g, 'g'), G, D, D, METRICS[metric],
+        gf = g.feats if isinstance(g, GalleryIndex) else g
+        call('pps_distmat', _dev(q, 'q'), Q, D, _dev(gf, 'g'), G, D, D, METRICS[metric],
              _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         return out
-    tiled = bool(q_planes) and D % 32 == 0 and (tile == 0 or tile >= TILE_P_FIRST)
     f = g.feats if isinstance(g, GalleryIndex) else g
+    same = (f.data_ptr() == q.data_ptr() and tuple(f.shape) == tuple(q.shape) and
+            f.stride() == q.stride() and q.is_contiguous() and D % 32 == 0)
+    if math == 'h2' and D % 32 == 0 and q.is_contiguous():
+        if symmetric is None:
+            symmetric = same
+        if symmetric:
+            x2, xrs, xsq = g.h2 if isinstance(g, GalleryIndex) and g.h2 is not None else \
+                split_h2_tiled(q)
+            call('pps_distmat_h2_self_tiled', _dev(x2, 'x2t', torch.int16), Q, _dev(xsq, 'xsq'),
+                 _dev(xrs, 'xrs'), D, METRICS[metric], _dev_rows(out, 'out'), _ld(out),
+                 int(tile), _stream())
+            out._pps_symmetric = True   # mirrored tiles: exactly symmetric
+            return out
+        idx = g if isinstance(g, GalleryIndex) and g.h2 is not None else \
+            GalleryIndex(f, math='h2')
+        q2, qrs, qsq = split_h2_tiled(q)
+        return distmat_h2(q2, qrs, qsq, idx, out, metric, tile, Q=Q)
+    if math == 'h2':
+        math, tile = 'x3', 0   # D % 32 != 0 (or strided queries): the bf16x3 kernels
+    tiled = bool(q_planes) and D % 32 == 0 and (tile == 0 or tile >= TILE_P_FIRST)
     if symmetric is None:
-        symmetric = (f.data_ptr() == q.data_ptr() and tuple(f.shape) == tuple(q.shape) and
-                     f.stride() == q.stride() and q.is_contiguous() and D % 32 == 0 and
-                     tile in SELF_TILES)
+        symmetric = same and tile in SELF_TILES
     if symmetric:
         # one read of x -> chunk-tiled planes + norms; both operands staged
         # from that copy by DMA (pps_distmat_x3_self_tiled)
@@ -216,7 +283,7 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
              D, METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
         out._pps_symmetric = True   # mirrored tiles: exactly symmetric (re_ranking uses it)
         return out
-    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g, tiled=tiled)
+    idx = g if isinstance(g, GalleryIndex) else GalleryIndex(g, tiled=tiled, math='x3')
     if q_planes:
         if tiled and q.is_contiguous():  # both operands chunk-tiled, queries in one pass
             qt, qsq = split_sqnorm_tiled(q)
@@ -227,6 +294,19 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     call('pps_distmat_x3', _dev(q, 'q'), Q, D, _dev(qsq, 'qsq'),
          _dev(idx.planes, 'g3', torch.int16), _dev(idx.sqnorm, 'gsq'), G, D, D,
          METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
+    return out
+
+
+def distmat_h2(q2, qrs, qsq, idx, out, metric='euclidean', tile=0, Q=None):
+    """The h2 distance GEMM alone on queries already split (split_h2_tiled)
+    against an h2 GalleryIndex: what compute_dist(math='h2') launches after
+    the split (pps_distmat_h2_tiled)."""
+    Q = qsq.shape[0] if Q is None else Q
+    G, D = idx.shape
+    g2, grs, gsq = idx.h2
+    call('pps_distmat_h2_tiled', _dev(q2, 'q2t', torch.int16), Q, _dev(qsq, 'qsq'),
+         _dev(qrs, 'qrs'), _dev(g2, 'g2t', torch.int16), _dev(gsq, 'gsq'), _dev(grs, 'grs'), G,
+         D, METRICS[metric], _dev_rows(out, 'out'), _ld(out), int(tile), _stream())
     return out
 
 

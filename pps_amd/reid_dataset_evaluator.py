@@ -240,8 +240,8 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
         ap, valid, first = rank_eval(dist, q_ids, g_ids, q_cams, g_cams)
         return scores_from_ranks(ap, valid, first, topk=10)
 
-    tiled = ops.default_math() == 'x3' and feat.shape[1] % 32 == 0
-    # re-ranking on the x3 path: ONE mirrored self-distance of [queries;
+    tiled = ops.dist_math() in ('h2', 'x3') and feat.shape[1] % 32 == 0
+    # re-ranking on the h2 / x3 paths: ONE mirrored self-distance of [queries;
     # gallery] gives q_g, q_q and g_g as blocks of one exactly symmetric
     # matrix (re-ranking then reads q_g^T in place, PPS_RERANK_WHOLE)
     whole = bool(cfg.REID.RERANK) and tiled
@@ -254,8 +254,8 @@ def evaluate_arrays(all_feats, ids, cams, marks, verbose=True, metric=None):
     with measure_time('Computing distance...', verbose):
         if verbose:
             print('Array size: ', tuple(qf.shape), tuple(gf.shape))
-        # the gallery split into chunk-tiled bf16x3 planes once: q_g and the
-        # multi-query mq_g read it
+        # the gallery split once (h2: f16x2 planes; x3: chunk-tiled bf16x3
+        # planes): q_g and the multi-query mq_g read it
         gsrc = ops.GalleryIndex(gf, tiled=True) if tiled else gf
         if whole:
             _, q_g, q_q, g_g = ops.self_distance_blocks(x, len(qi), metric=metric)

@@ -3,7 +3,7 @@ G=15913, D=3968) on synthetic features of the SURVEY §8(d) distribution,
 held to the north_star bar ("bit-exact on rank indices and within 1e-4 on
 distances; mAP/Rank-1 equal to the CPU reference"):
 
-* distances: GPU (x3 and exact-f32 kernels) vs the oracle's NumPy
+* distances: GPU (h2, x3 and exact-f32 kernels) vs the oracle's NumPy
   restatement of compute_dist (reid_dataset_evaluator.py:244-272), <= 1e-4;
 * rank indices: the GPU's stable top-10 / top-100 (pps_topk on the GPU
   distances) vs the stable argsort of the oracle's distances
@@ -46,7 +46,7 @@ def market():
                 order=order)
 
 
-@pytest.mark.parametrize('math', ['x3', 'f32'])
+@pytest.mark.parametrize('math', ['h2', 'x3', 'f32'])
 def test_market_scale_parity(market, math):
     from pps_amd import ops
     from pps_amd import reid_dataset_evaluator as gev

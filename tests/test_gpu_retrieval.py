@@ -55,7 +55,7 @@ def test_gallery_index_matches_plain_x3():
     rng = np.random.RandomState(11)
     q = _cuda(rng.randn(70, 256).astype(np.float32))
     g = _cuda(rng.randn(300, 256).astype(np.float32))
-    idx = ops.GalleryIndex(g)
+    idx = ops.GalleryIndex(g, math='x3')
     a = ops.compute_dist(q, idx).cpu().numpy()
     b = ops.compute_dist(q, g, math='x3').cpu().numpy()
     np.testing.assert_array_equal(a, b)
@@ -92,12 +92,13 @@ def test_distmat_tiled_planes_bits(Q, G, D, metric):
     rng = np.random.RandomState(Q + G)
     q = _cuda(rng.randn(Q, D).astype(np.float32))
     g = _cuda(rng.randn(G, D).astype(np.float32))
-    idx = ops.GalleryIndex(g)
+    idx = ops.GalleryIndex(g, math='x3')
     q3, qsq = ops.split_sqnorm(q)
     tiles = [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1))
     outs = []
     for tile in tiles:
-        a = ops.compute_dist(q, g, metric=metric, tile=tile, q_planes=True, pad_rows=True)
+        a = ops.compute_dist(q, g, metric=metric, tile=tile, q_planes=True, pad_rows=True,
+                             math='x3')
         b = ops.dist_buffer(Q, G, 'cuda')
         ops.call('pps_distmat_x3p', ops._dev(q3, 'q3', torch.int16), Q, D, ops._dev(qsq, 'qsq'),
                  ops._dev(idx.planes, 'g3', torch.int16), ops._dev(idx.sqnorm, 'gsq'), G, D, D,
@@ -548,10 +549,11 @@ def test_topk_long_rows_wave_kernel(G, k):
 
 @pytest.mark.parametrize('case', ['market_small', 'full_dim'])
 def test_sharded_evaluator_tiled_query_planes(golden, case):
-    """The distance path bench.py tunes (queries and gallery as chunk-tiled
-    bf16x3 planes, pps_distmat_x3p_tiled) inside the evaluator equals the
-    default path: the same distance bits, the same mAP / CMC, and the mAP of
-    the reference's own evaluation."""
+    """The distance paths bench.py tunes inside the evaluator (h2 tiles;
+    x3 with queries and gallery as chunk-tiled bf16x3 planes,
+    pps_distmat_x3p_tiled): every tile of one arithmetic gives the same
+    distance bits, all are within 1e-5 of the default path, and every run
+    reproduces the mAP of the reference's own evaluation."""
     from pps_amd import distributed as pdist
     g = golden(case)
     if 'qid' not in g:
@@ -559,22 +561,25 @@ def test_sharded_evaluator_tiled_query_planes(golden, case):
     qf, gf = _cuda(g['qf']), _cuda(g['gf'])
     ev_ = pdist.ShardedEvaluator(g['qid'], g['qcam'], g['gid'], g['gcam'], 0, 1)
     be = pdist.HipBackend
-    saved = (be.distmat_tile, be.distmat_qplanes)
+    saved = (be.distmat_math, be.distmat_tile, be.distmat_qplanes)
     outs = []
+    runs = ((None, 0, False), ('x3', 52, True), ('x3', 47, True), ('h2', 1, False),
+            ('h2', 5, False))
     try:
-        for tile, qp in ((0, False), (52, True), (47, True)):
-            be.distmat_tile, be.distmat_qplanes = tile, qp
+        for math, tile, qp in runs:
+            be.distmat_math, be.distmat_tile, be.distmat_qplanes = math, tile, qp
             outs.append(ev_.run(qf, gf, keep_dist=True))
     finally:
-        be.distmat_tile, be.distmat_qplanes = saved
+        be.distmat_math, be.distmat_tile, be.distmat_qplanes = saved
     if g['qf'].shape[1] % 32 == 0:
         assert torch.equal(outs[1]['dist'], outs[2]['dist'])
+        assert torch.equal(outs[3]['dist'], outs[4]['dist'])
+        assert torch.equal(outs[0]['dist'], outs[3]['dist'])   # the default is h2
     for o in outs[1:]:
         np.testing.assert_allclose(o['dist'].cpu().numpy(), outs[0]['dist'].cpu().numpy(),
                                    rtol=0, atol=1e-5)
-        assert abs(o['mAP'] - outs[0]['mAP']) < 1e-9
-        np.testing.assert_array_equal(o['cmc'], outs[0]['cmc'])
-    assert abs(outs[1]['mAP'] - float(g['mAP'])) < 1e-6
+    for o in outs:
+        assert abs(o['mAP'] - float(g['mAP'])) < 1e-6
 
 
 def test_rank_prepare_beyond_lds_merge_cap():

@@ -276,7 +276,7 @@ def test_distmat_query_planes_same_bits(Q, G, D):
     rng = np.random.RandomState(Q + G)
     qn = rng.randn(Q, D).astype(np.float32)
     gn = rng.randn(G, D).astype(np.float32)
-    q, idx = _cuda(qn), ops.GalleryIndex(_cuda(gn))
+    q, idx = _cuda(qn), ops.GalleryIndex(_cuda(gn), math='x3')
     for tile in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
         want = ops.compute_dist(q, idx, q_planes=False,
                                 tile=tile or ops.TILE_P16_FIRST + 4).cpu().numpy()
@@ -299,9 +299,9 @@ def test_self_distance_symmetric(N, D, metric):
     x = _cuda(xn)
     ref = ev.compute_dist(xn, xn, metric) if metric == 'euclidean' else None
     for tile in ops.SELF_TILES:
-        d = ops.compute_dist(x, x, metric=metric, tile=tile).cpu().numpy()
+        d = ops.compute_dist(x, x, metric=metric, tile=tile, math='x3').cpu().numpy()
         full = ops.compute_dist(x, x, metric=metric, tile=tile or ops.TILE_P16_FIRST,
-                                symmetric=False).cpu().numpy()
+                                symmetric=False, math='x3').cpu().numpy()
         np.testing.assert_array_equal(d, d.T, err_msg='tile %d' % tile)
         iu = np.triu_indices(N)           # the upper triangle is the full product's
         np.testing.assert_array_equal(d[iu], full[iu], err_msg='tile %d' % tile)
