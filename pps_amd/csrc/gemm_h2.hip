@@ -212,7 +212,7 @@ __device__ inline void h2_dist_epilogue(const GemmParams& p, f32x4 (&acc)[BM / W
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int BK = 32;
@@ -220,16 +220,20 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int ABLK = BM / 16, BBLK = BN / 16;  // 16-row blocks per plane and chunk
   constexpr int NPIECE = 2 * (ABLK + BBLK);      // KiB DMA pieces per chunk
-  static_assert(NPIECE % NW == 0, "DMA pieces split evenly over the waves");
-  constexpr int PPW = NPIECE / NW;
+  // pieces per wave; uneven tiles give the last waves dummy pieces (zeros
+  // into a spare KiB after the stages) so every wave's wait counts are equal
+  constexpr int PPW = (NPIECE + NW - 1) / NW;
+  constexpr bool EVEN = NPIECE % NW == 0;
   constexpr int STAGE = NPIECE * 1024;
   static_assert(TM % 2 == 0 && TM >= 2 && TN >= 1, "wave tile");
-  static_assert(2 * STAGE <= 160 * 1024, "two LDS stages");
-  static_assert(PPW <= 63, "vmcnt range");
+  static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
+  static_assert(PPW * (NS - 1) <= 63, "vmcnt range");
   constexpr int HB = BM * (BN + 4) * 4 <= 160 * 1024 ? 1 : 2;
   constexpr int EPI_BYTES = BM * (BN / HB + 4) * 4;
   static_assert(EPI_BYTES <= 160 * 1024, "epilogue image");
-  constexpr int LDS_BYTES = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  constexpr int PIPE_BYTES = NS * STAGE + (EVEN ? 0 : 1024);
+  constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
+  static_assert(PIPE_BYTES <= 160 * 1024, "LDS stages");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
   const int lane = threadIdx.x & 63;
@@ -255,9 +259,11 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int q = wave * PPW + i;
-    int blk, nblk;
-    int64_t pbase;
-    if (q < 2 * ABLK) {
+    int blk = 0, nblk = 0;
+    int64_t pbase = 0;
+    if (q >= NPIECE) {
+      // dummy piece (uneven tiles): reads zeros
+    } else if (q < 2 * ABLK) {
       const int pl = q / ABLK;
       blk = m0 / 16 + (q - pl * ABLK);
       nblk = ablocks;
@@ -277,7 +283,10 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
-      glds16(q < 2 * ABLK ? ra : rb, st + q * 1024, src[i] + kc * 1024);
+      if (EVEN || q < NPIECE)
+        glds16(q < 2 * ABLK ? ra : rb, st + q * 1024, src[i] + kc * 1024);
+      else
+        glds16(rb, lds + NS * STAGE, (int)0x80000000);
     }
   };
 
@@ -305,13 +314,15 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  if (nkc > 1) {
-    issue(1, 1);
-    wait_vmcnt<PPW>();  // chunk 0 landed (chunk 1 may still be in flight)
-  } else {
-    wait_vmcnt<0>();
-  }
+  // Chunk c lives in stage c % NS.  The prologue requests chunks 0 .. NS-1;
+  // the barrier in chunk c's tail (every wave done reading stage c % NS, and
+  // chunk c + 1 landed: the NS - 2 younger chunks may stay in flight) is
+  // followed by the request of chunk c + NS into the stage just freed.
+  // Requests past the last chunk stay inside the operand buffers (or read
+  // zeros beyond them) and are never consumed: every wait count is uniform.
+#pragma unroll
+  for (int c = 0; c < NS; ++c) issue(c, c);
+  wait_vmcnt<PPW * (NS - 1)>();  // chunk 0 landed
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -322,8 +333,9 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // block, the barrier that retires this stage's reads and the next chunk's
   // DMA, the request two chunks ahead into this stage, and the next chunk's B
   // fragments and first A block beside the last block's MFMAs.
+  int scur = 0;  // stage of chunk kc
   auto chunk = [&](int kc, f16x8 (&fbc)[TN][2], f16x8 (&fbn)[TN][2]) {
-    const unsigned char* st = lds + (kc & 1) * STAGE;
+    const unsigned char* st = lds + scur * STAGE;
 #pragma unroll
     for (int i = 0; i < TM - 1; ++i) {
       if (i & 1) {
@@ -340,11 +352,12 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
     }
     if (kc + 1 < nkc) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_vmcnt<0>();  // chunk kc + 1 (requested one chunk ago) landed
+      wait_vmcnt<PPW * (NS - 2)>();  // chunk kc + 1 landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kc + 2 < nkc) issue(kc + 2, kc & 1);
-      const unsigned char* sn = lds + ((kc + 1) & 1) * STAGE;
+      issue(kc + NS, scur);
+      scur = scur + 1 == NS ? 0 : scur + 1;
+      const unsigned char* sn = lds + scur * STAGE;
       readB(sn, fbn);
       readA(sn, 0, fa0);
     }
@@ -363,7 +376,7 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   h2_dist_epilogue<BM, BN, WM, WN, HB>(p, acc, lds, m0, n0, wm, wn, lane);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 static int launch_h2(const GemmParams& p, hipStream_t stream) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.Ncol + BN - 1) / BN;
@@ -376,24 +389,31 @@ static int launch_h2(const GemmParams& p, hipStream_t stream) {
     set_error("h2 distance GEMM: grid too large");
     return PPS_ERR_INVALID_ARG;
   }
-  hipLaunchKernelGGL((gemm_h2_kernel<BM, BN, WM, WN>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((gemm_h2_kernel<BM, BN, WM, WN, NS>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                      0, stream, p, tiles_m, tiles_n);
   PPS_CHECK_LAUNCH("gemm_h2_kernel");
   return PPS_OK;
 }
 
-// tile ids: 0 = default (1); 1 = 256 x 256, 8 waves (2 x 4, 128 x 64 per
-// wave); 2 = 256 x 256, 4 waves (2 x 2, 128 x 128 per wave); 3 = 128 x 256,
-// 8 waves (2 x 4); 4 = 256 x 128, 8 waves (4 x 2); 5 = 192 x 256, 8 waves
-// (2 x 4)
+// tile ids (every tile gives the same bits; speed only): 0 = default (1);
+//   1 = 256 x 256, 8 waves (2 x 4: 128 x 64 per wave), two LDS stages
+//   2 = 256 x 224, 8 waves (4 x 2: 64 x 112), two stages -- Market's
+//       3368 x 15913 in 14 x 72 tiles, 3.94 rounds of 256 CUs
+//   3 = 128 x 256, 8 waves (2 x 4), three stages
+//   4 = 256 x 128, 8 waves (4 x 2), three stages
+//   5 = 192 x 256, 8 waves (2 x 4), two stages
+//   6 = 192 x 192, 8 waves (2 x 4: 96 x 48), three stages
+//   7 = 256 x 192, 8 waves (2 x 4: 128 x 48), two stages
 int launch_gemm_h2(const GemmParams& p, hipStream_t stream, int tile) {
   switch (tile) {
     case 0:
-    case 1: return launch_h2<256, 256, 2, 4>(p, stream);
-    case 2: return launch_h2<256, 256, 2, 2>(p, stream);
-    case 3: return launch_h2<128, 256, 2, 4>(p, stream);
-    case 4: return launch_h2<256, 128, 4, 2>(p, stream);
-    case 5: return launch_h2<192, 256, 2, 4>(p, stream);
+    case 1: return launch_h2<256, 256, 2, 4, 2>(p, stream);
+    case 2: return launch_h2<256, 224, 4, 2, 2>(p, stream);
+    case 3: return launch_h2<128, 256, 2, 4, 3>(p, stream);
+    case 4: return launch_h2<256, 128, 4, 2, 3>(p, stream);
+    case 5: return launch_h2<192, 256, 2, 4, 2>(p, stream);
+    case 6: return launch_h2<192, 192, 2, 4, 3>(p, stream);
+    case 7: return launch_h2<256, 192, 2, 4, 2>(p, stream);
     default:
       set_error("unknown h2 distance tile " + std::to_string(tile));
       return PPS_ERR_INVALID_ARG;

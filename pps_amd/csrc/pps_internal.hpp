@@ -227,7 +227,7 @@ int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
 int x3c_tile_cols(int tile);
 
 // ---- f16x2 distance GEMM (gemm_h2.hip) ---------------------------------------
-constexpr int kH2NumTiles = 6;
+constexpr int kH2NumTiles = 8;
 int launch_gemm_h2(const GemmParams& p, hipStream_t stream, int tile);
 int split_h2_sqnorm_tiled(const float* x, int64_t rows, int D, int64_t ld, uint16_t* out2t,
                           float* rscale, float* sqnorm, hipStream_t stream);
