@@ -422,7 +422,20 @@ def conv_roofline(nm, x, reps=20):
     conv_bytes = sum(v['bytes'] for v in conv)
     n_launch = len(conv)
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
-    if nm.math == 'x3':
+    # f16x2 launches (PPS_TILE_H2) run 3 f16 MFMA terms per product, the rest
+    # 6 bf16 terms: the roof of a mixed table is the flop-weighted harmonic
+    # blend of the two (the time the whole stack takes at both peaks)
+    h2_flops = sum(v['flops'] for v in conv if v['tile'] & ops.TILE_H2)
+    if nm.math == 'x3' and h2_flops:
+        peak = conv_flops / (h2_flops / PEAK_H2_TFLOPS + (conv_flops - h2_flops) / PEAK_X3_TFLOPS)
+        kernel = ('implicit-GEMM conv, %d f16x2 launches (PPS_TILE_H2: 3 f16 MFMA terms per '
+                  'product, per-tensor power-of-two activation scale) + %d bf16x3 launches '
+                  '(6 bf16 terms): gemm_x3p_kernel<*>, gemm_x3c_kernel<*>, gemm_ws_kernel<*>, the '
+                  'fused stem; per-layer autotune; peak = flop-weighted blend of %.1f and %.1f '
+                  'TF/s' % (sum(1 for v in conv if v['tile'] & ops.TILE_H2),
+                            sum(1 for v in conv if not v['tile'] & ops.TILE_H2),
+                            PEAK_H2_TFLOPS, PEAK_X3_TFLOPS))
+    elif nm.math == 'x3':
         peak, kernel = PEAK_X3_TFLOPS, ('implicit-GEMM conv: gemm_x3p_kernel<*> (LDS-DMA pipelined), gemm_x3c_kernel<*> (3x3 '
                                         'from LDS input patches), gemm_ws_kernel<*> (weight-stationary 1x1), per-layer autotune; '
                                         '+ the fused stem (stem_ring_x3_kernel); f32 products as 6 '
@@ -442,7 +455,9 @@ def conv_roofline(nm, x, reps=20):
                 timing='pps_forward hipGraph replayed %d x between HIP events; per-launch split '
                        'from eager pps_forward_layers passes with events between layers (median '
                        'of 5), rescaled to the replay total' % reps,
-                frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4)), per
+                frac_of_f32_mfma_peak=round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                frac_of_x3_roof=round(achieved / PEAK_X3_TFLOPS, 4),
+                h2_flop_share=round(h2_flops / conv_flops, 4)), per
 
 
 def usable_cores():
@@ -564,11 +579,14 @@ def table_digest(nm):
         base = t & 0xff
         g = ('auto' if base == 0 else 'x32' if base < ops.TILE_P16_FIRST else
              'x16' if base < ops.TILE_C16_FIRST else 'patch')
+        if t & ops.TILE_H2:   # f16x2 arithmetic: its own rounding groups
+            g = 'h2_' + ('x16' if base < ops.TILE_C16_FIRST else 'patch')
         groups[g] = groups.get(g, 0) + 1
     return dict(sha1=hashlib.sha1('\n'.join(rows).encode()).hexdigest()[:16],
                 layers_per_rounding_group=groups, plane_edges=len(planes),
                 splitk_layers=sum(1 for L in layers if L['splitk'] > 1),
-                seam_pairs=sum(1 for L in layers if L['tile'] & ops.TILE_SEAM))
+                seam_pairs=sum(1 for L in layers if L['tile'] & ops.TILE_SEAM),
+                h2_layers=sum(1 for L in layers if L['tile'] & ops.TILE_H2))
 
 
 def e2e_stage(nm, rank, world, n_images, batch, threads):
@@ -817,7 +835,8 @@ def main():
     # (PPS_AUTOTUNE_SPLITK=1: also try conv split-K)
     nm, blobs, imgs, xbuf = build_bench_model(
         B, rank, table=saved, autotune=not args.no_autotune,
-        flags=native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1' else 0)
+        flags=(native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1' else 0) |
+        (native.AUTOTUNE_NO_H2 if os.environ.get('PPS_AUTOTUNE_NO_H2') == '1' else 0))
     cfg = market_cfg()
     H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
     feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')

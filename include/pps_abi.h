@@ -90,6 +90,16 @@ int pps_gemm_num_tiles(void);
  * group: same bits).  (Cin, Cout, next Cout) = (64, 256, 64) or (128, 512,
  * 128), f32 activations at both ends, no split-K. */
 #define PPS_TILE_SEAM 0x400
+/* Whole-network plan only, or-ed into a conv / fused-shortcut / conv_pps
+ * layer's tile: run the layer in the f16x2 arithmetic of
+ * pps_conv2d_bn_act_h2 (three f16 MFMA terms per product) on base tile 0,
+ * 38..53, 55 or, for stride-1 3x3 convs, 56..59 (conv_pps: its 192-row
+ * tiles >= 38), optionally with PPS_TILE_COL_ORDER; f32 activations at both
+ * ends (no plane edge), no split-K.  The handle keeps the f16x2 weight split
+ * beside the bf16x3 one; each forward zeroes its per-tensor activation maxima
+ * and every producer reports max|y| from its epilogue (the f16x2 layers'
+ * input scales). */
+#define PPS_TILE_H2 0x800
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
@@ -191,6 +201,47 @@ int pps_distmat_h2_self_tiled(const uint16_t* x2t, int64_t N, const float* xsq, 
                               int D, int metric, float* out, int64_t ldo, int tile,
                               void* stream);
 int pps_h2_num_tiles(void);
+
+/* ---- f16x2 convolutions ("h2", round 5) ---------------------------------
+ * The conv entry points above in the f16x2 arithmetic of pps_distmat_h2_*:
+ * three f16 MFMA terms per product instead of six bf16 ones.  Weights: the
+ * packed [Cout][Kpad] f32 weights split per output channel by
+ * pps_split_f16x2_sqnorm_tiled (w2t chunk-tiled [2][Cout16/16][Kpad/32][16]
+ * [32], wrs[c] = 2^-s_c).  Activations stay f32 NHWC; the kernel scales them
+ * by the power of two 2^s_a with max|x 2^s_a| in [2^14, 2^15), taken from
+ * *amax_x = max|x| (device float, e.g. written by the producer of x through
+ * its amax_y, or pps_amax), and splits them into two f16 terms after the
+ * LDS fragment read.  amax_y (device float or NULL) receives max|y| by an
+ * atomic max on the float bits: zero it before the launch.  Cin % 32 == 0,
+ * Kpad == KH*KW*Cin; tile 0 (= 38), the 16x16x32 pipelined tiles 38..53, 55
+ * and the patch tiles 56..59, or-ed with PPS_TILE_COL_ORDER; no planes, no
+ * split-K.  Same f32-level error as the x3 entries (tests/test_gpu_h2_conv.py). */
+int pps_conv2d_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx,
+                         const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
+                         int KW, int stride, int pad, int dil, const float* scale,
+                         const float* shift, const float* residual, int relu, float* y, int Ho,
+                         int Wo, int ldy, const float* amax_x, float* amax_y, int tile,
+                         void* stream);
+/* pps_conv2d_dual_bn_act_x3 (projection shortcut K-concatenated) in f16x2:
+ * both inputs share the scale of max(*amax_x, *amax_x2); Cin2 % 32 == 0. */
+int pps_conv2d_dual_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx, int KH,
+                              int KW, int stride, int pad, const float* x2, int H2, int W2,
+                              int Cin2, int ldx2, int stride2, const uint16_t* w2t,
+                              const float* wrs, int Cout, int Kpad1, int Kpad2,
+                              const float* shift, int relu, float* y, int Ho, int Wo, int ldy,
+                              const float* amax_x, const float* amax_x2, float* amax_y, int tile,
+                              void* stream);
+/* pps_conv2d_bn_act_pps_x3p (last conv + part pooling) in f16x2. */
+int pps_conv2d_bn_act_pps_h2(const float* x, int N, int H, int W, int Cin, int ldx,
+                             const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
+                             int KW, int stride, int pad, int dil, const float* scale,
+                             const float* shift, const float* residual, float* y, int Ho, int Wo,
+                             const int32_t* splits, int S, int max_ave, float* pps_out,
+                             const float* amax_x, int tile, void* stream);
+/* max |x| over n floats into *amax (atomic max on the float bits; zero it
+ * first): the activation max the f16x2 entries take, for a tensor whose
+ * producer did not report it. */
+int pps_amax(const float* x, int64_t n, float* amax, void* stream);
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
  * The diagonal is exactly 0 as in the reference's difference form. */
@@ -393,6 +444,15 @@ int pps_re_ranking_flags(const float* q_g, const float* q_q, const float* g_g, i
  * [q_g^T, g_g]] with one row stride (q_g = q_q + Q, g_g = q_q + Q * ld + Q;
  * e.g. the mirrored self-distance of the concatenated [queries; gallery]
  * features): q_g^T is read from its lower-left block, not transposed. */
+/* Workspace bytes of one pps_re_ranking_ld call with these blocks and flags:
+ * the in-place path (see above) reserves only q_g^T -- nothing with
+ * PPS_RERANK_WHOLE -- plus N ints of top-k scratch instead of the N x N
+ * normalised distance; calls that take the dense path get the dense size
+ * (= pps_rerank_workspace_bytes).  A call handed fewer bytes than its path
+ * needs fails with PPS_ERR_CAPACITY. */
+int64_t pps_rerank_workspace_bytes_ld(const float* q_g, int64_t ld_qg, const float* q_q,
+                                      int64_t ld_qq, const float* g_g, int64_t ld_gg, int64_t Q,
+                                      int64_t G, int k1, int k2, int flags);
 #define PPS_RERANK_WHOLE 2
 int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t ld_qq,
                       const float* g_g, int64_t ld_gg, int64_t Q, int64_t G, int k1, int k2,
@@ -673,6 +733,7 @@ int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets
 #define PPS_AUTOTUNE_NO_PLANES 1  /* keep the plane edges as they are     */
 #define PPS_AUTOTUNE_SPLITK 2     /* also try conv split-K 2..4           */
 #define PPS_AUTOTUNE_NO_SEAM 4    /* do not try PPS_TILE_SEAM pairs       */
+#define PPS_AUTOTUNE_NO_H2 8      /* do not try PPS_TILE_H2 (f16x2) tiles */
 
 typedef struct PpsBlob {     /* one Detectron blob, HOST float32 memory   */
   const char* name;          /* e.g. "res2_0_branch2a_w", "pps01_bn_riv"  */
@@ -704,6 +765,7 @@ typedef struct PpsLayerInfo {
   double flops;       /* algorithmic FLOP at batch N                       */
   double bytes;       /* algorithmic HBM bytes at batch N                  */
   int64_t out_shape[4];
+  const char* output; /* the output blob (pps_model_tensor's name)        */
 } PpsLayerInfo;
 
 typedef struct PpsModel PpsModel;
@@ -743,12 +805,18 @@ int pps_model_release(PpsModel* model, int N);   /* N <= 0: all */
  * device pointer, planes flag (bf16x3 [3][...]) and its 4-D shape. */
 int pps_model_tensor(const PpsModel* model, int N, const char* blob, void** ptr,
                      int* planes, int64_t* shape4);
+/* The activation max max|t| its producer reported for tensor `blob` in the
+ * last forward at batch N (the f16x2 layers' input scales; debug / parity),
+ * copied to *out (HOST).  Synchronous. */
+int pps_model_tensor_amax(const PpsModel* model, int N, const char* blob, float* out);
 /* feat [N][feat_dim] = reid_feature_concat_norm of x NHWC4 [N][H][W][4]
  * (pps_preprocess_bgr's layout: BGR minus PIXEL_MEANS, 4th channel 0). */
 int pps_forward(const PpsModel* model, const float* nhwc4, int N, float* feat,
                 void* stream);
 /* Layers [first, last) only (per-layer timing); the intermediates persist
- * in the handle, the last layer writes feat. */
+ * in the handle, the last layer writes feat.  With first > 0 the activation
+ * maxima of the tensors the range reads but does not produce are measured
+ * afresh (pps_amax) before it runs. */
 int pps_forward_layers(const PpsModel* model, const float* nhwc4, int N, float* feat,
                        int first, int last, void* stream);
 /* The reference's `data` blob as it is: NCHW [N][3][H][W] float32. */

@@ -42,6 +42,18 @@ SIGNATURES = {
                              c_int, c_ptr, c_i64, c_int, c_ptr],
     'pps_distmat_h2_self_tiled': [c_ptr, c_i64, c_ptr, c_ptr, c_int, c_int, c_ptr, c_i64, c_int,
                                   c_ptr],
+    'pps_conv2d_bn_act_h2': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_int, c_ptr,
+                             c_int, c_int, c_int, c_ptr, c_ptr, c_int, c_ptr],
+    'pps_conv2d_dual_bn_act_h2': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_int, c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr,
+                                  c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_int, c_int, c_int,
+                                  c_ptr, c_ptr, c_ptr, c_int, c_ptr],
+    'pps_conv2d_bn_act_pps_h2': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_int,
+                                 c_int, c_int, c_int, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr,
+                                 c_ptr, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr, c_int,
+                                 c_ptr],
+    'pps_amax': [c_ptr, c_i64, c_ptr, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
@@ -145,6 +157,7 @@ SIGNATURES = {
     'pps_model_reserve': [c_ptr, c_int],
     'pps_model_release': [c_ptr, c_int],
     'pps_model_tensor': [c_ptr, c_int, ctypes.c_char_p, c_ptr, c_ptr, c_ptr],
+    'pps_model_tensor_amax': [c_ptr, c_int, ctypes.c_char_p, c_ptr],
     'pps_forward': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
     'pps_forward_layers': [c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_ptr],
     'pps_forward_nchw': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
@@ -159,6 +172,8 @@ EXTRA = {
     'pps_stem_k': ([], ctypes.c_int),
     'pps_stem_variant': ([ctypes.c_int], ctypes.c_int),
     'pps_rerank_workspace_bytes': ([c_i64, c_i64, c_int, c_int], ctypes.c_int64),
+    'pps_rerank_workspace_bytes_ld': ([c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_int,
+                                       c_int, c_int], ctypes.c_int64),
     'pps_last_error': ([], ctypes.c_char_p),
     'pps_registered_ops': ([], ctypes.c_char_p),
     'pps_model_feat_dim': ([c_ptr], ctypes.c_int),

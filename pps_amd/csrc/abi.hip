@@ -20,8 +20,6 @@ bool debug_sync() {
   return on;
 }
 
-int maxpool2d(const float*, int, int, int, int, int, int, int, float*, int, int,
-              hipStream_t);
 int part_power_set(const float*, int, int, int, int, const int32_t*, int, int, float*,
                    hipStream_t);
 int l2_normalize(const float*, int64_t, int, float*, hipStream_t);
@@ -65,10 +63,12 @@ int rank_count_stream(const float*, int64_t, int64_t, int64_t, int64_t, int, con
 int rerank(const float*, int64_t, const float*, int64_t, const float*, int64_t, int64_t, int64_t,
            int, int, double, void*, size_t, float*, hipStream_t, int);
 size_t rerank_workspace_bytes(int64_t, int64_t, int, int);
+size_t rerank_workspace_bytes_for(const float*, int64_t, const float*, int64_t, const float*,
+                                  int64_t, int64_t, int64_t, int, int, int);
 int splitk_bn_act_normalize(const float*, int, int64_t, int, int, const float*,
                             const float*, int, int, float*, hipStream_t);
 int splitk_conv_epilogue(const float*, int, int64_t, int, const float*, const float*,
-                         const float*, int, float*, uint16_t*, int64_t, hipStream_t);
+                         const float*, int, float*, uint16_t*, int64_t, hipStream_t, float*);
 
 }  // namespace pps
 
@@ -529,6 +529,14 @@ int64_t pps_rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
   return (int64_t)rerank_workspace_bytes(Q, G, k1, k2);
 }
 
+int64_t pps_rerank_workspace_bytes_ld(const float* q_g, int64_t ld_qg, const float* q_q,
+                                      int64_t ld_qq, const float* g_g, int64_t ld_gg, int64_t Q,
+                                      int64_t G, int k1, int k2, int flags) {
+  if (Q < 0 || G < 0 || k1 < 1 || k2 < 1) return -1;
+  return (int64_t)rerank_workspace_bytes_for(q_g, ld_qg, q_q, ld_qq, g_g, ld_gg, Q, G, k1, k2,
+                                             flags);
+}
+
 int pps_re_ranking_ld(const float* q_g, int64_t ld_qg, const float* q_q, int64_t ld_qq,
                       const float* g_g, int64_t ld_gg, int64_t Q, int64_t G, int k1, int k2,
                       double lambda_value, int flags, void* workspace, int64_t ws_bytes,
@@ -592,14 +600,17 @@ int pps_conv1x1_seam_x3(const float* x, int64_t M, int K1, const uint16_t* w2c, 
 // weights either f32 [Cout][Kpad] (x3 = 0) or bf16x3 planes [3][Cout][Kpad]
 // x3p: bf16x3 activation planes (x_pl / y_pl, plane strides in elements)
 // instead of f32 x / y -- gemm_x3p.hip tiles only
-static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
+}  // extern "C"
+namespace pps {
+int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       const void* w, int x3, int Cout, int Kpad, int KH, int KW, int stride,
                       int pad, int dil, const float* scale, const float* shift,
                       const float* residual, int relu, float* y, int Ho, int Wo, int ldy,
                       int tile, void* stream, const uint16_t* x_pl = nullptr,
                       int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0,
                       int splitk = 1, float* part = nullptr, int* fix_cnt = nullptr,
-                      int64_t n_cnt = 0) {
+                      int64_t n_cnt = 0, float* amax_out = nullptr,
+                      const float* w_rs = nullptr, const float* amax_in = nullptr) {
   PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
               "exactly one of x / x planes and one of y / y planes must be given");
   // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled;
@@ -653,6 +664,26 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.scale = scale; p.shift = shift; p.residual = residual; p.ldr = ldy;
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   p.colmajor = colmajor ? 1 : 0;
+  p.amax_out = amax_out;
+  if (w_rs) {
+    // f16x2 (pps_conv2d_bn_act_h2, the whole-network plan's PPS_TILE_H2):
+    // f32 activations scaled by their tensor's max, chunk-tiled two-plane
+    // weights [2][Cout16 / 16][Kpad / 32][16][32] with per-channel scales
+    PPS_ENFORCE(!x_pl && !y_pl && splitk == 1, "f16x2 conv: f32 activations in and out, no split-K");
+    PPS_ENFORCE(amax_in != nullptr, "f16x2 conv: the input tensor's max (amax_x) is required");
+    PPS_ENFORCE(Cin % 32 == 0 && Kpad == KH * KW * Cin,
+                "f16x2 conv: Cin % 32 == 0 and Kpad == KH*KW*Cin");
+    PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile != GEMM_TILE_WS &&
+                              tile < GEMM_NUM_TILES),
+                "f16x2 conv: tile 0, 38..53 or 55..59");
+    p.b3 = static_cast<const uint16_t*>(w);
+    p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * Kpad;
+    p.b_bytes = (uint32_t)(p.b_plane * 2);
+    p.tiled = 2;
+    p.rs_b = w_rs;
+    p.amax_a = amax_in;
+    return launch_gemm_x3(p, EPI_CONV | EPI_F_H2, 1, as_stream(stream));
+  }
   if (x_pl) {
     p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
     p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
@@ -702,7 +733,7 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     const int rc = launch_gemm_x3(p, EPI_CONV | EPI_F_RAW, 1, as_stream(stream));
     if (rc != PPS_OK) return rc;
     return splitk_conv_epilogue(part, splitk, M, Cout, scale, shift, residual, relu,
-                                y_pl ? nullptr : y, y_pl, y_plane, as_stream(stream));
+                                y_pl ? nullptr : y, y_pl, y_plane, as_stream(stream), amax_out);
   }
   if (y_pl) { p.out = nullptr; p.out3 = y_pl; p.out_plane = y_plane; }
   if (x3) {
@@ -717,6 +748,8 @@ static int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.b = static_cast<const float*>(w);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
 }
+}  // namespace pps
+extern "C" {
 
 int pps_conv2d_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
                       const float* w, int Cout, int Kpad, int KH, int KW, int stride,
@@ -789,12 +822,15 @@ int pps_x3p_tile_shape(int tile, int planes, int* rows, int* cols) {
 // and writes the 2^S - 1 part subsets into pps_out [2^S - 1][N][Cout] as
 // pps_part_power_set does (same bits).  y (the conv output) may be null: it
 // is then never written.
-int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N,
+}  // extern "C"
+namespace pps {
+int conv_pps_impl(const float* x, const uint16_t* x3, int64_t x_plane, int N,
                               int H, int W, int Cin, int ldx, const uint16_t* w3, int Cout,
                               int Kpad, int KH, int KW, int stride, int pad, int dil,
                               const float* scale, const float* shift, const float* residual,
                               float* y, int Ho, int Wo, const int32_t* splits, int S,
-                              int max_ave, float* pps_out, int tile, void* stream) {
+                              int max_ave, float* pps_out, int tile, void* stream,
+                              const float* w_rs, const float* amax_in) {
   PPS_ENFORCE((x != nullptr) != (x3 != nullptr), "exactly one of x / x planes must be given");
   PPS_ENFORCE(w3 && scale && shift && residual && pps_out && splits, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cout % 4 == 0, "bad shape");
@@ -812,10 +848,13 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   }
   PPS_ENFORCE(hsum == Ho, "strip heights must sum to the output height");
   const bool pl = x3 != nullptr;
-  const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
+  // chunk-tiled weights (always for f16x2: two planes, per-channel scales)
+  const bool wtiled = w_rs != nullptr || (tile > 0 && (tile & PPS_TILE_B_TILED) != 0);
+  PPS_ENFORCE(!w_rs || (!pl && amax_in), "f16x2: f32 activations and their max");
   const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
   tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
+  PPS_ENFORCE(!w_rs || tile >= GEMM_TILE_P16_FIRST, "f16x2: a 16x16x32 tile (38+)");
   PPS_ENFORCE(x3p_tile_rows(tile, pl) == Ho * Wo && x3p_tile_cols(tile, pl) <= kPpsFuseMaxCols,
               "the fused pooling needs a pipelined tile of exactly Ho*Wo = " +
                   std::to_string(Ho * Wo) + " rows and <= 256 columns, tile " +
@@ -845,15 +884,73 @@ int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plan
   p.pps_write_y = y ? 1 : 0;
   for (int j = 0; j < S; ++j) p.pps_h[j] = splits[j];
   PPS_ENFORCE(x3p_eligible(p, EPI_CONV | EPI_F_RES | EPI_F_RELU), "shape not eligible for the pipelined GEMM");
-  return launch_gemm_x3p(p, EPI_CONV | EPI_F_RES | EPI_F_RELU | EPI_F_PPS, 1, as_stream(stream),
-                         tile - GEMM_TILE_P_FIRST);
+  const int h2 = w_rs ? EPI_F_H2 : 0;
+  p.rs_b = w_rs;
+  p.amax_a = amax_in;
+  return launch_gemm_x3p(p, EPI_CONV | EPI_F_RES | EPI_F_RELU | EPI_F_PPS | h2, 1,
+                         as_stream(stream), tile - GEMM_TILE_P_FIRST);
+}
+}  // namespace pps
+extern "C" {
+
+int pps_conv2d_bn_act_pps_x3p(const float* x, const uint16_t* x3, int64_t x_plane, int N,
+                              int H, int W, int Cin, int ldx, const uint16_t* w3, int Cout,
+                              int Kpad, int KH, int KW, int stride, int pad, int dil,
+                              const float* scale, const float* shift, const float* residual,
+                              float* y, int Ho, int Wo, const int32_t* splits, int S,
+                              int max_ave, float* pps_out, int tile, void* stream) {
+  return conv_pps_impl(x, x3, x_plane, N, H, W, Cin, ldx, w3, Cout, Kpad, KH, KW, stride, pad,
+                       dil, scale, shift, residual, y, Ho, Wo, splits, S, max_ave, pps_out, tile,
+                       stream, nullptr, nullptr);
 }
 
-static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
+// ---- f16x2 convolutions (include/pps_abi.h "f16x2 convolutions") ----------
+int pps_conv2d_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx,
+                         const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
+                         int KW, int stride, int pad, int dil, const float* scale,
+                         const float* shift, const float* residual, int relu, float* y, int Ho,
+                         int Wo, int ldy, const float* amax_x, float* amax_y, int tile,
+                         void* stream) {
+  PPS_ENFORCE(wrs != nullptr, "null weight scales");
+  return conv_impl(x, N, H, W, Cin, ldx, w2t, 1, Cout, Kpad, KH, KW, stride, pad, dil, scale,
+                   shift, residual, relu, y, Ho, Wo, ldy, tile, stream, nullptr, 0, nullptr, 0, 1,
+                   nullptr, nullptr, 0, amax_y, wrs, amax_x);
+}
+
+int pps_conv2d_dual_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx, int KH,
+                              int KW, int stride, int pad, const float* x2, int H2, int W2,
+                              int Cin2, int ldx2, int stride2, const uint16_t* w2t,
+                              const float* wrs, int Cout, int Kpad1, int Kpad2,
+                              const float* shift, int relu, float* y, int Ho, int Wo, int ldy,
+                              const float* amax_x, const float* amax_x2, float* amax_y, int tile,
+                              void* stream) {
+  PPS_ENFORCE(wrs != nullptr, "null weight scales");
+  return dual_impl(x, N, H, W, Cin, ldx, KH, KW, stride, pad, x2, H2, W2, Cin2, ldx2, stride2,
+                   w2t, 1, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream, amax_y,
+                   wrs, amax_x, amax_x2);
+}
+
+int pps_conv2d_bn_act_pps_h2(const float* x, int N, int H, int W, int Cin, int ldx,
+                             const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
+                             int KW, int stride, int pad, int dil, const float* scale,
+                             const float* shift, const float* residual, float* y, int Ho, int Wo,
+                             const int32_t* splits, int S, int max_ave, float* pps_out,
+                             const float* amax_x, int tile, void* stream) {
+  PPS_ENFORCE(wrs != nullptr, "null weight scales");
+  return conv_pps_impl(x, nullptr, 0, N, H, W, Cin, ldx, w2t, Cout, Kpad, KH, KW, stride, pad,
+                       dil, scale, shift, residual, y, Ho, Wo, splits, S, max_ave, pps_out, tile,
+                       stream, wrs, amax_x);
+}
+
+}  // extern "C"
+namespace pps {
+int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                            int KH, int KW, int stride, int pad, const float* x2, int H2,
                            int W2, int Cin2, int ldx2, int stride2, const void* w, int x3,
                            int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
-                           float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
+                           float* y, int Ho, int Wo, int ldy, int tile, void* stream,
+                           float* amax_out, const float* w_rs, const float* amax_in,
+                           const float* amax_in2) {
   PPS_ENFORCE(x && x2 && w && shift && y, "null pointer");
   PPS_ENFORCE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && Cin2 > 0, "bad shape");
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;  // chunk-tiled weights
@@ -891,6 +988,23 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.scale = nullptr; p.shift = shift; p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   p.colmajor = colmajor ? 1 : 0;
   PPS_ENFORCE((int64_t)Cout * (Kpad1 + Kpad2) * 6 < kMaxBufBytes, "weights larger than 2 GiB");
+  p.amax_out = amax_out;
+  if (w_rs) {  // f16x2: both operands share their maxima's scale (conv_impl)
+    PPS_ENFORCE(amax_in && amax_in2, "f16x2 conv: both inputs' maxima are required");
+    PPS_ENFORCE(Cin % 32 == 0 && Kpad1 == KH * KW * Cin && Kpad2 % 32 == 0,
+                "f16x2 conv: Cin % 32 == 0, Kpad1 == KH*KW*Cin, Cin2 % 32 == 0");
+    PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_TILE_C16_FIRST &&
+                              tile != GEMM_TILE_WS),
+                "f16x2 fused-shortcut conv: tile 0, 38..53 or 55");
+    p.b3 = static_cast<const uint16_t*>(w);
+    p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * (Kpad1 + Kpad2);
+    p.b_bytes = (uint32_t)(p.b_plane * 2);
+    p.tiled = 2;
+    p.rs_b = w_rs;
+    p.amax_a = amax_in;
+    p.amax_a2 = amax_in2;
+    return launch_gemm_x3(p, EPI_CONV | EPI_F_H2, 1, as_stream(stream));
+  }
   if (x3) {
     p.b3 = static_cast<const uint16_t*>(w);
     p.b_plane = (int64_t)(wtiled ? (Cout + 15) / 16 * 16 : Cout) * (Kpad1 + Kpad2);
@@ -902,6 +1016,8 @@ static int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.b_bytes = (uint32_t)((int64_t)Cout * (Kpad1 + Kpad2) * 4);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
 }
+}  // namespace pps
+extern "C" {
 
 int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx,
                            int KH, int KW, int stride, int pad, const float* x2, int H2,
@@ -909,7 +1025,8 @@ int pps_conv2d_dual_bn_act(const float* x, int N, int H, int W, int Cin, int ldx
                            int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
                            float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
   return dual_impl(x, N, H, W, Cin, ldx, KH, KW, stride, pad, x2, H2, W2, Cin2, ldx2, stride2,
-                   w, 0, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream);
+                   w, 0, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream, nullptr,
+                   nullptr, nullptr, nullptr);
 }
 
 int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin, int ldx,
@@ -918,7 +1035,8 @@ int pps_conv2d_dual_bn_act_x3(const float* x, int N, int H, int W, int Cin, int 
                               int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
                               float* y, int Ho, int Wo, int ldy, int tile, void* stream) {
   return dual_impl(x, N, H, W, Cin, ldx, KH, KW, stride, pad, x2, H2, W2, Cin2, ldx2, stride2,
-                   w3, 1, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream);
+                   w3, 1, Cout, Kpad1, Kpad2, shift, relu, y, Ho, Wo, ldy, tile, stream, nullptr,
+                   nullptr, nullptr, nullptr);
 }
 
 int pps_gemm_bn_act_batched(const float* x, int64_t x_bstride, int M, int K,
@@ -1006,7 +1124,7 @@ int pps_maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride,
   PPS_ENFORCE(Ho == (H + 2 * pad - k) / stride + 1 && Wo == (W + 2 * pad - k) / stride + 1,
               "output size does not match pooling arithmetic (floor)");
   PPS_ENFORCE(aligned16(x) && aligned16(y), "x/y must be 16-byte aligned");
-  return maxpool2d(x, N, H, W, C, k, stride, pad, y, Ho, Wo, as_stream(stream));
+  return maxpool2d(x, N, H, W, C, k, stride, pad, y, Ho, Wo, as_stream(stream), nullptr);
 }
 
 int pps_part_power_set(const float* x, int N, int H, int W, int C, const int32_t* splits,

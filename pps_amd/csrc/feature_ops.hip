@@ -19,7 +19,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <typename IDX>
 __global__ void maxpool_nhwc_kernel(const float* __restrict__ x, int N, int H, int W,
                                     int C, int k, int s, int pad,
-                                    float* __restrict__ y, int Ho, int Wo) {
+                                    float* __restrict__ y, int Ho, int Wo,
+                                    float* __restrict__ amax) {
+  float amx = 0.f;
   const IDX C4 = (IDX)(C >> 2);
   const IDX total = (IDX)N * (IDX)Ho * (IDX)Wo * C4;
   for (IDX t = (IDX)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -47,11 +49,13 @@ __global__ void maxpool_nhwc_kernel(const float* __restrict__ x, int N, int H, i
       }
     }
     *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oh) * Wo + ow) * C + c4 * 4) = m;
+    amx = fmaxf(amx, fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fmaxf(fabsf(m.z), fabsf(m.w))));
   }
+  if (amax) amax_commit(amax, amx);
 }
 
 int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad,
-              float* y, int Ho, int Wo, hipStream_t st) {
+              float* y, int Ho, int Wo, hipStream_t st, float* amax) {
   const int64_t total = (int64_t)N * Ho * Wo * (C / 4);
   const int block = 256;
   const int64_t want = (total + block - 1) / block;
@@ -59,11 +63,11 @@ int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int
   if (total < (int64_t)1 << 31) {
     // one thread per output vector (no grid-stride loop)
     hipLaunchKernelGGL(maxpool_nhwc_kernel<uint32_t>, dim3((unsigned)want), dim3(block), 0, st,
-                       x, N, H, W, C, k, stride, pad, y, Ho, Wo);
+                       x, N, H, W, C, k, stride, pad, y, Ho, Wo, amax);
   } else {
     const int grid = (int)(want < 8192 ? want : 8192);
     hipLaunchKernelGGL(maxpool_nhwc_kernel<int64_t>, dim3(grid), dim3(block), 0, st, x, N, H,
-                       W, C, k, stride, pad, y, Ho, Wo);
+                       W, C, k, stride, pad, y, Ho, Wo, amax);
   }
   PPS_CHECK_LAUNCH("maxpool_nhwc_kernel");
   return PPS_OK;
@@ -117,7 +121,8 @@ __global__ void splitk_conv_epilogue_kernel(const float* __restrict__ part, int 
                                             const float* __restrict__ shift,
                                             const float* __restrict__ res, int relu,
                                             float* __restrict__ y, uint16_t* __restrict__ y3,
-                                            int64_t plane) {
+                                            int64_t plane, float* __restrict__ amax) {
+  float amx = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total4;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int c4 = (int)(t % N4);
@@ -134,6 +139,7 @@ __global__ void splitk_conv_epilogue_kernel(const float* __restrict__ part, int 
       v[e] = __builtin_fmaf(v[e], sc[e], sh[e]);
       if (res) v[e] += rv[e];
       if (relu) v[e] = fmaxf(v[e], 0.f);
+      amx = fmaxf(amx, fabsf(v[e]));
     }
     if (y3) {
       unsigned h0, m0, l0, h1, m1, l1;
@@ -147,17 +153,18 @@ __global__ void splitk_conv_epilogue_kernel(const float* __restrict__ part, int 
       reinterpret_cast<f32x4*>(y)[t] = v;
     }
   }
+  if (amax) amax_commit(amax, amx);
 }
 
 int splitk_conv_epilogue(const float* part, int S, int64_t M, int N, const float* scale,
                          const float* shift, const float* res, int relu, float* y,
-                         uint16_t* y3, int64_t plane, hipStream_t st) {
+                         uint16_t* y3, int64_t plane, hipStream_t st, float* amax) {
   const int64_t total4 = M * N / 4;
   if (total4 == 0) return PPS_OK;
   const int64_t want = (total4 + 255) / 256;
   hipLaunchKernelGGL(splitk_conv_epilogue_kernel, dim3((unsigned)(want < 16384 ? want : 16384)),
                      dim3(256), 0, st, part, S, M * N, total4, N / 4, scale, shift, res, relu,
-                     y, y3, plane);
+                     y, y3, plane, amax);
   PPS_CHECK_LAUNCH("splitk_conv_epilogue_kernel");
   return PPS_OK;
 }
@@ -661,3 +668,38 @@ int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* off
 }
 
 }  // namespace pps
+
+namespace pps {
+// ---- max |x| of a tensor (f16x2 activation scales, when the producer did not
+// report it; also the reference for the producers' in-epilogue maxima) -------
+__global__ void amax_kernel(const float* __restrict__ x, int64_t n, int vec,
+                            float* __restrict__ amax) {
+  float m = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t n4 = vec ? n / 4 : 0;
+  for (int64_t i = t0; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (int64_t i = 4 * n4 + t0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  amax_commit(amax, m);
+}
+
+int amax_of(const float* x, int64_t n, float* amax, hipStream_t st) {
+  if (n <= 0) return PPS_OK;
+  const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int64_t want = ((vec ? n / 4 : n) + 255) / 256;
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)(want < 2048 ? (want > 0 ? want : 1) : 2048)),
+                     dim3(256), 0, st, x, n, vec, amax);
+  PPS_CHECK_LAUNCH("amax_kernel");
+  return PPS_OK;
+}
+}  // namespace pps
+
+int pps_amax(const float* x, int64_t n, float* amax, void* stream) {
+  using namespace pps;
+  PPS_ENFORCE(x && amax, "null pointer");
+  PPS_ENFORCE(n >= 0, "n must be >= 0");
+  return amax_of(x, n, amax, as_stream(stream));
+}

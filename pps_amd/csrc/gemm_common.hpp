@@ -221,6 +221,7 @@ __device__ inline void conv_epilogue(const GemmParams& p,
   const float* sh = RAW ? nullptr : p.shift + batch * p.ss_bstride + n0;
   const float* res = HAS_RES ? p.residual + (int64_t)m0 * p.ldr + n0 : nullptr;
   const int ldr = (int)p.ldr;
+  float amx = 0.f;  // max |y| of this thread's outputs (p.amax_out)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int c = wn * (BN / WN) + j * 32 + r32;  // column within the tile
@@ -246,8 +247,15 @@ __device__ inline void conv_epilogue(const GemmParams& p,
         if (HAS_RES) v += rv[r];
         if (RELU) v = fmaxf(v, 0.f);
         if (col_ok && rr < mrem) out[rr * ldo + c] = v;
+        amx = (col_ok && rr < mrem) ? fmaxf(amx, fabsf(v)) : amx;
       }
     }
+  }
+  if (p.amax_out) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o));
+    if ((threadIdx.x & 63) == 0)
+      atomicMax(reinterpret_cast<unsigned*>(p.amax_out), __builtin_bit_cast(unsigned, amx));
   }
 }
 

@@ -37,13 +37,6 @@
 
 namespace pps {
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-
-__device__ inline f32x4 mfma16_f16(const f16x8& a, const f16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
 // The three terms with the gallery fragment as the MFMA "A" operand, so the
 // accumulator is transposed like the x3p kernels': lane l keeps query row
 // (l & 15) and gallery columns 4 (l >> 4) + e, e = 0..3.
@@ -461,11 +454,8 @@ __global__ void split_h2_sqnorm_kernel(const float* __restrict__ x, int64_t rows
     mx = fmaxf(mx, __shfl_xor(mx, o2));
   }
   // max|x| = m 2^E with m in [0.5, 1)  ->  s = 15 - E, max|x 2^s| in [2^14, 2^15)
-  const unsigned ebits = (__builtin_bit_cast(unsigned, mx) >> 23) & 0xffu;
-  int sh = ebits == 0 ? 0 : 15 - ((int)ebits - 126);  // a zero row keeps 2^0
-  if (ebits == 0 && mx > 0.f) sh = 126;               // subnormal rows: as far as f32 goes
-  sh = sh > 126 ? 126 : (sh < -126 ? -126 : sh);
-  const float S = __builtin_bit_cast(float, (unsigned)(127 + sh) << 23);
+  float rs;
+  const float S = h2_scale_of(mx, &rs);
   for (int k0 = lane * 4; k0 < D; k0 += 256 * U) {
     f32x4 v[U];
 #pragma unroll
@@ -491,7 +481,7 @@ __global__ void split_h2_sqnorm_kernel(const float* __restrict__ x, int64_t rows
   }
   if (lane == 0 && real) {
     sqnorm[row] = s;
-    rscale[row] = __builtin_bit_cast(float, (unsigned)(127 - sh) << 23);
+    rscale[row] = rs;
   }
 }
 

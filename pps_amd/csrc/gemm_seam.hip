@@ -178,6 +178,7 @@ seam_kernel(SeamParams p, int ntiles) {
   wstore(0, 1, wr);
   __syncthreads();
 
+  float amt = 0.f, amy = 0.f;  // max of the trunk / next-branch2a outputs (ReLU: >= 0)
   for (int tile = t0; tile < ntiles; tile += gridDim.x) {
     const int tnext = tile + gridDim.x;
     bf16x8 fa[C::KC1][3];
@@ -233,6 +234,7 @@ seam_kernel(SeamParams p, int ntiles) {
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(__builtin_fmaf(a4[e], s4[e], t4[e]) + rcur[it][e], 0.f);
         const int m = mbase + row;
         const int o = m < p.M ? (m * N1 + cg * CG + col) * 4 : kOOB;
+        if (m < p.M) amt = fmaxf(amt, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rt, o, 0, kStAux);
         *reinterpret_cast<f32x4*>(scr + row * C::LDT + col) = v;
       }
@@ -299,12 +301,15 @@ seam_kernel(SeamParams p, int ntiles) {
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(__builtin_fmaf(a4[e], s4[e], t4[e]), 0.f);
         const int m = mbase + row;
         const int o = m < p.M ? (m * N2 + g * CG + col) * 4 : kOOB;
+        if (m < p.M) amy = fmaxf(amy, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, o, 0, kStAux);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (!C::PREA) aload(tnext, av);   // (res3: requested earlier it would spill)
   }
+  if (p.amax_t) amax_commit(p.amax_t, amt);
+  if (p.amax_y) amax_commit(p.amax_y, amy);
 }
 
 template <int K1, int N1, int N2, int CG, int W>

@@ -112,6 +112,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   // dropped), so the loop has no branch around a memory op and the compiler
   // counts the loads in flight exactly (a conditional load or store makes it
   // wait for everything).
+  float amx = 0.f;  // max |y| of this thread's outputs (p.amax_out)
   auto load = [&](int rt, bool valid, Ops& o) {
     const int m = rt * ROWS + wr * 16 + r16;
     const bool ok = valid && m < p.M;
@@ -183,12 +184,15 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
       const int mr = rt * ROWS + wr * 16 + row;
       const int oo = (valid && mr < p.M) ? (mr * (int)p.ldo + n0 + wcol + 4 * (lane & 15)) * 4 : kOOB;
       f32x4 v;
+      float m4 = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] = __builtin_fmaf(a[e], s4r[e], t4r[e]);
         if (HAS_RES) v[e] += o.r[it][e];
         if (RELU) v[e] = fmaxf(v[e], 0.f);
+        m4 = fmaxf(m4, fabsf(v[e]));
       }
+      amx = oo != kOOB ? fmaxf(amx, m4) : amx;  // rows of this launch only
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, kStAux);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next park
@@ -206,6 +210,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
       process(rt0 + t * rg, t < my, ring[u]);
     }
   }
+  if (p.amax_out) amax_commit(p.amax_out, amx);
 }
 
 // Shapes this kernel takes: a 1x1 / stride-1 / unpadded conv on f32 NHWC

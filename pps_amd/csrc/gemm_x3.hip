@@ -269,8 +269,9 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
-  if ((p.tiled & 2) && (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST ||
-                       (p.splitk > 1 && !p.ksplit_conv))) {
+  if ((p.tiled & 2) && !(epi & EPI_F_H2) &&
+      (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST ||
+       (p.splitk > 1 && !p.ksplit_conv))) {
     set_error("chunk-tiled weights run on the pipelined / patch tiles only");
     return PPS_ERR_INVALID_ARG;
   }
@@ -278,6 +279,21 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
                            p.tile == GEMM_TILE_WS || p.tile >= GEMM_TILE_C16_FIRST)) {
     set_error("one-launch conv split-K needs a pipelined tile, partials and counters");
     return PPS_ERR_INVALID_ARG;
+  }
+  if (epi & EPI_F_H2) {
+    // f16x2 convs: the patch tiles (56..59) where they apply, else the
+    // 16x16x32 pipelined tiles (38..53, 55; tile 38 for the patch ids'
+    // fallback and for 0)
+    if (p.tile >= GEMM_TILE_C16_FIRST && x3c_eligible(p, epi, batch, p.tile))
+      return launch_gemm_x3c(p, epi, stream, p.tile);
+    const int t = (p.tile == 0 || p.tile >= GEMM_TILE_C16_FIRST) ? GEMM_TILE_P16_FIRST : p.tile;
+    if (t < GEMM_TILE_P16_FIRST || t == GEMM_TILE_WS || batch != 1 || p.splitk != 1 ||
+        !x3p_eligible(p, epi)) {
+      set_error("f16x2 conv: a 16x16x32 pipelined or patch tile (38..53, 55..59), no split-K, "
+                "Cin % 32 == 0");
+      return PPS_ERR_INVALID_ARG;
+    }
+    return launch_gemm_x3p(p, epi, batch, stream, t - GEMM_TILE_P_FIRST);
   }
   if (p.tile == GEMM_TILE_WS) {
     // the weight-stationary kernel where it applies, else the 128x128

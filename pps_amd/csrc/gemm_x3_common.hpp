@@ -97,6 +97,58 @@ __device__ inline f32x4 mfma16_x3t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f
   return c;
 }
 
+// ---- f16x2 ("h2") arithmetic (gemm_h2.hip, and the EPI_F_H2 conv tiles of
+// gemm_x3p.hip / gemm_x3c.hip): x 2^s = h0 + h1 + r with h0 = f16(x 2^s),
+// h1 = f16(x 2^s - h0), |r| <= 2^-22 |x 2^s| (2^s from h2_scale_of), and a
+// product from the three terms h0 h0' + h0 h1' + h1 h0' on f16 MFMAs.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline f32x4 mfma16_f16(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Eight consecutive-K floats, scaled by S, -> the two f16x8 MFMA fragments
+// (kept in bf16x8 storage so the bf16x3 kernels' fragment arrays hold them).
+__device__ inline void split8_h2(const f32x4& x0, const f32x4& x1, float S, bf16x8& f0,
+                                 bf16x8& f1) {
+  f16x8 h0, h1;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float y = (e < 4 ? x0[e] : x1[e - 4]) * S;  // exact (a power of two)
+    h0[e] = (_Float16)y;
+    h1[e] = (_Float16)(y - (float)h0[e]);                // the remainder is exact in f32
+  }
+  f0 = __builtin_bit_cast(bf16x8, h0);
+  f1 = __builtin_bit_cast(bf16x8, h1);
+}
+
+// The three terms with the operands swapped as in mfma16_x3t (weights as the
+// MFMA "A": transposed accumulator), fixed order b0 a0, b1 a0, b0 a1.
+__device__ inline f32x4 mfma16_h2t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = mfma16_f16(__builtin_bit_cast(f16x8, b[0]), __builtin_bit_cast(f16x8, a[0]), c);
+  c = mfma16_f16(__builtin_bit_cast(f16x8, b[1]), __builtin_bit_cast(f16x8, a[0]), c);
+  c = mfma16_f16(__builtin_bit_cast(f16x8, b[0]), __builtin_bit_cast(f16x8, a[1]), c);
+  return c;
+}
+
+// max |y| of a wave's outputs into *dst (float bits compared as unsigned:
+// every value is >= 0).  All lanes of the wave must be converged here.
+__device__ inline void amax_commit(float* dst, float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(reinterpret_cast<unsigned*>(dst), __builtin_bit_cast(unsigned, v));
+}
+
+// The A operand scale of an EPI_F_H2 launch: from the max of its activation
+// tensor(s) (both operands of a fused-shortcut GEMM share one scale).
+__device__ inline float h2_act_scale(const GemmParams& p, bool dual, float* inv) {
+  float amx = *p.amax_a;
+  if (dual) amx = fmaxf(amx, *p.amax_a2);
+  return h2_scale_of(amx, inv);
+}
+
 // Distance epilogue from precomputed squared row norms (pps_row_sqnorm):
 //   sqeuclid = (-2 q.g + |q|^2) + |g|^2 clamped at 0 [sqrt]; cosine = 1 - q.g/(|q||g|)
 template <int BM, int BN, int WM, int WN>

@@ -44,8 +44,13 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   constexpr int TN = BN / WN / S;
   constexpr int TNH = TN / 2;
   static_assert(TN % 2 == 0 && TM >= 1 && (BM / WM) % S == 0, "wave tile");
+  // EPI_F_H2: f16x2 arithmetic (f32 patch split into two f16 terms after the
+  // fragment read, two chunk-tiled f16 weight planes, three MFMA terms)
+  constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  static_assert(!H2 || (!A3 && !(EPI & (EPI_F_PLANES | EPI_F_RAW))), "f16x2: f32 activations");
+  constexpr int NBP = H2 ? 2 : 3;  // weight planes
   constexpr int B_PLANE = BN * BK * 2;
-  constexpr int B_STAGE = 3 * B_PLANE;
+  constexpr int B_STAGE = NBP * B_PLANE;
   constexpr int NPB = BN / 16;  // weight pieces per plane and chunk
   // pieces per wave; with fewer pieces than waves the spare waves load zeros
   // into the dummy KiB, so every wave issues the same count
@@ -59,7 +64,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   constexpr int SL = kX3cTaps - NS + 2;               // issue slots per patch
   constexpr int NPPW = (NPT + NW * SL - 1) / (NW * SL);  // patch pieces per wave and slot
   constexpr int LA = A3 ? 3 : 1;
-  constexpr int NLOAD = 3 * BPW + LA * NPPW;          // DMA instructions per wave and issue
+  constexpr int NLOAD = NBP * BPW + LA * NPPW;        // DMA instructions per wave and issue
   static_assert(NS >= 2 && NS <= 4 && NLOAD * (NS - 2) <= 63, "stages / vmcnt range");
   constexpr int OFF_P = NS * B_STAGE;                 // patch buffers
   constexpr int OFF_D = OFF_P + 2 * P_BYTES;          // dummy KiB
@@ -168,7 +173,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
       const int pstep = mine ? B_PLANE : 0;
       glds16(rb0, d, off);
       glds16(rb1, d + pstep, off);
-      glds16(rb2, d + 2 * pstep, off);
+      if (!H2) glds16(rb2, d + 2 * pstep, off);
     }
     int pc = -1, s = 0;  // patch chunk this issue serves, its slot
     if (it == 0) {
@@ -204,6 +209,11 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
     pbase[i] = orow * PW + (r - orow * p.Wo);
   }
   const int bsw = (r32 >> 2) & 3;
+  float h2s = 1.f;  // f16x2: the activation scale 2^s_a
+  if constexpr (H2) {
+    float inv;
+    h2s = h2_act_scale(p, false, &inv);
+  }
 
   auto chunk_barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -229,7 +239,10 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
         const int sw = (pix >> 1) & 7;
         const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + (((2 * h) ^ sw) << 4));
         const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((2 * h + 1) ^ sw) << 4));
-        split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+        if (H2)
+          split8_h2(x0, x1, h2s, fa[i][0], fa[i][1]);
+        else
+          split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
       }
     }
   };
@@ -239,7 +252,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
       const unsigned char* bp =
           st + (wn * (BN / WN) + (half * TNH + jj) * 16 + r32) * 64 + ((h ^ bsw) << 4);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NBP; ++pl)
         fb[jj][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
     }
   };
@@ -249,7 +262,8 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int jj = 0; jj < TNH; ++jj)
-        acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
+        acc[i][half * TNH + jj] = H2 ? mfma16_h2t(fa[i], fb[jj], acc[i][half * TNH + jj])
+                                     : mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
     if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -323,6 +337,15 @@ static int launch_c(const GemmParams& p, int epi, hipStream_t stream) {
     X3C_CASE(C | RS | RL)
     X3C_CASE(C | PL)
     X3C_CASE(C | RL | PL)
+    case C | RL | EPI_F_H2:
+      if constexpr (!A3) {
+        hipLaunchKernelGGL((gemm_x3c_kernel<BM, BN, WM, WN, C | RL | EPI_F_H2, NS, A3, PMAX>), grid,
+                           block, 0, stream, p, tiles_n);
+        break;
+      } else {
+        set_error("f16x2 patch tiles take f32 activations");
+        return PPS_ERR_INVALID_ARG;
+      }
     default:
       set_error("patch-staged 3x3 GEMM: epilogue not built");
       return PPS_ERR_INVALID_ARG;
@@ -362,8 +385,9 @@ bool x3c_eligible(const GemmParams& p, int epi, int batch, int tile) {
   if (!bm || batch != 1 || p.splitk > 1 || p.ksplit_conv || p.a2 || p.sym) return false;
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
   if (epi != C && epi != (C | RL) && epi != (C | RS) && epi != (C | RS | RL) && epi != (C | PL) &&
-      epi != (C | RL | PL))
+      epi != (C | RL | PL) && epi != (C | RL | EPI_F_H2))
     return false;  // the epilogues launch_c builds
+  if ((epi & EPI_F_H2) && (p.a3 || !(p.tiled & 2) || !p.rs_b || !p.amax_a)) return false;
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.dil < 1 || p.pad != p.dil) return false;
   if (p.Ho != p.H || p.Wo != p.W || p.Cin % 32 != 0 || p.Kloop != 9 * p.Cin) return false;
   if (bm % p.Wo != 0 || (p.Ho * p.Wo) % bm != 0 || p.M % bm != 0) return false;

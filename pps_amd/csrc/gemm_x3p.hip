@@ -58,10 +58,17 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int TM = BM / WM / S;
   constexpr int TN = BN / WN / S;
   static_assert(S == 32 || (S == 16 && TN % 2 == 0), "MFMA block");
+  // EPI_F_H2: f16x2 arithmetic -- f32 activations split into two f16 terms
+  // after the fragment read (scale from their tensor's max), the weights as
+  // two chunk-tiled f16 planes, three MFMA terms (mfma16_h2t)
+  constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  static_assert(!H2 || (S == 16 && !A3 && !(EPI & (EPI_F_PLANES | EPI_F_RAW | EPI_F_FIX))),
+                "f16x2 tiles: f32 activations, 16x16x32 blocks, plain epilogues");
+  constexpr int NBP = H2 ? 2 : 3;       // weight planes
   constexpr int A_PLANE = BM * BK * 2;  // A3: bf16 rows of 64 B per plane
   constexpr int A_BYTES = A3 ? 3 * A_PLANE : BM * BK * 4;  // else f32 rows of 128 B
   constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
-  constexpr int STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int STAGE = A_BYTES + NBP * B_PLANE;
   constexpr int AROWS = A3 ? 16 : 8;    // rows per A piece (1 KiB)
   constexpr int NPA = BM / AROWS;       // A pieces per chunk (per plane if A3)
   constexpr int NPB = BN / 16;          // B pieces (16 rows each) per plane and chunk
@@ -73,7 +80,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool BEVEN = NPB % NW == 0;
   constexpr int AI = (NPA + NW - 1) / NW;
   constexpr int BPW = (NPB + NW - 1) / NW;
-  constexpr int NLOAD = (A3 ? 3 : 1) * AI + 3 * BPW;  // DMA instructions per wave and chunk
+  constexpr int NLOAD = (A3 ? 3 : 1) * AI + NBP * BPW;  // DMA instructions per wave and chunk
   static_assert(NPA * AROWS == BM && NPB * 16 == BN, "tile does not split into DMA pieces");
   // Uneven tiles: only a wave's last slot can be empty (round-robin), so a
   // wave issues NLOAD, NLOAD - (A3 ? 3 : 1) (A slot empty), NLOAD - 3 (B slot
@@ -339,7 +346,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const unsigned char* d = st + A_BYTES + bpiece(j) * 1024;
       glds16(rb0, d, off);
       glds16(rb1, d + B_PLANE, off);
-      glds16(rb2, d + 2 * B_PLANE, off);
+      if (!H2) glds16(rb2, d + 2 * B_PLANE, off);
     }
     ++kiss;
     siss = siss + 1 == NS ? 0 : siss + 1;
@@ -353,6 +360,11 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
       for (int r = 0; r < S * S / 64; ++r) acc[i][j][r] = 0.f;
 
+  float h2s = 1.f;  // f16x2: the activation scale 2^s_a
+  if constexpr (H2) {
+    float inv;
+    h2s = h2_act_scale(p, DUAL, &inv);
+  }
   // Fragment reads: the rows of this lane are r32 mod S, so both swizzles
   // are per-lane constants.
   const int asw = (r32 >> 1) & 7;
@@ -370,8 +382,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       const bool eb = !BEVEN && bpiece(BPW - 1) >= NPB;
       if (!ea && !eb) wait_vmcnt<NLOAD * (NS - 2)>();
       else if (ea && !eb) wait_vmcnt<(NLOAD - LA) * (NS - 2)>();
-      else if (!ea && eb) wait_vmcnt<(NLOAD - 3) * (NS - 2)>();
-      else wait_vmcnt<(NLOAD - LA - 3) * (NS - 2)>();
+      else if (!ea && eb) wait_vmcnt<(NLOAD - NBP) * (NS - 2)>();
+      else wait_vmcnt<(NLOAD - LA - NBP) * (NS - 2)>();
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -459,7 +471,10 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
           const unsigned char* rp = st + (wm * (BM / WM) + i * 16 + r32) * 128;
           const f32x4 x0 = *reinterpret_cast<const f32x4*>(rp + (((2 * h) ^ asw) << 4));
           const f32x4 x1 = *reinterpret_cast<const f32x4*>(rp + (((2 * h + 1) ^ asw) << 4));
-          split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
+          if (H2)
+            split8_h2(x0, x1, h2s, fa[i][0], fa[i][1]);
+          else
+            split8(x0, x1, fa[i][0], fa[i][1], fa[i][2]);
         }
       }
     };
@@ -470,7 +485,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
                                   (wn * (BN / WN) + (half * TNH + jj) * 16 + r32) * 64 +
                                   ((h ^ bsw) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NBP; ++pl)
           fb[jj][pl] = *reinterpret_cast<const bf16x8*>(bp + pl * B_PLANE);
       }
     };
@@ -480,7 +495,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int jj = 0; jj < TNH; ++jj)
-          acc[i][half * TNH + jj] = mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
+          acc[i][half * TNH + jj] = H2 ? mfma16_h2t(fa[i], fb[jj], acc[i][half * TNH + jj])
+                                       : mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
       if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     };
     bf16x8 fa0[TM][3], fa1[TM][3], fb0[TNH][3], fb1[TNH][3];
@@ -568,6 +584,41 @@ static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
 template <int BM, int BN, int WM, int WN, int NSF, int NSP, int S, bool FX = false>
 static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
+  if (epi & EPI_F_H2) {
+    // f16x2 arithmetic: f32 activations, chunk-tiled two-plane weights, the
+    // conv epilogues of a ResNet bottleneck (16x16x32 tiles only)
+    if constexpr (S == 16) {
+      constexpr int H = EPI_F_H2;
+      if (p.a3 || !(p.tiled & 2) || !p.rs_b || !p.amax_a || ((epi & EPI_F_DUAL) && !p.amax_a2)) {
+        set_error("f16x2 conv: f32 activations with their max, chunk-tiled weights and scales");
+        return PPS_ERR_INVALID_ARG;
+      }
+      switch (epi & ~H) {
+        case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, false, S>(p, batch, stream); break;
+        case C | RS | RL:
+          launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, false, S>(p, batch, stream); break;
+        case C | RL | EPI_F_DUAL:
+          launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL | H, false, S>(p, batch, stream);
+          break;
+        case C | RS | RL | EPI_F_PPS:
+          if constexpr (BM == 192 && BN <= 256) {
+            launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | EPI_F_PPS | H, false, S>(p, batch, stream);
+            break;
+          } else {
+            set_error("part-power-set epilogue needs a 192-row tile with at most 256 columns");
+            return PPS_ERR_INVALID_ARG;
+          }
+        default:
+          set_error("f16x2 conv: conv + BN + ReLU [+ residual | shortcut | part pooling] only");
+          return PPS_ERR_INVALID_ARG;
+      }
+      PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+      return PPS_OK;
+    } else {
+      set_error("f16x2 conv needs a 16x16x32 tile (38..53, 55)");
+      return PPS_ERR_INVALID_ARG;
+    }
+  }
   if (epi & EPI_F_FIX) {
     if constexpr (FX && NSP != 0) {
       constexpr int F = EPI_F_FIX;

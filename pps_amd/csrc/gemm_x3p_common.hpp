@@ -93,6 +93,12 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool RAW = (EPI & EPI_F_RAW) != 0;
   constexpr bool PLANES = (EPI & EPI_F_PLANES) != 0;
+  constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  // f16x2 launches: the accumulators hold dot * 2^(s_a + s_w[col]); the
+  // column scale takes 2^-(s_a + s_w) (exact: powers of two)
+  float inv_a = 1.f;
+  if (H2) h2_act_scale(p, DUAL, &inv_a);
+  float amx = 0.f;  // max |y| of this thread's outputs (p.amax_out)
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
   float* __restrict__ out = PLANES ? nullptr : p.out + obase;
   uint16_t* __restrict__ out3 = PLANES ? p.out3 + obase : nullptr;
@@ -114,6 +120,7 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
                                    : *reinterpret_cast<const f32x4*>(sc + cb + 8 * q);
       t4[q] = (RAW || !ok) ? (f32x4){0.f, 0.f, 0.f, 0.f}
                            : *reinterpret_cast<const f32x4*>(sh + cb + 8 * q);
+      if (H2 && ok) s4[q] = s4[q] * *reinterpret_cast<const f32x4*>(p.rs_b + n0 + cb + 8 * q) * inv_a;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -135,6 +142,7 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
           v[e] = RAW ? acc[i][j][4 * q + e] : __builtin_fmaf(acc[i][j][4 * q + e], s4[q][e], t4[q][e]);
           if (HAS_RES) v[e] += rv[q][e];
           if (RELU) v[e] = fmaxf(v[e], 0.f);
+          amx = fmaxf(amx, fabsf(v[e]));
         }
         if (PLANES) {
           unsigned h0, m0_, l0, h1, m1, l1;
@@ -150,6 +158,7 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
       }
     }
   }
+  if (p.amax_out) amax_commit(p.amax_out, amx);
 }
 
 // One-launch conv split-K (EPI_F_FIX): park this K slice's raw accumulators
@@ -244,8 +253,12 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool PPS = (EPI & EPI_F_PPS) != 0;
+  constexpr bool H2 = (EPI & EPI_F_H2) != 0;
   static_assert(HB == 1 || (PPS && (BN / WN) % S == 0 && BNH % (BN / WN) == 0),
                 "column passes: PPS tiles whose wave columns fall in one pass");
+  float inv_a = 1.f;  // f16x2: see conv_epilogue_t
+  if (H2) h2_act_scale(p, DUAL, &inv_a);
+  float amx = 0.f;
   float* t = reinterpret_cast<float*>(lds);
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
   const int ldo = (int)p.ldo;
@@ -299,7 +312,8 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       const int row = idx / C4, col = 4 * (idx - row * C4);
       if (row >= mrem || col >= nrem) return;
       const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + col);
-      const f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
+      f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + col);
+      if (H2) s4 = s4 * *reinterpret_cast<const f32x4*>(p.rs_b + n0 + c0h + col) * inv_a;
       const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + col);
       f32x4 v;
 #pragma unroll
@@ -307,6 +321,7 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
         v[e] = __builtin_fmaf(a[e], s4[e], t4[e]);
         if (HAS_RES) v[e] += rv[e];
         if (RELU) v[e] = fmaxf(v[e], 0.f);
+        amx = fmaxf(amx, fabsf(v[e]));
       }
       if (PPS) {  // the pooling below reads the tile back from LDS
         *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
@@ -440,6 +455,7 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       }
     }
   }
+  if (p.amax_out) amax_commit(p.amax_out, amx);
 }
 
 // The distance epilogue staged through LDS (not for self-distance tiles,

@@ -255,6 +255,18 @@ Buf split3(const Buf& w, int64_t n, int nbatch, hipStream_t st) {
   return b;
 }
 
+// f32 weights [rows][K] -> the f16x2 split (pps_split_f16x2_sqnorm_tiled):
+// chunk-tiled planes [2][rows16 / 16][K / 32][16][32] and per-row scales
+void split_h2w(const Buf& w, int rows, int64_t K, Buf& w2, Buf& wrs, hipStream_t st) {
+  const int64_t r16 = (rows + 15) / 16 * 16;
+  w2 = std::make_shared<DevBuf>((size_t)2 * r16 * K * sizeof(uint16_t));
+  wrs = std::make_shared<DevBuf>((size_t)rows * sizeof(float));
+  DevBuf sq((size_t)rows * sizeof(float));
+  rc_check(pps_split_f16x2_sqnorm_tiled(w->as<float>(), rows, (int)K, K, w2->as<uint16_t>(),
+                                        wrs->as<float>(), sq.as<float>(), st));
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
 // ---- weights (host) -------------------------------------------------------------
 struct Blob {
   const float* data;
@@ -324,6 +336,8 @@ struct Layer {
   Buf w, scale, shift;  // w: f32 [Cout][Kpad] or bf16x3 planes
   Buf wt;               // x3 plain convs with Kpad % 32 == 0: the planes chunk-tiled
                         // (pps_tile_planes), used when tile carries PPS_TILE_B_TILED
+  Buf w2, wrs;          // the f16x2 split (PPS_TILE_H2): two chunk-tiled f16 planes
+                        // [2][Cout16/16][K/32][16][32] and per-channel scales [Cout]
   std::vector<int> split;
   bool max_ave = false, normalize = false;
   int nsub = 0, dim = 0, dim_inner = 0;
@@ -346,6 +360,8 @@ struct Workspace {
   Buf cnt;                          // one-launch split-K tile counters (zero between launches)
   size_t cnt_ints = 0;
   Buf nhwc4;                        // input staging for pps_forward_nchw / _bgr
+  Buf amax;                         // per-tensor max |x| (PpsModel::slot), zeroed per forward
+  std::vector<char> amax_need;      // slots this forward reports (set by forward_range)
   // set by pps_model_reserve: a graph captured afterwards may hold these
   // buffers' addresses, so they are never reallocated until pps_model_release
   bool pinned = false;
@@ -361,6 +377,10 @@ struct PpsModel {
   std::vector<std::pair<int, int>> edges;  // plane-eligible (producer, consumer) layer indices
   std::set<std::string> plane_capable;     // outputs of edge producers
   bool x3 = true, fused_stem = false, fused_pps = false, act_planes = false;
+  std::map<std::string, int> slot;         // activation tensor -> its max |x| slot
+  // every producer reports its maximum (autotune: any layer may try an f16x2
+  // tile; env PPS_AMAX_ALL=1), else only the inputs of PPS_TILE_H2 layers
+  mutable bool amax_all = false;
   mutable std::map<int, pps::Workspace> ws;
   mutable std::vector<std::string> names;  // storage for pps_model_layer_info
 };
@@ -457,6 +477,12 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
   }
   if (m.x3) {
     for (auto& L : m.layers) {
+      // the f16x2 split beside the bf16x3 one where an f16x2 tile can run
+      // the layer (PPS_TILE_H2: Cin % 32 == 0, no K padding)
+      if ((L.op == Op::Conv || L.op == Op::ConvDual) && L.cin_eff % 32 == 0 &&
+          L.kpad == L.k * L.k * L.cin_eff && (L.op == Op::Conv || L.shortcut_cin % 32 == 0))
+        split_h2w(L.w, L.cout, L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad, L.w2,
+                  L.wrs, st);
       if (L.op == Op::Conv || L.op == Op::ConvDual)
         L.w = split3(L.w, (int64_t)L.cout * (L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad), 1, st);
       const int64_t kt = L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad;
@@ -539,6 +565,15 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
       m.layers[e.first].planes_out = m.layers[e.second].planes_in = on;
     }
   }
+  // one activation-max slot per tensor (the input and every layer output):
+  // each producer reports max |y| there, the f16x2 layers scale by it
+  m.slot["data"] = 0;
+  for (const auto& L : m.layers)
+    for (const std::string* t : {&L.output, &L.conv_output})
+      if (!t->empty() && !m.slot.count(*t)) {
+        const int n = (int)m.slot.size();
+        m.slot[*t] = n;
+      }
 }
 
 // ---- shapes / workspaces ------------------------------------------------------
@@ -620,6 +655,18 @@ bool seam_ok(const PpsModel& m, const Layer& L) {
   return !L.planes_in && !L.planes_out && !X.planes_out && L.splitk == 1 && X.splitk == 1;
 }
 
+// A PPS_TILE_H2 tile this layer can run (structure only; planes and split-K
+// are checked at run time, since they may change after the tile is set)
+bool h2_tile_ok(const Layer& L, int tile) {
+  const int base = tile & 0xff;
+  if (!L.w2 || (tile & PPS_TILE_SEAM)) return false;
+  if (L.op != Op::Conv && L.op != Op::ConvDual && L.op != Op::ConvPps) return false;
+  if (!L.relu && L.op == Op::Conv) return false;  // the f16x2 epilogues end in a ReLU
+  if (base == 0) return true;
+  if (base < GEMM_TILE_P16_FIRST || base == GEMM_TILE_WS || base >= GEMM_NUM_TILES) return false;
+  return L.op == Op::Conv || base < GEMM_TILE_C16_FIRST;
+}
+
 bool fix_tile(int tile) {
   const int t = tile & 0xff;
   return t == GEMM_TILE_P16_FIRST + 7 ||
@@ -699,6 +746,8 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
   w.part_floats = part_need(m, w.shapes);
   if (w.part_floats) w.part = std::make_shared<DevBuf>(w.part_floats * sizeof(float));
   grow_counters(w, cnt_need(m, w.shapes), st);
+  w.amax = std::make_shared<DevBuf>(m.slot.size() * sizeof(float));
+  hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
   return m.ws.emplace(N, std::move(w)).first->second;
 }
 
@@ -711,12 +760,21 @@ float* nhwc4_buffer(const PpsModel& m, Workspace& w, hipStream_t st) {
 }
 
 // ---- one layer ----------------------------------------------------------------
+const float* fbuf_of(const Workspace& w, const std::string& name) {
+  return w.bufs.at(name)->as<float>();
+}
+
 struct Act {  // an activation operand: f32 NHWC or bf16x3 planes
   const float* f = nullptr;
   const uint16_t* pl = nullptr;
   int64_t plane = 0;
   Shape s;
 };
+
+bool getenv_flag_on(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] && std::strcmp(v, "0") != 0;
+}
 
 void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, float* feat,
                bool last, int tile, int sk, hipStream_t st) {
@@ -730,6 +788,23 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     return a;
   };
   auto fbuf = [&](const std::string& name) { return w.bufs.at(name)->as<float>(); };
+  // activation-max slot of a tensor an f16x2 layer reads (its producer
+  // reports max |y| there), else null
+  auto slotp = [&](const std::string& t) -> float* {
+    auto it = m.slot.find(t);
+    return it == m.slot.end() || it->second >= (int)w.amax_need.size() || !w.amax_need[it->second]
+               ? nullptr
+               : w.amax->as<float>() + it->second;
+  };
+  // PPS_TILE_H2: the f16x2 arithmetic on the base tile (weights always the
+  // chunk-tiled f16x2 split; COL_ORDER kept)
+  const bool h2 = (tile & PPS_TILE_H2) != 0;
+  if (h2) {
+    PPS_MCHECK(L.w2 && !L.planes_in && !L.planes_out && sk == 1,
+               "layer '" + L.name + "': PPS_TILE_H2 needs the f16x2 weights, f32 activations "
+               "at both ends and no split-K");
+    tile &= ~(PPS_TILE_H2 | PPS_TILE_B_TILED | PPS_TILE_SEAM);
+  }
   // split convs run in one launch on the FIX tiles (same bits as the
   // two-pass split-K), else raw partials + the summing pass (plain weights)
   const bool fused_sk = sk > 1 && L.op == Op::Conv && fix_tile(tile) && L.relu &&
@@ -750,10 +825,13 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     const Layer& X = m.layers[L.seam_next];
     const Act a = act(L.input, false);
     const int64_t M = a.s.d[0] * a.s.d[1] * a.s.d[2];
-    rc_check(pps_conv1x1_seam_x3(a.f, M, L.cin_eff, L.w->as<uint16_t>(), L.cout, sc, sh,
-                                 fbuf(L.residual), fbuf(L.output), X.w->as<uint16_t>(), X.cout,
-                                 X.scale->as<float>(), X.shift->as<float>(), fbuf(X.output),
-                                 st));
+    // pps_conv1x1_seam_x3 with the two outputs' maxima reported
+    SeamParams sp{a.f, fbuf(L.residual), L.w->as<uint16_t>(), sc, sh, fbuf(L.output),
+                  X.w->as<uint16_t>(), X.scale->as<float>(), X.shift->as<float>(),
+                  fbuf(X.output), (int)M};
+    sp.amax_t = slotp(L.output);
+    sp.amax_y = slotp(X.output);
+    rc_check(launch_seam_x3(sp, L.cin_eff, L.cout, X.cout, st));
     return;
   }
   switch (L.op) {
@@ -763,29 +841,34 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const float* res = L.residual.empty() ? nullptr : fbuf(L.residual);
       const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
       const int Ho = (int)ys.d[1], Wo = (int)ys.d[2];
-      if (m.x3 && (L.planes_in || L.planes_out || sk > 1)) {
+      // the op-level entry points' implementation (same arguments as
+      // pps_conv2d_bn_act_x3p[_splitk[_fused]] / _x3 / _h2), reporting max |y|
+      float* amo = slotp(L.output);
+      if (h2) {
+        rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(), 1, L.cout, L.kpad,
+                           L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, L.relu, fbuf(L.output),
+                           Ho, Wo, L.cout, tile, st, nullptr, 0, nullptr, 0, 1, nullptr, nullptr,
+                           0, amo, L.wrs->as<float>(), slotp(L.input)));
+      } else if (m.x3 && (L.planes_in || L.planes_out || sk > 1)) {
         const int t = tile >= GEMM_TILE_P_FIRST ? tile : 0;
         float* yf = L.planes_out ? nullptr : fbuf(L.output);
         uint16_t* y3 = L.planes_out ? w.bufs.at(L.output)->as<uint16_t>() : nullptr;
         const int64_t ypl = L.planes_out ? ys.numel() : 0;
         if (fused_sk)
-          rc_check(pps_conv2d_bn_act_x3p_splitk_fused(
-              a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout, L.kpad, L.k, L.k, L.stride,
-              L.pad, L.dil, sc, sh, res, L.relu, yf, y3, ypl, Ho, Wo, L.cout, sk,
-              w.part->as<float>(), w.cnt->as<int>(), (int64_t)w.cnt_ints, t, st));
-        else if (sk > 1)
-          rc_check(pps_conv2d_bn_act_x3p_splitk(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3,
-                                                L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil,
-                                                sc, sh, res, L.relu, yf, y3, ypl, Ho, Wo, L.cout,
-                                                sk, w.part->as<float>(), t, st));
+          rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, w3, 1, L.cout, L.kpad, L.k, L.k,
+                             L.stride, L.pad, L.dil, sc, sh, res, L.relu, yf, Ho, Wo, L.cout, t,
+                             st, a.pl, a.plane, y3, ypl, sk, w.part->as<float>(),
+                             w.cnt->as<int>(), (int64_t)w.cnt_ints, amo, nullptr, nullptr));
         else
-          rc_check(pps_conv2d_bn_act_x3p(a.f, a.pl, a.plane, n, H, W, L.cin_eff, ldx, w3, L.cout,
-                                         L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res,
-                                         L.relu, yf, y3, ypl, Ho, Wo, L.cout, t, st));
+          rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, w3, 1, L.cout, L.kpad, L.k, L.k,
+                             L.stride, L.pad, L.dil, sc, sh, res, L.relu, yf, Ho, Wo, L.cout, t,
+                             st, a.pl, a.plane, y3, ypl, sk, sk > 1 ? w.part->as<float>() : nullptr,
+                             nullptr, 0, amo, nullptr, nullptr));
       } else if (m.x3) {
-        rc_check(pps_conv2d_bn_act_x3(a.f, n, H, W, L.cin_eff, ldx, w3, L.cout, L.kpad, L.k, L.k,
-                                      L.stride, L.pad, L.dil, sc, sh, res, L.relu,
-                                      fbuf(L.output), Ho, Wo, L.cout, tile, st));
+        rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, w3, 1, L.cout, L.kpad, L.k, L.k,
+                           L.stride, L.pad, L.dil, sc, sh, res, L.relu, fbuf(L.output), Ho, Wo,
+                           L.cout, tile, st, nullptr, 0, nullptr, 0, 1, nullptr, nullptr, 0, amo,
+                           nullptr, nullptr));
       } else {
         rc_check(pps_conv2d_bn_act(a.f, n, H, W, L.cin_eff, ldx, wf, L.cout, L.kpad, L.k, L.k,
                                    L.stride, L.pad, L.dil, sc, sh, res, L.relu, fbuf(L.output),
@@ -798,11 +881,13 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const Shape ys = w.shapes.at(L.output);
       const int C2 = (int)b.s.d[3];
       if (m.x3)
-        rc_check(pps_conv2d_dual_bn_act_x3(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2],
-                                           L.cin_eff, (int)a.s.d[3], L.k, L.k, L.stride, L.pad,
-                                           b.f, (int)b.s.d[1], (int)b.s.d[2], C2, C2, L.stride2,
-                                           w3, L.cout, L.kpad, C2, sh, L.relu, fbuf(L.output),
-                                           (int)ys.d[1], (int)ys.d[2], L.cout, tile, st));
+        rc_check(dual_impl(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], L.cin_eff,
+                           (int)a.s.d[3], L.k, L.k, L.stride, L.pad, b.f, (int)b.s.d[1],
+                           (int)b.s.d[2], C2, C2, L.stride2,
+                           h2 ? L.w2->as<uint16_t>() : w3, 1, L.cout, L.kpad, C2, sh, L.relu,
+                           fbuf(L.output), (int)ys.d[1], (int)ys.d[2], L.cout, tile, st,
+                           slotp(L.output), h2 ? L.wrs->as<float>() : nullptr,
+                           h2 ? slotp(L.input) : nullptr, h2 ? slotp(L.input2) : nullptr));
       else
         rc_check(pps_conv2d_dual_bn_act(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2],
                                         L.cin_eff, (int)a.s.d[3], L.k, L.k, L.stride, L.pad, b.f,
@@ -814,15 +899,19 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     case Op::MaxPool: {
       const Act a = act(L.input, false);
       const Shape ys = w.shapes.at(L.output);
-      rc_check(pps_maxpool2d(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], (int)a.s.d[3],
-                             L.k, L.stride, L.pad, fbuf(L.output), (int)ys.d[1], (int)ys.d[2], st));
+      PPS_MCHECK(a.s.d[3] % 4 == 0, "max pooling needs C % 4 == 0");
+      rc_check(maxpool2d(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], (int)a.s.d[3], L.k,
+                         L.stride, L.pad, fbuf(L.output), (int)ys.d[1], (int)ys.d[2], st,
+                         slotp(L.output)));
       return;
     }
     case Op::StemPool: {
       const Act a = act(L.input, false);
       const Shape ys = w.shapes.at(L.output);
-      rc_check(pps_stem_conv_pool_x3(a.f, (int)a.s.d[0], (int)a.s.d[1], (int)a.s.d[2], w3, sc,
-                                     sh, fbuf(L.output), (int)ys.d[1], (int)ys.d[2], st));
+      // pps_stem_conv_pool_x3 (shapes checked when the stem was fused), max |y| reported
+      const int Hin = (int)a.s.d[1];
+      rc_check(stem_conv_pool_x3(a.f, (int)a.s.d[0], Hin, w3, sc, sh, fbuf(L.output),
+                                 (Hin + 2 * 3 - 7) / 2 + 1, (int)ys.d[1], st, slotp(L.output)));
       return;
     }
     case Op::Pps: {
@@ -838,7 +927,20 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const float* res = fbuf(L.residual);
       const std::vector<int> ok = pps_tiles(m, L, cs);
       const int n = (int)a.s.d[0], H = (int)a.s.d[1], W = (int)a.s.d[2], ldx = (int)a.s.d[3];
-      if (!ok.empty()) {
+      if (h2) {  // f16x2: the 192-row tiles on 16x16x32 blocks
+        std::vector<int> ok16;
+        for (int t : ok)
+          if (t >= GEMM_TILE_P16_FIRST) ok16.push_back(t);
+        PPS_MCHECK(!ok16.empty(), "layer '" + L.name + "': no f16x2 tile holds one image");
+        const int tb = tile & ~PPS_TILE_COL_ORDER;
+        int t = std::find(ok16.begin(), ok16.end(), tb) != ok16.end() ? tb : ok16[0];
+        t |= tile & PPS_TILE_COL_ORDER;
+        rc_check(conv_pps_impl(a.f, nullptr, 0, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(),
+                               L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res,
+                               nullptr, (int)cs.d[1], (int)cs.d[2], L.split.data(),
+                               (int)L.split.size(), L.max_ave, fbuf(L.output), t, st,
+                               L.wrs->as<float>(), slotp(L.input)));
+      } else if (!ok.empty()) {
         const int tb = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
         int t = std::find(ok.begin(), ok.end(), tb) != ok.end() ? tb : ok[0];
         t |= tile & PPS_TILE_COL_ORDER;
@@ -884,6 +986,42 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
 void forward_range(const PpsModel& m, const float* x, int N, float* feat, int first, int last,
                    hipStream_t st) {
   Workspace& w = workspace(m, N, st, true);
+  // the tensors whose maxima this forward needs
+  const bool all = m.amax_all || getenv_flag_on("PPS_AMAX_ALL");
+  w.amax_need.assign(m.slot.size(), all ? 1 : 0);
+  if (!all)
+    for (const Layer& L : m.layers)
+      if (L.tile & PPS_TILE_H2)
+        for (const std::string* t : {&L.input, &L.input2})
+          if (!t->empty() && m.slot.count(*t)) w.amax_need[m.slot.at(*t)] = 1;
+  if (first == 0) {
+    // a forward: every producer reports its output's max afresh
+    hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
+  } else {
+    // a layer range: the f32 tensors it reads but does not produce are
+    // measured afresh (their producers ran in an earlier call)
+    std::set<std::string> made, done;
+    for (int i = first; i < last; ++i) {
+      const Layer& L = m.layers[i];
+      for (const std::string* t : {&L.input, &L.input2}) {
+        if (t->empty() || made.count(*t) || done.count(*t) || !m.slot.count(*t) ||
+            !w.amax_need[m.slot.at(*t)])
+          continue;
+        bool planes = false;
+        for (const auto& P : m.layers)
+          if (P.output == *t && P.planes_out) planes = true;
+        const float* src = *t == "data" ? x : (w.bufs.count(*t) ? fbuf_of(w, *t) : nullptr);
+        if (planes || !src) continue;
+        float* slot = w.amax->as<float>() + m.slot.at(*t);
+        hip_check(hipMemsetAsync(slot, 0, sizeof(float), st), "hipMemsetAsync");
+        rc_check(amax_of(src, w.shapes.at(*t).numel(), slot, st));
+        done.insert(*t);
+      }
+      made.insert(L.output);
+      if (!L.conv_output.empty()) made.insert(L.conv_output);
+      if (L.seam_next >= 0 && (L.tile & PPS_TILE_SEAM)) made.insert(m.layers[L.seam_next].output);
+    }
+  }
   for (int i = first; i < last; ++i) {
     const Layer& L = m.layers[i];
     // computed by the previous layer's seam launch (when that ran here too)
@@ -920,7 +1058,7 @@ double layer_flops(const PpsModel& m, const Layer& L, const std::map<std::string
 // algorithmic HBM bytes per launch: every operand read once, the output
 // written once (model.py PPSModel._alloc)
 double layer_bytes(const PpsModel& m, const Layer& L, const std::map<std::string, Shape>& s, int N) {
-  const double wb = m.x3 ? 6.0 : 4.0;
+  const double wb = m.x3 && !(L.tile & PPS_TILE_H2) ? 6.0 : 4.0;  // f16x2 weights: 4 B
   switch (L.op) {
     case Op::StemPool:
       return 4.0 * s.at(L.input).numel() + 4.0 * s.at(L.output).numel() +
@@ -1120,6 +1258,7 @@ int pps_model_layer_info(const PpsModel* m, int i, int N, PpsLayerInfo* info) {
     info->bytes = layer_bytes(*m, L, shapes, N);
     const Shape& y = shapes.at(L.op == Op::ConvPps ? L.output : L.output);
     for (int d = 0; d < 4; ++d) info->out_shape[d] = y.d[d];
+    info->output = L.output.c_str();
   });
 }
 
@@ -1127,8 +1266,12 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
-    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM);
+    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM | PPS_TILE_H2);
     PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
+    PPS_MCHECK(!(tile & PPS_TILE_H2) || h2_tile_ok(*L, tile),
+               std::string("PPS_TILE_H2: '") + layer +
+                   "' has no f16x2 weights (Cin % 32 == 0) or the base tile is not 0, 38..53, "
+                   "55 or (3x3 convs) 56..59");
     PPS_MCHECK(!(tile & PPS_TILE_SEAM) ||
                    (L->seam_next >= 0 && base == GEMM_TILE_WS &&
                     !(tile & (PPS_TILE_B_TILED | PPS_TILE_COL_ORDER))),
@@ -1148,6 +1291,8 @@ int pps_model_set_splitk(PpsModel* m, const char* layer, int splitk) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(L->op == Op::Conv, std::string("split-K applies to plain convs, not '") + layer + "'");
+    PPS_MCHECK(splitk == 1 || !(L->tile & PPS_TILE_H2),
+               std::string("'") + layer + "' runs an f16x2 tile: no split-K");
     PPS_MCHECK(splitk >= 1 && splitk <= kMaxSplitK, "splitk must be in [1, 4]");
     PPS_MCHECK(splitk == 1 || (m->x3 && L->cin_eff % 32 == 0 && L->kpad == L->k * L->k * L->cin_eff &&
                                L->kpad % (32 * splitk) == 0),
@@ -1175,6 +1320,9 @@ int pps_model_set_planes(PpsModel* m, const char* producer, int on) {
     PPS_MCHECK(m && producer, "null argument");
     for (auto& e : m->edges)
       if (m->layers[e.first].name == producer) {
+        PPS_MCHECK(!on || !((m->layers[e.first].tile | m->layers[e.second].tile) & PPS_TILE_H2),
+                   std::string("plane edge '") + producer + "': an f16x2 (PPS_TILE_H2) layer "
+                   "takes and writes f32 activations");
         m->layers[e.first].planes_out = m->layers[e.second].planes_in = on != 0;
         return;
       }
@@ -1215,6 +1363,19 @@ int pps_model_tensor(const PpsModel* m, int N, const char* blob, void** ptr, int
       if (L.output == blob && L.planes_out) *planes = 1;
     const Shape& s = it->second.shapes.at(blob);
     for (int d = 0; d < 4; ++d) shape4[d] = s.d[d];
+  });
+}
+
+int pps_model_tensor_amax(const PpsModel* m, int N, const char* blob, float* out) {
+  return guarded([&] {
+    PPS_MCHECK(m && blob && out, "null argument");
+    auto it = m->ws.find(N);
+    PPS_MCHECK(it != m->ws.end(), "no workspace for this batch size (pps_model_reserve)");
+    auto s = m->slot.find(blob);
+    PPS_MCHECK(s != m->slot.end(), std::string("no activation-max slot for '") + blob + "'");
+    hip_check(hipMemcpy(out, it->second.amax->as<float>() + s->second, sizeof(float),
+                        hipMemcpyDeviceToHost),
+              "hipMemcpy");
   });
 }
 
@@ -1274,19 +1435,39 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
 #endif
     const int reps = 3, finalists = PPS_TUNE_FINALISTS, final_reps = 10, final_rounds = 3;
     Workspace* w = &workspace(*m, N, st, true);
+    // every candidate may be an f16x2 tile: all producers report maxima
+    struct AmaxAll {
+      const PpsModel* m;
+      ~AmaxAll() { m->amax_all = false; }
+    } amax_guard{m};
+    m->amax_all = true;
     std::vector<float> scratch((size_t)N * m->plan.feat_dim);
     DevBuf feat(scratch.size() * sizeof(float));
     forward_range(*m, x, N, feat.as<float>(), 0, (int)m->layers.size(), st);
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     Timer t;
+    // f16x2 candidates (PPS_TILE_H2) beside the bf16x3 tiles of a layer with
+    // f32 activations at both ends and no split-K
+    const bool try_h2 = m->x3 && !(flags & PPS_AUTOTUNE_NO_H2);
     auto cands_of = [&](const Layer& L) {
       std::vector<int> c;
+      const bool h2ok = try_h2 && L.w2 && !L.planes_in && !L.planes_out && L.splitk == 1;
       if (L.op == Op::ConvPps) {
         c = pps_tiles(*m, L, w->shapes.at(L.conv_output));
+        if (h2ok) {
+          const size_t n = c.size();
+          for (size_t i = 0; i < n; ++i)
+            if (c[i] >= GEMM_TILE_P16_FIRST) c.push_back(c[i] | PPS_TILE_H2);
+        }
       } else {
         const bool pipelined_only = L.planes_in || L.planes_out;
         for (int tl = pipelined_only ? GEMM_TILE_P_FIRST : 1; tl < GEMM_NUM_TILES; ++tl)
           c.push_back(tl);
+        if (h2ok)
+          for (int tl = GEMM_TILE_P16_FIRST; tl < GEMM_NUM_TILES; ++tl)
+            if (h2_tile_ok(L, tl | PPS_TILE_H2) &&
+                !(tl >= GEMM_TILE_C16_FIRST && (L.k != 3 || L.stride != 1)))
+              c.push_back(tl | PPS_TILE_H2);
       }
       if (c.empty()) c.push_back(0);
       return c;
@@ -1305,7 +1486,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS)
           for (int f : {PPS_TILE_B_TILED, PPS_TILE_COL_ORDER,
                         PPS_TILE_B_TILED | PPS_TILE_COL_ORDER})
-            if (!(f & PPS_TILE_B_TILED) || L.wt) var.push_back(tl | f);
+            if (!(f & PPS_TILE_B_TILED) || (L.wt && !(tl & PPS_TILE_H2))) var.push_back(tl | f);
       }
       std::vector<float> tmin(var.size(), 1e30f);
       for (int r = 0; r < final_rounds; ++r)

@@ -56,8 +56,11 @@ enum Epi {
   EPI_CONV = 0, EPI_DIST = 1, EPI_F_RELU = 2, EPI_F_RES = 4, EPI_F_DUAL = 8, EPI_F_RAW = 16,
   EPI_F_PLANES = 32,  // gemm_x3p.hip: result written as three bf16 planes (out3)
   EPI_F_PPS = 64,     // gemm_x3p.hip: + strip pooling and part power set of each image
-  EPI_F_FIX = 128     // gemm_x3p.hip conv split-K: the last K slice of a tile to finish
+  EPI_F_FIX = 128,    // gemm_x3p.hip conv split-K: the last K slice of a tile to finish
                       // sums the parked partials and runs the epilogue (no second pass)
+  EPI_F_H2 = 256      // gemm_x3p.hip / gemm_x3c.hip: f16x2 arithmetic (f32 activations
+                      // scaled by 2^s from their tensor's max and split into two f16
+                      // terms, weights as two f16 planes, three MFMA terms)
 };
 enum GemmTile {
   GEMM_TILE_AUTO = 0,
@@ -199,9 +202,17 @@ struct GemmParams {
   int64_t part_sstride;
   int* fix_cnt;
   // f16x2 distance GEMM (gemm_h2.hip): per-row power-of-two inverse scales of
-  // the A / B rows (the split stores x * 2^s, the dot product is scaled back)
+  // the A / B rows (the split stores x * 2^s, the dot product is scaled back);
+  // f16x2 convs (EPI_F_H2): rs_b = the weight rows' (output channels') scales
   const float* rs_a;
   const float* rs_b;
+  // activation maxima (f16x2 convs): amax_a / amax_a2 = max|x| of the A
+  // operand tensor(s), written by their producers; amax_out (any conv
+  // epilogue, may be null) receives max|y| of this launch's output by an
+  // atomic max on the float bits (the caller zeroes it before the producer)
+  const float* amax_a;
+  const float* amax_a2;
+  float* amax_out;
 };
 constexpr int kPpsFuseMaxStrips = 10;
 constexpr int kPpsFuseMaxCols = 256;  // widest tile the fused pooling takes (two column passes)
@@ -226,6 +237,48 @@ int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
 int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
 int x3c_tile_cols(int tile);
 
+// f16x2 activation split: x 2^s with s = 15 - E for max|x| = m 2^E, m in
+// [0.5, 1) (a zero max keeps 2^0; the exponent clamped to f32's range), so
+// max|x 2^s| lies in [2^14, 2^15).  Returns 2^s; *inv = 2^-s.
+__host__ __device__ inline float h2_scale_of(float amax, float* inv) {
+  const unsigned ebits = (__builtin_bit_cast(unsigned, amax) >> 23) & 0xffu;
+  int sh = ebits == 0 ? (amax > 0.f ? 126 : 0) : 15 - ((int)ebits - 126);
+  sh = sh > 126 ? 126 : (sh < -126 ? -126 : sh);
+  *inv = __builtin_bit_cast(float, (unsigned)(127 - sh) << 23);
+  return __builtin_bit_cast(float, (unsigned)(127 + sh) << 23);
+}
+
+// ---- op-level implementations behind the pps_conv* / pps_stem / pps_maxpool
+// entry points (abi.hip, stem.hip, feature_ops.hip), with the activation-max
+// plumbing the whole-network plan uses (model.hip): amax_out (may be null)
+// receives max|y| of the launch's output; w_rs != null selects the f16x2
+// arithmetic (two-plane chunk-tiled weights w, per-channel scales w_rs, the
+// input tensors' maxima amax_in / amax_in2)
+int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx, const void* w, int x3,
+              int Cout, int Kpad, int KH, int KW, int stride, int pad, int dil,
+              const float* scale, const float* shift, const float* residual, int relu, float* y,
+              int Ho, int Wo, int ldy, int tile, void* stream, const uint16_t* x_pl,
+              int64_t x_plane, uint16_t* y_pl, int64_t y_plane, int splitk, float* part,
+              int* fix_cnt, int64_t n_cnt, float* amax_out, const float* w_rs,
+              const float* amax_in);
+int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx, int KH, int KW, int stride,
+              int pad, const float* x2, int H2, int W2, int Cin2, int ldx2, int stride2,
+              const void* w, int x3, int Cout, int Kpad1, int Kpad2, const float* shift, int relu,
+              float* y, int Ho, int Wo, int ldy, int tile, void* stream, float* amax_out,
+              const float* w_rs, const float* amax_in, const float* amax_in2);
+int conv_pps_impl(const float* x, const uint16_t* x3, int64_t x_plane, int N, int H, int W,
+                  int Cin, int ldx, const uint16_t* w3, int Cout, int Kpad, int KH, int KW,
+                  int stride, int pad, int dil, const float* scale, const float* shift,
+                  const float* residual, float* y, int Ho, int Wo, const int32_t* splits, int S,
+                  int max_ave, float* pps_out, int tile, void* stream, const float* w_rs,
+                  const float* amax_in);
+int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const float* scale,
+                      const float* shift, float* y, int Hc, int Hp, hipStream_t st, float* amax);
+int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
+              int Ho, int Wo, hipStream_t st, float* amax);
+// max |x| of n floats into *amax (atomic max on the float bits; zero it first)
+int amax_of(const float* x, int64_t n, float* amax, hipStream_t st);
+
 // ---- f16x2 distance GEMM (gemm_h2.hip) ---------------------------------------
 constexpr int kH2NumTiles = 8;
 int launch_gemm_h2(const GemmParams& p, hipStream_t stream, int tile);
@@ -245,6 +298,8 @@ struct SeamParams {
   const float* t2a;
   float* y;              // [M][N2] next branch2a out
   int M;
+  float* amax_t = nullptr;  // max |trunk| / max |y| (atomic max, may be null)
+  float* amax_y = nullptr;
 };
 bool seam_supported(int K1, int N1, int N2);
 int launch_seam_x3(const SeamParams& p, int K1, int N1, int N2, hipStream_t st);

@@ -810,6 +810,40 @@ struct RrLayout {  // V-row capacities of a (k1, k2) configuration
 };
 }  // namespace
 
+// The N x N OD region of a call: the dense normalised distance, or in place
+// (symmetric, N >= 16384, 16-byte block rows) only q_g^T ([G][Q rounded up to
+// 4]; none with PPS_RERANK_WHOLE, where it is M's lower-left block) plus the
+// squared top-k's scratch.  The OD region is the workspace's first carve, so
+// its base is the workspace's (256-B aligned) and decides nothing here.
+static bool rr_inplace(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq,
+                       const float* gg, int64_t ldgg, int64_t Q, int64_t G, int K1, int flags,
+                       float* od) {
+  const bool whole = (flags & PPS_RERANK_WHOLE) != 0;
+  const RrMatrix M{qg, qq, gg, whole ? qq + Q * ldqq : od, ldqg, ldqq, ldgg,
+                   whole ? ldqq : (Q + 3) / 4 * 4, Q, G, nullptr};
+  return (flags & PPS_RERANK_SYMMETRIC) && topk_rr_eligible(M, K1) &&
+         getenv_flag_off("PPS_RERANK_INPLACE") == false;
+}
+
+static size_t rr_od_bytes(bool inplace, bool whole, int64_t Q, int64_t G, int K1) {
+  const int64_t N = Q + G;
+  if (!inplace) return sizeof(float) * (size_t)(N * od_stride(N));
+  const size_t tb = whole ? 0 : (sizeof(float) * (size_t)(G * ((Q + 3) / 4 * 4)) + 255) / 256 * 256;
+  return tb + topk_rr_sq_scratch_bytes(N, K1);
+}
+
+// Everything past the OD region
+static size_t rr_rest_bytes(int64_t Q, int64_t G, int k1, int k2) {
+  const int64_t N = Q + G;
+  const RrLayout L(k1, k2);
+  const int64_t K1 = L.K1, vcap = L.vcap, qcap = L.qcap;
+  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+  size_t s = r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
+  s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
+  s += r(4 * N) + r(4);   // V_qe overflow rows + count
+  return s;
+}
+
 int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const float* gg,
            int64_t ldgg, int64_t Q, int64_t G, int k1, int k2, double lambda, void* ws,
            size_t ws_bytes, float* out, hipStream_t st, int flags) {
@@ -820,6 +854,10 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   const RrLayout L(k1, k2);
   const int K1 = L.K1, Kh = L.Kh, vcap = L.vcap, qcap = L.qcap;
   const int64_t ldT = (Q + 3) / 4 * 4;
+  const bool whole = (flags & PPS_RERANK_WHOLE) != 0;
+  const bool inplace = rr_inplace(qg, ldqg, qq, ldqq, gg, ldgg, Q, G, K1, flags,
+                                  reinterpret_cast<float*>(ws));
+  const size_t odb = rr_od_bytes(inplace, whole, Q, G, K1);
   // workspace carve-up (all 256-B aligned)
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t bytes) {
@@ -827,7 +865,7 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
     p += (bytes + 255) / 256 * 256;
     return r;
   };
-  float* od = reinterpret_cast<float*>(take(sizeof(float) * N * ldo));
+  float* od = reinterpret_cast<float*>(take(odb));
   float* colmax = reinterpret_cast<float*>(take(sizeof(float) * N));
   float* topv = reinterpret_cast<float*>(take(sizeof(float) * N * K1));
   int32_t* rank = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * N * K1));
@@ -855,11 +893,8 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
   // compute (m * m) / colmax on the fly; q_g^T (the block that is nobody's
   // row) goes where OD would start.
   // PPS_RERANK_WHOLE: q_g^T is the matrix's own lower-left block
-  const bool whole = (flags & PPS_RERANK_WHOLE) != 0;
   RrMatrix M{qg, qq, gg, whole ? qq + Q * ldqq : od, ldqg, ldqq, ldgg, whole ? ldqq : ldT,
              Q, G, colmax};
-  const bool inplace = (flags & PPS_RERANK_SYMMETRIC) && topk_rr_eligible(M, K1) &&
-                       getenv_flag_off("PPS_RERANK_INPLACE") == false;
   // colmax = np.max(M^2, axis=0) (:453), from the four blocks of M (in place:
   // the top-k pass computes it, = the row maxima of the symmetric M)
   unsigned* cm = reinterpret_cast<unsigned*>(colmax);
@@ -886,12 +921,7 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
       PPS_CHECK_LAUNCH_S("rerank_transpose_kernel", st);
     }
     // scratch for the squared top-k: the OD region past q_g^T
-    const size_t tb = (sizeof(float) * (size_t)(G * ldT) + 255) / 256 * 256;
-    const size_t odb = sizeof(float) * (size_t)(N * ldo);
-    if (tb + topk_rr_sq_scratch_bytes(N, K1) > odb) {
-      set_error("rerank: OD region too small for the in-place top-k scratch");
-      return PPS_ERR_CAPACITY;
-    }
+    const size_t tb = whole ? 0 : (sizeof(float) * (size_t)(G * ldT) + 255) / 256 * 256;
     const int rc = topk_rr_sq(M, K1, colmax, reinterpret_cast<char*>(od) + tb, odb - tb, topv,
                               rank, st);
     if (rc != PPS_OK) return rc;
@@ -976,16 +1006,18 @@ int rerank(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq, const f
 }
 
 size_t rerank_workspace_bytes(int64_t Q, int64_t G, int k1, int k2) {
-  const int64_t N = Q + G;
-  const RrLayout L(k1, k2);
-  const int64_t K1 = L.K1, vcap = L.vcap, qcap = L.qcap;
-  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
-  size_t s = 0;
-  // the OD buffer also holds q_g^T ([G][Q rounded up to 4] <= N x od_stride)
-  s += r(4 * N * od_stride(N)) + r(4 * N) + r(4 * N * K1) * 2 + r(4 * N * vcap) * 2 + r(4 * N);
-  s += r(4 * N * qcap) * 2 + r(4 * N) + r(4 * (N + 1)) * 3 + r(4 * N * qcap) * 2;
-  s += r(4 * N) + r(4);   // V_qe overflow rows + count
-  return s;
+  // the dense path's size: enough for every call with these shapes
+  return (rr_od_bytes(false, false, Q, G, k1 + 1) + 255) / 256 * 256 + rr_rest_bytes(Q, G, k1, k2);
+}
+
+size_t rerank_workspace_bytes_for(const float* qg, int64_t ldqg, const float* qq, int64_t ldqq,
+                                  const float* gg, int64_t ldgg, int64_t Q, int64_t G, int k1,
+                                  int k2, int flags) {
+  // the OD region's base is 256-B aligned: any such pointer stands in for it
+  float* od_probe = reinterpret_cast<float*>((uintptr_t)256);
+  const bool inplace = rr_inplace(qg, ldqg, qq, ldqq, gg, ldgg, Q, G, k1 + 1, flags, od_probe);
+  const size_t odb = rr_od_bytes(inplace, (flags & PPS_RERANK_WHOLE) != 0, Q, G, k1 + 1);
+  return (odb + 255) / 256 * 256 + rr_rest_bytes(Q, G, k1, k2);
 }
 
 }  // namespace pps

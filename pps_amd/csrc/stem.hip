@@ -52,8 +52,9 @@ __global__ void __launch_bounds__(256, 2)
 stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
                          const uint16_t* __restrict__ w3, const float* __restrict__ scale,
                          const float* __restrict__ shift, float* __restrict__ y, int Hc,
-                         int Hp) {
+                         int Hp, float* __restrict__ amax) {
   extern __shared__ __attribute__((aligned(16))) unsigned char slds[];
+  float amx = 0.f;  // max of this thread's pooled outputs (ReLU: >= 0)
   uint16_t* tile = reinterpret_cast<uint16_t*>(slds);
   float* rowbuf = reinterpret_cast<float*>(slds + kStemTileBytes);
   const int n = blockIdx.x / tiles_h;
@@ -197,6 +198,8 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
           float* o = yimg + ((int64_t)ph * kStemWp + pw) * kStemCout + cg;
           *reinterpret_cast<f32x4*>(o) = cur0;
           *reinterpret_cast<f32x4*>(o + 4) = cur1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) amx = fmaxf(amx, fmaxf(cur0[e], cur1[e]));
         }
       }
       cur0 = h0;
@@ -211,6 +214,7 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
     __syncthreads();  // the row buffer is rewritten by the next conv row
     }
   }
+  if (amax) amax_commit(amax, amx);
 }
 
 // ---------------------------------------------------------------------------
@@ -247,8 +251,10 @@ constexpr int kRingThreads = 128 * RING_STREAMS;
 __global__ void __launch_bounds__(kRingThreads, 2)
 stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
                     const uint16_t* __restrict__ w3, const float* __restrict__ scale,
-                    const float* __restrict__ shift, float* __restrict__ y, int Hc, int Hp) {
+                    const float* __restrict__ shift, float* __restrict__ y, int Hc, int Hp,
+                    float* __restrict__ amax) {
   __shared__ __attribute__((aligned(16))) uint16_t ring[RING_STREAMS * 3 * kRingSlots * kRingRow];
+  float amx = 0.f;  // max of this thread's pooled outputs (ReLU: >= 0)
   const int n = blockIdx.x / tiles_h;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nb = wid & 1;        // channel half
@@ -433,7 +439,9 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int pw = 16 * (q >> 3) + 4 * ((q >> 1) & 3) + 2 * h + (q & 1);
-            o[pw * kStemCout] = fmaxf(cur[q], hp[q]);
+            const float v = fmaxf(cur[q], hp[q]);
+            o[pw * kStemCout] = v;
+            amx = fmaxf(amx, v);
           }
         }
       }
@@ -453,24 +461,26 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
     y[2 * blockIdx.x + 1] = (float)(rt1 - rt0);
   }
 #endif
+  if (amax) amax_commit(amax, amx);
 }
 
 static int g_stem_variant = 0;  // 0: ring-staged, 1: whole-tile staged + LDS epilogue
 
 int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const float* scale,
-                      const float* shift, float* y, int Hc, int Hp, hipStream_t st) {
+                      const float* shift, float* y, int Hc, int Hp, hipStream_t st,
+                      float* amax) {
   if (N <= 0) return PPS_OK;
   if (g_stem_variant == 0) {
     const int tiles_h = (Hp + kRingPR * RING_STREAMS - 1) / (kRingPR * RING_STREAMS);
     hipLaunchKernelGGL(stem_ring_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(kRingThreads), 0,
                        st, x,
-                       H, tiles_h, w3, scale, shift, y, Hc, Hp);
+                       H, tiles_h, w3, scale, shift, y, Hc, Hp, amax);
     PPS_CHECK_LAUNCH("stem_ring_x3_kernel");
     return PPS_OK;
   }
   const int tiles_h = (Hp + kStemPR - 1) / kStemPR;
   hipLaunchKernelGGL(stem_conv_pool_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(256),
-                     kStemLdsBytes, st, x, H, tiles_h, w3, scale, shift, y, Hc, Hp);
+                     kStemLdsBytes, st, x, H, tiles_h, w3, scale, shift, y, Hc, Hp, amax);
   PPS_CHECK_LAUNCH("stem_conv_pool_x3_kernel");
   return PPS_OK;
 }
@@ -501,7 +511,7 @@ int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w
               "output must be the 3x3/2 pad 1 max pool of the 7x7/2 pad 3 conv");
   PPS_ENFORCE(aligned16(x) && aligned16(w3) && aligned16(y), "16-byte aligned pointers");
   PPS_ENFORCE((int64_t)N * H * W * 4 < (1ll << 31), "input larger than 2^31 floats");
-  return stem_conv_pool_x3(x, N, H, w3, scale, shift, y, Hc, Hp, as_stream(stream));
+  return stem_conv_pool_x3(x, N, H, w3, scale, shift, y, Hc, Hp, as_stream(stream), nullptr);
 }
 
 }  // extern "C"

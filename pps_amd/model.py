@@ -370,6 +370,8 @@ class PPSModel(object):
             self.layers.append(L)
         if self.math == 'x3':
             for L in self.layers:
+                if L['op'] in ('conv', 'conv_dual'):
+                    L['w32'] = L['w']   # the f16x2 split is taken from it on first use
                 if L['op'] in ('conv', 'conv_dual', 'heads'):
                     L['w'] = ops.split_bf16x3(L['w'], batched=L['op'] == 'heads')
         if fused_stem is None:
@@ -582,10 +584,58 @@ class PPSModel(object):
         """Algorithmic HBM bytes of the GEMM launches of one forward."""
         return sum(L['bytes'] for L in self.layers if L['op'] in kinds)
 
+    def h2_capable(self, L):
+        """Whether PPS_TILE_H2 can run the layer (the C plan's h2_tile_ok):
+        a conv / fused-shortcut conv / conv_pps with Cin % 32 == 0 and no K
+        padding, ending in a ReLU."""
+        return (self.math == 'x3' and L['op'] in ('conv', 'conv_dual', 'conv_pps') and
+                'w32' in L and L['cin_eff'] % 32 == 0 and
+                L['kpad'] == L['k'] ** 2 * L['cin_eff'] and
+                (L['op'] != 'conv_dual' or L['shortcut_cin'] % 32 == 0) and
+                (L['op'] != 'conv' or L['relu']))
+
+    def _run_h2(self, L, bufs, tile):
+        """PPS_TILE_H2: the layer in f16x2 arithmetic (ops.conv2d_bn_act_h2 and
+        siblings); the input's max comes from ops.amax (the C plan's producers
+        report the same value from their epilogues, so the scale and the bits
+        agree)."""
+        if L.get('planes_in') or L.get('planes_out') or L.get('splitk', 1) > 1:
+            raise RuntimeError("layer '%s': PPS_TILE_H2 needs f32 activations at both ends "
+                               "and no split-K" % L.get('name', L['output']))
+        if '_w2' not in L:
+            L['_w2'] = ops.split_weights_h2(L['w32'])
+        w2, wrs = L['_w2']
+        base = tile & ~(ops.TILE_H2 | ops.TILE_B_TILED | ops.TILE_SEAM | ops.TILE_COL_ORDER)
+        flags = tile & ops.TILE_COL_ORDER
+        x = bufs[L['input']]
+        amx = ops.amax(x)
+        op = L['op']
+        if op == 'conv':
+            res = bufs[L['residual']] if L['residual'] else None
+            ops.conv2d_bn_act_h2(x, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
+                                 L['pad'], L['dil'], L['scale'], L['shift'], res, L['relu'],
+                                 bufs[L['output']], amx, tile=base | flags)
+        elif op == 'conv_dual':
+            x2 = bufs[L['input2']]
+            ops.conv2d_dual_bn_act_h2(x, L['cin_eff'], L['k'], L['stride'], L['pad'], x2,
+                                      L['stride2'], w2, wrs, L['kpad'], L['shift'], L['relu'],
+                                      bufs[L['output']], amx, ops.amax(x2), tile=base | flags)
+        else:   # conv_pps
+            ok = [t for t in self.pps_tiles(L) if t >= ops.TILE_P16_FIRST]
+            if not ok:
+                raise RuntimeError("layer '%s': no f16x2 tile holds one image" % L['name'])
+            t = (base if base in ok else ok[0]) | flags
+            ops.conv2d_bn_act_pps_h2(x, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
+                                     L['pad'], L['dil'], L['scale'], L['shift'],
+                                     bufs[L['residual']], L['split_arr'], L['max_ave'],
+                                     bufs[L['output']], amx, y=None, tile=t)
+
     def _run(self, L, bufs, out=None, tile=None, splitk=None):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
         tile &= ~ops.TILE_SEAM   # one layer alone (forward() runs the seam pairs)
+        if tile & ops.TILE_H2:
+            return self._run_h2(L, bufs, tile)
         sk = L.get('splitk', 1) if splitk is None else splitk
         w = L.get('w')
         # split convs run in one launch on the FIX tiles (same bits as the
@@ -682,6 +732,10 @@ class PPSModel(object):
                 # PPS_TILE_SEAM (set by the C autotune): this branch2c and the
                 # next block's branch2a in one launch, as the C plan runs them
                 fused = self.layers[i + 1]
+                if (L.get('planes_in') or L.get('planes_out') or fused.get('planes_out') or
+                        L.get('splitk', 1) > 1 or fused.get('splitk', 1) > 1):
+                    raise RuntimeError("layer '%s': PPS_TILE_SEAM needs f32 activations at "
+                                       "both ends and no split-K" % L['name'])
                 ops.conv1x1_seam(bufs[L['input']], L['w'], L['scale'], L['shift'],
                                  bufs[L['residual']], bufs[L['output']], fused['w'],
                                  fused['scale'], fused['shift'], bufs[fused['output']])
@@ -831,9 +885,40 @@ class PPSModel(object):
         return {L.get('name', L['output']): int(L.get('tile', 0)) for L in self.layers
                 if L['op'] in ('conv', 'conv_dual', 'heads', 'conv_pps')}
 
+    def _check_tile(self, i, tile):
+        """The C plan's set_tile / seam_ok / h2_tile_ok conditions: a table
+        the C plan refuses is refused here too (a stale or hand-edited table
+        must not run a wrong launch silently)."""
+        L = self.layers[i]
+        name = L.get('name', L['output'])
+        if tile & ops.TILE_SEAM:
+            X = self.layers[i + 1] if i + 1 < len(self.layers) else None
+
+            def plain1x1(A):
+                return (A['op'] == 'conv' and A['k'] == 1 and A['stride'] == 1 and
+                        A['pad'] == 0 and A['relu'] and A['kpad'] == A['cin_eff'])
+            ok = (self.math == 'x3' and X is not None and plain1x1(L) and plain1x1(X) and
+                  L.get('residual') and not X.get('residual') and X['input'] == L['output'] and
+                  X['cin_eff'] == L['cout'] and
+                  (L['cin_eff'], L['cout'], X['cout']) in ((64, 256, 64), (128, 512, 128)) and
+                  (tile & ~ops.TILE_SEAM) == ops.TILE_WS)
+            if not ok:
+                raise ValueError("PPS_TILE_SEAM: '%s' is not a branch2c feeding a seam-capable "
+                                 "branch2a (base tile 54)" % name)
+        if tile & ops.TILE_H2:
+            base = tile & 0xff
+            if not self.h2_capable(L) or not (
+                    base == 0 or (ops.TILE_P16_FIRST <= base <= ops.num_tiles() and
+                                  base != ops.TILE_WS and
+                                  (L['op'] == 'conv' or base < ops.TILE_C16_FIRST))):
+                raise ValueError("PPS_TILE_H2: '%s' has no f16x2 arithmetic or the base tile "
+                                 "%d is not 0, 38..53, 55 or (3x3 convs) 56..59" % (name, base))
+
     def set_tiles(self, tiles):
-        """Apply a tiles() mapping (e.g. a saved autotune result)."""
-        for L in self.layers:
+        """Apply a tiles() mapping (e.g. a saved autotune result).  Seam and
+        f16x2 flags are validated as the C plan does."""
+        for i, L in enumerate(self.layers):
             k = L.get('name', L['output'])
             if k in tiles:
+                self._check_tile(i, int(tiles[k]))
                 L['tile'] = int(tiles[k])

@@ -21,7 +21,7 @@ from ._lib import call
 from .config import cfg as _cfg
 
 MATH = {'x3': 0, 'f32': 1}
-AUTOTUNE_NO_PLANES, AUTOTUNE_SPLITK = 1, 2
+AUTOTUNE_NO_PLANES, AUTOTUNE_SPLITK, AUTOTUNE_NO_SEAM, AUTOTUNE_NO_H2 = 1, 2, 4, 8
 
 
 class PpsBlob(ctypes.Structure):
@@ -42,7 +42,7 @@ class PpsLayerInfo(ctypes.Structure):
                 ('splitk', ctypes.c_int), ('planes_in', ctypes.c_int),
                 ('planes_out', ctypes.c_int), ('gemm', ctypes.c_int),
                 ('flops', ctypes.c_double), ('bytes', ctypes.c_double),
-                ('out_shape', ctypes.c_int64 * 4)]
+                ('out_shape', ctypes.c_int64 * 4), ('output', ctypes.c_char_p)]
 
 
 def _env_flag(name):
@@ -126,7 +126,7 @@ class NativeModel(object):
                             splitk=info.splitk, planes_in=bool(info.planes_in),
                             planes_out=bool(info.planes_out), gemm=bool(info.gemm),
                             flops=info.flops, bytes=info.bytes,
-                            out_shape=tuple(info.out_shape)))
+                            out_shape=tuple(info.out_shape), output=info.output.decode()))
         return out
 
     def tiles(self):
@@ -264,6 +264,14 @@ class NativeModel(object):
         raw = (ctypes.c_float * n)()
         _memcpy_d2h(raw, p.value, 4 * n)
         return np.frombuffer(raw, np.float32).reshape(tuple(shape)).copy()
+
+    def tensor_amax(self, N, blob):
+        """max |t| the producer of tensor `blob` reported in the last forward
+        at batch N (the f16x2 layers' input scales)."""
+        torch.cuda.synchronize()
+        v = ctypes.c_float()
+        call('pps_model_tensor_amax', self._h, int(N), blob.encode(), ctypes.addressof(v))
+        return float(v.value)
 
 
 _HIP = None

@@ -24,6 +24,9 @@ TILE_C16_FIRST = 56  # patch-staged 3x3 tiles (gemm_x3c.hip): K in (channel chun
 TILE_B_TILED = 0x100  # PPS_TILE_B_TILED: or-ed into a conv tile, the weights are chunk-tiled
 TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (same bits)
 TILE_SEAM = 0x400  # PPS_TILE_SEAM (whole-network plan): branch2c + next branch2a in one launch
+TILE_H2 = 0x800    # PPS_TILE_H2 (whole-network plan): the layer in f16x2 arithmetic
+TILE_WS = 54       # the weight-stationary 1x1 tile (gemm_ws.hip)
+TILE_FLAGS = TILE_B_TILED | TILE_COL_ORDER | TILE_SEAM | TILE_H2   # every or-ed flag
 # tiles built with the one-launch split-K epilogue (conv2d_bn_act_x3p(..., counters=))
 FIX_TILES = (45, 47, 48, 49, 50)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)
@@ -629,14 +632,16 @@ def re_ranking(q_g, q_q, g_g, k1=20, k2=6, lambda_value=0.3, symmetric=None, who
     if symmetric is None:
         symmetric = bool(getattr(q_q, '_pps_symmetric', False) and
                          getattr(g_g, '_pps_symmetric', False))
-    nbytes = _lib.lib().pps_rerank_workspace_bytes(Q, G, k1, k2)
+    flags = (RERANK_SYMMETRIC if symmetric else 0) | (RERANK_WHOLE if whole else 0)
+    blocks = (_dev_rows(q_g, 'q_g'), _ld(q_g), _dev_rows(q_q, 'q_q'), _ld(q_q),
+              _dev_rows(g_g, 'g_g'), _ld(g_g))
+    # the size of the path this call takes (in place: no N x N region)
+    nbytes = _lib.lib().pps_rerank_workspace_bytes_ld(*blocks, Q, G, k1, k2, flags)
     if nbytes < 0:
         raise RuntimeError('bad re-ranking arguments')
     ws = torch.empty((int(nbytes),), dtype=torch.uint8, device=q_g.device)
     out = torch.empty((Q, G), dtype=torch.float32, device=q_g.device)
-    call('pps_re_ranking_ld', _dev_rows(q_g, 'q_g'), _ld(q_g), _dev_rows(q_q, 'q_q'), _ld(q_q),
-         _dev_rows(g_g, 'g_g'), _ld(g_g), Q, G, k1, k2, float(lambda_value),
-         (RERANK_SYMMETRIC if symmetric else 0) | (RERANK_WHOLE if whole else 0),
+    call('pps_re_ranking_ld', *blocks, Q, G, k1, k2, float(lambda_value), flags,
          ws.data_ptr(), int(nbytes), out.data_ptr(), _stream())
     return out
 
@@ -851,6 +856,85 @@ def conv2d_dual_bn_act(x, cin, k, stride, pad, x2, stride2, w, kpad1, shift, rel
          _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout, int(tile),
          _stream())
     return y
+
+
+# ---- f16x2 convolutions (include/pps_abi.h "f16x2 convolutions") ----------
+def split_weights_h2(w_packed):
+    """Packed [Cout, Kpad] f32 conv weights (Kpad % 32 == 0) -> (w2t, wrs):
+    the two chunk-tiled f16 planes [2, Cout16, Kpad] (int16) and the
+    per-output-channel inverse scales [Cout] the f16x2 conv entries take."""
+    planes, rs, _ = split_h2_tiled(w_packed.contiguous())
+    return planes, rs
+
+
+def amax(x, out=None):
+    """max |x| as a device float [1] (pps_amax: atomic max, zeroed here)."""
+    if out is None:
+        out = torch.zeros((1,), dtype=torch.float32, device=x.device)
+    else:
+        out.zero_()
+    call('pps_amax', _dev(x, 'x'), x.numel(), _dev(out, 'amax'), _stream())
+    return out
+
+
+def _amax_arg(a, name):
+    if a is None:
+        return 0
+    return _dev(a, name)
+
+
+def conv2d_bn_act_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, residual, relu, y,
+                     amax_x, amax_y=None, tile=0):
+    """conv2d_bn_act in f16x2 arithmetic (pps_conv2d_bn_act_h2): w2 / wrs from
+    split_weights_h2, amax_x = max|x| as a device float (amax() or the
+    producer's amax_y), amax_y (optional, zeroed by the caller) receives
+    max|y|."""
+    N, H, W, ldx = x.shape
+    _, Ho, Wo, Cout = y.shape
+    rp = 0
+    if residual is not None:
+        if tuple(residual.shape) != tuple(y.shape):
+            raise RuntimeError('residual shape %s != output %s'
+                               % (tuple(residual.shape), tuple(y.shape)))
+        rp = _dev(residual, 'residual')
+    call('pps_conv2d_bn_act_h2', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w2, 'w2t', torch.int16),
+         _dev(wrs, 'wrs'), Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'),
+         _dev(shift, 'shift'), rp, int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout,
+         _dev(amax_x, 'amax_x'), _amax_arg(amax_y, 'amax_y'), int(tile), _stream())
+    return y
+
+
+def conv2d_dual_bn_act_h2(x, cin, k, stride, pad, x2, stride2, w2, wrs, kpad1, shift, relu, y,
+                          amax_x, amax_x2, amax_y=None, tile=0):
+    """conv2d_dual_bn_act in f16x2 arithmetic (pps_conv2d_dual_bn_act_h2)."""
+    N, H, W, ldx = x.shape
+    _, H2, W2, C2 = x2.shape
+    _, Ho, Wo, Cout = y.shape
+    call('pps_conv2d_dual_bn_act_h2', _dev(x, 'x'), N, H, W, cin, ldx, k, k, stride, pad,
+         _dev(x2, 'x2'), H2, W2, C2, C2, stride2, _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'),
+         Cout, kpad1, C2, _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout,
+         _dev(amax_x, 'amax_x'), _dev(amax_x2, 'amax_x2'), _amax_arg(amax_y, 'amax_y'),
+         int(tile), _stream())
+    return y
+
+
+def conv2d_bn_act_pps_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, residual,
+                         split, max_ave, pps_out, amax_x, y=None, tile=0):
+    """conv2d_bn_act_pps in f16x2 arithmetic (pps_conv2d_bn_act_pps_h2)."""
+    N, H, W, ldx = x.shape
+    nsub, n2, Cout = pps_out.shape
+    split = np.ascontiguousarray(split, dtype=np.int32)
+    Ho = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    if nsub != (1 << len(split)) - 1 or n2 != N:
+        raise RuntimeError('pps_out must be [2^S - 1, N, Cout]')
+    call('pps_conv2d_bn_act_pps_h2', _dev(x, 'x'), N, H, W, cin, ldx,
+         _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'), Cout, kpad, k, k, stride, pad, dil,
+         _dev(scale, 'scale'), _dev(shift, 'shift'), _dev(residual, 'residual'),
+         _dev(y, 'y') if y is not None else 0, Ho, Wo,
+         split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
+         _dev(pps_out, 'pps_out'), _dev(amax_x, 'amax_x'), int(tile), _stream())
+    return pps_out
 
 
 def gemm_bn_act_batched(x, w, scale, shift, relu, y, tile=0):

@@ -337,14 +337,20 @@ def test_duke_full_size_cosine_rerank_properties():
     print('Duke full size: re-ranked %s' % r)
 
 
-def test_rerank_whole_matrix_blocks():
+@pytest.mark.parametrize('Q', [1000, 1001])
+def test_rerank_whole_matrix_blocks(Q):
     """re-ranking inputs as the blocks of ONE mirrored self-distance of
     [queries; gallery] (ops.self_distance_blocks, PPS_RERANK_WHOLE: q_g^T read
     from the matrix's lower-left block, no transpose): the blocks equal the
     three separate compute_dist calls bit for bit, and so does the re-ranked
-    result (in place, N >= 16384); the flag is refused on separate buffers."""
-    from pps_amd import ops
-    Q, G, D = 1000, 15500, 64
+    result (Q = 1000: in place, N >= 16384, with a workspace that holds no
+    N x N region; Q = 1001: q_g's rows are not 16-byte aligned, the dense
+    path runs on the dense workspace); the flag is refused on separate
+    buffers, and the ranking of the (possibly misaligned) q_g view equals
+    that of its contiguous copy."""
+    from pps_amd import _lib, ops
+    from pps_amd import reid_dataset_evaluator as gev
+    G, D = 15500, 64
     gen = torch.Generator(device='cuda')
     gen.manual_seed(11)
     rng = np.random.RandomState(11)
@@ -361,3 +367,20 @@ def test_rerank_whole_matrix_blocks():
     assert torch.equal(a, b)
     with pytest.raises(RuntimeError, match='PPS_RERANK_WHOLE'):
         ops.re_ranking(sq_g, sq_q, sg_g, 20, 6, 0.3, symmetric=True, whole=True)
+    L = _lib.lib()
+    dense = L.pps_rerank_workspace_bytes(Q, G, 20, 6)
+    need = L.pps_rerank_workspace_bytes_ld(q_g.data_ptr(), M.stride(0), q_q.data_ptr(),
+                                           M.stride(0), g_g.data_ptr(), M.stride(0), Q, G, 20,
+                                           6, ops.RERANK_SYMMETRIC | ops.RERANK_WHOLE)
+    N = Q + G
+    if Q % 4 == 0:
+        assert need < dense - 4 * N * N + 4 * N * 64, (need, dense)   # no N x N region
+    else:
+        assert need == dense
+    rng2 = np.random.RandomState(12)
+    qid, gid = rng2.randint(0, 300, Q), rng2.randint(0, 300, G)
+    qcam, gcam = rng2.randint(0, 6, Q), rng2.randint(0, 6, G)
+    r1 = gev.rank_eval(q_g, qid, gid, qcam, gcam)
+    r2 = gev.rank_eval(q_g.contiguous(), qid, gid, qcam, gcam)
+    for u, v in zip(r1, r2):
+        assert torch.equal(u, v)

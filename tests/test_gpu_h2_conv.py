@@ -1,0 +1,180 @@
+"""The f16x2 ("h2") convolutions (EPI_F_H2 tiles of gemm_x3p.hip / gemm_x3c.hip,
+include/pps_abi.h "f16x2 convolutions"):
+
+* error: against an fp64 reference the h2 kernels' max error stays within
+  H2_VS_X3 x the bf16x3 kernel's on the same data (the x3 kernels are held
+  to 4x the exact-f32 MFMA kernel's in test_gpu_x3.py) -- f32-level, far
+  from f16 (~5e-4) -- also for inputs scaled by 1e-20 / 1e20 (the per-tensor
+  power-of-two scale keeps them inside the f16 range);
+* every tile of a rounding group gives the same bits (16x16x32 pipelined
+  38..55; patch tiles 56..59 run K in (channel chunk, tap) order);
+* amax_y is max|y| exactly, and the activation max every producer reports
+  (x3 tiles, the weight-stationary tile, the fused stem, max pooling) equals
+  max|y| of its output.
+"""
+import numpy as np
+from _tiles import check_tile_bits
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+H2_VS_X3 = 3.0       # max error of h2 <= H2_VS_X3 * max error of x3 (+ floor)
+ERR_FLOOR = 2e-7     # relative to max |ref|
+
+
+def _cuda(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+
+
+def _rel_err(got, ref):
+    return float(np.abs(got.astype(np.float64) - ref).max() / max(1e-30, np.abs(ref).max()))
+
+
+def _h2_tiles():
+    from pps_amd import ops
+    return [0] + [t for t in range(ops.TILE_P16_FIRST, ops.num_tiles() + 1) if t != 54]
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 24, 8, 256, 256, 3, 1, 1),     # res4 branch2b (patch tiles apply)
+    (1, 24, 8, 512, 512, 3, 1, 1),     # res5 branch2b
+    (2, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
+    (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1 (STRIDE_1X1 branch2a)
+    (2, 96, 32, 64, 64, 3, 1, 1),      # res2 branch2b
+    (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+])
+@pytest.mark.parametrize('residual', [False, True])
+@pytest.mark.parametrize('mag', [1.0, 1e-20, 1e20])
+def test_conv_h2_error_tiles_amax(N, H, W, Cin, Cout, k, s, p, residual, mag):
+    from pps_amd import model, ops
+    if mag != 1.0 and (k != 3 or Cin != 256 or residual):
+        pytest.skip('magnitude sweep on one shape')
+    rng = np.random.RandomState(N + H + Cin + Cout + k)
+    x = (rng.randn(N, Cin, H, W) * mag).astype(np.float32)
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    scale = rng.uniform(0.5, 1.5, Cout).astype(np.float32)
+    shift = (rng.randn(Cout) * 0.1 * mag).astype(np.float32)
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w).double(), stride=s,
+                   padding=p)
+    ref = ref * torch.from_numpy(scale).double()[None, :, None, None] + \
+        torch.from_numpy(shift).double()[None, :, None, None]
+    res = None
+    if residual:
+        res_np = (rng.randn(*ref.shape) * mag).astype(np.float32)
+        ref = ref + torch.from_numpy(res_np).double()
+        res = _cuda(res_np.transpose(0, 2, 3, 1))
+    ref = torch.clamp_min(ref, 0).numpy().transpose(0, 2, 3, 1)
+    wp, kpad = model.pack_conv_weight(w)
+    xd = _cuda(x.transpose(0, 2, 3, 1))
+    y = torch.empty(ref.shape, dtype=torch.float32, device='cuda')
+    ops.conv2d_bn_act(xd, Cin, ops.split_bf16x3(_cuda(wp)), kpad, k, s, p, 1, _cuda(scale),
+                      _cuda(shift), res, True, y, tile=ops.TILE_P16_FIRST)
+    e_x3 = _rel_err(y.cpu().numpy(), ref)
+    w2, wrs = ops.split_weights_h2(_cuda(wp))
+    amx = ops.amax(xd)
+    assert float(amx) == float(np.abs(x).max())
+    tiles = _h2_tiles()
+    outs = []
+    for tile in tiles:
+        y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+        ay = torch.zeros((1,), device='cuda')
+        ops.conv2d_bn_act_h2(xd, Cin, w2, wrs, kpad, k, s, p, 1, _cuda(scale), _cuda(shift), res,
+                             True, y, amx, ay, tile=tile)
+        yn = y.cpu().numpy()
+        assert float(ay) == float(np.abs(yn).max()), tile
+        outs.append(yn)
+    for t, o in zip(tiles, outs):
+        e_h2 = _rel_err(o, ref)
+        assert e_h2 <= H2_VS_X3 * e_x3 + ERR_FLOOR, (t, e_h2, e_x3)
+    print('conv h2 err %.3g  x3 err %.3g' % (_rel_err(outs[0], ref), e_x3))
+    check_tile_bits(tiles, outs, ops.TILE_P16_FIRST)
+
+
+@pytest.mark.parametrize('N,H,W,C1,C2,Cout,s2', [(2, 24, 8, 128, 256, 512, 2),
+                                                 (1, 24, 8, 512, 1024, 2048, 1),
+                                                 (2, 96, 32, 64, 64, 256, 1),
+                                                 (1, 12, 8, 32, 32, 64, 2)])
+def test_conv_dual_h2(N, H, W, C1, C2, Cout, s2):
+    """The fused projection shortcut: both operands scaled by the larger of
+    their two maxima (here 100x apart), one K-concatenated f16x2 GEMM."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(C1 + Cout)
+    x = rng.randn(N, C1, H, W).astype(np.float32)
+    x2 = (rng.randn(N, C2, (H - 1) * s2 + 1, (W - 1) * s2 + 1) * 100).astype(np.float32)
+    w1 = (rng.randn(Cout, C1, 1, 1) / np.sqrt(C1)).astype(np.float32)
+    w2 = (rng.randn(Cout, C2, 1, 1) / np.sqrt(C2) / 100).astype(np.float32)
+    sh = rng.randn(Cout).astype(np.float32)
+    p1, k1 = model.pack_conv_weight(w1)
+    p2, _ = model.pack_conv_weight(w2)
+    w = np.concatenate([p1, p2], 1)
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w1).double()) + \
+        F.conv2d(torch.from_numpy(x2).double(), torch.from_numpy(w2).double(), stride=s2) + \
+        torch.from_numpy(sh).double()[:, None, None]
+    ref = torch.clamp_min(ref, 0).numpy().transpose(0, 2, 3, 1)
+    xd, x2d = _cuda(x.transpose(0, 2, 3, 1)), _cuda(x2.transpose(0, 2, 3, 1))
+    y = torch.empty(ref.shape, device='cuda')
+    ops.conv2d_dual_bn_act(xd, C1, 1, 1, 0, x2d, s2, ops.split_bf16x3(_cuda(w)), k1, _cuda(sh),
+                           True, y, tile=ops.TILE_P16_FIRST)
+    e_x3 = _rel_err(y.cpu().numpy(), ref)
+    wq, wrs = ops.split_weights_h2(_cuda(w))
+    tiles = [0] + [t for t in range(ops.TILE_P16_FIRST, 56) if t != 54]
+    outs = []
+    for tile in tiles:
+        y = torch.full(ref.shape, float('nan'), device='cuda')
+        ay = torch.zeros((1,), device='cuda')
+        ops.conv2d_dual_bn_act_h2(xd, C1, 1, 1, 0, x2d, s2, wq, wrs, k1, _cuda(sh), True, y,
+                                  ops.amax(xd), ops.amax(x2d), ay, tile=tile)
+        yn = y.cpu().numpy()
+        assert float(ay) == float(np.abs(yn).max())
+        outs.append(yn)
+    for t, o in zip(tiles, outs):
+        assert _rel_err(o, ref) <= H2_VS_X3 * e_x3 + ERR_FLOOR, (t, _rel_err(o, ref), e_x3)
+    check_tile_bits(tiles, outs, ops.TILE_P16_FIRST)
+
+
+def test_conv_pps_h2_equals_conv_then_pooling():
+    """The last conv with the part pooling fused (f16x2): the pooled subsets
+    equal part_power_set of the same tile group's conv output bit for bit."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(5)
+    N, H, W, Cin, Cout = 2, 24, 8, 512, 256
+    x = np.maximum(rng.randn(N, H, W, Cin), 0).astype(np.float32)
+    w = (rng.randn(Cout, Cin, 1, 1) / np.sqrt(Cin)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, Cout).astype(np.float32)
+    sh = (rng.randn(Cout) * 0.1).astype(np.float32)
+    res = np.maximum(rng.randn(N, H, W, Cout), 0).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w2, wrs = ops.split_weights_h2(_cuda(wp))
+    xd = _cuda(x)
+    amx = ops.amax(xd)
+    split = [5, 5, 5, 5, 4]
+    y = torch.empty((N, H, W, Cout), device='cuda')
+    ops.conv2d_bn_act_h2(xd, Cin, w2, wrs, kpad, 1, 1, 0, 1, _cuda(sc), _cuda(sh), _cuda(res),
+                         True, y, amx, tile=ops.TILE_P16_FIRST)
+    want = torch.empty((31, N, Cout), device='cuda')
+    ops.part_power_set(y, split, True, want)
+    for tile in (39, 46, 47, 52):
+        got = torch.full((31, N, Cout), float('nan'), device='cuda')
+        y2 = torch.full((N, H, W, Cout), float('nan'), device='cuda')
+        ops.conv2d_bn_act_pps_h2(xd, Cin, w2, wrs, kpad, 1, 1, 0, 1, _cuda(sc), _cuda(sh),
+                                 _cuda(res), split, True, got, amx, y=y2, tile=tile)
+        assert torch.equal(got, want), tile
+        assert torch.equal(y2, y), tile
+
+
+def test_conv_h2_enforces():
+    from pps_amd import model, ops
+    x = torch.zeros((1, 8, 8, 64), device='cuda')
+    w = np.zeros((64, 64, 1, 1), np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w2, wrs = ops.split_weights_h2(_cuda(wp))
+    y = torch.empty((1, 8, 8, 64), device='cuda')
+    one = torch.ones((64,), device='cuda')
+    with pytest.raises(RuntimeError, match='relu|ReLU'):   # f16x2 epilogues end in a ReLU
+        ops.conv2d_bn_act_h2(x, 64, w2, wrs, kpad, 1, 1, 0, 1, one, one, None, False, y,
+                             ops.amax(x))
+    with pytest.raises(RuntimeError, match='tile'):
+        ops.conv2d_bn_act_h2(x, 64, w2, wrs, kpad, 1, 1, 0, 1, one, one, None, True, y,
+                             ops.amax(x), tile=30)

@@ -1,0 +1,145 @@
+"""The f16x2 layers in the whole-network plan (PPS_TILE_H2, include/pps_abi.h):
+
+* every producer reports max|y| of its output in the forward (x3 pipelined,
+  patch, weight-stationary and register-staged tiles, the bottleneck seam,
+  the fused stem and the unfused max pooling): the slot equals max|t| of the
+  tensor exactly -- these are the f16x2 layers' input scales;
+* a table with PPS_TILE_H2 layers (every base tile family) runs the same
+  bits in the C plan and in the Python orchestrator (which measures its
+  inputs' maxima with pps_amax), also under hipGraph replay, and stays
+  within FWD_ATOL of the CPU oracle;
+* the C autotune with f16x2 candidates gives a table the Python orchestrator
+  reproduces bit for bit;
+* the plan refuses PPS_TILE_H2 where it cannot run."""
+import numpy as np
+import pytest
+import torch
+
+from tests.test_gpu_native import FWD_ATOL, _input, _models
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('variant', ['default', 'mixed_tiles', 'unfused_stem'])
+def test_producers_report_tensor_max(variant, monkeypatch):
+    from pps_amd import ops
+    monkeypatch.setenv('PPS_AMAX_ALL', '1')   # all producers, not only those h2 layers read
+    kw = dict(fused_stem=False) if variant == 'unfused_stem' else {}
+    _, pm, nm = _models(seed=3, **kw)
+    N = 2
+    _, x = _input(N, seed=4)
+    if variant == 'mixed_tiles':
+        # register-staged, pipelined 32x32 / 16x16, weight-stationary, patch
+        # and a seam pair -- every epilogue family reports its maximum
+        fam = [1, 11, 22, 30, 36, 40, 47, 52, 54, 56]
+        t = {}
+        for i, L in enumerate(nm.layers(N)):
+            if L['op'] in ('conv', 'conv_dual'):
+                t[L['name']] = fam[i % len(fam)]
+        t['res2_1_branch2c'] = 54 | ops.TILE_SEAM
+        nm.set_planes([])
+        nm.set_tiles(t)
+    nm.forward(x)
+    checked = 0
+    for L in nm.layers(N):
+        if L['op'] not in ('conv', 'conv_dual', 'maxpool', 'stem_pool') or L['planes_out']:
+            continue
+        t = nm.tensor(N, L['output'])
+        got = nm.tensor_amax(N, L['output'])
+        assert got == float(np.abs(t).max()), (L['output'], got, float(np.abs(t).max()))
+        checked += 1
+    assert checked >= 35
+
+
+def _h2_table(nm, N):
+    """Every f16x2-capable layer on an f16x2 tile, cycling the base families."""
+    from pps_amd import ops
+    fam = [0, 38, 43, 47, 50, 52, 55, 56, 59]
+    t = {}
+    k = 0
+    for L in nm.layers(N):
+        if L['op'] in ('conv', 'conv_dual', 'conv_pps'):
+            t[L['name']] = L['tile']
+    for name in list(t):
+        L = next(M for M in nm.layers(N) if M['name'] == name)
+        base = fam[k % len(fam)]
+        k += 1
+        if L['op'] == 'conv_dual' and base >= 56:
+            base = 47
+        if L['op'] == 'conv_pps':
+            base = 47
+        t[name] = base | ops.TILE_H2
+    return t
+
+
+def test_h2_table_c_plan_equals_twin_and_oracle():
+    from oracle.forward import GraphForward
+    from pps_amd import ops
+    blobs, pm, nm = _models(seed=5)
+    N = 3
+    x, xd = _input(N, seed=6)
+    nm.set_planes([])
+    pm.set_planes([])
+    table = _h2_table(nm, N)
+    ok = {}
+    for name, t in table.items():   # the layers the plan accepts (Cin % 32 == 0)
+        try:
+            nm.set_tiles({name: t})
+            ok[name] = t
+        except RuntimeError:
+            nm.set_tiles({name: 0})
+    assert len(ok) >= 45, len(ok)
+    pm.set_tiles(ok)
+    a = pm.forward(xd).cpu().numpy()
+    b = nm.forward(xd).cpu().numpy()
+    assert np.array_equal(a, b)
+    ref = GraphForward(blobs)(x).numpy()
+    err = float(np.abs(b - ref).max())
+    print('f16x2 table (%d layers) forward max|err| vs oracle %.3g' % (len(ok), err))
+    assert err <= FWD_ATOL
+    # graph replay (the amax slots are zeroed by a memset node every replay)
+    nm.reserve(N)
+    out = torch.empty((N, nm.feat_dim), device='cuda')
+    nm.forward(xd, out=out)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nm.forward(xd, out=out)
+    out.zero_()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), b)
+
+
+def test_autotune_with_h2_candidates_then_twin():
+    from pps_amd import ops
+    _, pm, nm = _models(seed=7)
+    _, x = _input(2, seed=8)
+    tiles = nm.autotune(x)
+    nh2 = sum(1 for t in tiles.values() if t & ops.TILE_H2)
+    print('autotune: %d of %d layers on f16x2 tiles' % (nh2, len(tiles)))
+    pm.set_tiles(tiles)
+    pm.set_planes(nm.planes())
+    pm.set_splitks(nm.splitks())
+    assert np.array_equal(pm.forward(x).cpu().numpy(), nm.forward(x).cpu().numpy())
+    # the flag keeps the bf16x3 table
+    tiles2 = nm.autotune(x, flags=8)
+    assert not any(t & ops.TILE_H2 for t in tiles2.values())
+
+
+def test_h2_tile_refused_where_it_cannot_run():
+    from pps_amd import ops
+    _, pm, nm = _models(seed=9)
+    with pytest.raises(RuntimeError, match='PPS_TILE_H2'):
+        nm.set_tiles({'reid_feature_concat_norm': 38 | ops.TILE_H2})   # heads
+    with pytest.raises(RuntimeError, match='PPS_TILE_H2'):
+        nm.set_tiles({'res2_0_branch2b': 30 | ops.TILE_H2})           # a 32x32 tile
+    with pytest.raises(ValueError, match='PPS_TILE_H2'):
+        pm.set_tiles({'res2_0_branch2b': 30 | ops.TILE_H2})
+    # a plane edge into an f16x2 layer is refused, in either order
+    edges = nm.plane_edges()
+    p, c, _ = edges[0]
+    nm.set_planes([])
+    nm.set_tiles({c: 38 | ops.TILE_H2})
+    with pytest.raises(RuntimeError, match='f16x2'):
+        nm.set_planes([p])

@@ -131,7 +131,7 @@ def test_native_autotune_then_python_twin():
     _, x = _input(2, seed=2)
     tiles = nm.autotune(x)
     from pps_amd import ops
-    assert all(0 <= (t & ~(ops.TILE_B_TILED | ops.TILE_COL_ORDER)) <= ops.num_tiles()
+    assert all(0 <= (t & ~ops.TILE_FLAGS) <= ops.num_tiles()
                for t in tiles.values())
     assert any(t != 0 for t in tiles.values())
     pm.set_tiles(tiles)
