@@ -396,7 +396,7 @@ def conv_roofline(nm, x, reps=20):
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(units) + 1)]
         evs[0].record()
         for u, (i, n) in enumerate(units):
-            nm.forward_layers(x, i, i + n, out=out)
+            nm.forward_layers(x, i, i + n, out=out, keep_amax=True)
             evs[u + 1].record()
         torch.cuda.synchronize()
         splits.append([evs[u].elapsed_time(evs[u + 1]) for u in range(len(units))])

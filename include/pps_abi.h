@@ -202,6 +202,12 @@ int pps_distmat_h2_self_tiled(const uint16_t* x2t, int64_t N, const float* xsq, 
                               void* stream);
 int pps_h2_num_tiles(void);
 
+/* An activation-max slot: PPS_AMAX_SLOT_FLOATS device floats, zeroed before
+ * its producer runs.  Producers fold max|y| into it by atomic maxima on the
+ * float bits, spread over 16 partial maxima 64 floats (256 B) apart; the
+ * tensor's max is the max of slot[0], slot[64], ..., slot[960]. */
+#define PPS_AMAX_SLOT_FLOATS 1024
+
 /* ---- f16x2 convolutions ("h2", round 5) ---------------------------------
  * The conv entry points above in the f16x2 arithmetic of pps_distmat_h2_*:
  * three f16 MFMA terms per product instead of six bf16 ones.  Weights: the
@@ -209,10 +215,10 @@ int pps_h2_num_tiles(void);
  * pps_split_f16x2_sqnorm_tiled (w2t chunk-tiled [2][Cout16/16][Kpad/32][16]
  * [32], wrs[c] = 2^-s_c).  Activations stay f32 NHWC; the kernel scales them
  * by the power of two 2^s_a with max|x 2^s_a| in [2^14, 2^15), taken from
- * *amax_x = max|x| (device float, e.g. written by the producer of x through
- * its amax_y, or pps_amax), and splits them into two f16 terms after the
- * LDS fragment read.  amax_y (device float or NULL) receives max|y| by an
- * atomic max on the float bits: zero it before the launch.  Cin % 32 == 0,
+ * the activation-max slot amax_x (above; e.g. filled by the producer of x
+ * through its amax_y, or by pps_amax), and splits them into two f16 terms
+ * after the LDS fragment read.  amax_y (a zeroed slot or NULL) receives
+ * max|y|.  Cin % 32 == 0,
  * Kpad == KH*KW*Cin; tile 0 (= 38), the 16x16x32 pipelined tiles 38..53, 55
  * and the patch tiles 56..59, or-ed with PPS_TILE_COL_ORDER; no planes, no
  * split-K.  Same f32-level error as the x3 entries (tests/test_gpu_h2_conv.py). */
@@ -238,9 +244,9 @@ int pps_conv2d_bn_act_pps_h2(const float* x, int N, int H, int W, int Cin, int l
                              const float* shift, const float* residual, float* y, int Ho, int Wo,
                              const int32_t* splits, int S, int max_ave, float* pps_out,
                              const float* amax_x, int tile, void* stream);
-/* max |x| over n floats into *amax (atomic max on the float bits; zero it
- * first): the activation max the f16x2 entries take, for a tensor whose
- * producer did not report it. */
+/* max |x| over n floats into the activation-max slot amax (zero it first):
+ * the input scale the f16x2 entries take, for a tensor whose producer did
+ * not report it. */
 int pps_amax(const float* x, int64_t n, float* amax, void* stream);
 /* Caffe2 operator `PairWiseDistance` (detectron/ops/pairwise_distance_op.cu
  * :9-21,26-41): Z[p,q] = sum_d (X[p,d]-X[q,d])^2, X [N][D], Z [N][N].
@@ -819,6 +825,12 @@ int pps_forward(const PpsModel* model, const float* nhwc4, int N, float* feat,
  * afresh (pps_amax) before it runs. */
 int pps_forward_layers(const PpsModel* model, const float* nhwc4, int N, float* feat,
                        int first, int last, void* stream);
+/* The same with flags.  PPS_FWD_KEEP_AMAX: the activation maxima are kept as
+ * the previous call left them (no re-measure, no reset) -- for timing a range
+ * whose inputs have not changed since the forward that reported them. */
+#define PPS_FWD_KEEP_AMAX 1
+int pps_forward_layers_flags(const PpsModel* model, const float* nhwc4, int N, float* feat,
+                             int first, int last, int flags, void* stream);
 /* The reference's `data` blob as it is: NCHW [N][3][H][W] float32. */
 int pps_forward_nchw(const PpsModel* model, const float* nchw, int N, float* feat,
                      void* stream);

@@ -160,6 +160,7 @@ SIGNATURES = {
     'pps_model_tensor_amax': [c_ptr, c_int, ctypes.c_char_p, c_ptr],
     'pps_forward': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
     'pps_forward_layers': [c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_ptr],
+    'pps_forward_layers_flags': [c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_int, c_ptr],
     'pps_forward_nchw': [c_ptr, c_ptr, c_int, c_ptr, c_ptr],
     'pps_forward_bgr': [c_ptr, c_ptr, c_int, c_int, c_int, c_ptr, c_ptr],
 }

@@ -77,8 +77,13 @@ sgs_groups_kernel(const float* __restrict__ skeys, const int32_t* __restrict__ p
       if (j + 1 == G || (int)krow[j + 1] != x) ge[x] = j + 1;
     }
     __syncthreads();
-    // exclusive prefix of the popcounts, W <= kSgsThreads words
-    const int c = t < W ? __popc(bits[t]) : 0;
+    // exclusive prefix of the popcounts: thread t owns words [t * PW, t * PW + PW)
+    const int PW = (W + kSgsThreads - 1) / kSgsThreads;
+    int c = 0;
+    for (int j = 0; j < PW; ++j) {
+      const int wd = t * PW + j;
+      if (wd < W) c += __popc(bits[wd]);
+    }
     int v = c;
     const int lane = t & 63, wv = t >> 6;
 #pragma unroll
@@ -90,7 +95,11 @@ sgs_groups_kernel(const float* __restrict__ skeys, const int32_t* __restrict__ p
     __syncthreads();
     int base = 0;
     for (int w = 0; w < wv; ++w) base += wsum[w];
-    if (t < W) pre[t] = base + v - c;
+    int run = base + v - c;
+    for (int j = 0; j < PW; ++j) {
+      const int wd = t * PW + j;
+      if (wd < W) { pre[wd] = run; run += __popc(bits[wd]); }
+    }
     if (t == kSgsThreads - 1) nids[q] = base + v;
     __syncthreads();
     int32_t* gsq = gstart + q * U;

@@ -251,12 +251,7 @@ __device__ inline void conv_epilogue(const GemmParams& p,
       }
     }
   }
-  if (p.amax_out) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o));
-    if ((threadIdx.x & 63) == 0)
-      atomicMax(reinterpret_cast<unsigned*>(p.amax_out), __builtin_bit_cast(unsigned, amx));
-  }
+  if (p.amax_out) amax_commit(p.amax_out, amx);
 }
 
 }  // namespace pps

@@ -132,20 +132,11 @@ __device__ inline f32x4 mfma16_h2t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f
   return c;
 }
 
-// max |y| of a wave's outputs into *dst (float bits compared as unsigned:
-// every value is >= 0).  All lanes of the wave must be converged here.
-__device__ inline void amax_commit(float* dst, float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  if ((threadIdx.x & 63) == 0)
-    atomicMax(reinterpret_cast<unsigned*>(dst), __builtin_bit_cast(unsigned, v));
-}
-
 // The A operand scale of an EPI_F_H2 launch: from the max of its activation
 // tensor(s) (both operands of a fused-shortcut GEMM share one scale).
 __device__ inline float h2_act_scale(const GemmParams& p, bool dual, float* inv) {
-  float amx = *p.amax_a;
-  if (dual) amx = fmaxf(amx, *p.amax_a2);
+  float amx = amax_read(p.amax_a);
+  if (dual) amx = fmaxf(amx, amax_read(p.amax_a2));
   return h2_scale_of(amx, inv);
 }
 

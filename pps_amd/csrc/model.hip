@@ -746,7 +746,7 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
   w.part_floats = part_need(m, w.shapes);
   if (w.part_floats) w.part = std::make_shared<DevBuf>(w.part_floats * sizeof(float));
   grow_counters(w, cnt_need(m, w.shapes), st);
-  w.amax = std::make_shared<DevBuf>(m.slot.size() * sizeof(float));
+  w.amax = std::make_shared<DevBuf>(m.slot.size() * PPS_AMAX_SLOT_FLOATS * sizeof(float));
   hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
   return m.ws.emplace(N, std::move(w)).first->second;
 }
@@ -794,7 +794,7 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
     auto it = m.slot.find(t);
     return it == m.slot.end() || it->second >= (int)w.amax_need.size() || !w.amax_need[it->second]
                ? nullptr
-               : w.amax->as<float>() + it->second;
+               : w.amax->as<float>() + (size_t)it->second * PPS_AMAX_SLOT_FLOATS;
   };
   // PPS_TILE_H2: the f16x2 arithmetic on the base tile (weights always the
   // chunk-tiled f16x2 split; COL_ORDER kept)
@@ -984,7 +984,7 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
 }
 
 void forward_range(const PpsModel& m, const float* x, int N, float* feat, int first, int last,
-                   hipStream_t st) {
+                   hipStream_t st, bool keep_amax = false) {
   Workspace& w = workspace(m, N, st, true);
   // the tensors whose maxima this forward needs
   const bool all = m.amax_all || getenv_flag_on("PPS_AMAX_ALL");
@@ -994,10 +994,10 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
       if (L.tile & PPS_TILE_H2)
         for (const std::string* t : {&L.input, &L.input2})
           if (!t->empty() && m.slot.count(*t)) w.amax_need[m.slot.at(*t)] = 1;
-  if (first == 0) {
+  if (first == 0 && !keep_amax) {
     // a forward: every producer reports its output's max afresh
     hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
-  } else {
+  } else if (!keep_amax) {
     // a layer range: the f32 tensors it reads but does not produce are
     // measured afresh (their producers ran in an earlier call)
     std::set<std::string> made, done;
@@ -1012,8 +1012,9 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
           if (P.output == *t && P.planes_out) planes = true;
         const float* src = *t == "data" ? x : (w.bufs.count(*t) ? fbuf_of(w, *t) : nullptr);
         if (planes || !src) continue;
-        float* slot = w.amax->as<float>() + m.slot.at(*t);
-        hip_check(hipMemsetAsync(slot, 0, sizeof(float), st), "hipMemsetAsync");
+        float* slot = w.amax->as<float>() + (size_t)m.slot.at(*t) * PPS_AMAX_SLOT_FLOATS;
+        hip_check(hipMemsetAsync(slot, 0, PPS_AMAX_SLOT_FLOATS * sizeof(float), st),
+                  "hipMemsetAsync");
         rc_check(amax_of(src, w.shapes.at(*t).numel(), slot, st));
         done.insert(*t);
       }
@@ -1373,21 +1374,31 @@ int pps_model_tensor_amax(const PpsModel* m, int N, const char* blob, float* out
     PPS_MCHECK(it != m->ws.end(), "no workspace for this batch size (pps_model_reserve)");
     auto s = m->slot.find(blob);
     PPS_MCHECK(s != m->slot.end(), std::string("no activation-max slot for '") + blob + "'");
-    hip_check(hipMemcpy(out, it->second.amax->as<float>() + s->second, sizeof(float),
-                        hipMemcpyDeviceToHost),
+    float h[PPS_AMAX_SLOT_FLOATS];
+    hip_check(hipMemcpy(h, it->second.amax->as<float>() + (size_t)s->second * PPS_AMAX_SLOT_FLOATS,
+                        sizeof(h), hipMemcpyDeviceToHost),
               "hipMemcpy");
+    float mx = 0.f;
+    for (int j = 0; j < kAmaxSubs; ++j) mx = std::max(mx, h[j * kAmaxStride]);
+    *out = mx;
   });
 }
 
-int pps_forward_layers(const PpsModel* m, const float* x, int N, float* feat, int first,
-                       int last, void* stream) {
+int pps_forward_layers_flags(const PpsModel* m, const float* x, int N, float* feat, int first,
+                             int last, int flags, void* stream) {
   return guarded([&] {
     PPS_MCHECK(m && x && feat, "null pointer");
     PPS_MCHECK(N > 0, "N must be positive");
     PPS_MCHECK(0 <= first && first <= last && last <= (int)m->layers.size(), "bad layer range");
     PPS_MCHECK(aligned16(x) && aligned16(feat), "x / feat must be 16-byte aligned");
-    forward_range(*m, x, N, feat, first, last, as_stream(stream));
+    PPS_MCHECK((flags & ~PPS_FWD_KEEP_AMAX) == 0, "unknown pps_forward_layers flags");
+    forward_range(*m, x, N, feat, first, last, as_stream(stream), (flags & PPS_FWD_KEEP_AMAX) != 0);
   });
+}
+
+int pps_forward_layers(const PpsModel* m, const float* x, int N, float* feat, int first,
+                       int last, void* stream) {
+  return pps_forward_layers_flags(m, x, N, feat, first, last, 0, stream);
 }
 
 int pps_forward(const PpsModel* m, const float* nhwc4, int N, float* feat, void* stream) {

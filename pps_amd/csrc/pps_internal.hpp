@@ -237,6 +237,35 @@ int launch_gemm_x3c(const GemmParams& p, int epi, hipStream_t stream, int tile);
 int x3c_tile_rows(int tile);  // rows (BM) of a patch-staged tile id, 0 if none
 int x3c_tile_cols(int tile);
 
+// An activation-max slot (PPS_AMAX_SLOT_FLOATS floats, zeroed before its
+// producer runs): kAmaxSubs partial maxima kAmaxStride floats (256 B) apart,
+// each wave folds its max into one of them (spread by workgroup and wave, so
+// thousands of same-address atomics do not queue at one memory channel); the
+// tensor's max is the max of the partials.
+constexpr int kAmaxSubs = 16;
+constexpr int kAmaxStride = 64;
+static_assert(kAmaxSubs * kAmaxStride == PPS_AMAX_SLOT_FLOATS, "amax slot layout");
+
+// max |y| of a wave's outputs (every value >= 0: float bits compare as
+// unsigned) folded into the slot.  All lanes of the wave must be converged.
+__device__ inline void amax_commit(float* slot, float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  const unsigned sub = (blockIdx.x + 5u * blockIdx.y + 3u * blockIdx.z + (threadIdx.x >> 6)) &
+                       (kAmaxSubs - 1);
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(reinterpret_cast<unsigned*>(slot + sub * kAmaxStride),
+              __builtin_bit_cast(unsigned, v));
+}
+
+// The tensor max a slot holds
+__device__ inline float amax_read(const float* slot) {
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < kAmaxSubs; ++j) m = fmaxf(m, slot[j * kAmaxStride]);
+  return m;
+}
+
 // f16x2 activation split: x 2^s with s = 15 - E for max|x| = m 2^E, m in
 // [0.5, 1) (a zero max keeps 2^0; the exponent clamped to f32's range), so
 // max|x 2^s| lies in [2^14, 2^15).  Returns 2^s; *inv = 2^-s.

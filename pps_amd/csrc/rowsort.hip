@@ -36,6 +36,21 @@ constexpr int kSortBigMax = 18432 / kSortSmall;   // buckets that can exceed kSo
 constexpr int kSortCap = (160 * 1024 - 4 * kSortBuckets - 4 * kSortBigMax - 256) / 8 / 64 * 64;
 constexpr int kSortU = (kSortCap + kSortThreads - 1) / kSortThreads;            // entries per thread
 
+#ifdef PPS_SORT_PROBE
+// phase cycle counts of workgroup 0 (scripts/probes/argsort_phases.py)
+__device__ unsigned long long g_sort_phase[16];
+#define SORT_PHASE(k)                                  \
+  do {                                                 \
+    if (t == 0 && blockIdx.x == 0) {                   \
+      const unsigned long long c = clock64();          \
+      ph[k] += c - ph_last;                            \
+      ph_last = c;                                     \
+    }                                                  \
+  } while (0)
+#else
+#define SORT_PHASE(k) do {} while (0)
+#endif
+
 // -0.0 is keyed as +0.0 (they compare equal, so NumPy's stable sort keeps
 // them in index order)
 __device__ inline uint32_t sort_key(float f) {
@@ -67,9 +82,13 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       dst[u] = (q < Q && i < G) ? __builtin_nontemporal_load(row + i) : 0.f;
     }
   };
+#ifdef PPS_SORT_PROBE
+  unsigned long long ph[16] = {}, ph_last = clock64();
+#endif
   int64_t q = blockIdx.x;
   load(q, cur);
   for (; q < Q; q += gridDim.x) {
+    SORT_PHASE(0);
     load(q + gridDim.x, nxt);   // the next row's loads fly under this row's sort
     // 1) keys, min / max
     uint32_t kmn = 0xffffffffu, kmx = 0u;
@@ -90,6 +109,7 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
     if (lane == 0) { red_min[wave] = kmn; red_max[wave] = kmx; }
     for (int b = t; b < kSortBuckets; b += kSortThreads) off[b] = 0u;
     __syncthreads();
+    SORT_PHASE(1);
     kmn = red_min[0];
     kmx = red_max[0];
     for (int w = 1; w < NW; ++w) {
@@ -110,6 +130,7 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       if (i < G) atomicAdd(&off[bucket(sort_key(cur[u]))], 1u);
     }
     __syncthreads();
+    SORT_PHASE(2);
     {  // block exclusive scan of off[] (kSortBuckets / kSortThreads per thread)
       constexpr int PER = kSortBuckets / kSortThreads;
       unsigned v[PER], s = 0;
@@ -130,6 +151,7 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       for (int j = 0; j < PER; ++j) { off[t * PER + j] = run; run += v[j]; }
     }
     __syncthreads();
+    SORT_PHASE(3);
 #pragma unroll
     for (int u = 0; u < kSortU; ++u) {
       const int i = t + u * kSortThreads;
@@ -140,6 +162,7 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       }
     }
     __syncthreads();
+    SORT_PHASE(4);
     // 3) the buckets holding more than kSortSmall entries (ties, degenerate
     // rows): a list in LDS, found by every thread over its own buckets
     if (t == 0) s_nbig = 0;
@@ -179,9 +202,11 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       }
     }
     __syncthreads();
+    SORT_PHASE(5);
 #pragma unroll
     for (int u = 0; u < kSortU; ++u)
       if (sp[u] >= 0) pk[sp[u]] = sv[u];
+    SORT_PHASE(6);
     // large buckets: one wave each, bitonic network for any length in place
     // (mirror step, then half-cleaners; partners past the end are skipped)
     for (int bi = wave; bi < s_nbig; bi += NW) {
@@ -216,6 +241,7 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       }
     }
     __syncthreads();
+    SORT_PHASE(7);
     // 5) the sorted row out, coalesced
     int32_t* orow = idx + q * ldi;
     float* vrow = vals ? vals + q * ldv : nullptr;
@@ -225,14 +251,29 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       if (vrow) vrow[p] = sort_key_float((uint32_t)(v >> 32));
     }
     __syncthreads();   // pk / off are rebuilt for the next row
+    SORT_PHASE(8);
 #pragma unroll
     for (int u = 0; u < kSortU; ++u) cur[u] = nxt[u];
+    SORT_PHASE(9);
   }
+#ifdef PPS_SORT_PROBE
+  if (t == 0 && blockIdx.x == 0) {
+    ph[15] = 1;
+    for (int k = 0; k < 16; ++k) g_sort_phase[k] = ph[k];
+  }
+#endif
 }
 
 }  // namespace
 
 int argsort_rows_cap() { return kSortCap; }
+
+#ifdef PPS_SORT_PROBE
+extern "C" int pps_sort_probe_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_phase), sizeof(g_sort_phase)) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 
 int argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32_t* idx,
                  int64_t ldi, float* vals, int64_t ldv, hipStream_t st) {

@@ -22,6 +22,7 @@ from .config import cfg as _cfg
 
 MATH = {'x3': 0, 'f32': 1}
 AUTOTUNE_NO_PLANES, AUTOTUNE_SPLITK, AUTOTUNE_NO_SEAM, AUTOTUNE_NO_H2 = 1, 2, 4, 8
+FWD_KEEP_AMAX = 1   # pps_abi.h PPS_FWD_KEEP_AMAX
 
 
 class PpsBlob(ctypes.Structure):
@@ -216,11 +217,14 @@ class NativeModel(object):
 
     __call__ = forward
 
-    def forward_layers(self, x, first, last, out=None):
+    def forward_layers(self, x, first, last, out=None, keep_amax=False):
+        """Layers [first, last).  keep_amax: trust the activation maxima the
+        previous call reported (PPS_FWD_KEEP_AMAX; timing a range whose inputs
+        are unchanged), else ranges with first > 0 re-measure them."""
         N = self._check_x(x)
         out = self._out(N, out, x.device)
-        call('pps_forward_layers', self._h, x.data_ptr(), N, out.data_ptr(), int(first),
-             int(last), _stream())
+        call('pps_forward_layers_flags', self._h, x.data_ptr(), N, out.data_ptr(), int(first),
+             int(last), FWD_KEEP_AMAX if keep_amax else 0, _stream())
         return out
 
     def forward_nchw(self, x, out=None):

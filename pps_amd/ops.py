@@ -867,11 +867,25 @@ def split_weights_h2(w_packed):
     return planes, rs
 
 
+AMAX_SLOT_FLOATS = 1024   # pps_abi.h PPS_AMAX_SLOT_FLOATS: 16 partial maxima, 64 apart
+
+
+def amax_slot(device='cuda'):
+    """A zeroed activation-max slot (the f16x2 entries' amax_x / amax_y)."""
+    return torch.zeros((AMAX_SLOT_FLOATS,), dtype=torch.float32, device=device)
+
+
+def amax_value(slot):
+    """The tensor max a slot holds (max of its partial maxima)."""
+    return float(slot[::64].max())
+
+
 def amax(x, out=None):
-    """max |x| as a device float [1] (pps_amax: atomic max, zeroed here)."""
+    """max |x| into an activation-max slot (pps_amax; the slot is zeroed here)."""
     if out is None:
-        out = torch.zeros((1,), dtype=torch.float32, device=x.device)
+        out = amax_slot(x.device)
     else:
+        _amax_arg(out, 'amax')
         out.zero_()
     call('pps_amax', _dev(x, 'x'), x.numel(), _dev(out, 'amax'), _stream())
     return out
@@ -880,6 +894,9 @@ def amax(x, out=None):
 def _amax_arg(a, name):
     if a is None:
         return 0
+    if a.dtype != torch.float32 or a.numel() < AMAX_SLOT_FLOATS:
+        raise RuntimeError('%s must be an activation-max slot of %d float32 (ops.amax_slot)'
+                           % (name, AMAX_SLOT_FLOATS))
     return _dev(a, name)
 
 
@@ -900,7 +917,7 @@ def conv2d_bn_act_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, r
     call('pps_conv2d_bn_act_h2', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w2, 'w2t', torch.int16),
          _dev(wrs, 'wrs'), Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'),
          _dev(shift, 'shift'), rp, int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout,
-         _dev(amax_x, 'amax_x'), _amax_arg(amax_y, 'amax_y'), int(tile), _stream())
+         _amax_arg(amax_x, 'amax_x'), _amax_arg(amax_y, 'amax_y'), int(tile), _stream())
     return y
 
 
@@ -913,7 +930,7 @@ def conv2d_dual_bn_act_h2(x, cin, k, stride, pad, x2, stride2, w2, wrs, kpad1, s
     call('pps_conv2d_dual_bn_act_h2', _dev(x, 'x'), N, H, W, cin, ldx, k, k, stride, pad,
          _dev(x2, 'x2'), H2, W2, C2, C2, stride2, _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'),
          Cout, kpad1, C2, _dev(shift, 'shift'), int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout,
-         _dev(amax_x, 'amax_x'), _dev(amax_x2, 'amax_x2'), _amax_arg(amax_y, 'amax_y'),
+         _amax_arg(amax_x, 'amax_x'), _amax_arg(amax_x2, 'amax_x2'), _amax_arg(amax_y, 'amax_y'),
          int(tile), _stream())
     return y
 
@@ -933,7 +950,7 @@ def conv2d_bn_act_pps_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shif
          _dev(scale, 'scale'), _dev(shift, 'shift'), _dev(residual, 'residual'),
          _dev(y, 'y') if y is not None else 0, Ho, Wo,
          split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
-         _dev(pps_out, 'pps_out'), _dev(amax_x, 'amax_x'), int(tile), _stream())
+         _dev(pps_out, 'pps_out'), _amax_arg(amax_x, 'amax_x'), int(tile), _stream())
     return pps_out
 
 

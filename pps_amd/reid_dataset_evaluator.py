@@ -149,6 +149,9 @@ def cmc(distmat, query_ids=None, gallery_ids=None, query_cams=None, gallery_cams
     return ret, valid.astype(np.float64)
 
 
+SGS_MAX_IDS = 16384   # pps_sgs_keys / pps_sgs_groups (include/pps_abi.h)
+
+
 def _cmc_sgs(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk,
              separate_camera_set, first_match_break, rng, repeat=100):
     """CMC single_gallery_shot (reid_dataset_evaluator.py:321-363 with
@@ -156,14 +159,27 @@ def _cmc_sgs(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk,
     in `ids_dict` order (pps_sgs_keys / pps_sgs_groups), the reference's
     draws (`_unique_sample` :275-280: one np.random.choice per identity and
     repeat, reproduced call for call by one randint per query), and the
-    query identity's rank among the draws (pps_sgs_ranks)."""
-    rng = rng or np.random
+    query identity's rank among the draws (pps_sgs_ranks).  rng: a legacy
+    np.random.RandomState or the np.random module (the reference's stream);
+    a np.random.Generator draws with .integers -- valid draws, but not the
+    reference's sequence."""
+    rng = np.random if rng is None else rng
+    if isinstance(rng, np.random.Generator):
+        randint = rng.integers
+    elif hasattr(rng, 'randint'):
+        randint = rng.randint
+    else:
+        raise TypeError('rng must be a np.random.RandomState, the np.random module or a '
+                        'np.random.Generator, got %r' % type(rng).__name__)
     d = _to_dev(distmat)
     Q, G = d.shape
     gid = np.asarray(gallery_ids).astype(np.int64)
     qid = np.asarray(query_ids).astype(np.int64)
     uniq = np.unique(gid)
     U = len(uniq)
+    if U > SGS_MAX_IDS:
+        raise ValueError('single_gallery_shot: %d distinct gallery identities, the device '
+                         'grouping holds at most %d' % (U, SGS_MAX_IDS))
     gdense = np.searchsorted(uniq, gid)
     qpos = np.minimum(np.searchsorted(uniq, qid), U - 1)
     qdense = np.where(uniq[qpos] == qid, qpos, -1)
@@ -187,7 +203,7 @@ def _cmc_sgs(distmat, query_ids, gallery_ids, query_cams, gallery_cams, topk,
             draws = np.zeros((len(rs), repeat, ldd), dtype=np.int32)
             for i, q in enumerate(rs):   # query order, as the reference draws
                 n = int(nids_h[q])
-                draws[i, :, :n] = rng.randint(0, np.tile(glen_h[q, :n], repeat)).reshape(repeat, n)
+                draws[i, :, :n] = randint(0, np.tile(glen_h[q, :n], repeat)).reshape(repeat, n)
             k = _np(ops.sgs_ranks(perm, gstart, glen, nids, qt, i32(rs), i32(draws)))
             qq = np.repeat(rs, repeat)
             kk = k.reshape(-1)

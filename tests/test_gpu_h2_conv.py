@@ -74,16 +74,16 @@ def test_conv_h2_error_tiles_amax(N, H, W, Cin, Cout, k, s, p, residual, mag):
     e_x3 = _rel_err(y.cpu().numpy(), ref)
     w2, wrs = ops.split_weights_h2(_cuda(wp))
     amx = ops.amax(xd)
-    assert float(amx) == float(np.abs(x).max())
+    assert ops.amax_value(amx) == float(np.abs(x).max())
     tiles = _h2_tiles()
     outs = []
     for tile in tiles:
         y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
-        ay = torch.zeros((1,), device='cuda')
+        ay = ops.amax_slot()
         ops.conv2d_bn_act_h2(xd, Cin, w2, wrs, kpad, k, s, p, 1, _cuda(scale), _cuda(shift), res,
                              True, y, amx, ay, tile=tile)
         yn = y.cpu().numpy()
-        assert float(ay) == float(np.abs(yn).max()), tile
+        assert ops.amax_value(ay) == float(np.abs(yn).max()), tile
         outs.append(yn)
     for t, o in zip(tiles, outs):
         e_h2 = _rel_err(o, ref)
@@ -123,11 +123,11 @@ def test_conv_dual_h2(N, H, W, C1, C2, Cout, s2):
     outs = []
     for tile in tiles:
         y = torch.full(ref.shape, float('nan'), device='cuda')
-        ay = torch.zeros((1,), device='cuda')
+        ay = ops.amax_slot()
         ops.conv2d_dual_bn_act_h2(xd, C1, 1, 1, 0, x2d, s2, wq, wrs, k1, _cuda(sh), True, y,
                                   ops.amax(xd), ops.amax(x2d), ay, tile=tile)
         yn = y.cpu().numpy()
-        assert float(ay) == float(np.abs(yn).max())
+        assert ops.amax_value(ay) == float(np.abs(yn).max())
         outs.append(yn)
     for t, o in zip(tiles, outs):
         assert _rel_err(o, ref) <= H2_VS_X3 * e_x3 + ERR_FLOOR, (t, _rel_err(o, ref), e_x3)
