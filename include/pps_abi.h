@@ -377,7 +377,7 @@ int pps_cmc_finalize(int64_t Q, int Ptot, const int32_t* pos_total, const int32_
  *    is the reference's np.random.choice stream, call for call;
  *  - pps_sgs_ranks: k [nr][repeat] = the number of drawn entries ranked
  *    before the query identity's draw (the reference's one hit per repeat).
- * G <= pps_argsort_rows_cap(), U <= 16384. */
+ * G <= pps_argsort_rows_cap(), U <= 16384, 8 U + 8 ceil(G / 32) <= 160 KiB. */
 int pps_sgs_keys(const int32_t* order, int64_t Q, int64_t G, int64_t ldo, const int32_t* gid,
                  const int32_t* gcam, const int32_t* qid, const int32_t* qcam,
                  int separate_camera_set, int U, float* keys, void* stream);
@@ -393,9 +393,11 @@ int pps_sgs_ranks(const int32_t* perm, int64_t Q, int64_t G, const int32_t* rows
  * (distance, index) order -- np.argsort(distmat, axis=1, kind='stable'), the
  * reference's `indices = np.argsort(distmat, axis=1)`
  * (reid_dataset_evaluator.py:319,420) with ties in index order; vals
- * (optional, [Q][ldv]) the sorted distances.  One row per workgroup in LDS
- * (bucket map of the row's own range + in-bucket ranks): G <=
- * pps_argsort_rows_cap() (18240), else PPS_ERR_INVALID_ARG. */
+ * (optional, [Q][ldv]) the sorted distances.  One row per workgroup:
+ * rows up to 18,432 columns sorted in LDS in one pass (equalised bucket map
+ * of the row's own range, one sorting network per bucket), longer rows in
+ * segments of <= 7,168 words cut by exact word ranges.  G <=
+ * pps_argsort_rows_cap() (458,752), else PPS_ERR_INVALID_ARG. */
 int pps_argsort_rows(const float* dist, int64_t Q, int64_t G, int64_t ldd, int32_t* idx,
                      int64_t ldi, float* vals, int64_t ldv, void* stream);
 int pps_argsort_rows_cap(void);

@@ -12,8 +12,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from pps_amd import _lib, ops  # noqa: E402
 
-NAMES = ['load-issue', 'minmax', 'histogram', 'scan', 'scatter', 'rank(small)', 'write(small)',
-         'big buckets', 'out', 'swap']
+NAMES = ['cur<-nxt', 'minmax..coarse hist', 'fine alloc', 'fine hist+scan', 'scatter',
+         'networks', 'big buckets', 'out']
 
 
 def main():
@@ -39,7 +39,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     assert fn(buf) == 0
-    ph = np.array(list(buf[:10]), dtype=np.float64)
+    ph = np.array(list(buf[:8]), dtype=np.float64)
     rows = (Q + 255) // 256
     print('Q %d G %d %s: %.1f us; workgroup 0 rows %d, cycles/row %.0f' %
           (Q, G, kind, e0.elapsed_time(e1) * 1e3, rows, ph.sum() / rows))

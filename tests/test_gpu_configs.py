@@ -23,6 +23,8 @@ import torch
 from _parity import check_rank_metrics, check_topk, tie_eps
 
 from oracle import evaluator as ev
+
+ev_compute_dist = ev.compute_dist
 from oracle.rank_counts import merge_topk
 
 pytestmark = pytest.mark.gpu
@@ -73,11 +75,16 @@ def test_topk_merge_enforces_limits():
 # ---------------------------------------------------------------- CUHK03
 def test_cuhk03_four_shards_in_process():
     """BASELINE configs[3]: 1400 queries x 5332 gallery, 4 gallery shards as
-    the 4 ranks hold them; the collectives are replaced by their definitions
-    (concatenate the lists, sum the counts)."""
+    the 4 ranks hold them, through the product sharded kernels exactly as
+    ShardedEvaluator.run drives them (pps_amd/distributed.py:253-276):
+    per rank collect_matches on its shard, the lists "all-gathered"
+    (stacked), rank_prepare + rank_count_stream per rank, hist / before
+    summed as the all-reduce does, ap_finalize.  Equal to the one-shard
+    rank_eval and near-tie-exact vs the oracle; the merged top-100 rank list
+    equals the whole matrix's."""
     from pps_amd import ops
     from pps_amd import reid_dataset_evaluator as gev
-    from pps_amd.distributed import shard_range
+    from pps_amd.distributed import HipBackend, ShardedEvaluator
     Q, G, D, R = 1400, 5332, 3968, 4
     rng = np.random.RandomState(3)
     qid = rng.randint(1, 701, Q)
@@ -89,30 +96,35 @@ def test_cuhk03_four_shards_in_process():
     f = _feats(700, np.concatenate([qid, gid]), D, gen)
     qf, gf = f[:Q].contiguous(), f[Q:].contiguous()
     full = ops.compute_dist(qf, gf, tile=DIST_TILE)
-    dq = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32)).cuda()
-    ranges = [shard_range(G, r, R) for r in range(R)]
-    blocks = [ops.compute_dist(qf, gf[a:b].contiguous(), tile=DIST_TILE) for a, b in ranges]
-    for (a, b), blk in zip(ranges, blocks):   # a shard block = that slice of the full matrix
-        assert torch.equal(blk, full[:, a:b])
-    pmax = 64
-    lists = [ops.collect_positives(blk, dq(qid), dq(qcam), dq(gid[a:b]), dq(gcam[a:b]), a,
-                                   pmax) for (a, b), blk in zip(ranges, blocks)]
+    evs = [ShardedEvaluator(qid, qcam, gid, gcam, r, R) for r in range(R)]
+    be = HipBackend
+    blocks, lists, junks, states = [], [], [], []
+    for ev in evs:   # each rank: its shard's distances and lists
+        a, b = ev.g_ranges[ev.rank]
+        blk = be.distmat(qf, gf[a:b].contiguous(), ev.metric)
+        assert torch.equal(blk, full[:, a:b])   # a shard block = that slice of the matrix
+        st = be.prepare(ev)
+        pd, pi, pc, junk = be.collect(blk, ev, st, ev.pmax)
+        blocks.append(blk)
+        lists.append((pd, pi, pc))
+        junks.append(junk)
+        states.append(st)
+    # the all-gather of the lists (ShardedEvaluator._gather_lists)
     pos_d = torch.stack([l[0] for l in lists])
     pos_i = torch.stack([l[1] for l in lists])
     pos_c = torch.stack([l[2] for l in lists])
-    assert int(pos_c.max()) <= pmax
-    hist = before = sd = ptot = None
-    for (a, b), blk in zip(ranges, blocks):
-        sd, _, ptot, h, bf = ops.rank_counts(blk, dq(qid), dq(qcam), dq(gid[a:b]),
-                                             dq(gcam[a:b]), a, pos_d, pos_i, pos_c)
+    hist = before = None
+    for ev, blk, st, junk in zip(evs, blocks, states, junks):
+        sd, _, ptot, h, bf = be.counts(blk, ev, st, pos_d, pos_i, pos_c, junk)
         hist = h if hist is None else hist + h      # the all-reduce(SUM)
         before = bf if before is None else before + bf
-    ap, valid, first = ops.ap_finalize(sd, ptot, hist, before)
+    ap, valid, first = be.finalize(sd, ptot, hist, before)
     ap1, valid1, first1 = gev.rank_eval(full, qid, gid, qcam, gcam)
     np.testing.assert_array_equal(valid.cpu().numpy(), valid1.cpu().numpy())
     np.testing.assert_array_equal(first.cpu().numpy(), first1.cpu().numpy())
     np.testing.assert_allclose(ap.cpu().numpy(), ap1.cpu().numpy(), rtol=0, atol=1e-12)
     # merged rank list == top-k of the whole matrix
+    ranges = [ev.g_ranges[ev.rank] for ev in evs]
     tops = [ops.topk(blk, 100) for blk in blocks]
     mv, mi = ops.topk_merge(torch.stack([t[0] for t in tops]),
                             torch.stack([t[1] for t in tops]), [a for a, _ in ranges], 100)
@@ -120,7 +132,7 @@ def test_cuhk03_four_shards_in_process():
     assert torch.equal(mi, fi) and torch.equal(mv, fv)
     # vs the oracle (NumPy distances, stable argsort, mean_ap / cmc)
     qn, gn = qf.cpu().numpy(), gf.cpu().numpy()
-    ref = ev.compute_dist(qn, gn)
+    ref = ev_compute_dist(qn, gn)
     dn = full.cpu().numpy()
     eps = tie_eps(dn, ref)
     flips = check_topk(mi.cpu().numpy(), ref, 100, eps)

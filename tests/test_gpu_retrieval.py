@@ -645,13 +645,17 @@ def test_rank_prepare_beyond_lds_merge_cap():
 
 @pytest.mark.parametrize('Q,G,kind', [(3368, 15913, 'market'), (64, 17661, 'ties'),
                                       (37, 1, 'plain'), (5, 4099, 'degenerate'),
-                                      (40, 18240, 'plain')])
+                                      (40, 18432, 'plain'), (300, 19889, 'market'),
+                                      (24, 19889, 'ties'), (5, 30001, 'degenerate'),
+                                      (12, 125000, 'market'), (6, 125000, 'ties')])
 def test_argsort_rows_equals_stable_argsort(Q, G, kind):
     """pps_argsort_rows == np.argsort(kind='stable') on every row (VERDICT
     r03 item 8): Market-sized rows of L2 distances (the reference's full rank
     list, reid_dataset_evaluator.py:319,420), rows with heavy ties and
     negative zeros, all-equal and two-valued rows (one bucket: the wave
-    bitonic path), the maximum row length."""
+    bitonic path), the one-pass kernel's longest row (18,432), and longer
+    rows through the segmented kernel: Duke-plus (19,889) and a 1M-config
+    gallery shard (125,000)."""
     from pps_amd import ops
     rng = np.random.RandomState(G + Q)
     if kind == 'market':
@@ -679,7 +683,10 @@ def test_argsort_rows_equals_stable_argsort(Q, G, kind):
 
 
 def test_argsort_rows_capacity_error():
+    """Rows past the segmented kernel's capacity (458,752 columns) are refused
+    with a pointer to pps_topk."""
     from pps_amd import ops
     cap = ops._lib.lib().pps_argsort_rows_cap()
+    assert cap >= 400000
     with pytest.raises(RuntimeError, match='pps_topk'):
-        ops.argsort_rows(torch.zeros((2, cap + 1), device='cuda'))
+        ops.argsort_rows(torch.zeros((1, cap + 1), device='cuda'))
