@@ -586,7 +586,8 @@ def table_digest(nm):
                 layers_per_rounding_group=groups, plane_edges=len(planes),
                 splitk_layers=sum(1 for L in layers if L['splitk'] > 1),
                 seam_pairs=sum(1 for L in layers if L['tile'] & ops.TILE_SEAM),
-                h2_layers=sum(1 for L in layers if L['tile'] & ops.TILE_H2))
+                h2_layers=sum(1 for L in layers if L['tile'] & ops.TILE_H2),
+                h2_plane_inputs=sum(1 for L in layers if L['tile'] & ops.TILE_H2P))
 
 
 def e2e_stage(nm, rank, world, n_images, batch, threads):

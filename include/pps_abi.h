@@ -65,7 +65,8 @@ const char* pps_registered_ops(void);
  * 58 / 59 = patch-staged stride-1 3x3 convs (192x128 8 waves / 192x64 4
  * waves / 96x128 8 waves / 192x64 8 waves; the tile's input patch staged once per 32-channel chunk,
  * K in (channel chunk, tap) order: their own rounding group; other shapes
- * run tile 38).  Results
+ * run tile 38); 60 = 192x128 as 4 x 1 waves (48 x 128 per wave) for the
+ * f16x2 entries (the bf16x3 entries run tile 47 for it).  Results
  * are identical for every tile below 38 (same per-element fp32 MFMA
  * accumulation order) and identical among the tiles from 38 on (one MFMA
  * sums a 32-wide K chunk: a different rounding
@@ -100,6 +101,11 @@ int pps_gemm_num_tiles(void);
  * and every producer reports max|y| from its epilogue (the f16x2 layers'
  * input scales). */
 #define PPS_TILE_H2 0x800
+/* With PPS_TILE_H2 on a conv / conv_pps layer: the layer's input is split
+ * into f16x2 activation planes by one pass (pps_split_f16x2_act) just before
+ * the conv, which then reads the planes (same bits, no split arithmetic in
+ * its main loop; a workspace buffer of 4 B per input element). */
+#define PPS_TILE_H2P 0x1000
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
@@ -244,6 +250,26 @@ int pps_conv2d_bn_act_pps_h2(const float* x, int N, int H, int W, int Cin, int l
                              const float* shift, const float* residual, float* y, int Ho, int Wo,
                              const int32_t* splits, int S, int max_ave, float* pps_out,
                              const float* amax_x, int tile, void* stream);
+/* f16x2 activation planes: planes [2][plane] f16 (int16 storage) =
+ * f16(x 2^s), f16(x 2^s - hi) with 2^s from the slot amax -- the split the
+ * f16x2 conv kernels make after an f32 fragment read, done once per element.
+ * n % 8 == 0, plane >= n, 16-byte aligned.  The _planes conv entries take
+ * them in place of x (same bits as the f32 entries on x with that max). */
+int pps_split_f16x2_act(const float* x, int64_t n, const float* amax, uint16_t* planes,
+                        int64_t plane, void* stream);
+int pps_conv2d_bn_act_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int H, int W,
+                                int Cin, int ldx, const uint16_t* w2t, const float* wrs, int Cout,
+                                int Kpad, int KH, int KW, int stride, int pad, int dil,
+                                const float* scale, const float* shift, const float* residual,
+                                int relu, float* y, int Ho, int Wo, int ldy, const float* amax_x,
+                                float* amax_y, int tile, void* stream);
+int pps_conv2d_bn_act_pps_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int H, int W,
+                                    int Cin, int ldx, const uint16_t* w2t, const float* wrs,
+                                    int Cout, int Kpad, int KH, int KW, int stride, int pad,
+                                    int dil, const float* scale, const float* shift,
+                                    const float* residual, float* y, int Ho, int Wo,
+                                    const int32_t* splits, int S, int max_ave, float* pps_out,
+                                    const float* amax_x, int tile, void* stream);
 /* max |x| over n floats into the activation-max slot amax (zero it first):
  * the input scale the f16x2 entries take, for a tensor whose producer did
  * not report it. */

@@ -54,6 +54,15 @@ SIGNATURES = {
                                  c_ptr, c_int, c_int, c_ptr, c_int, c_int, c_ptr, c_ptr, c_int,
                                  c_ptr],
     'pps_amax': [c_ptr, c_i64, c_ptr, c_ptr],
+    'pps_split_f16x2_act': [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
+    'pps_conv2d_bn_act_h2_planes': [c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                                    c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_int,
+                                    c_ptr, c_ptr, c_int, c_ptr],
+    'pps_conv2d_bn_act_pps_h2_planes': [c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                                        c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_ptr, c_int,
+                                        c_int, c_ptr, c_ptr, c_int, c_ptr],
     'pps_collect_positives': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_i64, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
     'pps_rank_counts': [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,

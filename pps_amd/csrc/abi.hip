@@ -669,19 +669,25 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     // f16x2 (pps_conv2d_bn_act_h2, the whole-network plan's PPS_TILE_H2):
     // f32 activations scaled by their tensor's max, chunk-tiled two-plane
     // weights [2][Cout16 / 16][Kpad / 32][16][32] with per-channel scales
-    PPS_ENFORCE(!x_pl && !y_pl && splitk == 1, "f16x2 conv: f32 activations in and out, no split-K");
+    // x_pl: f16x2 activation planes [2][x_plane] (pps_split_f16x2_act of x
+    // with the same max): same bits as the f32 input, no split in the loop
+    PPS_ENFORCE(!y_pl && splitk == 1, "f16x2 conv: f32 output, no split-K");
     PPS_ENFORCE(amax_in != nullptr, "f16x2 conv: the input tensor's max (amax_x) is required");
     PPS_ENFORCE(Cin % 32 == 0 && Kpad == KH * KW * Cin,
                 "f16x2 conv: Cin % 32 == 0 and Kpad == KH*KW*Cin");
     PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile != GEMM_TILE_WS &&
                               tile < GEMM_NUM_TILES),
-                "f16x2 conv: tile 0, 38..53 or 55..59");
+                "f16x2 conv: tile 0, 38..53 or 55..60");
     p.b3 = static_cast<const uint16_t*>(w);
     p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * Kpad;
     p.b_bytes = (uint32_t)(p.b_plane * 2);
     p.tiled = 2;
     p.rs_b = w_rs;
     p.amax_a = amax_in;
+    if (x_pl) {
+      p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
+      p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
+    }
     return launch_gemm_x3(p, EPI_CONV | EPI_F_H2, 1, as_stream(stream));
   }
   if (x_pl) {
@@ -850,7 +856,7 @@ int conv_pps_impl(const float* x, const uint16_t* x3, int64_t x_plane, int N,
   const bool pl = x3 != nullptr;
   // chunk-tiled weights (always for f16x2: two planes, per-channel scales)
   const bool wtiled = w_rs != nullptr || (tile > 0 && (tile & PPS_TILE_B_TILED) != 0);
-  PPS_ENFORCE(!w_rs || (!pl && amax_in), "f16x2: f32 activations and their max");
+  PPS_ENFORCE(!w_rs || amax_in, "f16x2: the activations' max is required");
   const bool colmajor = tile > 0 && (tile & PPS_TILE_COL_ORDER) != 0;
   tile &= ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER);
   if (tile == 0) tile = pl ? GEMM_TILE_P16_FIRST + 1 : GEMM_TILE_P16_192x128W42;
@@ -930,6 +936,31 @@ int pps_conv2d_dual_bn_act_h2(const float* x, int N, int H, int W, int Cin, int 
                    wrs, amax_x, amax_x2);
 }
 
+int pps_conv2d_bn_act_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int H, int W,
+                                int Cin, int ldx, const uint16_t* w2t, const float* wrs, int Cout,
+                                int Kpad, int KH, int KW, int stride, int pad, int dil,
+                                const float* scale, const float* shift, const float* residual,
+                                int relu, float* y, int Ho, int Wo, int ldy, const float* amax_x,
+                                float* amax_y, int tile, void* stream) {
+  PPS_ENFORCE(wrs != nullptr && x2 != nullptr, "null pointer");
+  return conv_impl(nullptr, N, H, W, Cin, ldx, w2t, 1, Cout, Kpad, KH, KW, stride, pad, dil,
+                   scale, shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x2, x_plane,
+                   nullptr, 0, 1, nullptr, nullptr, 0, amax_y, wrs, amax_x);
+}
+
+int pps_conv2d_bn_act_pps_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int H, int W,
+                                    int Cin, int ldx, const uint16_t* w2t, const float* wrs,
+                                    int Cout, int Kpad, int KH, int KW, int stride, int pad,
+                                    int dil, const float* scale, const float* shift,
+                                    const float* residual, float* y, int Ho, int Wo,
+                                    const int32_t* splits, int S, int max_ave, float* pps_out,
+                                    const float* amax_x, int tile, void* stream) {
+  PPS_ENFORCE(wrs != nullptr && x2 != nullptr, "null pointer");
+  return conv_pps_impl(nullptr, x2, x_plane, N, H, W, Cin, ldx, w2t, Cout, Kpad, KH, KW, stride,
+                       pad, dil, scale, shift, residual, y, Ho, Wo, splits, S, max_ave, pps_out,
+                       tile, stream, wrs, amax_x);
+}
+
 int pps_conv2d_bn_act_pps_h2(const float* x, int N, int H, int W, int Cin, int ldx,
                              const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
                              int KW, int stride, int pad, int dil, const float* scale,
@@ -993,9 +1024,10 @@ int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     PPS_ENFORCE(amax_in && amax_in2, "f16x2 conv: both inputs' maxima are required");
     PPS_ENFORCE(Cin % 32 == 0 && Kpad1 == KH * KW * Cin && Kpad2 % 32 == 0,
                 "f16x2 conv: Cin % 32 == 0, Kpad1 == KH*KW*Cin, Cin2 % 32 == 0");
-    PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_TILE_C16_FIRST &&
-                              tile != GEMM_TILE_WS),
-                "f16x2 fused-shortcut conv: tile 0, 38..53 or 55");
+    PPS_ENFORCE(tile == 0 || tile == GEMM_TILE_P16_192x128W41 ||
+                    (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_TILE_C16_FIRST &&
+                     tile != GEMM_TILE_WS),
+                "f16x2 fused-shortcut conv: tile 0, 38..53, 55 or 60");
     p.b3 = static_cast<const uint16_t*>(w);
     p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * (Kpad1 + Kpad2);
     p.b_bytes = (uint32_t)(p.b_plane * 2);

@@ -686,6 +686,38 @@ __global__ void amax_kernel(const float* __restrict__ x, int64_t n, int vec,
   amax_commit(amax, m);
 }
 
+// f16x2 activation planes: planes[0][i] = f16(x[i] 2^s), planes[1][i] =
+// f16(x[i] 2^s - planes[0][i]) with 2^s from the slot's max -- exactly the
+// split the f16x2 conv kernels apply after an f32 fragment read (split8_h2),
+// done once per element instead of once per wave and column tile.  8
+// elements per thread.
+__global__ void split_act_h2_kernel(const float* __restrict__ x, int64_t n8,
+                                    const float* __restrict__ slot, uint16_t* __restrict__ out,
+                                    int64_t plane) {
+  float inv;
+  const float S = h2_scale_of(amax_read(slot), &inv);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const f32x4 x0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x) + 2 * i);
+    const f32x4 x1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x) + 2 * i + 1);
+    bf16x8 f0, f1;
+    split8_h2(x0, x1, S, f0, f1);
+    *reinterpret_cast<bf16x8*>(out + 8 * i) = f0;
+    *reinterpret_cast<bf16x8*>(out + plane + 8 * i) = f1;
+  }
+}
+
+int split_act_h2(const float* x, int64_t n, const float* slot, uint16_t* planes, int64_t plane,
+                 hipStream_t st) {
+  if (n <= 0) return PPS_OK;
+  const int64_t n8 = n / 8;
+  const int64_t want = (n8 + 255) / 256;
+  hipLaunchKernelGGL(split_act_h2_kernel, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(256),
+                     0, st, x, n8, slot, planes, plane);
+  PPS_CHECK_LAUNCH("split_act_h2_kernel");
+  return PPS_OK;
+}
+
 int amax_of(const float* x, int64_t n, float* amax, hipStream_t st) {
   if (n <= 0) return PPS_OK;
   const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -702,4 +734,14 @@ int pps_amax(const float* x, int64_t n, float* amax, void* stream) {
   PPS_ENFORCE(x && amax, "null pointer");
   PPS_ENFORCE(n >= 0, "n must be >= 0");
   return amax_of(x, n, amax, as_stream(stream));
+}
+
+int pps_split_f16x2_act(const float* x, int64_t n, const float* amax, uint16_t* planes,
+                        int64_t plane, void* stream) {
+  using namespace pps;
+  PPS_ENFORCE(x && amax && planes, "null pointer");
+  PPS_ENFORCE(n >= 0 && n % 8 == 0 && plane >= n && plane % 8 == 0,
+              "n % 8 == 0 and plane >= n, plane % 8 == 0");
+  PPS_ENFORCE(aligned16(x) && aligned16(planes), "16-byte aligned x / planes");
+  return split_act_h2(x, n, amax, planes, plane, as_stream(stream));
 }

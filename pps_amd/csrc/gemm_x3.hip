@@ -264,6 +264,12 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     return PPS_ERR_INVALID_ARG;
   }
   const int epi_in = epi;
+  if (p.tile == GEMM_TILE_P16_192x128W41 && !(epi & EPI_F_H2)) {
+    // the f16x2-only tile: bf16x3 runs its 4 x 2-wave twin (same rounding)
+    GemmParams q = p;
+    q.tile = GEMM_TILE_P16_192x128W42;
+    return launch_gemm_x3(q, epi, batch, stream);
+  }
   if (!(epi & EPI_DIST) && !(epi & EPI_F_RAW)) {
     if (p.residual) epi |= EPI_F_RES;
     if (p.relu) epi |= EPI_F_RELU;
@@ -286,10 +292,13 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     // fallback and for 0)
     if (p.tile >= GEMM_TILE_C16_FIRST && x3c_eligible(p, epi, batch, p.tile))
       return launch_gemm_x3c(p, epi, stream, p.tile);
-    const int t = (p.tile == 0 || p.tile >= GEMM_TILE_C16_FIRST) ? GEMM_TILE_P16_FIRST : p.tile;
+    const int t = (p.tile == 0 || (p.tile >= GEMM_TILE_C16_FIRST &&
+                                   p.tile != GEMM_TILE_P16_192x128W41))
+                      ? GEMM_TILE_P16_FIRST
+                      : p.tile;
     if (t < GEMM_TILE_P16_FIRST || t == GEMM_TILE_WS || batch != 1 || p.splitk != 1 ||
         !x3p_eligible(p, epi)) {
-      set_error("f16x2 conv: a 16x16x32 pipelined or patch tile (38..53, 55..59), no split-K, "
+      set_error("f16x2 conv: a 16x16x32 pipelined or patch tile (38..53, 55..60), no split-K, "
                 "Cin % 32 == 0");
       return PPS_ERR_INVALID_ARG;
     }

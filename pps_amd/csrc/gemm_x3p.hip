@@ -61,12 +61,15 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // EPI_F_H2: f16x2 arithmetic -- f32 activations split into two f16 terms
   // after the fragment read (scale from their tensor's max), the weights as
   // two chunk-tiled f16 planes, three MFMA terms (mfma16_h2t)
+  // With A3 the activations are two f16 planes already scaled and split
+  // (pps_split_f16x2_act): no split arithmetic in the main loop, same bits.
   constexpr bool H2 = (EPI & EPI_F_H2) != 0;
-  static_assert(!H2 || (S == 16 && !A3 && !(EPI & (EPI_F_PLANES | EPI_F_RAW | EPI_F_FIX))),
-                "f16x2 tiles: f32 activations, 16x16x32 blocks, plain epilogues");
+  static_assert(!H2 || (S == 16 && !(EPI & (EPI_F_PLANES | EPI_F_RAW | EPI_F_FIX))),
+                "f16x2 tiles: 16x16x32 blocks, plain epilogues");
   constexpr int NBP = H2 ? 2 : 3;       // weight planes
-  constexpr int A_PLANE = BM * BK * 2;  // A3: bf16 rows of 64 B per plane
-  constexpr int A_BYTES = A3 ? 3 * A_PLANE : BM * BK * 4;  // else f32 rows of 128 B
+  constexpr int NAP = H2 ? 2 : 3;       // activation planes (A3)
+  constexpr int A_PLANE = BM * BK * 2;  // A3: bf16 / f16 rows of 64 B per plane
+  constexpr int A_BYTES = A3 ? NAP * A_PLANE : BM * BK * 4;  // else f32 rows of 128 B
   constexpr int B_PLANE = BN * BK * 2;  // bf16 rows of 64 B
   constexpr int STAGE = A_BYTES + NBP * B_PLANE;
   constexpr int AROWS = A3 ? 16 : 8;    // rows per A piece (1 KiB)
@@ -80,13 +83,13 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool BEVEN = NPB % NW == 0;
   constexpr int AI = (NPA + NW - 1) / NW;
   constexpr int BPW = (NPB + NW - 1) / NW;
-  constexpr int NLOAD = (A3 ? 3 : 1) * AI + NBP * BPW;  // DMA instructions per wave and chunk
+  constexpr int NLOAD = (A3 ? NAP : 1) * AI + NBP * BPW;  // DMA instructions per wave and chunk
   static_assert(NPA * AROWS == BM && NPB * 16 == BN, "tile does not split into DMA pieces");
   // Uneven tiles: only a wave's last slot can be empty (round-robin), so a
   // wave issues NLOAD, NLOAD - (A3 ? 3 : 1) (A slot empty), NLOAD - 3 (B slot
   // empty) or both fewer DMA instructions per chunk; the chunk wait counts
   // its own (see chunk_barrier).
-  constexpr int LA = A3 ? 3 : 1;
+  constexpr int LA = A3 ? NAP : 1;
   static_assert(!(A3 && (EPI & EPI_F_DUAL)), "fused shortcut reads f32 activations");
   static_assert(TM >= 1 && TN >= 1 && (BM / WM) % S == 0 && (BN / WN) % S == 0, "wave tile");
   static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS stages");
@@ -325,7 +328,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
           const unsigned char* d = st + apiece(i) * 1024;
           glds16(ra, d, off);
           glds16(ra1, d + A_PLANE, off);
-          glds16(ra2, d + 2 * A_PLANE, off);
+          if (!H2) glds16(ra2, d + 2 * A_PLANE, off);
         } else {
           glds16(ra, st + apiece(i) * 1024, ok ? (abase[i] + toff + tc) * 4 : kOOB);
         }
@@ -361,7 +364,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       for (int r = 0; r < S * S / 64; ++r) acc[i][j][r] = 0.f;
 
   float h2s = 1.f;  // f16x2: the activation scale 2^s_a
-  if constexpr (H2) {
+  if constexpr (H2 && !A3) {
     float inv;
     h2s = h2_act_scale(p, DUAL, &inv);
   }
@@ -465,7 +468,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
           const unsigned char* ap =
               st + (wm * (BM / WM) + i * 16 + r32) * 64 + ((h ^ bsw) << 4);
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
+          for (int pl = 0; pl < NAP; ++pl)
             fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * A_PLANE);
         } else {
           const unsigned char* rp = st + (wm * (BM / WM) + i * 16 + r32) * 128;
@@ -578,6 +581,60 @@ static void launch_one_p(const GemmParams& p, int batch, hipStream_t stream) {
                      tiles_n);
 }
 
+// f16x2 arithmetic: f32 activations, chunk-tiled two-plane weights, the
+// conv epilogues of a ResNet bottleneck (16x16x32 tiles only)
+template <int BM, int BN, int WM, int WN, int NSF>
+static int launch_tile_h2(const GemmParams& p, int epi, int batch, hipStream_t stream) {
+  constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, H = EPI_F_H2, S = 16;
+  if (!(p.tiled & 2) || !p.rs_b || !p.amax_a || ((epi & EPI_F_DUAL) && (!p.amax_a2 || p.a3))) {
+    set_error("f16x2 conv: activations (f32, or f16x2 planes) with their max, chunk-tiled "
+              "weights and scales; the fused shortcut reads f32");
+    return PPS_ERR_INVALID_ARG;
+  }
+  if (p.a3) {   // f16x2 activation planes (pps_split_f16x2_act)
+    switch (epi & ~H) {
+      case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, true, S>(p, batch, stream); break;
+      case C | RS | RL:
+        launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, true, S>(p, batch, stream); break;
+      case C | RS | RL | EPI_F_PPS:
+        if constexpr (BM == 192 && BN <= 256) {
+          launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | EPI_F_PPS | H, true, S>(p, batch, stream);
+          break;
+        } else {
+          set_error("part-power-set epilogue needs a 192-row tile with at most 256 columns");
+          return PPS_ERR_INVALID_ARG;
+        }
+      default:
+        set_error("f16x2 conv on activation planes: conv + BN + ReLU [+ residual | part "
+                  "pooling] only");
+        return PPS_ERR_INVALID_ARG;
+    }
+    PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+    return PPS_OK;
+  }
+  switch (epi & ~H) {
+    case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, false, S>(p, batch, stream); break;
+    case C | RS | RL:
+      launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, false, S>(p, batch, stream); break;
+    case C | RL | EPI_F_DUAL:
+      launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL | H, false, S>(p, batch, stream);
+      break;
+    case C | RS | RL | EPI_F_PPS:
+      if constexpr (BM == 192 && BN <= 256) {
+        launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | EPI_F_PPS | H, false, S>(p, batch, stream);
+        break;
+      } else {
+        set_error("part-power-set epilogue needs a 192-row tile with at most 256 columns");
+        return PPS_ERR_INVALID_ARG;
+      }
+    default:
+      set_error("f16x2 conv: conv + BN + ReLU [+ residual | shortcut | part pooling] only");
+      return PPS_ERR_INVALID_ARG;
+  }
+  PPS_CHECK_LAUNCH("gemm_x3p_kernel");
+  return PPS_OK;
+}
+
 // NSF / NSP: LDS stages with f32 / bf16-plane A operands (NSP = 0: the tile
 // does not take plane activations)
 // FX: also built with the one-launch split-K epilogues (EPI_F_FIX)
@@ -585,37 +642,10 @@ template <int BM, int BN, int WM, int WN, int NSF, int NSP, int S, bool FX = fal
 static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t stream) {
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, PL = EPI_F_PLANES;
   if (epi & EPI_F_H2) {
-    // f16x2 arithmetic: f32 activations, chunk-tiled two-plane weights, the
-    // conv epilogues of a ResNet bottleneck (16x16x32 tiles only)
     if constexpr (S == 16) {
-      constexpr int H = EPI_F_H2;
-      if (p.a3 || !(p.tiled & 2) || !p.rs_b || !p.amax_a || ((epi & EPI_F_DUAL) && !p.amax_a2)) {
-        set_error("f16x2 conv: f32 activations with their max, chunk-tiled weights and scales");
-        return PPS_ERR_INVALID_ARG;
-      }
-      switch (epi & ~H) {
-        case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, false, S>(p, batch, stream); break;
-        case C | RS | RL:
-          launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, false, S>(p, batch, stream); break;
-        case C | RL | EPI_F_DUAL:
-          launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL | H, false, S>(p, batch, stream);
-          break;
-        case C | RS | RL | EPI_F_PPS:
-          if constexpr (BM == 192 && BN <= 256) {
-            launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | EPI_F_PPS | H, false, S>(p, batch, stream);
-            break;
-          } else {
-            set_error("part-power-set epilogue needs a 192-row tile with at most 256 columns");
-            return PPS_ERR_INVALID_ARG;
-          }
-        default:
-          set_error("f16x2 conv: conv + BN + ReLU [+ residual | shortcut | part pooling] only");
-          return PPS_ERR_INVALID_ARG;
-      }
-      PPS_CHECK_LAUNCH("gemm_x3p_kernel");
-      return PPS_OK;
+      return launch_tile_h2<BM, BN, WM, WN, NSF>(p, epi, batch, stream);
     } else {
-      set_error("f16x2 conv needs a 16x16x32 tile (38..53, 55)");
+      set_error("f16x2 conv needs a 16x16x32 tile (38..53, 55, 60)");
       return PPS_ERR_INVALID_ARG;
     }
   }
@@ -773,9 +803,10 @@ static int launch_variant(const GemmParams& p, int epi, int batch, hipStream_t s
 // launch_gemm_x3p map it), 0 for a non-pipelined id.
 int x3p_tile_rows(int tile, bool a3) {
   if (tile == GEMM_TILE_P16_64x128W24S4) return 64;
+  if (tile == GEMM_TILE_P16_192x128W41) return 192;
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_192x64W41 ||
-      tile == GEMM_TILE_P16_192x128W42S3)
+      tile == GEMM_TILE_P16_192x128W42S3 || tile == GEMM_TILE_P16_192x128W41)
     return 192;
   if (tile == GEMM_TILE_P16_128x128W42S3) return 128;
   if (tile == GEMM_TILE_P16_96x128W22 || tile == GEMM_TILE_P16_96x128W24 ||
@@ -796,7 +827,7 @@ int x3p_tile_rows(int tile, bool a3) {
 
 // Columns (BN) of that tile.
 int x3p_tile_cols(int tile, bool a3) {
-  if (tile == GEMM_TILE_P16_64x128W24S4) return 128;
+  if (tile == GEMM_TILE_P16_64x128W24S4 || tile == GEMM_TILE_P16_192x128W41) return 128;
   if (tile < GEMM_TILE_P_FIRST || tile >= GEMM_TILE_WS) return 0;
   if (tile == GEMM_TILE_P16_192x128W42 || tile == GEMM_TILE_P16_96x128W22 ||
       tile == GEMM_TILE_P16_96x128W24 || tile == GEMM_TILE_P16_128x128W42S3 ||
@@ -845,6 +876,14 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
   // 64-row split-K head GEMMs, whose 8-chunk slices are all pipeline fill
   if (variant == GEMM_TILE_P16_64x128W24S4 - GEMM_TILE_P_FIRST)
     return launch_tile_p<64, 128, 2, 4, 4, 4, 16>(p, epi, batch, stream);
+  // f16x2 only: 192x128 as 4 x 1 waves (48 x 128 per wave): each activation
+  // fragment split once feeds eight 16x16 column blocks (the split is the
+  // f16x2 kernels' VALU cost; 4 x 2 waves split every fragment twice and
+  // feed four).  bf16x3 launches of this id run tile 47 (same rounding group).
+  if (variant == GEMM_TILE_P16_192x128W41 - GEMM_TILE_P_FIRST) {
+    if (epi & EPI_F_H2) return launch_tile_h2<192, 128, 4, 1, 2>(p, epi, batch, stream);
+    return launch_tile_p<192, 128, 4, 2, 2, 2, 16, true>(p, epi, batch, stream);
+  }
   if (variant >= NV) return launch_variant<16>(p, epi, batch, stream, variant - NV);
   return launch_variant<32>(p, epi, batch, stream, variant);
 }

@@ -357,6 +357,8 @@ struct Workspace {
   std::map<std::string, Buf> bufs;  // plane-capable tensors hold 6 B per element
   Buf part;                         // conv split-K partials
   size_t part_floats = 0;
+  Buf h2p;                          // f16x2 activation planes of a PPS_TILE_H2P layer's input
+  size_t h2p_elems = 0;
   Buf cnt;                          // one-launch split-K tile counters (zero between launches)
   size_t cnt_ints = 0;
   Buf nhwc4;                        // input staging for pps_forward_nchw / _bgr
@@ -627,6 +629,15 @@ std::vector<int> pps_tiles(const PpsModel& m, const Layer& L, const Shape& conv_
   return out;
 }
 
+// f16x2 activation planes of the largest PPS_TILE_H2P input (2 x int16 per element)
+size_t h2p_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) {
+  size_t need = 0;
+  for (const auto& L : m.layers)
+    if ((L.tile & PPS_TILE_H2P) && (L.tile & PPS_TILE_H2))
+      need = std::max(need, (size_t)shapes.at(L.input).numel());
+  return need;
+}
+
 size_t part_need(const PpsModel& m, const std::map<std::string, Shape>& shapes) {
   size_t need = 0;
   for (const auto& L : m.layers)
@@ -660,11 +671,13 @@ bool seam_ok(const PpsModel& m, const Layer& L) {
 bool h2_tile_ok(const Layer& L, int tile) {
   const int base = tile & 0xff;
   if (!L.w2 || (tile & PPS_TILE_SEAM)) return false;
+  // activation planes: plain convs and conv_pps (the fused shortcut reads f32)
+  if ((tile & PPS_TILE_H2P) && L.op == Op::ConvDual) return false;
   if (L.op != Op::Conv && L.op != Op::ConvDual && L.op != Op::ConvPps) return false;
   if (!L.relu && L.op == Op::Conv) return false;  // the f16x2 epilogues end in a ReLU
   if (base == 0) return true;
   if (base < GEMM_TILE_P16_FIRST || base == GEMM_TILE_WS || base >= GEMM_NUM_TILES) return false;
-  return L.op == Op::Conv || base < GEMM_TILE_C16_FIRST;
+  return L.op == Op::Conv || base < GEMM_TILE_C16_FIRST || base == GEMM_TILE_P16_192x128W41;
 }
 
 bool fix_tile(int tile) {
@@ -715,6 +728,18 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
       w.part = std::make_shared<DevBuf>(need * sizeof(float));
       w.part_floats = need;
     }
+    const size_t hneed = h2p_need(m, w.shapes);
+    if (hneed > w.h2p_elems) {
+      PPS_MCHECK(!w.pinned, "the buffers of batch " + std::to_string(N) +
+                                " are pinned by pps_model_reserve and the tuning table now needs "
+                                "larger f16x2 activation planes: pps_model_release, reserve "
+                                "again, recapture");
+      PPS_MCHECK(allow_alloc && !capturing(st),
+                 "f16x2 activation planes grew after pps_model_reserve: reserve again outside "
+                 "capture");
+      w.h2p = std::make_shared<DevBuf>(hneed * 2 * sizeof(uint16_t));
+      w.h2p_elems = hneed;
+    }
     const size_t cneed = cnt_need(m, w.shapes);
     if (cneed > w.cnt_ints) {
       PPS_MCHECK(!w.pinned, pinned_msg + "counters: pps_model_release, reserve again, recapture");
@@ -745,6 +770,8 @@ Workspace& workspace(const PpsModel& m, int N, hipStream_t st, bool allow_alloc)
   }
   w.part_floats = part_need(m, w.shapes);
   if (w.part_floats) w.part = std::make_shared<DevBuf>(w.part_floats * sizeof(float));
+  w.h2p_elems = h2p_need(m, w.shapes);
+  if (w.h2p_elems) w.h2p = std::make_shared<DevBuf>(w.h2p_elems * 2 * sizeof(uint16_t));
   grow_counters(w, cnt_need(m, w.shapes), st);
   w.amax = std::make_shared<DevBuf>(m.slot.size() * PPS_AMAX_SLOT_FLOATS * sizeof(float));
   hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
@@ -799,12 +826,23 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
   // PPS_TILE_H2: the f16x2 arithmetic on the base tile (weights always the
   // chunk-tiled f16x2 split; COL_ORDER kept)
   const bool h2 = (tile & PPS_TILE_H2) != 0;
+  const bool h2p = h2 && (tile & PPS_TILE_H2P) != 0;
   if (h2) {
     PPS_MCHECK(L.w2 && !L.planes_in && !L.planes_out && sk == 1,
                "layer '" + L.name + "': PPS_TILE_H2 needs the f16x2 weights, f32 activations "
                "at both ends and no split-K");
-    tile &= ~(PPS_TILE_H2 | PPS_TILE_B_TILED | PPS_TILE_SEAM);
+    tile &= ~(PPS_TILE_H2 | PPS_TILE_H2P | PPS_TILE_B_TILED | PPS_TILE_SEAM);
   }
+  // PPS_TILE_H2P: the input's f16x2 planes, split once (same bits)
+  auto h2_planes = [&](const Act& a, int64_t* plane) -> const uint16_t* {
+    const int64_t n = a.s.numel();
+    PPS_MCHECK(w.h2p && (size_t)n <= w.h2p_elems, "layer '" + L.name +
+                                                     "': no f16x2 activation-plane workspace");
+    uint16_t* pl = w.h2p->as<uint16_t>();
+    rc_check(split_act_h2(a.f, n, slotp(L.input), pl, n, st));
+    *plane = n;
+    return pl;
+  };
   // split convs run in one launch on the FIX tiles (same bits as the
   // two-pass split-K), else raw partials + the summing pass (plain weights)
   const bool fused_sk = sk > 1 && L.op == Op::Conv && fix_tile(tile) && L.relu &&
@@ -845,10 +883,12 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       // pps_conv2d_bn_act_x3p[_splitk[_fused]] / _x3 / _h2), reporting max |y|
       float* amo = slotp(L.output);
       if (h2) {
-        rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(), 1, L.cout, L.kpad,
-                           L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, L.relu, fbuf(L.output),
-                           Ho, Wo, L.cout, tile, st, nullptr, 0, nullptr, 0, 1, nullptr, nullptr,
-                           0, amo, L.wrs->as<float>(), slotp(L.input)));
+        int64_t xpl = 0;
+        const uint16_t* xp = h2p ? h2_planes(a, &xpl) : nullptr;
+        rc_check(conv_impl(xp ? nullptr : a.f, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(), 1,
+                           L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, L.relu,
+                           fbuf(L.output), Ho, Wo, L.cout, tile, st, xp, xpl, nullptr, 0, 1,
+                           nullptr, nullptr, 0, amo, L.wrs->as<float>(), slotp(L.input)));
       } else if (m.x3 && (L.planes_in || L.planes_out || sk > 1)) {
         const int t = tile >= GEMM_TILE_P_FIRST ? tile : 0;
         float* yf = L.planes_out ? nullptr : fbuf(L.output);
@@ -935,7 +975,10 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
         const int tb = tile & ~PPS_TILE_COL_ORDER;
         int t = std::find(ok16.begin(), ok16.end(), tb) != ok16.end() ? tb : ok16[0];
         t |= tile & PPS_TILE_COL_ORDER;
-        rc_check(conv_pps_impl(a.f, nullptr, 0, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(),
+        int64_t xpl = 0;
+        const uint16_t* xp = h2p ? h2_planes(a, &xpl) : nullptr;
+        rc_check(conv_pps_impl(xp ? nullptr : a.f, xp, xpl, n, H, W, L.cin_eff, ldx,
+                               L.w2->as<uint16_t>(),
                                L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res,
                                nullptr, (int)cs.d[1], (int)cs.d[2], L.split.data(),
                                (int)L.split.size(), L.max_ave, fbuf(L.output), t, st,
@@ -1267,12 +1310,15 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
-    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM | PPS_TILE_H2);
+    const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM | PPS_TILE_H2 |
+                              PPS_TILE_H2P);
     PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
     PPS_MCHECK(!(tile & PPS_TILE_H2) || h2_tile_ok(*L, tile),
                std::string("PPS_TILE_H2: '") + layer +
                    "' has no f16x2 weights (Cin % 32 == 0) or the base tile is not 0, 38..53, "
-                   "55 or (3x3 convs) 56..59");
+                   "55, 60 or (convs) 56..59; PPS_TILE_H2P: plain convs and conv_pps only");
+    PPS_MCHECK(!(tile & PPS_TILE_H2P) || (tile & PPS_TILE_H2),
+               "PPS_TILE_H2P goes with PPS_TILE_H2");
     PPS_MCHECK(!(tile & PPS_TILE_SEAM) ||
                    (L->seam_next >= 0 && base == GEMM_TILE_WS &&
                     !(tile & (PPS_TILE_B_TILED | PPS_TILE_COL_ORDER))),
@@ -1460,6 +1506,18 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
     // f16x2 candidates (PPS_TILE_H2) beside the bf16x3 tiles of a layer with
     // f32 activations at both ends and no split-K
     const bool try_h2 = m->x3 && !(flags & PPS_AUTOTUNE_NO_H2);
+    if (try_h2) {   // planes workspace for the PPS_TILE_H2P candidates
+      size_t hneed = 0;
+      for (const Layer& L : m->layers)
+        if (L.w2 && (L.op == Op::Conv || L.op == Op::ConvPps))
+          hneed = std::max(hneed, (size_t)w->shapes.at(L.input).numel());
+      if (hneed > w->h2p_elems) {
+        PPS_MCHECK(!w->pinned, "autotune: the batch's buffers are pinned (pps_model_reserve); "
+                               "release them first");
+        w->h2p = std::make_shared<DevBuf>(hneed * 2 * sizeof(uint16_t));
+        w->h2p_elems = hneed;
+      }
+    }
     auto cands_of = [&](const Layer& L) {
       std::vector<int> c;
       const bool h2ok = try_h2 && L.w2 && !L.planes_in && !L.planes_out && L.splitk == 1;
@@ -1473,11 +1531,12 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       } else {
         const bool pipelined_only = L.planes_in || L.planes_out;
         for (int tl = pipelined_only ? GEMM_TILE_P_FIRST : 1; tl < GEMM_NUM_TILES; ++tl)
-          c.push_back(tl);
+          if (tl != GEMM_TILE_P16_192x128W41) c.push_back(tl);   // (f16x2 only)
         if (h2ok)
           for (int tl = GEMM_TILE_P16_FIRST; tl < GEMM_NUM_TILES; ++tl)
             if (h2_tile_ok(L, tl | PPS_TILE_H2) &&
-                !(tl >= GEMM_TILE_C16_FIRST && (L.k != 3 || L.stride != 1)))
+                !(tl >= GEMM_TILE_C16_FIRST && tl != GEMM_TILE_P16_192x128W41 &&
+                  (L.k != 3 || L.stride != 1)))
               c.push_back(tl | PPS_TILE_H2);
       }
       if (c.empty()) c.push_back(0);
@@ -1494,6 +1553,8 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       for (int i = 0; i < (int)screen.size() && i < finalists; ++i) {
         const int tl = screen[i].second;
         var.push_back(tl);
+        // f16x2 finalists also with the input split once into planes
+        if ((tl & PPS_TILE_H2) && h2_tile_ok(L, tl | PPS_TILE_H2P)) var.push_back(tl | PPS_TILE_H2P);
         if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS)
           for (int f : {PPS_TILE_B_TILED, PPS_TILE_COL_ORDER,
                         PPS_TILE_B_TILED | PPS_TILE_COL_ORDER})

@@ -115,7 +115,9 @@ enum GemmTile {
   GEMM_TILE_C16_192x64 = 57,
   GEMM_TILE_C16_96x128 = 58,
   GEMM_TILE_C16_192x64W42 = 59,  // 192x64 with 8 waves (4 x 2)
-  GEMM_NUM_TILES = 60
+  // pipelined 16x16x32, 192x128 as 4 x 1 waves: f16x2 only (bf16x3 runs 47)
+  GEMM_TILE_P16_192x128W41 = 60,
+  GEMM_NUM_TILES = 61
 };
 
 struct GemmParams {
@@ -306,6 +308,8 @@ int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const fl
 int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
               int Ho, int Wo, hipStream_t st, float* amax);
 // max |x| of n floats into *amax (atomic max on the float bits; zero it first)
+int split_act_h2(const float* x, int64_t n, const float* slot, uint16_t* planes, int64_t plane,
+                 hipStream_t st);
 int amax_of(const float* x, int64_t n, float* amax, hipStream_t st);
 
 // ---- f16x2 distance GEMM (gemm_h2.hip) ---------------------------------------

@@ -605,14 +605,16 @@ class PPSModel(object):
         if '_w2' not in L:
             L['_w2'] = ops.split_weights_h2(L['w32'])
         w2, wrs = L['_w2']
-        base = tile & ~(ops.TILE_H2 | ops.TILE_B_TILED | ops.TILE_SEAM | ops.TILE_COL_ORDER)
+        base = tile & ~(ops.TILE_H2 | ops.TILE_H2P | ops.TILE_B_TILED | ops.TILE_SEAM |
+                        ops.TILE_COL_ORDER)
         flags = tile & ops.TILE_COL_ORDER
         x = bufs[L['input']]
         amx = ops.amax(x)
         op = L['op']
+        xin = ops.split_act_h2(x, amx) if tile & ops.TILE_H2P else x   # PPS_TILE_H2P
         if op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
-            ops.conv2d_bn_act_h2(x, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
+            ops.conv2d_bn_act_h2(xin, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
                                  L['pad'], L['dil'], L['scale'], L['shift'], res, L['relu'],
                                  bufs[L['output']], amx, tile=base | flags)
         elif op == 'conv_dual':
@@ -625,7 +627,7 @@ class PPSModel(object):
             if not ok:
                 raise RuntimeError("layer '%s': no f16x2 tile holds one image" % L['name'])
             t = (base if base in ok else ok[0]) | flags
-            ops.conv2d_bn_act_pps_h2(x, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
+            ops.conv2d_bn_act_pps_h2(xin, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
                                      L['pad'], L['dil'], L['scale'], L['shift'],
                                      bufs[L['residual']], L['split_arr'], L['max_ave'],
                                      bufs[L['output']], amx, y=None, tile=t)
@@ -905,14 +907,18 @@ class PPSModel(object):
             if not ok:
                 raise ValueError("PPS_TILE_SEAM: '%s' is not a branch2c feeding a seam-capable "
                                  "branch2a (base tile 54)" % name)
+        if tile & ops.TILE_H2P and (not tile & ops.TILE_H2 or L['op'] == 'conv_dual'):
+            raise ValueError("PPS_TILE_H2P: '%s' needs PPS_TILE_H2 on a plain conv or conv_pps"
+                             % name)
         if tile & ops.TILE_H2:
             base = tile & 0xff
             if not self.h2_capable(L) or not (
                     base == 0 or (ops.TILE_P16_FIRST <= base <= ops.num_tiles() and
                                   base != ops.TILE_WS and
-                                  (L['op'] == 'conv' or base < ops.TILE_C16_FIRST))):
+                                  (L['op'] == 'conv' or base < ops.TILE_C16_FIRST or
+                                   base == ops.TILE_H2_WIDE))):
                 raise ValueError("PPS_TILE_H2: '%s' has no f16x2 arithmetic or the base tile "
-                                 "%d is not 0, 38..53, 55 or (3x3 convs) 56..59" % (name, base))
+                                 "%d is not 0, 38..53, 55, 60 or (convs) 56..59" % (name, base))
 
     def set_tiles(self, tiles):
         """Apply a tiles() mapping (e.g. a saved autotune result).  Seam and

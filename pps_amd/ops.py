@@ -25,8 +25,10 @@ TILE_B_TILED = 0x100  # PPS_TILE_B_TILED: or-ed into a conv tile, the weights ar
 TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (same bits)
 TILE_SEAM = 0x400  # PPS_TILE_SEAM (whole-network plan): branch2c + next branch2a in one launch
 TILE_H2 = 0x800    # PPS_TILE_H2 (whole-network plan): the layer in f16x2 arithmetic
+TILE_H2P = 0x1000  # PPS_TILE_H2P: with TILE_H2, the input split once into f16x2 planes
 TILE_WS = 54       # the weight-stationary 1x1 tile (gemm_ws.hip)
-TILE_FLAGS = TILE_B_TILED | TILE_COL_ORDER | TILE_SEAM | TILE_H2   # every or-ed flag
+TILE_H2_WIDE = 60  # 192x128 as 4 x 1 waves: f16x2 only (bf16x3 launches run tile 47)
+TILE_FLAGS = TILE_B_TILED | TILE_COL_ORDER | TILE_SEAM | TILE_H2 | TILE_H2P   # every or-ed flag
 # tiles built with the one-launch split-K epilogue (conv2d_bn_act_x3p(..., counters=))
 FIX_TILES = (45, 47, 48, 49, 50)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)
@@ -900,13 +902,32 @@ def _amax_arg(a, name):
     return _dev(a, name)
 
 
+def split_act_h2(x, amax_x, out=None):
+    """f16x2 activation planes [2, *x.shape] (int16 storage) of f32 x with the
+    scale of the slot amax_x (pps_split_f16x2_act): what the f16x2 kernels
+    split after an f32 fragment read, done once per element."""
+    n = x.numel()
+    if out is None:
+        out = torch.empty((2,) + tuple(x.shape), dtype=torch.int16, device=x.device)
+    call('pps_split_f16x2_act', _dev(x, 'x'), n, _amax_arg(amax_x, 'amax_x'),
+         _dev(out, 'planes', torch.int16), out[0].numel(), _stream())
+    return out
+
+
+def _h2_planes(x):
+    """x is f16x2 activation planes [2, N, H, W, C] (split_act_h2)?"""
+    return x.dtype == torch.int16 and x.dim() == 5 and x.shape[0] == 2
+
+
 def conv2d_bn_act_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, residual, relu, y,
                      amax_x, amax_y=None, tile=0):
     """conv2d_bn_act in f16x2 arithmetic (pps_conv2d_bn_act_h2): w2 / wrs from
     split_weights_h2, amax_x = max|x| as a device float (amax() or the
     producer's amax_y), amax_y (optional, zeroed by the caller) receives
-    max|y|."""
-    N, H, W, ldx = x.shape
+    max|y|.  x may be f16x2 activation planes (split_act_h2 with amax_x;
+    pps_conv2d_bn_act_h2_planes, same bits)."""
+    planes = _h2_planes(x)
+    N, H, W, ldx = x.shape[1:] if planes else x.shape
     _, Ho, Wo, Cout = y.shape
     rp = 0
     if residual is not None:
@@ -914,10 +935,14 @@ def conv2d_bn_act_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, r
             raise RuntimeError('residual shape %s != output %s'
                                % (tuple(residual.shape), tuple(y.shape)))
         rp = _dev(residual, 'residual')
-    call('pps_conv2d_bn_act_h2', _dev(x, 'x'), N, H, W, cin, ldx, _dev(w2, 'w2t', torch.int16),
-         _dev(wrs, 'wrs'), Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'),
-         _dev(shift, 'shift'), rp, int(bool(relu)), _dev(y, 'y'), Ho, Wo, Cout,
-         _amax_arg(amax_x, 'amax_x'), _amax_arg(amax_y, 'amax_y'), int(tile), _stream())
+    rest = (N, H, W, cin, ldx, _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'), Cout, kpad, k, k,
+            stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'), rp, int(bool(relu)),
+            _dev(y, 'y'), Ho, Wo, Cout, _amax_arg(amax_x, 'amax_x'), _amax_arg(amax_y, 'amax_y'),
+            int(tile), _stream())
+    if planes:
+        call('pps_conv2d_bn_act_h2_planes', _dev(x, 'x planes', torch.int16), x.stride(0), *rest)
+    else:
+        call('pps_conv2d_bn_act_h2', _dev(x, 'x'), *rest)
     return y
 
 
@@ -937,20 +962,26 @@ def conv2d_dual_bn_act_h2(x, cin, k, stride, pad, x2, stride2, w2, wrs, kpad1, s
 
 def conv2d_bn_act_pps_h2(x, cin, w2, wrs, kpad, k, stride, pad, dil, scale, shift, residual,
                          split, max_ave, pps_out, amax_x, y=None, tile=0):
-    """conv2d_bn_act_pps in f16x2 arithmetic (pps_conv2d_bn_act_pps_h2)."""
-    N, H, W, ldx = x.shape
+    """conv2d_bn_act_pps in f16x2 arithmetic (pps_conv2d_bn_act_pps_h2); x may
+    be f16x2 activation planes (pps_conv2d_bn_act_pps_h2_planes)."""
+    planes = _h2_planes(x)
+    N, H, W, ldx = x.shape[1:] if planes else x.shape
     nsub, n2, Cout = pps_out.shape
     split = np.ascontiguousarray(split, dtype=np.int32)
     Ho = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
     Wo = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
     if nsub != (1 << len(split)) - 1 or n2 != N:
         raise RuntimeError('pps_out must be [2^S - 1, N, Cout]')
-    call('pps_conv2d_bn_act_pps_h2', _dev(x, 'x'), N, H, W, cin, ldx,
-         _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'), Cout, kpad, k, k, stride, pad, dil,
-         _dev(scale, 'scale'), _dev(shift, 'shift'), _dev(residual, 'residual'),
-         _dev(y, 'y') if y is not None else 0, Ho, Wo,
-         split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
-         _dev(pps_out, 'pps_out'), _amax_arg(amax_x, 'amax_x'), int(tile), _stream())
+    rest = (N, H, W, cin, ldx, _dev(w2, 'w2t', torch.int16), _dev(wrs, 'wrs'), Cout, kpad, k, k,
+            stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'),
+            _dev(residual, 'residual'), _dev(y, 'y') if y is not None else 0, Ho, Wo,
+            split.ctypes.data_as(_lib.ctypes.c_void_p), len(split), int(bool(max_ave)),
+            _dev(pps_out, 'pps_out'), _amax_arg(amax_x, 'amax_x'), int(tile), _stream())
+    if planes:
+        call('pps_conv2d_bn_act_pps_h2_planes', _dev(x, 'x planes', torch.int16), x.stride(0),
+             *rest)
+    else:
+        call('pps_conv2d_bn_act_pps_h2', _dev(x, 'x'), *rest)
     return pps_out
 
 

@@ -33,11 +33,23 @@ def main():
     sh = torch.zeros(Cout, device='cuda')
     y = torch.empty((N, H, W, Cout), device='cuda')
     p = k // 2
-    if math == 'h2':
+    if math in ('h2', 'h2p'):
         w2, wrs = ops.split_weights_h2(wp)
         amx = ops.amax(x)
-        run = lambda: ops.conv2d_bn_act_h2(x, Cin, w2, wrs, kpad, k, 1, p, 1, sc, sh, None, True,
+        xin = ops.split_act_h2(x, amx) if math == 'h2p' else x
+        run = lambda: ops.conv2d_bn_act_h2(xin, Cin, w2, wrs, kpad, k, 1, p, 1, sc, sh, None, True,
                                            y, amx, tile=tile)
+        if math == 'h2p':   # the split pass, timed separately
+            pl = torch.empty_like(xin)
+            ops.split_act_h2(x, amx, out=pl)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                ops.split_act_h2(x, amx, out=pl)
+            e1.record()
+            torch.cuda.synchronize()
+            print('split pass: %.1f us' % (e0.elapsed_time(e1) * 1e3 / reps))
     else:
         w3 = ops.split_bf16x3(wp)
         run = lambda: ops.conv2d_bn_act(x, Cin, w3, kpad, k, 1, p, 1, sc, sh, None, True, y,

@@ -119,7 +119,7 @@ def test_conv_dual_h2(N, H, W, C1, C2, Cout, s2):
                            True, y, tile=ops.TILE_P16_FIRST)
     e_x3 = _rel_err(y.cpu().numpy(), ref)
     wq, wrs = ops.split_weights_h2(_cuda(w))
-    tiles = [0] + [t for t in range(ops.TILE_P16_FIRST, 56) if t != 54]
+    tiles = [0] + [t for t in range(ops.TILE_P16_FIRST, 56) if t != 54] + [60]
     outs = []
     for tile in tiles:
         y = torch.full(ref.shape, float('nan'), device='cuda')
@@ -178,3 +178,63 @@ def test_conv_h2_enforces():
     with pytest.raises(RuntimeError, match='tile'):
         ops.conv2d_bn_act_h2(x, 64, w2, wrs, kpad, 1, 1, 0, 1, one, one, None, True, y,
                              ops.amax(x), tile=30)
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 24, 8, 256, 256, 3, 1, 1),     # res4 branch2b
+    (2, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
+    (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1
+    (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+])
+@pytest.mark.parametrize('residual', [False, True])
+def test_conv_h2_activation_planes_same_bits(N, H, W, Cin, Cout, k, s, p, residual):
+    """f16x2 activation planes (pps_split_f16x2_act, once per element) in
+    place of the f32 input: the same fragments reach the MFMAs, so every tile
+    gives the f32-input kernel's bits, and the same max|y|."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(Cin + Cout + k + s)
+    x = rng.randn(N, H, W, Cin).astype(np.float32)
+    x[0, 0, 0, :5] = [1e-30, -3e-8, 0.0, -0.0, 7.5e4]   # subnormal f16 parts, a large max
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w2, wrs = ops.split_weights_h2(_cuda(wp))
+    sc, sh = _cuda(rng.uniform(0.5, 1.5, Cout)), _cuda(rng.randn(Cout) * 0.1)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = _cuda(rng.randn(N, Ho, Wo, Cout)) if residual else None
+    xd = _cuda(x)
+    amx = ops.amax(xd)
+    planes = ops.split_act_h2(xd, amx)
+    for tile in (0, 38, 45, 47, 52, 60):
+        y1 = torch.full((N, Ho, Wo, Cout), float('nan'), device='cuda')
+        y2 = torch.full((N, Ho, Wo, Cout), float('nan'), device='cuda')
+        a1, a2 = ops.amax_slot(), ops.amax_slot()
+        ops.conv2d_bn_act_h2(xd, Cin, w2, wrs, kpad, k, s, p, 1, sc, sh, res, True, y1, amx, a1,
+                             tile=tile)
+        ops.conv2d_bn_act_h2(planes, Cin, w2, wrs, kpad, k, s, p, 1, sc, sh, res, True, y2, amx,
+                             a2, tile=tile)
+        assert torch.equal(y1, y2), tile
+        assert ops.amax_value(a1) == ops.amax_value(a2), tile
+
+
+def test_conv_pps_h2_activation_planes_same_bits():
+    from pps_amd import model, ops
+    rng = np.random.RandomState(6)
+    N, H, W, Cin, Cout = 2, 24, 8, 512, 256
+    x = np.maximum(rng.randn(N, H, W, Cin), 0).astype(np.float32)
+    w = (rng.randn(Cout, Cin, 1, 1) / np.sqrt(Cin)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    w2, wrs = ops.split_weights_h2(_cuda(wp))
+    sc, sh = _cuda(rng.uniform(0.5, 1.5, Cout)), _cuda(rng.randn(Cout) * 0.1)
+    res = _cuda(np.maximum(rng.randn(N, H, W, Cout), 0))
+    xd = _cuda(x)
+    amx = ops.amax(xd)
+    planes = ops.split_act_h2(xd, amx)
+    split = [5, 5, 5, 5, 4]
+    for tile in (47, 52, 60):
+        a = torch.full((31, N, Cout), float('nan'), device='cuda')
+        b = torch.full((31, N, Cout), float('nan'), device='cuda')
+        ops.conv2d_bn_act_pps_h2(xd, Cin, w2, wrs, kpad, 1, 1, 0, 1, sc, sh, res, split, True, a,
+                                 amx, tile=tile)
+        ops.conv2d_bn_act_pps_h2(planes, Cin, w2, wrs, kpad, 1, 1, 0, 1, sc, sh, res, split,
+                                 True, b, amx, tile=tile)
+        assert torch.equal(a, b), tile

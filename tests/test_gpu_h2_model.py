@@ -69,6 +69,8 @@ def _h2_table(nm, N):
         if L['op'] == 'conv_pps':
             base = 47
         t[name] = base | ops.TILE_H2
+        if L['op'] != 'conv_dual' and k % 2:   # every other one on split-once input planes
+            t[name] |= ops.TILE_H2P
     return t
 
 
@@ -89,6 +91,7 @@ def test_h2_table_c_plan_equals_twin_and_oracle():
         except RuntimeError:
             nm.set_tiles({name: 0})
     assert len(ok) >= 45, len(ok)
+    assert sum(1 for t in ok.values() if t & ops.TILE_H2P) >= 15
     pm.set_tiles(ok)
     a = pm.forward(xd).cpu().numpy()
     b = nm.forward(xd).cpu().numpy()
@@ -136,6 +139,13 @@ def test_h2_tile_refused_where_it_cannot_run():
         nm.set_tiles({'res2_0_branch2b': 30 | ops.TILE_H2})           # a 32x32 tile
     with pytest.raises(ValueError, match='PPS_TILE_H2'):
         pm.set_tiles({'res2_0_branch2b': 30 | ops.TILE_H2})
+    dual = next(L['name'] for L in nm.layers() if L['op'] == 'conv_dual')
+    with pytest.raises(RuntimeError, match='PPS_TILE_H2P'):
+        nm.set_tiles({dual: 47 | ops.TILE_H2 | ops.TILE_H2P})   # the shortcut reads f32
+    with pytest.raises(RuntimeError, match='PPS_TILE_H2P'):
+        nm.set_tiles({'res2_0_branch2b': 38 | ops.TILE_H2P})     # without PPS_TILE_H2
+    with pytest.raises(ValueError, match='PPS_TILE_H2P'):
+        pm.set_tiles({dual: 47 | ops.TILE_H2 | ops.TILE_H2P})
     # a plane edge into an f16x2 layer is refused, in either order
     edges = nm.plane_edges()
     p, c, _ = edges[0]

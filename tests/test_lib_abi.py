@@ -61,7 +61,7 @@ def test_pipelined_tile_shapes():
             44: (128, 256), 45: (128, 128), 46: (192, 128), 47: (192, 128), 48: (192, 64),
             49: (96, 128), 50: (96, 128), 51: (128, 128), 52: (192, 128), 53: (96, 128),
             55: (64, 128)}
-    assert ops.num_tiles() == 59
+    assert ops.num_tiles() == 60
     for t, shape in want.items():
         assert ops.tile_shape(t) == shape, t
     assert ops.tile_shape(28) == (0, 0) and ops.tile_shape(54) == (0, 0)  # 54: gemm_ws
