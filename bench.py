@@ -34,7 +34,7 @@ PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 # f16x2 distance path (csrc/gemm_h2.hip): 3 f16 MFMA terms per f32-level
 # product (f16 MFMA: the bf16 rate) -> its roof in f32-equivalent TFLOP/s
 PEAK_H2_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r04', 'pmc_traffic.json')
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r05', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -328,7 +328,7 @@ def argsort_roofline(dist, reps=10):
 
 def _pmc_traffic(key, math, batch):
     """HBM bytes per launch measured by rocprofv3 PMC passes of this bench
-    (scripts/pmc_traffic.py -> profiles/r04/pmc_traffic.json): FETCH_SIZE x 2
+    (scripts/pmc_traffic.py -> profiles/r05/pmc_traffic.json): FETCH_SIZE x 2
     (gfx950 reports half of wide streaming reads) + WRITE_SIZE, per launch.
     None unless the file was measured for the same math and batch."""
     try:

@@ -17,6 +17,22 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 
 Q, G, D = 2228, 17661, 3968
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'profiles', 'r05',
+                            'pmc_duke.json')
+
+
+def _traffic(key, math):
+    """Memory-side bytes per call measured by the PMC passes of this script
+    (scripts/gpu_duke_pmc.sh -> profiles/r05/pmc_duke.json), None unless
+    measured for the same distance arithmetic."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get('math') != math or key not in t:
+        return None
+    return t[key]['bytes_per_call']
 
 
 # feature noise of the synthetic identities: 5.0 keeps the plain mAP well
@@ -87,8 +103,10 @@ def run_duke(reps=3, noise=NOISE):
     rr_us = e0.elapsed_time(e1) * 200.0
     N = Q + G
     rr_bytes = N * N * 4 + Q * G * 4
+    dm = ops.dist_math()
     roof_rr = dict(bound='hbm', achieved=round(rr_bytes / rr_us / 1e3, 1), peak=8000.0,
-                   unit='GB/s', frac=round(rr_bytes / rr_us / 1e3 / 8000.0, 4), traffic=None,
+                   unit='GB/s', frac=round(rr_bytes / rr_us / 1e3 / 8000.0, 4),
+                   traffic=_traffic('rerank', dm),
                    kernel='pps_re_ranking (OD build, top-%d, V / V_qe, Jaccard)' % 21,
                    avg_call_us=round(rr_us, 1), algorithmic_bytes_per_call=rr_bytes)
     # the [N, N] self-distance alone: upper-triangle super-blocks on the
@@ -103,10 +121,10 @@ def run_duke(reps=3, noise=NOISE):
     e1.synchronize()
     sd_us = e0.elapsed_time(e1) * 200.0
     sd_flops = N * (N + 1) / 2 * 2.0 * D
-    dm = ops.dist_math()
     sd_peak = {'h2': 2517.0 / 3, 'x3': 2517.0 / 6}.get(dm, 157.3)
     roof_sd = dict(bound='mfma', achieved=round(sd_flops / sd_us / 1e6, 1), peak=round(sd_peak, 1),
-                   unit='TFLOP/s', frac=round(sd_flops / sd_us / 1e6 / sd_peak, 4), traffic=None,
+                   unit='TFLOP/s', frac=round(sd_flops / sd_us / 1e6 / sd_peak, 4),
+                   traffic=_traffic('selfdist', dm),
                    kernel='%s over [queries; gallery] (norms + split + triangle GEMM)' % (
                        {'h2': 'pps_distmat_h2_self_tiled', 'x3': 'pps_distmat_x3_self_tiled'}
                        .get(dm, 'pps_distmat')),

@@ -1,10 +1,14 @@
 #!/bin/bash
-# PMC passes over the Duke configuration (re-ranking kernels): instruction
-# mix / stall cycles, then HBM fetch.  One counter set per run.
+# PMC passes over the Duke configuration (scripts/bench_duke_rerank.py):
+# FETCH_SIZE, WRITE_SIZE (separate runs, --kernel-trace only) ->
+# profiles/r05/pmc_duke.json (scripts/pmc_duke.py), which the Duke leg reads
+# for its roofline traffic.  Each GPU step under its own time limit.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/duke_pmc
-rm -rf $OUT && mkdir -p $OUT
-timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $OUT/p1 -o run --output-format csv -- python3 scripts/bench_duke_rerank.py --reps 1 > $OUT/p1.log 2>&1 || { tail -5 $OUT/p1.log; exit 1; }
-timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $OUT/p2 -o run --output-format csv -- python3 scripts/bench_duke_rerank.py --reps 1 > $OUT/p2.log 2>&1 || { tail -5 $OUT/p2.log; exit 1; }
-ls -R $OUT | head -20
+R=${ROUND_DIR:-profiles/r05}
+rm -rf $OUT && mkdir -p $OUT $R
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/p1 -o run --output-format csv -- python3 scripts/bench_duke_rerank.py --reps 1 > $OUT/p1.log 2>&1 || { tail -5 $OUT/p1.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/p2 -o run --output-format csv -- python3 scripts/bench_duke_rerank.py --reps 1 > $OUT/p2.log 2>&1 || { tail -5 $OUT/p2.log; exit 1; }
+python3 scripts/pmc_duke.py $OUT ${DIST_MATH:-h2} > $R/pmc_duke.json || exit 1
+cat $R/pmc_duke.json

@@ -10,7 +10,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out
-R=${ROUND_DIR:-profiles/r04}
+R=${ROUND_DIR:-profiles/r05}
 mkdir -p $OUT $R
 TILES=$OUT/tiles.json
 rm -f $TILES

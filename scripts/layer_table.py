@@ -17,6 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_traffic import epi_of, load, load_all  # noqa: E402
 
 PEAK_X3 = 2516.8 / 6  # bf16 dense MFMA peak / 6 product terms (bench.py)
+PEAK_H2 = 2516.8 / 3  # f16 dense MFMA peak / 3 product terms (PPS_TILE_H2 layers)
+H2 = 0x800
 
 
 def is_mfma(nm):
@@ -37,10 +39,10 @@ def main():
                              'WRITE_SIZE') if is_mfma(nm)][-n:]
     p3 = [r for r in load_all(glob.glob(os.path.join(d, 'p3', '*counter_collection.csv'))[0])
           if is_mfma(r[0]) and 'GRBM_GUI_ACTIVE' in r[1]][-n:]
-    print('| layer | op | tile | GFLOP | alg. MB | us | TF | frac of x3 roof | MFMA busy '
-          '| clock GHz | fetch MB | write MB | traffic / alg. |')
-    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|')
-    tot = dict(fl=0.0, ms=0.0, by=0.0, tr=0.0)
+    print('| layer | op | tile | math | GFLOP | alg. MB | us | TF | frac of its roof | frac of x3 '
+          'roof | MFMA busy | clock GHz | fetch MB | write MB | traffic / alg. |')
+    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|')
+    tot = dict(fl=0.0, ms=0.0, by=0.0, tr=0.0, roof_ms=0.0)
     for i, (name, v) in enumerate(gemm):
         fl, ms, by = v['flops'], v['ms'], v['bytes']
         tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
@@ -53,18 +55,22 @@ def main():
             clk = act / dur if dur else 0.0
         else:
             busy = clk = float('nan')
+        h2 = bool(v.get('tile', 0) & H2)
+        peak = PEAK_H2 if h2 else PEAK_X3
         tot['fl'] += fl
         tot['ms'] += ms
         tot['by'] += by
         tot['tr'] += fb + wb
-        print('| %s | %s | %d | %.2f | %.1f | %.1f | %.1f | %.3f | %.3f | %.2f | %.1f | %.1f '
-              '| %.2f |' % (name, v['op'], v.get('tile', 0), fl / 1e9, by / 1e6, ms * 1e3, tf,
-                            tf / PEAK_X3, busy, clk, fb / 1e6, wb / 1e6,
-                            (fb + wb) / by if by else float('nan')))
+        tot['roof_ms'] += fl / (peak * 1e12) * 1e3
+        print('| %s | %s | %#x | %s | %.2f | %.1f | %.1f | %.1f | %.3f | %.3f | %.3f | %.2f | %.1f '
+              '| %.1f | %.2f |' % (name, v['op'], v.get('tile', 0), 'f16x2' if h2 else 'bf16x3',
+                                   fl / 1e9, by / 1e6, ms * 1e3, tf, tf / peak, tf / PEAK_X3,
+                                   busy, clk, fb / 1e6, wb / 1e6,
+                                   (fb + wb) / by if by else float('nan')))
     tf = tot['fl'] / (tot['ms'] * 1e-3) / 1e12
-    print('| **all %d** | | | %.1f | %.1f | %.1f | %.1f | %.3f | | | | | %.2f |'
-          % (n, tot['fl'] / 1e9, tot['by'] / 1e6, tot['ms'] * 1e3, tf, tf / PEAK_X3,
-             tot['tr'] / tot['by']))
+    print('| **all %d** | | | | %.1f | %.1f | %.1f | %.1f | %.3f | %.3f | | | | | %.2f |'
+          % (n, tot['fl'] / 1e9, tot['by'] / 1e6, tot['ms'] * 1e3, tf,
+             tot['roof_ms'] / tot['ms'], tf / PEAK_X3, tot['tr'] / tot['by']))
 
 
 if __name__ == '__main__':

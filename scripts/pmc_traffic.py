@@ -9,8 +9,11 @@ gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE (KB) counts half of
 the bytes of wide streaming reads -> x2; WRITE_SIZE (KB) is exact for 16-B
 stores.  Infinity-Cache hits are counted too, so this is memory-side
 traffic, an upper bound on HBM bytes.  conv = the last forward's implicit-GEMM
-launches (the bench's conv_roofline forward); distmat = the last EPI_DIST launch;
-rank = the last rank_count_stream launch (the rank roofline's kernel).
+launches (the bench's conv_roofline forward; bf16x3 and f16x2 tiles alike),
+conv_splits = that forward's f16x2 activation-split passes
+(split_act_h2_kernel, PPS_TILE_H2P); distmat = the last distance launch
+(gemm_h2_kernel, or gemm_x3p_kernel with EPI_DIST); rank = the last
+rank_count_stream launch (the rank roofline's kernel).
 """
 import csv
 import glob
@@ -59,19 +62,38 @@ def main():
     def is_gemm(nm):   # the forward's MFMA launches (the fused stem included)
         return any(k + '<' in nm for k in knames + ('seam_kernel',)) or (
             'stem_conv_pool_x3_kernel' in nm or 'stem_ring_x3_kernel' in nm)
+
+    def is_dist(nm):
+        return 'gemm_h2_kernel<' in nm or (is_gemm(nm) and epi_of(nm) == 1)
+
+    def is_conv(nm):
+        return is_gemm(nm) and epi_of(nm) != 1
     out = dict(source='rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) '
                       'of bench.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch')
-    for key, sel, n in (('conv', lambda e: e != 1, nconv), ('distmat', lambda e: e == 1, 1)):
-        f = [v for nm, v in fetch if is_gemm(nm) and sel(epi_of(nm))][-n:]
-        w = [v for nm, v in write if is_gemm(nm) and sel(epi_of(nm))][-n:]
+    dmath = 'h2' if any('gemm_h2_kernel<' in nm for nm, _ in fetch) else math
+    for key, sel, n in (('conv', is_conv, nconv), ('distmat', is_dist, 1)):
+        f = [v for nm, v in fetch if sel(nm)][-n:]
+        w = [v for nm, v in write if sel(nm)][-n:]
         if len(f) < n or len(w) < n:
             continue
         fb = 2 * 1024 * sum(f)
         wb = 1024 * sum(w)
-        out[key] = dict(math=math, launches=n, fetch_bytes=fb, write_bytes=wb,
-                        bytes_per_launch=round((fb + wb) / n))
+        out[key] = dict(math=math if key == 'conv' else dmath, launches=n, fetch_bytes=fb,
+                        write_bytes=wb, bytes_per_launch=round((fb + wb) / n))
         if key == 'conv':
             out[key]['batch'] = batch
+    # the activation-split passes of the same forward (those after its first conv)
+    if 'conv' in out:
+        idx = [i for i, (nm, _) in enumerate(fetch) if is_conv(nm)]
+        if len(idx) >= nconv:
+            lo, hi = idx[-nconv], idx[-1]
+            fs = [v for nm, v in fetch[lo:hi] if 'split_act_h2_kernel' in nm]
+            wi = [i for i, (nm, _) in enumerate(write) if is_conv(nm)]
+            ws = [v for nm, v in write[wi[-nconv]:wi[-1]] if 'split_act_h2_kernel' in nm] \
+                if len(wi) >= nconv else []
+            if fs and len(fs) == len(ws):
+                out['conv_splits'] = dict(launches=len(fs), fetch_bytes=2 * 1024 * sum(fs),
+                                          write_bytes=1024 * sum(ws))
     f = [v for nm, v in fetch if 'rank_count_stream_kernel' in nm][-1:]
     w = [v for nm, v in write if 'rank_count_stream_kernel' in nm][-1:]
     if f and w:
@@ -84,7 +106,7 @@ def main():
     p3 = glob.glob(os.path.join(d, 'p3', '*counter_collection.csv'))
     if p3:
         rows = [(nm, c, dur) for nm, c, dur in load_all(p3[0])
-                if is_gemm(nm) and epi_of(nm) != 1 and 'GRBM_GUI_ACTIVE' in c][-nconv:]
+                if is_conv(nm) and 'GRBM_GUI_ACTIVE' in c][-nconv:]
         if len(rows) == nconv:
             dur = sum(r[2] for r in rows)
             act = sum(r[1]['GRBM_GUI_ACTIVE'] for r in rows) / 8.0
@@ -98,13 +120,13 @@ def main():
         # the same for the last distance-matrix launch (the distmat roofline's
         # kernel): its clock and MFMA-busy fraction
         rows = [(nm, c, dur) for nm, c, dur in load_all(p3[0])
-                if is_gemm(nm) and epi_of(nm) == 1 and 'GRBM_GUI_ACTIVE' in c][-1:]
+                if is_dist(nm) and 'GRBM_GUI_ACTIVE' in c][-1:]
         if rows:
             nm, c, dur = rows[0]
             act = c['GRBM_GUI_ACTIVE'] / 8.0
             busy = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0)
             out['distmat_mfma'] = dict(
-                math=math, duration_us=round(dur / 1e3, 1), clock_GHz=round(act / dur, 3),
+                math=dmath, duration_us=round(dur / 1e3, 1), clock_GHz=round(act / dur, 3),
                 mfma_busy_frac=round(busy / (1024.0 * act), 4),
                 mfma_busy_frac_at_2p4GHz=round(busy / (1024.0 * dur * 2.4), 4),
                 source='rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (third pass)')
