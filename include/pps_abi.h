@@ -270,6 +270,30 @@ int pps_conv2d_bn_act_pps_h2_planes(const uint16_t* x2, int64_t x_plane, int N, 
                                     const float* residual, float* y, int Ho, int Wo,
                                     const int32_t* splits, int S, int max_ave, float* pps_out,
                                     const float* amax_x, int tile, void* stream);
+/* A conv + BN + ReLU producer whose output feeds one f16x2 conv: the
+ * output is written as f16x2 planes y2 [2][y_plane] on the power-of-two
+ * scale of the bound B = bound_w * max|x| + bound_b >= max|y| (max|x| from
+ * the slot bound_in; bound_w / bound_b from pps_h2_out_bound on the packed
+ * f32 weights, BN scale and shift), and B goes to the slot bound_out -- the
+ * consumer's activation slot, so it takes the same scale and reads the
+ * fragments it would split from the f32 output (same bits as the f32 path
+ * given that slot).  w: bf16x3 planes (wrs NULL; pipelined 16x16x32 tiles,
+ * f32 x) or chunk-tiled f16x2 weights with wrs (x or planes x2 [2][x_plane]
+ * with amax_x, as pps_conv2d_bn_act_h2[_planes]).  No residual, no split-K,
+ * Cin % 32 == 0. */
+int pps_conv2d_bn_act_h2out(const float* x, const uint16_t* x2, int64_t x_plane, int N, int H,
+                            int W, int Cin, int ldx, const void* w, const float* wrs, int Cout,
+                            int Kpad, int KH, int KW, int stride, int pad, int dil,
+                            const float* scale, const float* shift, uint16_t* y2, int64_t y_plane,
+                            int Ho, int Wo, int ldy, const float* amax_x, const float* bound_in,
+                            float bound_w, float bound_b, float* bound_out, int tile,
+                            void* stream);
+/* out2 (HOST) = {max_c |scale_c| * sum_k |w[c][k]|, max(0, max_c shift_c)}
+ * of packed f32 conv weights w [Cout][Kpad] (scale may be NULL: 1), padded
+ * up by 2^-20 relative: the bound constants of pps_conv2d_bn_act_h2out.
+ * Synchronous; the same value on every call. */
+int pps_h2_out_bound(const float* w, int Cout, int Kpad, const float* scale, const float* shift,
+                     float* out2, void* stream);
 /* max |x| over n floats into the activation-max slot amax (zero it first):
  * the input scale the f16x2 entries take, for a tensor whose producer did
  * not report it. */

@@ -55,6 +55,11 @@ SIGNATURES = {
                                  c_ptr],
     'pps_amax': [c_ptr, c_i64, c_ptr, c_ptr],
     'pps_split_f16x2_act': [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
+    'pps_h2_out_bound': [c_ptr, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_conv2d_bn_act_h2out': [c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                                c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
+                                c_ptr, c_ptr, c_i64, c_int, c_int, c_int, c_ptr, c_ptr,
+                                ctypes.c_float, ctypes.c_float, c_ptr, c_int, c_ptr],
     'pps_conv2d_bn_act_h2_planes': [c_ptr, c_i64, c_int, c_int, c_int, c_int, c_int, c_ptr,
                                     c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_int, c_int, c_int,

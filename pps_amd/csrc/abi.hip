@@ -610,9 +610,22 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
                       int64_t x_plane = 0, uint16_t* y_pl = nullptr, int64_t y_plane = 0,
                       int splitk = 1, float* part = nullptr, int* fix_cnt = nullptr,
                       int64_t n_cnt = 0, float* amax_out = nullptr,
-                      const float* w_rs = nullptr, const float* amax_in = nullptr) {
-  PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) && (y != nullptr) != (y_pl != nullptr),
-              "exactly one of x / x planes and one of y / y planes must be given");
+                      const float* w_rs = nullptr, const float* amax_in = nullptr,
+                      uint16_t* y_h2, int64_t y_h2_plane, const float* h2o_in, float h2o_bw,
+                      float h2o_bb) {
+  // y_h2: the output as f16x2 planes on the scale of the bound
+  // h2o_bw * max|x| + h2o_bb (EPI_F_H2OUT; the bound goes to amax_out)
+  PPS_ENFORCE((x != nullptr) != (x_pl != nullptr) &&
+                  (int)(y != nullptr) + (int)(y_pl != nullptr) + (int)(y_h2 != nullptr) == 1,
+              "exactly one of x / x planes and one of y / y planes / y f16x2 planes must be given");
+  if (y_h2) {
+    PPS_ENFORCE(relu && !residual && splitk == 1 && h2o_in && amax_out && x3 &&
+                    y_h2_plane >= (int64_t)N * Ho * Wo * ldy && Cin % 32 == 0 &&
+                    Kpad == KH * KW * Cin && h2o_bw >= 0.f && h2o_bb >= 0.f,
+                "f16x2 planes out: conv + BN + ReLU (no residual, no split-K), Cin % 32 == 0, "
+                "the input's slot, an output slot, a plane stride >= N*Ho*Wo*ldy");
+    y = reinterpret_cast<float*>(y_h2);  // for the shared checks below
+  }
   // PPS_TILE_B_TILED or-ed into tile: the bf16x3 weights are chunk-tiled;
   // PPS_TILE_COL_ORDER: column-major tile order
   const bool wtiled = tile > 0 && (tile & PPS_TILE_B_TILED) != 0;
@@ -665,6 +678,12 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
   p.out = y; p.ldo = ldy; p.relu = relu; p.tile = tile;
   p.colmajor = colmajor ? 1 : 0;
   p.amax_out = amax_out;
+  int h2o = 0;
+  if (y_h2) {
+    p.out = nullptr; p.out3 = y_h2; p.out_plane = y_h2_plane;
+    p.h2o_in = h2o_in; p.h2o_bw = h2o_bw; p.h2o_bb = h2o_bb;
+    h2o = EPI_F_H2OUT;
+  }
   if (w_rs) {
     // f16x2 (pps_conv2d_bn_act_h2, the whole-network plan's PPS_TILE_H2):
     // f32 activations scaled by their tensor's max, chunk-tiled two-plane
@@ -688,7 +707,7 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
       p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
       p.a_bytes = (uint32_t)((int64_t)N * H * W * ldx * 2);
     }
-    return launch_gemm_x3(p, EPI_CONV | EPI_F_H2, 1, as_stream(stream));
+    return launch_gemm_x3(p, EPI_CONV | EPI_F_H2 | h2o, 1, as_stream(stream));
   }
   if (x_pl) {
     p.a = nullptr; p.a3 = x_pl; p.a_plane = x_plane;
@@ -749,7 +768,9 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
       p.tiled = 2;
     }
     p.b_bytes = (uint32_t)(p.b_plane * 2);
-    return launch_gemm_x3(p, y_pl ? EPI_CONV | EPI_F_PLANES : EPI_CONV, 1, as_stream(stream));
+    PPS_ENFORCE(!h2o || !x_pl, "f16x2 planes out from a bf16x3 conv: f32 activations in");
+    return launch_gemm_x3(p, (y_pl ? EPI_CONV | EPI_F_PLANES : EPI_CONV) | h2o, 1,
+                          as_stream(stream));
   }
   p.b = static_cast<const float*>(w);
   return launch_gemm(p, EPI_CONV, 1, as_stream(stream));
@@ -946,6 +967,21 @@ int pps_conv2d_bn_act_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int 
   return conv_impl(nullptr, N, H, W, Cin, ldx, w2t, 1, Cout, Kpad, KH, KW, stride, pad, dil,
                    scale, shift, residual, relu, y, Ho, Wo, ldy, tile, stream, x2, x_plane,
                    nullptr, 0, 1, nullptr, nullptr, 0, amax_y, wrs, amax_x);
+}
+
+int pps_conv2d_bn_act_h2out(const float* x, const uint16_t* x2, int64_t x_plane, int N, int H,
+                            int W, int Cin, int ldx, const void* w, const float* wrs, int Cout,
+                            int Kpad, int KH, int KW, int stride, int pad, int dil,
+                            const float* scale, const float* shift, uint16_t* y2, int64_t y_plane,
+                            int Ho, int Wo, int ldy, const float* amax_x, const float* bound_in,
+                            float bound_w, float bound_b, float* bound_out, int tile,
+                            void* stream) {
+  PPS_ENFORCE(w && y2 && bound_in && bound_out, "null pointer");
+  PPS_ENFORCE(!x2 || wrs, "f16x2 activation planes in: f16x2 weights (wrs) only");
+  return conv_impl(x2 ? nullptr : x, N, H, W, Cin, ldx, w, 1, Cout, Kpad, KH, KW, stride, pad,
+                   dil, scale, shift, nullptr, 1, nullptr, Ho, Wo, ldy, tile, stream, x2, x_plane,
+                   nullptr, 0, 1, nullptr, nullptr, 0, bound_out, wrs, wrs ? amax_x : nullptr, y2,
+                   y_plane, bound_in, bound_w, bound_b);
 }
 
 int pps_conv2d_bn_act_pps_h2_planes(const uint16_t* x2, int64_t x_plane, int N, int H, int W,

@@ -718,6 +718,37 @@ int split_act_h2(const float* x, int64_t n, const float* slot, uint16_t* planes,
   return PPS_OK;
 }
 
+// The constants of an f16x2-planes-out conv's output bound (EPI_F_H2OUT):
+// out[0] = max_c |scale_c| * sum_k |w[c][k]| (k in order, one thread per
+// channel), out[1] = max(0, max_c shift_c).  One workgroup; max is
+// order-free, so the value is the same on every launch.
+__global__ void __launch_bounds__(256)
+h2_out_bound_kernel(const float* __restrict__ w, int Cout, int Kpad,
+                    const float* __restrict__ scale, const float* __restrict__ shift,
+                    float* __restrict__ out) {
+  __shared__ float s_w[256], s_b[256];
+  float mw = 0.f, mb = 0.f;
+  for (int c = threadIdx.x; c < Cout; c += 256) {
+    float a = 0.f;
+    for (int k = 0; k < Kpad; ++k) a += fabsf(w[(int64_t)c * Kpad + k]);
+    mw = fmaxf(mw, fabsf(scale ? scale[c] : 1.f) * a);
+    mb = fmaxf(mb, shift[c]);
+  }
+  s_w[threadIdx.x] = mw;
+  s_b[threadIdx.x] = mb;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 256; ++i) {
+      mw = fmaxf(mw, s_w[i]);
+      mb = fmaxf(mb, s_b[i]);
+    }
+    // one ulp of headroom per 2^20 (the f32 sum is not an upper bound of the
+    // exact one by itself)
+    out[0] = mw * (1.f + 0x1p-20f);
+    out[1] = mb * (1.f + 0x1p-20f);
+  }
+}
+
 int amax_of(const float* x, int64_t n, float* amax, hipStream_t st) {
   if (n <= 0) return PPS_OK;
   const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -734,6 +765,23 @@ int pps_amax(const float* x, int64_t n, float* amax, void* stream) {
   PPS_ENFORCE(x && amax, "null pointer");
   PPS_ENFORCE(n >= 0, "n must be >= 0");
   return amax_of(x, n, amax, as_stream(stream));
+}
+
+int pps_h2_out_bound(const float* w, int Cout, int Kpad, const float* scale, const float* shift,
+                     float* out2, void* stream) {
+  using namespace pps;
+  PPS_ENFORCE(w && shift && out2, "null pointer");
+  PPS_ENFORCE(Cout > 0 && Kpad > 0, "bad shape");
+  const hipStream_t st = as_stream(stream);
+  float* d = nullptr;
+  PPS_ENFORCE(hipMallocAsync(&d, 2 * sizeof(float), st) == hipSuccess, "hipMallocAsync");
+  hipLaunchKernelGGL(h2_out_bound_kernel, dim3(1), dim3(256), 0, st, w, Cout, Kpad, scale, shift,
+                     d);
+  const hipError_t e1 = hipMemcpyAsync(out2, d, 2 * sizeof(float), hipMemcpyDeviceToHost, st);
+  const hipError_t e2 = hipStreamSynchronize(st);
+  (void)hipFreeAsync(d, st);
+  PPS_ENFORCE(e1 == hipSuccess && e2 == hipSuccess, "h2_out_bound_kernel");
+  return PPS_OK;
 }
 
 int pps_split_f16x2_act(const float* x, int64_t n, const float* amax, uint16_t* planes,

@@ -218,7 +218,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
 // f32 output, the conv epilogues C [| RELU] [| RES] [| DUAL].
 bool ws_eligible(const GemmParams& p, int epi, int batch) {
   if (batch != 1 || p.splitk != 1 || p.ksplit_conv || p.a3 || !p.a || !p.b3 || p.sym) return false;
-  if (epi & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES | EPI_F_PPS)) return false;
+  if (epi & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES | EPI_F_PPS | EPI_F_H2OUT)) return false;
   if (p.KH != 1 || p.KW != 1 || p.stride != 1 || p.pad != 0 || p.H != p.Ho || p.W != p.Wo)
     return false;
   const int K = p.Kloop;

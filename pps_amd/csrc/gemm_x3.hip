@@ -275,6 +275,18 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     if (p.relu) epi |= EPI_F_RELU;
     if (p.a2) epi |= EPI_F_DUAL;
   }
+  if ((epi & EPI_F_H2OUT) && !(epi & EPI_F_H2)) {
+    // a bf16x3 producer writing f16x2 planes: pipelined tiles (the others
+    // run tile 38, the pipelined 16x16x32 group)
+    if (p.a3 || p.splitk != 1 || p.ksplit_conv || batch != 1 || !p.out3 || !p.h2o_in ||
+        !x3p_eligible(p, epi)) {
+      set_error("f16x2 planes out: f32 activations, no split-K, Cin % 32 == 0");
+      return PPS_ERR_INVALID_ARG;
+    }
+    const int t = (p.tile < GEMM_TILE_P16_FIRST || p.tile == GEMM_TILE_WS ||
+                   p.tile >= GEMM_TILE_C16_FIRST) ? GEMM_TILE_P16_FIRST : p.tile;
+    return launch_gemm_x3p(p, epi, batch, stream, t - GEMM_TILE_P_FIRST);
+  }
   if ((p.tiled & 2) && !(epi & EPI_F_H2) &&
       (p.tile == GEMM_TILE_WS || p.tile < GEMM_TILE_P_FIRST ||
        (p.splitk > 1 && !p.ksplit_conv))) {

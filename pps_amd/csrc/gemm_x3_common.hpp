@@ -123,6 +123,26 @@ __device__ inline void split8_h2(const f32x4& x0, const f32x4& x1, float S, bf16
   f1 = __builtin_bit_cast(bf16x8, h1);
 }
 
+// Four outputs as f16x2 planes on the scale S (EPI_F_H2OUT): split8_h2's
+// split, so a consumer reading the planes gets the fragments it would split
+// from the f32 values on that scale.
+__device__ inline void split4_h2(const f32x4& v, float S, u32x2& hi, u32x2& lo) {
+  f16x4 h0, h1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float y = v[e] * S;
+    h0[e] = (_Float16)y;
+    h1[e] = (_Float16)(y - (float)h0[e]);
+  }
+  hi = __builtin_bit_cast(u32x2, h0);
+  lo = __builtin_bit_cast(u32x2, h1);
+}
+
+// The bound B >= max|y| of an EPI_F_H2OUT conv output (GemmParams::h2o_*)
+__device__ inline float h2o_bound(const GemmParams& p) {
+  return p.h2o_bw * amax_read(p.h2o_in) + p.h2o_bb;
+}
+
 // The three terms with the operands swapped as in mfma16_x3t (weights as the
 // MFMA "A": transposed accumulator), fixed order b0 a0, b1 a0, b0 a1.
 __device__ inline f32x4 mfma16_h2t(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {

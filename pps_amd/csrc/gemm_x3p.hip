@@ -591,9 +591,12 @@ static int launch_tile_h2(const GemmParams& p, int epi, int batch, hipStream_t s
               "weights and scales; the fused shortcut reads f32");
     return PPS_ERR_INVALID_ARG;
   }
-  if (p.a3) {   // f16x2 activation planes (pps_split_f16x2_act)
+  constexpr int HO = EPI_F_H2OUT;
+  if (p.a3) {   // f16x2 activation planes (pps_split_f16x2_act or a producer's EPI_F_H2OUT)
     switch (epi & ~H) {
       case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, true, S>(p, batch, stream); break;
+      case C | RL | HO:
+        launch_one_p<BM, BN, WM, WN, NSF, C | RL | HO | H, true, S>(p, batch, stream); break;
       case C | RS | RL:
         launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, true, S>(p, batch, stream); break;
       case C | RS | RL | EPI_F_PPS:
@@ -614,6 +617,8 @@ static int launch_tile_h2(const GemmParams& p, int epi, int batch, hipStream_t s
   }
   switch (epi & ~H) {
     case C | RL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | H, false, S>(p, batch, stream); break;
+    case C | RL | HO:
+      launch_one_p<BM, BN, WM, WN, NSF, C | RL | HO | H, false, S>(p, batch, stream); break;
     case C | RS | RL:
       launch_one_p<BM, BN, WM, WN, NSF, C | RS | RL | H, false, S>(p, batch, stream); break;
     case C | RL | EPI_F_DUAL:
@@ -735,6 +740,14 @@ static int launch_tile_p(const GemmParams& p, int epi, int batch, hipStream_t st
       launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_DUAL, false, S>(p, batch, stream); break;
     case C | PL: launch_one_p<BM, BN, WM, WN, NSF, C | PL, false, S>(p, batch, stream); break;
     case C | RL | PL: launch_one_p<BM, BN, WM, WN, NSF, C | RL | PL, false, S>(p, batch, stream); break;
+    case C | RL | EPI_F_H2OUT:
+      if constexpr (S == 16) {
+        launch_one_p<BM, BN, WM, WN, NSF, C | RL | EPI_F_H2OUT, false, S>(p, batch, stream);
+        break;
+      } else {
+        set_error("f16x2 planes out: a 16x16x32 tile");
+        return PPS_ERR_INVALID_ARG;
+      }
     default:
       set_error("unknown epilogue for the pipelined bf16x3 GEMM");
       return PPS_ERR_INVALID_ARG;
@@ -756,7 +769,8 @@ bool x3p_eligible(const GemmParams& p, int epi) {
   // 16-byte epilogue vectors (the distance epilogue falls back per row)
   if (!(epi & EPI_DIST)) {
     if (p.Ncol % 4 != 0 || p.ldo % 4 != 0) return false;
-    if ((epi & EPI_F_PLANES) ? (!p.out3 || !al16(p.out3) || p.out_plane % 4 != 0) : !al16(p.out))
+    if ((epi & (EPI_F_PLANES | EPI_F_H2OUT)) ? (!p.out3 || !al16(p.out3) || p.out_plane % 4 != 0)
+                                              : !al16(p.out))
       return false;
     if (p.residual && (p.ldr % 4 != 0 || !al16(p.residual))) return false;
     if ((p.scale && !al16(p.scale)) || (p.shift && !al16(p.shift)) || p.out_bstride % 4 != 0 ||

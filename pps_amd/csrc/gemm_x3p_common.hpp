@@ -94,14 +94,21 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   constexpr bool RAW = (EPI & EPI_F_RAW) != 0;
   constexpr bool PLANES = (EPI & EPI_F_PLANES) != 0;
   constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  constexpr bool H2O = (EPI & EPI_F_H2OUT) != 0;
   // f16x2 launches: the accumulators hold dot * 2^(s_a + s_w[col]); the
   // column scale takes 2^-(s_a + s_w) (exact: powers of two)
   float inv_a = 1.f;
   if (H2) h2_act_scale(p, DUAL, &inv_a);
   float amx = 0.f;  // max |y| of this thread's outputs (p.amax_out)
+  float so = 1.f, bnd = 0.f;  // f16x2 planes out: the bound and its scale
+  if (H2O) {
+    float inv;
+    bnd = h2o_bound(p);
+    so = h2_scale_of(bnd, &inv);
+  }
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
-  float* __restrict__ out = PLANES ? nullptr : p.out + obase;
-  uint16_t* __restrict__ out3 = PLANES ? p.out3 + obase : nullptr;
+  float* __restrict__ out = (PLANES || H2O) ? nullptr : p.out + obase;
+  uint16_t* __restrict__ out3 = (PLANES || H2O) ? p.out3 + obase : nullptr;
   const int ldo = (int)p.ldo;
   const int mrem = p.M - m0;
   const int nrem = p.Ncol - n0;
@@ -152,13 +159,19 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
           st_out2(o, (u32x2){h0, h1});
           st_out2(o + p.out_plane, (u32x2){m0_, m1});
           st_out2(o + 2 * p.out_plane, (u32x2){l0, l1});
+        } else if (H2O) {
+          u32x2 hi, lo;
+          split4_h2(v, so, hi, lo);
+          uint16_t* o = out3 + rr * ldo + cb + 8 * q;
+          st_out2(o, hi);
+          st_out2(o + p.out_plane, lo);
         } else {
           st_out4(out + rr * ldo + cb + 8 * q, v);
         }
       }
     }
   }
-  if (p.amax_out) amax_commit(p.amax_out, amx);
+  if (p.amax_out) amax_commit(p.amax_out, H2O ? bnd : amx);
 }
 
 // One-launch conv split-K (EPI_F_FIX): park this K slice's raw accumulators
@@ -254,11 +267,19 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool PPS = (EPI & EPI_F_PPS) != 0;
   constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  constexpr bool H2O = (EPI & EPI_F_H2OUT) != 0;
   static_assert(HB == 1 || (PPS && (BN / WN) % S == 0 && BNH % (BN / WN) == 0),
                 "column passes: PPS tiles whose wave columns fall in one pass");
+  static_assert(!(H2O && PPS), "f16x2 planes out: plain conv epilogues");
   float inv_a = 1.f;  // f16x2: see conv_epilogue_t
   if (H2) h2_act_scale(p, DUAL, &inv_a);
   float amx = 0.f;
+  float so = 1.f, bnd = 0.f;  // f16x2 planes out: see conv_epilogue_t
+  if (H2O) {
+    float inv;
+    bnd = h2o_bound(p);
+    so = h2_scale_of(bnd, &inv);
+  }
   float* t = reinterpret_cast<float*>(lds);
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
   const int ldo = (int)p.ldo;
@@ -272,7 +293,8 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
 #pragma unroll
   for (int hb = 0; hb < HB; ++hb) {
     const int c0h = hb * BNH;
-    float* __restrict__ out = p.out + obase + c0h;
+    float* __restrict__ out = H2O ? nullptr : p.out + obase + c0h;
+    uint16_t* __restrict__ out3 = H2O ? p.out3 + obase + c0h : nullptr;
     const int nrem = p.Ncol - n0 - c0h;
     const float* sc = DUAL ? nullptr : p.scale + batch * p.ss_bstride + n0 + c0h;
     const float* sh = p.shift + batch * p.ss_bstride + n0 + c0h;
@@ -326,6 +348,11 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       if (PPS) {  // the pooling below reads the tile back from LDS
         *reinterpret_cast<f32x4*>(t + row * LD + col) = v;
         if (p.pps_write_y) st_out4(out + row * ldo + col, v);
+      } else if (H2O) {
+        u32x2 hi, lo;
+        split4_h2(v, so, hi, lo);
+        st_out2(out3 + row * ldo + col, hi);
+        st_out2(out3 + row * ldo + col + p.out_plane, lo);
       } else {
         st_out4(out + row * ldo + col, v);
       }
@@ -455,7 +482,7 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
       }
     }
   }
-  if (p.amax_out) amax_commit(p.amax_out, amx);
+  if (p.amax_out) amax_commit(p.amax_out, H2O ? bnd : amx);
 }
 
 // The distance epilogue staged through LDS (not for self-distance tiles,

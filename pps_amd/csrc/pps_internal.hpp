@@ -58,6 +58,8 @@ enum Epi {
   EPI_F_PPS = 64,     // gemm_x3p.hip: + strip pooling and part power set of each image
   EPI_F_FIX = 128,    // gemm_x3p.hip conv split-K: the last K slice of a tile to finish
                       // sums the parked partials and runs the epilogue (no second pass)
+  EPI_F_H2OUT = 512,  // gemm_x3p.hip conv: result written as f16x2 planes (out3) on the
+                      // scale of a bound (h2o_*), the bound into amax_out
   EPI_F_H2 = 256      // gemm_x3p.hip / gemm_x3c.hip: f16x2 arithmetic (f32 activations
                       // scaled by 2^s from their tensor's max and split into two f16
                       // terms, weights as two f16 planes, three MFMA terms)
@@ -215,6 +217,14 @@ struct GemmParams {
   const float* amax_a;
   const float* amax_a2;
   float* amax_out;
+  // EPI_F_H2OUT (a conv + BN + ReLU producer feeding one f16x2 consumer): the
+  // output y <= B = h2o_bw * max|x| + h2o_bb (h2o_bw = max_c |scale_c| |W_c|_1,
+  // h2o_bb = max(0, max_c shift_c), max|x| from the input's slot h2o_in) is
+  // written as two f16 planes on the power-of-two scale of B (out3 +
+  // k * out_plane), and B goes to amax_out: the consumer takes its scale from
+  // that slot, so it reads the same fragments its own split of y would make
+  const float* h2o_in;
+  float h2o_bw, h2o_bb;
 };
 constexpr int kPpsFuseMaxStrips = 10;
 constexpr int kPpsFuseMaxCols = 256;  // widest tile the fused pooling takes (two column passes)
@@ -291,7 +301,8 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx, const void*
               int Ho, int Wo, int ldy, int tile, void* stream, const uint16_t* x_pl,
               int64_t x_plane, uint16_t* y_pl, int64_t y_plane, int splitk, float* part,
               int* fix_cnt, int64_t n_cnt, float* amax_out, const float* w_rs,
-              const float* amax_in);
+              const float* amax_in, uint16_t* y_h2 = nullptr, int64_t y_h2_plane = 0,
+              const float* h2o_in = nullptr, float h2o_bw = 0.f, float h2o_bb = 0.f);
 int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx, int KH, int KW, int stride,
               int pad, const float* x2, int H2, int W2, int Cin2, int ldx2, int stride2,
               const void* w, int x3, int Cout, int Kpad1, int Kpad2, const float* shift, int relu,

@@ -914,6 +914,39 @@ def split_act_h2(x, amax_x, out=None):
     return out
 
 
+def h2_out_bound(w_packed, scale, shift):
+    """(bound_w, bound_b) of a conv whose output is written as f16x2 planes
+    (pps_h2_out_bound on the packed f32 weights [Cout, Kpad], BN scale / shift):
+    max|y| <= bound_w * max|x| + bound_b."""
+    Cout, Kpad = w_packed.shape
+    out = (_lib.ctypes.c_float * 2)()
+    call('pps_h2_out_bound', _dev(w_packed.contiguous(), 'w'), Cout, Kpad,
+         _dev(scale, 'scale') if scale is not None else 0, _dev(shift, 'shift'), out, _stream())
+    return float(out[0]), float(out[1])
+
+
+def conv2d_bn_act_h2out(x, cin, w, wrs, kpad, k, stride, pad, dil, scale, shift, y2, amax_x,
+                        bound_in, bound, bound_out, tile=0):
+    """Conv + BN + ReLU whose output y2 [2, N, Ho, Wo, Cout] (int16) is f16x2
+    planes on the scale of the bound bound[0] * max|x| + bound[1] (max|x| from
+    the slot bound_in, `bound` from h2_out_bound), the bound written to the slot
+    bound_out (pps_conv2d_bn_act_h2out).  w: bf16x3 planes [3, Cout, Kpad] with
+    wrs None, or split_weights_h2 output with its wrs (then x may be f16x2
+    planes, and amax_x is the f16x2 input slot)."""
+    planes = _h2_planes(x)
+    N, H, W, ldx = x.shape[1:] if planes else x.shape
+    _, _, Ho, Wo, Cout = y2.shape
+    call('pps_conv2d_bn_act_h2out', 0 if planes else _dev(x, 'x'),
+         _dev(x, 'x planes', torch.int16) if planes else 0, x.stride(0) if planes else 0,
+         N, H, W, cin, ldx, _dev(w, 'w', torch.int16), _dev(wrs, 'wrs') if wrs is not None else 0,
+         Cout, kpad, k, k, stride, pad, dil, _dev(scale, 'scale'), _dev(shift, 'shift'),
+         _dev(y2, 'y2', torch.int16), y2.stride(0), Ho, Wo, Cout,
+         _amax_arg(amax_x, 'amax_x') if amax_x is not None else 0,
+         _amax_arg(bound_in, 'bound_in'), float(bound[0]), float(bound[1]),
+         _amax_arg(bound_out, 'bound_out'), int(tile), _stream())
+    return y2
+
+
 def _h2_planes(x):
     """x is f16x2 activation planes [2, N, H, W, C] (split_act_h2)?"""
     return x.dtype == torch.int16 and x.dim() == 5 and x.shape[0] == 2

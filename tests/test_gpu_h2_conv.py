@@ -238,3 +238,63 @@ def test_conv_pps_h2_activation_planes_same_bits():
         ops.conv2d_bn_act_pps_h2(planes, Cin, w2, wrs, kpad, 1, 1, 0, 1, sc, sh, res, split,
                                  True, b, amx, tile=tile)
         assert torch.equal(a, b), tile
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+    (2, 24, 8, 512, 512, 1, 1, 0),     # res5 branch2a -> 2b
+    (2, 24, 8, 256, 256, 3, 1, 1),     # res4 branch2b -> 2c
+    (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1
+    (3, 7, 5, 64, 96, 3, 1, 1),        # ragged M (N and the consumer's K: multiples of 32)
+])
+@pytest.mark.parametrize('arith', ['x3', 'h2', 'h2_planes_in'])
+def test_conv_h2out_planes_equal_split_of_f32_output(N, H, W, Cin, Cout, k, s, p, arith):
+    """A producer writing f16x2 planes on its output bound's scale
+    (pps_conv2d_bn_act_h2out): the planes equal pps_split_f16x2_act of the same
+    conv's f32 output with the bound in the slot, the bound is >= max|y|, and
+    a consumer f16x2 conv reading the planes gives the bits of one reading the
+    f32 output with that slot."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(Cin + Cout + k)
+    x = np.maximum(rng.randn(N, H, W, Cin), 0).astype(np.float32)
+    w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)
+    wp, kpad = model.pack_conv_weight(w)
+    wpd = _cuda(wp)
+    sc, sh = _cuda(rng.uniform(0.5, 1.5, Cout)), _cuda(rng.randn(Cout) * 0.1)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    xd = _cuda(x)
+    ax = ops.amax(xd)
+    bound = ops.h2_out_bound(wpd, sc, sh)
+    y = torch.empty((N, Ho, Wo, Cout), device='cuda')
+    y2 = torch.full((2, N, Ho, Wo, Cout), -1, dtype=torch.int16, device='cuda')
+    by = ops.amax_slot()
+    tile = ops.TILE_P16_FIRST
+    if arith == 'x3':
+        w3 = ops.split_bf16x3(wpd)
+        ops.conv2d_bn_act(xd, Cin, w3, kpad, k, s, p, 1, sc, sh, None, True, y, tile=tile)
+        ops.conv2d_bn_act_h2out(xd, Cin, w3, None, kpad, k, s, p, 1, sc, sh, y2, None, ax, bound,
+                                by, tile=tile)
+    else:
+        w2, wrs = ops.split_weights_h2(wpd)
+        xin = ops.split_act_h2(xd, ax) if arith == 'h2_planes_in' else xd
+        ops.conv2d_bn_act_h2(xd, Cin, w2, wrs, kpad, k, s, p, 1, sc, sh, None, True, y, ax,
+                             tile=tile)
+        ops.conv2d_bn_act_h2out(xin, Cin, w2, wrs, kpad, k, s, p, 1, sc, sh, y2, ax, ax, bound,
+                                by, tile=tile)
+    B = ops.amax_value(by)
+    assert B >= float(y.abs().max())
+    assert B == np.float32(bound[0]) * np.float32(ops.amax_value(ax)) + np.float32(bound[1]) or \
+        abs(B - (bound[0] * ops.amax_value(ax) + bound[1])) <= 1e-6 * B
+    want = ops.split_act_h2(y, by)
+    assert torch.equal(y2, want)
+    # a consumer (1x1 to 96 channels): planes in == f32 in with the bound slot
+    w_c = (rng.randn(96, Cout, 1, 1) / np.sqrt(Cout)).astype(np.float32)
+    wpc, kpc = model.pack_conv_weight(w_c)
+    w2c, wrsc = ops.split_weights_h2(_cuda(wpc))
+    one, zero = torch.ones(96, device='cuda'), torch.zeros(96, device='cuda')
+    z1 = torch.empty((N, Ho, Wo, 96), device='cuda')
+    z2 = torch.empty((N, Ho, Wo, 96), device='cuda')
+    ops.conv2d_bn_act_h2(y, Cout, w2c, wrsc, kpc, 1, 1, 0, 1, one, zero, None, True, z1, by,
+                         tile=tile)
+    ops.conv2d_bn_act_h2(y2, Cout, w2c, wrsc, kpc, 1, 1, 0, 1, one, zero, None, True, z2, by,
+                         tile=tile)
+    assert torch.equal(z1, z2)
