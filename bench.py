@@ -587,7 +587,8 @@ def table_digest(nm):
                 splitk_layers=sum(1 for L in layers if L['splitk'] > 1),
                 seam_pairs=sum(1 for L in layers if L['tile'] & ops.TILE_SEAM),
                 h2_layers=sum(1 for L in layers if L['tile'] & ops.TILE_H2),
-                h2_plane_inputs=sum(1 for L in layers if L['tile'] & ops.TILE_H2P))
+                h2_plane_inputs=sum(1 for L in layers if L['tile'] & ops.TILE_H2P),
+                h2_plane_edges=sum(1 for L in layers if L['tile'] & ops.TILE_H2E))
 
 
 def e2e_stage(nm, rank, world, n_images, batch, threads):
@@ -837,7 +838,8 @@ def main():
     nm, blobs, imgs, xbuf = build_bench_model(
         B, rank, table=saved, autotune=not args.no_autotune,
         flags=(native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1' else 0) |
-        (native.AUTOTUNE_NO_H2 if os.environ.get('PPS_AUTOTUNE_NO_H2') == '1' else 0))
+        (native.AUTOTUNE_NO_H2 if os.environ.get('PPS_AUTOTUNE_NO_H2') == '1' else 0) |
+        (native.AUTOTUNE_NO_H2E if os.environ.get('PPS_AUTOTUNE_NO_H2E') == '1' else 0))
     cfg = market_cfg()
     H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
     feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')

@@ -106,6 +106,14 @@ int pps_gemm_num_tiles(void);
  * the conv, which then reads the planes (same bits, no split arithmetic in
  * its main loop; a workspace buffer of 4 B per input element). */
 #define PPS_TILE_H2P 0x1000
+/* With PPS_TILE_H2 on a conv / conv_pps layer C whose input is the output of
+ * a conv + BN + ReLU layer P read by C alone (no residual, Cin % 32 == 0, not
+ * the second half of a seam pair): P writes its output as f16x2 planes on
+ * the scale of its output bound (pps_conv2d_bn_act_h2out; P in either
+ * arithmetic, on a pipelined 16x16x32 tile) and C reads them -- no split in
+ * C's main loop and no split pass, same bits as C splitting the f32 output on
+ * that scale. */
+#define PPS_TILE_H2E 0x2000
 
 /* ---- retrieval: distance matrix ------------------------------------------
  * Replaces reid_dataset_evaluator.py:244-272 `compute_dist(array1, array2,
@@ -792,6 +800,7 @@ int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets
 #define PPS_AUTOTUNE_SPLITK 2     /* also try conv split-K 2..4           */
 #define PPS_AUTOTUNE_NO_SEAM 4    /* do not try PPS_TILE_SEAM pairs       */
 #define PPS_AUTOTUNE_NO_H2 8      /* do not try PPS_TILE_H2 (f16x2) tiles */
+#define PPS_AUTOTUNE_NO_H2E 16    /* do not try PPS_TILE_H2E planes edges */
 
 typedef struct PpsBlob {     /* one Detectron blob, HOST float32 memory   */
   const char* name;          /* e.g. "res2_0_branch2a_w", "pps01_bn_riv"  */
@@ -863,6 +872,8 @@ int pps_model_release(PpsModel* model, int N);   /* N <= 0: all */
  * device pointer, planes flag (bf16x3 [3][...]) and its 4-D shape. */
 int pps_model_tensor(const PpsModel* model, int N, const char* blob, void** ptr,
                      int* planes, int64_t* shape4);
+/* (*planes == 2: f16x2 planes [2][...] of the PPS_TILE_H2E edge, on the
+ * power-of-two scale of the bound pps_model_tensor_amax reports.) */
 /* The activation max max|t| its producer reported for tensor `blob` in the
  * last forward at batch N (the f16x2 layers' input scales; debug / parity),
  * copied to *out (HOST).  Synchronous. */

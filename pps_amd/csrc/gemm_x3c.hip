@@ -210,10 +210,8 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   }
   const int bsw = (r32 >> 2) & 3;
   float h2s = 1.f;  // f16x2: the activation scale 2^s_a
-  if constexpr (H2) {
-    float inv;
-    h2s = h2_act_scale(p, false, &inv);
-  }
+  float inv_a = 0.f;  // and its inverse, for the epilogue (read once, here)
+  if constexpr (H2) h2s = h2_act_scale(p, false, &inv_a);
 
   auto chunk_barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -315,9 +313,10 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
 
   if constexpr (LDSEPI)
-    conv_epilogue_lds<EPI, BM, BN, WM, WN, S, 1>(p, acc, lds, 0, 0, m0, n0, wm, wn, r32, h);
+    conv_epilogue_lds<EPI, BM, BN, WM, WN, S, 1>(p, acc, lds, 0, 0, m0, n0, wm, wn, r32, h, 0.f,
+                                                 inv_a);
   else
-    conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, 0, 0, m0, n0, wm, wn, r32, h);
+    conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, 0, 0, m0, n0, wm, wn, r32, h, 0.f, inv_a);
 }
 
 template <int BM, int BN, int WM, int WN, int NS, bool A3, int PMAX>

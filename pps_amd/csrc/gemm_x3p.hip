@@ -47,8 +47,13 @@ namespace pps {
 __device__ float g_x3p_clk[2 * 65536];
 #endif
 
+// (f16x2 128x128 8-wave tiles: four waves per SIMD -- two workgroups per CU,
+// <= 128 VGPRs; HIP's second bound is waves per execution unit --
+// the planes-out epilogue would otherwise tip them to 130 and one workgroup)
 template <int BM, int BN, int WM, int WN, int EPI, int NS, bool A3, int S = 32>
-__global__ void __launch_bounds__(64 * WM * WN)
+__global__ void __launch_bounds__(64 * WM * WN,
+                                  ((EPI & EPI_F_H2) && BM == 128 && BN == 128 && WM * WN == 8 &&
+                                   NS == 2) ? 4 : 1)
 gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #if X3P_CLK
   const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -99,7 +104,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // conv epilogue through LDS where the [BM][BN+4] tile fits the 160 KB:
   // 5-12 % faster on the epilogue-bound branch2c layers (residual + output
   // streams) for the 128-row tiles; the 8-wave 192x128 tile is faster
-  // without it (scripts/gemm_probe.py --residual)
+  // without it (scripts/gemm_probe.py --residual) except for f16x2 planes out,
+  // whose 2-byte elements would leave as 32-byte row pieces
+  // (scripts/probes/h2out_probe.py)
 #ifndef X3P_LDSEPI
 #define X3P_LDSEPI 1
 #endif
@@ -114,7 +121,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool LDSEPI = (X3P_LDSEPI || PPSEPI) &&
                           !(EPI & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES)) &&
                           lds_epi_bytes<BM, BN / EHB>() <= 160 * 1024 &&
-                          (PPSEPI || !(BM == 192 && BN == 128 && NW == 8));
+                          (PPSEPI || (EPI & EPI_F_H2OUT) != 0 ||
+                           !(BM == 192 && BN == 128 && NW == 8));
 #ifndef X3P_DISTLDS
 #define X3P_DISTLDS 1
 #endif
@@ -364,10 +372,12 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       for (int r = 0; r < S * S / 64; ++r) acc[i][j][r] = 0.f;
 
   float h2s = 1.f;  // f16x2: the activation scale 2^s_a
-  if constexpr (H2 && !A3) {
-    float inv;
-    h2s = h2_act_scale(p, DUAL, &inv);
-  }
+  float inv_a = 0.f;  // and its inverse, for the epilogue (read once, here)
+  if constexpr (H2) h2s = h2_act_scale(p, DUAL, &inv_a);
+  // f16x2 planes out: the output bound, read now so its latency hides under
+  // the main loop instead of stalling the epilogue
+  float bnd_pre = 0.f;
+  if constexpr ((EPI & EPI_F_H2OUT) != 0) bnd_pre = h2o_bound(p);
   // Fragment reads: the rows of this lane are r32 mod S, so both swizzles
   // are per-lane constants.
   const int asw = (r32 >> 1) & 7;
@@ -562,9 +572,10 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     dist_epilogue_t<BM, BN, WM, WN, S>(p, acc, m0, n0, wm, wn, r32, h);
   else if constexpr (LDSEPI)
     conv_epilogue_lds<EPI, BM, BN, WM, WN, S, EHB>(p, acc, lds, batch, kslice, m0, n0, wm, wn, r32,
-                                                  h);
+                                                  h, bnd_pre, inv_a);
   else
-    conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h);
+    conv_epilogue_t<EPI, BM, BN, WM, WN, S>(p, acc, batch, kslice, m0, n0, wm, wn, r32, h,
+                                            bnd_pre, inv_a);
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int EPI, bool A3, int S>

@@ -84,7 +84,8 @@ template <int EPI, int BM, int BN, int WM, int WN, int S = 32>
 __device__ inline void conv_epilogue_t(const GemmParams& p,
                                        typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
                                        int batch, int kslice, int m0, int n0, int wm, int wn,
-                                       int r32, int h) {
+                                       int r32, int h, float bnd_pre = 0.f,
+                                       float inv_a_pre = 0.f) {
   constexpr int TM = BM / WM / S;
   constexpr int TN = BN / WN / S;
   constexpr int NQ = S * S / 256;  // 16-byte column groups per lane and block
@@ -97,13 +98,19 @@ __device__ inline void conv_epilogue_t(const GemmParams& p,
   constexpr bool H2O = (EPI & EPI_F_H2OUT) != 0;
   // f16x2 launches: the accumulators hold dot * 2^(s_a + s_w[col]); the
   // column scale takes 2^-(s_a + s_w) (exact: powers of two)
-  float inv_a = 1.f;
-  if (H2) h2_act_scale(p, DUAL, &inv_a);
+  float inv_a = 1.f;  // (inv_a_pre > 0: read by the kernel before its main loop)
+  if (H2) {
+    if (inv_a_pre > 0.f)
+      inv_a = inv_a_pre;
+    else
+      h2_act_scale(p, DUAL, &inv_a);
+  }
   float amx = 0.f;  // max |y| of this thread's outputs (p.amax_out)
-  float so = 1.f, bnd = 0.f;  // f16x2 planes out: the bound and its scale
+  // f16x2 planes out: the bound (read by the kernel before its main loop,
+  // h2o_bound) and its scale
+  float so = 1.f, bnd = bnd_pre;
   if (H2O) {
     float inv;
-    bnd = h2o_bound(p);
     so = h2_scale_of(bnd, &inv);
   }
   const int64_t obase = batch * p.out_bstride + kslice * p.out_sstride + (int64_t)m0 * p.ldo + n0;
@@ -257,7 +264,8 @@ template <int EPI, int BM, int BN, int WM, int WN, int S, int HB = 1>
 __device__ inline void conv_epilogue_lds(const GemmParams& p,
                                          typename AccT<S>::type (&acc)[BM / WM / S][BN / WN / S],
                                          unsigned char* lds, int batch, int kslice, int m0,
-                                         int n0, int wm, int wn, int r32, int h) {
+                                         int n0, int wm, int wn, int r32, int h,
+                                         float bnd_pre = 0.f, float inv_a_pre = 0.f) {
   constexpr int TM = BM / WM / S, TN = BN / WN / S, NQ = S * S / 256;
   constexpr int BNH = BN / HB;  // columns per pass
   constexpr int LD = BNH + 4;
@@ -272,12 +280,16 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
                 "column passes: PPS tiles whose wave columns fall in one pass");
   static_assert(!(H2O && PPS), "f16x2 planes out: plain conv epilogues");
   float inv_a = 1.f;  // f16x2: see conv_epilogue_t
-  if (H2) h2_act_scale(p, DUAL, &inv_a);
+  if (H2) {
+    if (inv_a_pre > 0.f)
+      inv_a = inv_a_pre;
+    else
+      h2_act_scale(p, DUAL, &inv_a);
+  }
   float amx = 0.f;
-  float so = 1.f, bnd = 0.f;  // f16x2 planes out: see conv_epilogue_t
+  float so = 1.f, bnd = bnd_pre;  // f16x2 planes out: see conv_epilogue_t
   if (H2O) {
     float inv;
-    bnd = h2o_bound(p);
     so = h2_scale_of(bnd, &inv);
   }
   float* t = reinterpret_cast<float*>(lds);
@@ -357,7 +369,50 @@ __device__ inline void conv_epilogue_lds(const GemmParams& p,
         st_out4(out + row * ldo + col, v);
       }
     };
-    if constexpr (PRE) {
+    if constexpr (H2O) {
+      // f16x2 planes out: eight columns per lane, so each plane leaves as
+      // 16-byte stores (whole rows across the wave); no residual here
+      static_assert(!HAS_RES && !PPS && C4 % 2 == 0, "f16x2 planes out: plain conv tiles");
+      constexpr int C8 = C4 / 2;
+      for (int idx = threadIdx.x; idx < BM * C8; idx += NT) {
+        const int row = idx / C8, col = 8 * (idx - row * C8);
+        if (row >= mrem || col >= nrem) continue;
+        u32x4 hw, lw;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int c = col + 4 * g;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(t + row * LD + c);
+          f32x4 s4 = DUAL ? (f32x4){1.f, 1.f, 1.f, 1.f} : *reinterpret_cast<const f32x4*>(sc + c);
+          if (H2) s4 = s4 * *reinterpret_cast<const f32x4*>(p.rs_b + n0 + c0h + c) * inv_a;
+          const f32x4 t4 = *reinterpret_cast<const f32x4*>(sh + c);
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf(a[e], s4[e], t4[e]);
+            if (RELU) v[e] = fmaxf(v[e], 0.f);
+            amx = fmaxf(amx, fabsf(v[e]));
+          }
+          u32x2 hi, lo;
+          split4_h2(v, so, hi, lo);
+          hw[2 * g] = hi[0];
+          hw[2 * g + 1] = hi[1];
+          lw[2 * g] = lo[0];
+          lw[2 * g + 1] = lo[1];
+        }
+        uint16_t* o = out3 + row * ldo + col;
+        if (col + 4 < nrem && ((ldo | p.out_plane) & 7) == 0) {
+          *reinterpret_cast<u32x4*>(o) = hw;
+          *reinterpret_cast<u32x4*>(o + p.out_plane) = lw;
+        } else {
+          st_out2(o, (u32x2){hw[0], hw[1]});
+          st_out2(o + p.out_plane, (u32x2){lw[0], lw[1]});
+          if (col + 4 < nrem) {
+            st_out2(o + 4, (u32x2){hw[2], hw[3]});
+            st_out2(o + 4 + p.out_plane, (u32x2){lw[2], lw[3]});
+          }
+        }
+      }
+    } else if constexpr (PRE) {
 #pragma unroll
       for (int it = 0; it < IT; ++it) finish(it * NT + threadIdx.x, rpre[it]);
     } else {

@@ -336,6 +336,7 @@ struct Layer {
   Buf w, scale, shift;  // w: f32 [Cout][Kpad] or bf16x3 planes
   Buf wt;               // x3 plain convs with Kpad % 32 == 0: the planes chunk-tiled
                         // (pps_tile_planes), used when tile carries PPS_TILE_B_TILED
+  float h2o_bw = 0.f, h2o_bb = 0.f;  // output bound constants (pps_h2_out_bound; 0: none)
   Buf w2, wrs;          // the f16x2 split (PPS_TILE_H2): two chunk-tiled f16 planes
                         // [2][Cout16/16][K/32][16][32] and per-channel scales [Cout]
   std::vector<int> split;
@@ -485,6 +486,16 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
           L.kpad == L.k * L.k * L.cin_eff && (L.op == Op::Conv || L.shortcut_cin % 32 == 0))
         split_h2w(L.w, L.cout, L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad, L.w2,
                   L.wrs, st);
+      // a conv + BN + ReLU that may write f16x2 planes for its consumer
+      // (PPS_TILE_H2E): the bound constants, from the f32 weights
+      if (L.op == Op::Conv && L.relu && L.residual.empty() && L.cin_eff % 32 == 0 &&
+          L.kpad == L.k * L.k * L.cin_eff && L.scale && L.shift) {
+        float b2[2];
+        rc_check(pps_h2_out_bound(L.w->as<float>(), L.cout, L.kpad, L.scale->as<float>(),
+                                  L.shift->as<float>(), b2, st));
+        L.h2o_bw = b2[0];
+        L.h2o_bb = b2[1];
+      }
       if (L.op == Op::Conv || L.op == Op::ConvDual)
         L.w = split3(L.w, (int64_t)L.cout * (L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad), 1, st);
       const int64_t kt = L.op == Op::ConvDual ? L.kpad + L.shortcut_cin : L.kpad;
@@ -672,12 +683,28 @@ bool h2_tile_ok(const Layer& L, int tile) {
   const int base = tile & 0xff;
   if (!L.w2 || (tile & PPS_TILE_SEAM)) return false;
   // activation planes: plain convs and conv_pps (the fused shortcut reads f32)
-  if ((tile & PPS_TILE_H2P) && L.op == Op::ConvDual) return false;
+  if ((tile & (PPS_TILE_H2P | PPS_TILE_H2E)) && L.op == Op::ConvDual) return false;
+  if ((tile & PPS_TILE_H2P) && (tile & PPS_TILE_H2E)) return false;
   if (L.op != Op::Conv && L.op != Op::ConvDual && L.op != Op::ConvPps) return false;
   if (!L.relu && L.op == Op::Conv) return false;  // the f16x2 epilogues end in a ReLU
   if (base == 0) return true;
   if (base < GEMM_TILE_P16_FIRST || base == GEMM_TILE_WS || base >= GEMM_NUM_TILES) return false;
   return L.op == Op::Conv || base < GEMM_TILE_C16_FIRST || base == GEMM_TILE_P16_192x128W41;
+}
+
+// The producer whose f16x2-planes output a PPS_TILE_H2E layer C reads
+// (structure only; planes / split-K at run time), or -1
+int h2e_producer(const PpsModel& m, const Layer& C) {
+  if (C.op != Op::Conv && C.op != Op::ConvPps) return -1;
+  for (size_t i = 0; i < m.layers.size(); ++i) {
+    const Layer& P = m.layers[i];
+    if (P.output != C.input) continue;
+    if (P.op != Op::Conv || !P.relu || !P.residual.empty() || P.h2o_bw <= 0.f) return -1;
+    if (count_readers(m, P.output, true) != 1) return -1;
+    if (i > 0 && m.layers[i - 1].seam_next == (int)i) return -1;  // a seam pair's second half
+    return (int)i;
+  }
+  return -1;
 }
 
 bool fix_tile(int tile) {
@@ -827,14 +854,34 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
   // chunk-tiled f16x2 split; COL_ORDER kept)
   const bool h2 = (tile & PPS_TILE_H2) != 0;
   const bool h2p = h2 && (tile & PPS_TILE_H2P) != 0;
+  const bool h2e = h2 && (tile & PPS_TILE_H2E) != 0;
   if (h2) {
     PPS_MCHECK(L.w2 && !L.planes_in && !L.planes_out && sk == 1,
                "layer '" + L.name + "': PPS_TILE_H2 needs the f16x2 weights, f32 activations "
                "at both ends and no split-K");
-    tile &= ~(PPS_TILE_H2 | PPS_TILE_H2P | PPS_TILE_B_TILED | PPS_TILE_SEAM);
+    tile &= ~(PPS_TILE_H2 | PPS_TILE_H2P | PPS_TILE_H2E | PPS_TILE_B_TILED | PPS_TILE_SEAM);
   }
+  // PPS_TILE_H2E on the layer that reads this one's output: write it as
+  // f16x2 planes on the output bound's scale (the bound into the slot)
+  const Layer* h2e_c = nullptr;
+  if (L.op == Op::Conv && L.h2o_bw > 0.f)
+    for (const Layer& C : m.layers)
+      if (C.input == L.output && (C.tile & PPS_TILE_H2E) && (C.tile & PPS_TILE_H2)) h2e_c = &C;
+  if (h2e_c) {
+    PPS_MCHECK(h2e_producer(m, *h2e_c) == (int)(&L - &m.layers[0]) && !L.planes_in &&
+                   !L.planes_out && sk == 1 && !(tile & PPS_TILE_SEAM),
+               "layer '" + h2e_c->name + "': PPS_TILE_H2E needs its producer '" + L.name +
+                   "' to be a conv + BN + ReLU read by it alone, f32 input, no split-K");
+    tile &= ~(PPS_TILE_B_TILED | PPS_TILE_SEAM);
+  }
+  // PPS_TILE_H2E: this layer's input, as f16x2 planes its producer wrote
+  auto h2e_input = [&](const Act& a, int64_t* plane) -> const uint16_t* {
+    *plane = a.s.numel();
+    return w.bufs.at(L.input)->as<uint16_t>();
+  };
   // PPS_TILE_H2P: the input's f16x2 planes, split once (same bits)
   auto h2_planes = [&](const Act& a, int64_t* plane) -> const uint16_t* {
+    if (h2e) return h2e_input(a, plane);
     const int64_t n = a.s.numel();
     PPS_MCHECK(w.h2p && (size_t)n <= w.h2p_elems, "layer '" + L.name +
                                                      "': no f16x2 activation-plane workspace");
@@ -882,13 +929,26 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       // the op-level entry points' implementation (same arguments as
       // pps_conv2d_bn_act_x3p[_splitk[_fused]] / _x3 / _h2), reporting max |y|
       float* amo = slotp(L.output);
+      // f16x2 planes out (the consumer's PPS_TILE_H2E): the output buffer
+      // holds the two planes, the bound goes to the output's slot
+      uint16_t* yh2 = h2e_c ? w.bufs.at(L.output)->as<uint16_t>() : nullptr;
+      const int64_t yh2_plane = ys.numel();
+      if (h2e_c)
+        PPS_MCHECK(amo && slotp(L.input), "layer '" + L.name + "': f16x2 planes out needs the "
+                                          "input's and the output's activation slots");
       if (h2) {
         int64_t xpl = 0;
-        const uint16_t* xp = h2p ? h2_planes(a, &xpl) : nullptr;
+        const uint16_t* xp = (h2p || h2e) ? h2_planes(a, &xpl) : nullptr;
         rc_check(conv_impl(xp ? nullptr : a.f, n, H, W, L.cin_eff, ldx, L.w2->as<uint16_t>(), 1,
                            L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res, L.relu,
-                           fbuf(L.output), Ho, Wo, L.cout, tile, st, xp, xpl, nullptr, 0, 1,
-                           nullptr, nullptr, 0, amo, L.wrs->as<float>(), slotp(L.input)));
+                           yh2 ? nullptr : fbuf(L.output), Ho, Wo, L.cout, tile, st, xp, xpl,
+                           nullptr, 0, 1, nullptr, nullptr, 0, amo, L.wrs->as<float>(),
+                           slotp(L.input), yh2, yh2_plane, slotp(L.input), L.h2o_bw, L.h2o_bb));
+      } else if (yh2) {   // bf16x3 arithmetic, f16x2 planes out
+        rc_check(conv_impl(a.f, n, H, W, L.cin_eff, ldx, w3, 1, L.cout, L.kpad, L.k, L.k,
+                           L.stride, L.pad, L.dil, sc, sh, res, L.relu, nullptr, Ho, Wo, L.cout,
+                           tile, st, nullptr, 0, nullptr, 0, 1, nullptr, nullptr, 0, amo, nullptr,
+                           nullptr, yh2, yh2_plane, slotp(L.input), L.h2o_bw, L.h2o_bb));
       } else if (m.x3 && (L.planes_in || L.planes_out || sk > 1)) {
         const int t = tile >= GEMM_TILE_P_FIRST ? tile : 0;
         float* yf = L.planes_out ? nullptr : fbuf(L.output);
@@ -976,7 +1036,7 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
         int t = std::find(ok16.begin(), ok16.end(), tb) != ok16.end() ? tb : ok16[0];
         t |= tile & PPS_TILE_COL_ORDER;
         int64_t xpl = 0;
-        const uint16_t* xp = h2p ? h2_planes(a, &xpl) : nullptr;
+        const uint16_t* xp = (h2p || h2e) ? h2_planes(a, &xpl) : nullptr;
         rc_check(conv_pps_impl(xp ? nullptr : a.f, xp, xpl, n, H, W, L.cin_eff, ldx,
                                L.w2->as<uint16_t>(),
                                L.cout, L.kpad, L.k, L.k, L.stride, L.pad, L.dil, sc, sh, res,
@@ -1034,9 +1094,14 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
   w.amax_need.assign(m.slot.size(), all ? 1 : 0);
   if (!all)
     for (const Layer& L : m.layers)
-      if (L.tile & PPS_TILE_H2)
+      if (L.tile & PPS_TILE_H2) {
         for (const std::string* t : {&L.input, &L.input2})
           if (!t->empty() && m.slot.count(*t)) w.amax_need[m.slot.at(*t)] = 1;
+        // PPS_TILE_H2E: the producer's bound reads its own input's max
+        const int pi = (L.tile & PPS_TILE_H2E) ? h2e_producer(m, L) : -1;
+        if (pi >= 0 && m.slot.count(m.layers[pi].input))
+          w.amax_need[m.slot.at(m.layers[pi].input)] = 1;
+      }
   if (first == 0 && !keep_amax) {
     // a forward: every producer reports its output's max afresh
     hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
@@ -1053,6 +1118,8 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
         bool planes = false;
         for (const auto& P : m.layers)
           if (P.output == *t && P.planes_out) planes = true;
+        // an f16x2-planes edge (PPS_TILE_H2E): its slot keeps the producer's bound
+        if (L.input == *t && (L.tile & PPS_TILE_H2E) && (L.tile & PPS_TILE_H2)) planes = true;
         const float* src = *t == "data" ? x : (w.bufs.count(*t) ? fbuf_of(w, *t) : nullptr);
         if (planes || !src) continue;
         float* slot = w.amax->as<float>() + (size_t)m.slot.at(*t) * PPS_AMAX_SLOT_FLOATS;
@@ -1311,7 +1378,7 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
     Layer* L = find_layer(m, layer);
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
     const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM | PPS_TILE_H2 |
-                              PPS_TILE_H2P);
+                              PPS_TILE_H2P | PPS_TILE_H2E);
     PPS_MCHECK(tile >= 0 && base < GEMM_NUM_TILES, "tile out of range");
     PPS_MCHECK(!(tile & PPS_TILE_H2) || h2_tile_ok(*L, tile),
                std::string("PPS_TILE_H2: '") + layer +
@@ -1319,6 +1386,9 @@ int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
                    "55, 60 or (convs) 56..59; PPS_TILE_H2P: plain convs and conv_pps only");
     PPS_MCHECK(!(tile & PPS_TILE_H2P) || (tile & PPS_TILE_H2),
                "PPS_TILE_H2P goes with PPS_TILE_H2");
+    PPS_MCHECK(!(tile & PPS_TILE_H2E) || ((tile & PPS_TILE_H2) && h2e_producer(*m, *L) >= 0),
+               std::string("PPS_TILE_H2E: '") + layer + "' needs PPS_TILE_H2 and a producer "
+               "that is a conv + BN + ReLU read by it alone (Cin % 32 == 0)");
     PPS_MCHECK(!(tile & PPS_TILE_SEAM) ||
                    (L->seam_next >= 0 && base == GEMM_TILE_WS &&
                     !(tile & (PPS_TILE_B_TILED | PPS_TILE_COL_ORDER))),
@@ -1406,8 +1476,13 @@ int pps_model_tensor(const PpsModel* m, int N, const char* blob, void** ptr, int
     PPS_MCHECK(b != it->second.bufs.end(), std::string("no device tensor '") + blob + "'");
     *ptr = b->second->p;
     *planes = 0;
-    for (const auto& L : m->layers)
+    for (const auto& L : m->layers) {
       if (L.output == blob && L.planes_out) *planes = 1;
+      // read by a PPS_TILE_H2E layer: f16x2 planes on the slot's scale
+      if (L.input == blob && (L.tile & PPS_TILE_H2E) && (L.tile & PPS_TILE_H2) &&
+          h2e_producer(*m, L) >= 0)
+        *planes = 2;
+    }
     const Shape& s = it->second.shapes.at(blob);
     for (int d = 0; d < 4; ++d) shape4[d] = s.d[d];
   });
@@ -1642,6 +1717,31 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
           cost[L.seam_next] = 0.f;
         } else {
           L.tile = save;
+        }
+      }
+    }
+    if (try_h2 && !(flags & PPS_AUTOTUNE_NO_H2E)) {
+      // f16x2 planes from the producer's epilogue (PPS_TILE_H2E): kept if
+      // the producer + consumer pair is > 2 % faster
+      for (size_t ci = 0; ci < m->layers.size(); ++ci) {
+        Layer& C = m->layers[ci];
+        if (!(C.tile & PPS_TILE_H2) || C.planes_in) continue;
+        const int pi = h2e_producer(*m, C);
+        if (pi < 0) continue;
+        Layer& P = m->layers[pi];
+        if (P.planes_in || P.planes_out || P.splitk != 1 || (P.tile & PPS_TILE_SEAM)) continue;
+        const int save = C.tile;
+        C.tile = (save & ~PPS_TILE_H2P) | PPS_TILE_H2E;
+        float tp = 1e30f, tc = 1e30f;
+        for (int r = 0; r < final_rounds; ++r) {
+          tp = std::min(tp, time_layer(*m, P, *w, x, P.tile, 1, final_reps, st, t));
+          tc = std::min(tc, time_layer(*m, C, *w, x, C.tile, 1, final_reps, st, t));
+        }
+        if (tp + tc < 0.98f * (cost[pi] + cost[ci])) {
+          cost[pi] = tp;
+          cost[ci] = tc;
+        } else {
+          C.tile = save;
         }
       }
     }

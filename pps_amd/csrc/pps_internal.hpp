@@ -275,7 +275,9 @@ __device__ inline float amax_read(const float* slot) {
   float m = 0.f;
 #pragma unroll
   for (int j = 0; j < kAmaxSubs; ++j) m = fmaxf(m, slot[j * kAmaxStride]);
-  return m;
+  // the same value in every lane: kept in a scalar register (the GEMM main
+  // loops carry the scales derived from it)
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
 }
 
 // f16x2 activation split: x 2^s with s = 15 - E for max|x| = m 2^E, m in

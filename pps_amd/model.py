@@ -391,6 +391,7 @@ class PPSModel(object):
                          if C['k'] > 1 and C['cin'] >= 256])
         self.feat_dim = self.plan.feat_dim
         self._batch = None
+        self._h2e_slot = {}   # PPS_TILE_H2E edges of the last forward: blob -> bound slot
 
     def _fuse_stem(self, blobs):
         """Replace the stem conv + maxpool pair by one 'stem_pool' layer (its
@@ -605,13 +606,20 @@ class PPSModel(object):
         if '_w2' not in L:
             L['_w2'] = ops.split_weights_h2(L['w32'])
         w2, wrs = L['_w2']
-        base = tile & ~(ops.TILE_H2 | ops.TILE_H2P | ops.TILE_B_TILED | ops.TILE_SEAM |
-                        ops.TILE_COL_ORDER)
+        base = tile & ~(ops.TILE_H2 | ops.TILE_H2P | ops.TILE_H2E | ops.TILE_B_TILED |
+                        ops.TILE_SEAM | ops.TILE_COL_ORDER)
         flags = tile & ops.TILE_COL_ORDER
         x = bufs[L['input']]
-        amx = ops.amax(x)
         op = L['op']
-        xin = ops.split_act_h2(x, amx) if tile & ops.TILE_H2P else x   # PPS_TILE_H2P
+        if tile & ops.TILE_H2E:   # the producer wrote f16x2 planes and their bound's slot
+            amx = self._h2e_slot.get(L['input'])
+            if amx is None:
+                raise RuntimeError("layer '%s': PPS_TILE_H2E but the producer wrote no f16x2 "
+                                   "planes" % L['name'])
+            xin = self._h2e_view(L['input'], bufs)
+        else:
+            amx = self._in_slot(L['input'], x)
+            xin = ops.split_act_h2(x, amx) if tile & ops.TILE_H2P else x   # PPS_TILE_H2P
         if op == 'conv':
             res = bufs[L['residual']] if L['residual'] else None
             ops.conv2d_bn_act_h2(xin, L['cin_eff'], w2, wrs, L['kpad'], L['k'], L['stride'],
@@ -632,10 +640,96 @@ class PPSModel(object):
                                      bufs[L['residual']], L['split_arr'], L['max_ave'],
                                      bufs[L['output']], amx, y=None, tile=t)
 
+    def _h2e_view(self, blob, bufs):
+        """The f16x2 planes [2, N, H, W, C] (int16) an H2E edge's f32 buffer holds
+        (the two planes numel() apart, as the C plan writes them)."""
+        b = bufs[blob]
+        return b.view(-1).view(torch.int16).view((2,) + tuple(b.shape))
+
+    def _in_slot(self, blob, x):
+        """The activation-max slot an f16x2 layer reads for its input: the
+        bound slot of an H2E edge, else max|x| measured here (the C plan's
+        producers report the same value from their epilogues)."""
+        s = self._h2e_slot.get(blob)
+        return s if s is not None else ops.amax(x)
+
+    def h2e_producer(self, C):
+        """Index of the conv + BN + ReLU whose output layer C may read as f16x2
+        planes (PPS_TILE_H2E; the C plan's h2e_producer), or -1."""
+        if C['op'] not in ('conv', 'conv_pps'):
+            return -1
+        for i, P in enumerate(self.layers):
+            if P['output'] != C['input']:
+                continue
+            if (P['op'] != 'conv' or not P['relu'] or P['residual'] or 'w32' not in P or
+                    P['cin_eff'] % 32 or P['kpad'] != P['k'] ** 2 * P['cin_eff']):
+                return -1
+            readers = sum((Q['input'] == P['output']) + (Q.get('input2') == P['output']) +
+                          (Q.get('residual') == P['output']) for Q in self.layers)
+            if readers != 1 or (i > 0 and self._seam_pair(i - 1)):
+                return -1
+            return i
+        return -1
+
+    def _seam_pair(self, i):
+        """Layers i, i + 1 are a seam-capable branch2c + branch2a (seam_pair)."""
+        if self.math != 'x3' or i + 1 >= len(self.layers):
+            return False
+        L, X = self.layers[i], self.layers[i + 1]
+
+        def plain1x1(A):
+            return (A['op'] == 'conv' and A['k'] == 1 and A['stride'] == 1 and
+                    A['pad'] == 0 and A['relu'] and A['kpad'] == A['cin_eff'])
+        return bool(plain1x1(L) and plain1x1(X) and L.get('residual') and
+                    not X.get('residual') and X['input'] == L['output'] and
+                    X['cin_eff'] == L['cout'] and
+                    (L['cin_eff'], L['cout'], X['cout']) in ((64, 256, 64), (128, 512, 128)))
+
+    def _h2e_consumer(self, L):
+        for C in self.layers:
+            if (C['input'] == L['output'] and C.get('tile', 0) & ops.TILE_H2E and
+                    C.get('tile', 0) & ops.TILE_H2):
+                return C
+        return None
+
+    def _run_h2out(self, L, bufs, tile):
+        """Producer of a PPS_TILE_H2E edge: conv + BN + ReLU writing f16x2
+        planes on the scale of the bound bw * max|x| + bb (its arithmetic as
+        its own tile says), the bound into the edge's slot."""
+        if L.get('planes_in') or L.get('planes_out') or L.get('splitk', 1) > 1:
+            raise RuntimeError("layer '%s': f16x2 planes out needs an f32 input and no split-K"
+                               % L['name'])
+        if '_h2o' not in L:
+            L['_h2o'] = ops.h2_out_bound(L['w32'], L['scale'], L['shift'])
+        x = bufs[L['input']]
+        base = tile & ~(ops.TILE_H2 | ops.TILE_H2P | ops.TILE_H2E | ops.TILE_B_TILED |
+                        ops.TILE_SEAM)
+        in_slot = self._in_slot(L['input'], x) if not tile & ops.TILE_H2E else \
+            self._h2e_slot[L['input']]
+        out_slot = ops.amax_slot(x.device)
+        y2 = self._h2e_view(L['output'], bufs)
+        if tile & ops.TILE_H2:
+            if '_w2' not in L:
+                L['_w2'] = ops.split_weights_h2(L['w32'])
+            w, wrs = L['_w2']
+            if tile & ops.TILE_H2E:
+                xin = self._h2e_view(L['input'], bufs)
+            else:
+                xin = ops.split_act_h2(x, in_slot) if tile & ops.TILE_H2P else x
+            amx = in_slot
+        else:
+            w, wrs, xin, amx = L['w'], None, x, None
+        ops.conv2d_bn_act_h2out(xin, L['cin_eff'], w, wrs, L['kpad'], L['k'], L['stride'],
+                                L['pad'], L['dil'], L['scale'], L['shift'], y2, amx, in_slot,
+                                L['_h2o'], out_slot, tile=base)
+        self._h2e_slot[L['output']] = out_slot
+
     def _run(self, L, bufs, out=None, tile=None, splitk=None):
         op = L['op']
         tile = L.get('tile', 0) if tile is None else tile
         tile &= ~ops.TILE_SEAM   # one layer alone (forward() runs the seam pairs)
+        if op == 'conv' and self._h2e_consumer(L) is not None:
+            return self._run_h2out(L, bufs, tile)
         if tile & ops.TILE_H2:
             return self._run_h2(L, bufs, tile)
         sk = L.get('splitk', 1) if splitk is None else splitk
@@ -722,6 +816,7 @@ class PPSModel(object):
             self._alloc(N, H, W)
         bufs = dict(self._bufs)
         bufs['data'] = x
+        self._h2e_slot = {}   # f16x2-planes edges (PPS_TILE_H2E): blob -> bound slot
         fused = None   # the branch2a the previous seam launch computed
         for i, L in enumerate(self.layers):
             if L is fused:
@@ -907,6 +1002,10 @@ class PPSModel(object):
             if not ok:
                 raise ValueError("PPS_TILE_SEAM: '%s' is not a branch2c feeding a seam-capable "
                                  "branch2a (base tile 54)" % name)
+        if tile & ops.TILE_H2E and (not tile & ops.TILE_H2 or tile & ops.TILE_H2P or
+                                    self.h2e_producer(L) < 0):
+            raise ValueError("PPS_TILE_H2E: '%s' needs PPS_TILE_H2 (not H2P) and a producer that "
+                             "is a conv + BN + ReLU read by it alone" % name)
         if tile & ops.TILE_H2P and (not tile & ops.TILE_H2 or L['op'] == 'conv_dual'):
             raise ValueError("PPS_TILE_H2P: '%s' needs PPS_TILE_H2 on a plain conv or conv_pps"
                              % name)

@@ -22,6 +22,7 @@ from .config import cfg as _cfg
 
 MATH = {'x3': 0, 'f32': 1}
 AUTOTUNE_NO_PLANES, AUTOTUNE_SPLITK, AUTOTUNE_NO_SEAM, AUTOTUNE_NO_H2 = 1, 2, 4, 8
+AUTOTUNE_NO_H2E = 16
 FWD_KEEP_AMAX = 1   # pps_abi.h PPS_FWD_KEEP_AMAX
 
 
@@ -259,6 +260,13 @@ class NativeModel(object):
              ctypes.addressof(pl), ctypes.addressof(shape))
         n = int(np.prod(list(shape)))
         torch.cuda.synchronize()
+        if pl.value == 2:   # f16x2 planes of a PPS_TILE_H2E edge, on the bound's scale
+            raw = (ctypes.c_uint16 * (2 * n))()
+            _memcpy_d2h(raw, p.value, 4 * n)
+            h = np.frombuffer(raw, np.float16).astype(np.float64).reshape(2, n).sum(0)
+            bnd = np.float32(self.tensor_amax(N, blob))
+            e = int(np.frexp(bnd)[1]) if bnd > 0 else 0
+            return (h * 2.0 ** (e - 15)).astype(np.float32).reshape(tuple(shape))
         if pl.value:
             raw = (ctypes.c_uint16 * (3 * n))()
             _memcpy_d2h(raw, p.value, 6 * n)

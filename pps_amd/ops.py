@@ -26,9 +26,11 @@ TILE_COL_ORDER = 0x200  # PPS_TILE_COL_ORDER: column-major output tile order (sa
 TILE_SEAM = 0x400  # PPS_TILE_SEAM (whole-network plan): branch2c + next branch2a in one launch
 TILE_H2 = 0x800    # PPS_TILE_H2 (whole-network plan): the layer in f16x2 arithmetic
 TILE_H2P = 0x1000  # PPS_TILE_H2P: with TILE_H2, the input split once into f16x2 planes
+TILE_H2E = 0x2000  # PPS_TILE_H2E: with TILE_H2, the input arrives as f16x2 planes its
+                   # producer wrote on the scale of an output bound (conv2d_bn_act_h2out)
 TILE_WS = 54       # the weight-stationary 1x1 tile (gemm_ws.hip)
 TILE_H2_WIDE = 60  # 192x128 as 4 x 1 waves: f16x2 only (bf16x3 launches run tile 47)
-TILE_FLAGS = TILE_B_TILED | TILE_COL_ORDER | TILE_SEAM | TILE_H2 | TILE_H2P   # every or-ed flag
+TILE_FLAGS = TILE_B_TILED | TILE_COL_ORDER | TILE_SEAM | TILE_H2 | TILE_H2P | TILE_H2E   # every or-ed flag
 # tiles built with the one-launch split-K epilogue (conv2d_bn_act_x3p(..., counters=))
 FIX_TILES = (45, 47, 48, 49, 50)
 PPS_FUSE_MAX_COLS = 256  # widest tile the fused part pooling takes (pps_internal.hpp)

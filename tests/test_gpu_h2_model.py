@@ -8,6 +8,10 @@
   bits in the C plan and in the Python orchestrator (which measures its
   inputs' maxima with pps_amax), also under hipGraph replay, and stays
   within FWD_ATOL of the CPU oracle;
+* PPS_TILE_H2E edges (the producer writes f16x2 planes on the scale of its
+  output bound, bf16x3 or f16x2 producers): C plan == twin bit for bit,
+  within FWD_ATOL of the oracle, under graph replay; the planes decode to the
+  producer's f32 output within 2^-21 of the bound;
 * the C autotune with f16x2 candidates gives a table the Python orchestrator
   reproduces bit for bit;
 * the plan refuses PPS_TILE_H2 where it cannot run."""
@@ -114,6 +118,90 @@ def test_h2_table_c_plan_equals_twin_and_oracle():
     assert np.array_equal(out.cpu().numpy(), b)
 
 
+def _h2e_table(nm, pm, N):
+    """_h2_table with PPS_TILE_H2E on every consumer the plan accepts; every
+    third accepted edge gets a bf16x3 producer (tile 47).  Returns (table, edges)
+    with edges = [(producer, consumer)]."""
+    from pps_amd import ops
+    layers = nm.layers(N)
+    ok = {}
+    for name, t in _h2_table(nm, N).items():
+        try:
+            nm.set_tiles({name: t})
+            ok[name] = t
+        except RuntimeError:
+            nm.set_tiles({name: 0})
+    edges = []
+    for L in layers:
+        name = L['name']
+        if name not in ok or not ok[name] & ops.TILE_H2 or L['op'] not in ('conv', 'conv_pps'):
+            continue
+        t = (ok[name] & ~ops.TILE_H2P) | ops.TILE_H2E
+        try:
+            nm.set_tiles({name: t})
+        except RuntimeError:
+            continue
+        ok[name] = t
+        C = next(M for M in pm.layers if M.get('name') == name)   # the twin has the inputs
+        P = next(M['name'] for M in pm.layers if M['output'] == C['input'])
+        if len(edges) % 3 == 0 and not ok.get(P, 0) & ops.TILE_H2E:
+            ok[P] = 47
+            nm.set_tiles({P: 47})
+        edges.append((P, name))
+    return ok, edges
+
+
+def test_h2e_edges_c_plan_equals_twin_and_oracle():
+    from oracle.forward import GraphForward
+    from pps_amd import ops
+    blobs, pm, nm = _models(seed=11)
+    N = 3
+    x, xd = _input(N, seed=12)
+    nm.set_planes([])
+    pm.set_planes([])
+    ok, edges = _h2e_table(nm, pm, N)
+    print('PPS_TILE_H2E edges: %d' % len(edges))
+    assert len(edges) >= 18, edges
+    assert any(not ok[p] & ops.TILE_H2 for p, _ in edges)   # bf16x3 producers too
+    pm.set_tiles(ok)
+    a = pm.forward(xd).cpu().numpy()
+    b = nm.forward(xd).cpu().numpy()
+    assert np.array_equal(a, b)
+    ref = GraphForward(blobs)(x).numpy()
+    err = float(np.abs(b - ref).max())
+    print('f16x2 table with planes edges: max|err| vs oracle %.3g' % err)
+    assert err <= FWD_ATOL
+    # the planes decode to the producer's f32 output (the same table without
+    # that edge's flag: everything upstream of the producer is unchanged)
+    layers = {L['name']: L for L in nm.layers(N)}
+    for p, c in (edges[0], edges[1], edges[-1]):
+        if ok[p] & ops.TILE_H2E:
+            continue
+        blob = layers[p]['output']
+        dec = nm.tensor(N, blob)
+        bnd = nm.tensor_amax(N, blob)
+        nm.set_tiles({c: ok[c] & ~ops.TILE_H2E})
+        nm.forward(xd)
+        y = nm.tensor(N, blob)
+        nm.set_tiles({c: ok[c]})
+        assert bnd >= float(np.abs(y).max()) > 0
+        d = float(np.abs(dec.astype(np.float64) - y).max())
+        assert d <= bnd * 2.0 ** -21, (p, c, d, bnd)
+    # graph replay
+    nm.forward(xd)
+    nm.reserve(N)
+    out = torch.empty((N, nm.feat_dim), device='cuda')
+    nm.forward(xd, out=out)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nm.forward(xd, out=out)
+    out.zero_()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), b)
+
+
 def test_autotune_with_h2_candidates_then_twin():
     from pps_amd import ops
     _, pm, nm = _models(seed=7)
@@ -146,6 +234,18 @@ def test_h2_tile_refused_where_it_cannot_run():
         nm.set_tiles({'res2_0_branch2b': 38 | ops.TILE_H2P})     # without PPS_TILE_H2
     with pytest.raises(ValueError, match='PPS_TILE_H2P'):
         pm.set_tiles({dual: 47 | ops.TILE_H2 | ops.TILE_H2P})
+    # PPS_TILE_H2E: not on the pool's reader (maxpool producer), not without
+    # PPS_TILE_H2, not with PPS_TILE_H2P, not on a conv_dual
+    for bad in [('res2_0_branch2a', 38 | ops.TILE_H2 | ops.TILE_H2E),
+                ('res2_0_branch2b', 38 | ops.TILE_H2E),
+                ('res2_0_branch2b', 38 | ops.TILE_H2 | ops.TILE_H2P | ops.TILE_H2E),
+                (dual, 47 | ops.TILE_H2 | ops.TILE_H2E)]:
+        with pytest.raises(RuntimeError, match='PPS_TILE_H2'):
+            nm.set_tiles(dict([bad]))
+        with pytest.raises(ValueError, match='PPS_TILE_H2'):
+            pm.set_tiles(dict([bad]))
+    nm.set_tiles({'res2_0_branch2b': 38 | ops.TILE_H2 | ops.TILE_H2E})
+    pm.set_tiles({'res2_0_branch2b': 38 | ops.TILE_H2 | ops.TILE_H2E})
     # a plane edge into an f16x2 layer is refused, in either order
     edges = nm.plane_edges()
     p, c, _ = edges[0]
