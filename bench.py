@@ -839,7 +839,8 @@ def main():
         B, rank, table=saved, autotune=not args.no_autotune,
         flags=(native.AUTOTUNE_SPLITK if os.environ.get('PPS_AUTOTUNE_SPLITK') == '1' else 0) |
         (native.AUTOTUNE_NO_H2 if os.environ.get('PPS_AUTOTUNE_NO_H2') == '1' else 0) |
-        (native.AUTOTUNE_NO_H2E if os.environ.get('PPS_AUTOTUNE_NO_H2E') == '1' else 0))
+        (native.AUTOTUNE_NO_H2E if os.environ.get('PPS_AUTOTUNE_NO_H2E') == '1' else 0) |
+        (native.AUTOTUNE_NO_GROUPS if os.environ.get('PPS_AUTOTUNE_NO_GROUPS') == '1' else 0))
     cfg = market_cfg()
     H, W = cfg.REID.SCALE[1], cfg.REID.SCALE[0]
     feat = torch.empty((B, nm.feat_dim), dtype=torch.float32, device='cuda')

@@ -801,6 +801,8 @@ int pps_preprocess_bgr_ragged(const uint8_t* blob, int N, const int64_t* offsets
 #define PPS_AUTOTUNE_NO_SEAM 4    /* do not try PPS_TILE_SEAM pairs       */
 #define PPS_AUTOTUNE_NO_H2 8      /* do not try PPS_TILE_H2 (f16x2) tiles */
 #define PPS_AUTOTUNE_NO_H2E 16    /* do not try PPS_TILE_H2E planes edges */
+#define PPS_AUTOTUNE_NO_GROUPS 32 /* skip the in-forward pass over layers of
+                                     one shape (each layer keeps its own pick) */
 
 typedef struct PpsBlob {     /* one Detectron blob, HOST float32 memory   */
   const char* name;          /* e.g. "res2_0_branch2a_w", "pps01_bn_riv"  */
@@ -858,7 +860,11 @@ int pps_model_plane_edge(const PpsModel* model, int edge, const char** producer,
                          const char** consumer, int* on);
 int pps_model_set_planes(PpsModel* model, const char* producer, int on);
 /* Time every tile per layer on this device (then plane edges, optionally
- * split-K) with x [N][H][W][4] as input; not capturable. */
+ * split-K, seams, f16x2-plane edges) with x [N][H][W][4] as input; last, the
+ * layers of one shape (e.g. the five res4 3x3 convs) are tried on each of
+ * their members' two best tiles inside whole forwards, so the pick holds
+ * where the layer actually runs (isolated repeats of one launch can rank
+ * near-equal tiles differently).  Not capturable. */
 int pps_model_autotune(PpsModel* model, const float* x, int N, int flags, void* stream);
 /* Allocate (synchronously) the activation buffers for batch N and pin them:
  * from here on they are never reallocated, so a hipGraph captured around

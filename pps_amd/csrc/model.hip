@@ -1209,6 +1209,89 @@ struct Timer {
   }
 };
 
+float time_forward(const PpsModel& m, const float* x, int N, float* feat, int reps,
+                   hipStream_t st, Timer& t) {
+  forward_range(m, x, N, feat, 0, (int)m.layers.size(), st);
+  hip_check(hipEventRecord(t.e0, st), "hipEventRecord");
+  for (int i = 0; i < reps; ++i) forward_range(m, x, N, feat, 0, (int)m.layers.size(), st);
+  hip_check(hipEventRecord(t.e1, st), "hipEventRecord");
+  hip_check(hipEventSynchronize(t.e1), "hipEventSynchronize");
+  float ms = 0.f;
+  hip_check(hipEventElapsedTime(&ms, t.e0, t.e1), "hipEventElapsedTime");
+  return ms / reps;
+}
+
+// The in-forward pass of pps_model_autotune over layers of one shape: the
+// members' two best distinct tiles (their own f16x2-plane flags kept), each
+// applied to the whole group and timed as whole forwards in interleaved
+// rounds; the group moves to the best one if it beats the current
+// assignment by > 0.5 %.  Seam pairs keep their launch.
+void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
+                const std::map<const Layer*, std::vector<std::pair<float, int>>>& ranked,
+                hipStream_t st, Timer& t) {
+  constexpr int kKeep = PPS_TILE_H2E | PPS_TILE_H2P;
+  std::map<std::string, std::vector<int>> groups;
+  for (size_t i = 0; i < m.layers.size(); ++i) {
+    const Layer& L = m.layers[i];
+    if (!ranked.count(&L) || (L.tile & PPS_TILE_SEAM) || L.op == Op::Heads) continue;
+    if (i > 0 && (m.layers[i - 1].tile & PPS_TILE_SEAM) && m.layers[i - 1].seam_next == (int)i)
+      continue;
+    const Shape& s = w.shapes.at(L.input);
+    std::string key = std::to_string((int)L.op);
+    for (int v : {L.cin_eff, L.cout, L.kpad, L.k, L.stride, L.pad, L.dil, L.shortcut_cin,
+                  (int)L.relu, (int)L.residual.empty(), (int)L.planes_in, (int)L.planes_out,
+                  L.splitk})
+      key += "," + std::to_string(v);
+    for (int d = 0; d < 4; ++d) key += "," + std::to_string(s.d[d]);
+    groups[key].push_back((int)i);
+  }
+  DevBuf feat((size_t)N * m.plan.feat_dim * sizeof(float));
+  constexpr int reps = 6, rounds = 3;
+  for (const auto& g : groups) {
+    const std::vector<int>& mem = g.second;
+    if (mem.size() < 2) continue;
+    std::vector<int> cands;
+    for (int i : mem) {
+      int taken = 0;
+      for (const auto& r : ranked.at(&m.layers[i])) {
+        const int c = r.second & ~kKeep;
+        if (std::find(cands.begin(), cands.end(), c) == cands.end()) cands.push_back(c);
+        if (++taken == 2) break;
+      }
+    }
+    if (cands.size() < 2) continue;
+    std::vector<int> save;
+    for (int i : mem) save.push_back(m.layers[i].tile);
+    auto apply = [&](int c) {
+      for (size_t j = 0; j < mem.size(); ++j) {
+        Layer& L = m.layers[mem[j]];
+        L.tile = c | ((c & PPS_TILE_H2) ? (save[j] & kKeep) : 0);
+        if ((L.tile & PPS_TILE_H2P) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2P;
+        if ((L.tile & PPS_TILE_H2E) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2E;
+      }
+    };
+    // times[0]: the current assignment
+    std::vector<float> tmin(cands.size() + 1, 1e30f);
+    for (int r = 0; r < rounds; ++r)
+      for (size_t v = 0; v <= cands.size(); ++v) {
+        if (v == 0) {
+          for (size_t j = 0; j < mem.size(); ++j) m.layers[mem[j]].tile = save[j];
+        } else {
+          apply(cands[v - 1]);
+        }
+        tmin[v] = std::min(tmin[v], time_forward(m, x, N, feat.as<float>(), reps, st, t));
+      }
+    size_t best = 0;
+    for (size_t v = 1; v <= cands.size(); ++v)
+      if (tmin[v] < tmin[best]) best = v;
+    if (best > 0 && tmin[best] < 0.995f * tmin[0]) {
+      apply(cands[best - 1]);
+    } else {
+      for (size_t j = 0; j < mem.size(); ++j) m.layers[mem[j]].tile = save[j];
+    }
+  }
+}
+
 float time_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, int tile,
                  int sk, int reps, hipStream_t st, Timer& t) {
   for (int i = 0; i < 2; ++i) run_layer(m, L, w, x, nullptr, false, tile, sk, st);
@@ -1617,9 +1700,17 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       if (c.empty()) c.push_back(0);
       return c;
     };
-    auto tune = [&](Layer& L) {
+    // every tuned layer's finalists, best first (the in-forward group pass)
+    std::map<const Layer*, std::vector<std::pair<float, int>>> ranked;
+    // extra: flags or-ed into every candidate (PPS_TILE_H2E: the f16x2 tiles
+    // only, reading the planes the producer wrote)
+    auto tune = [&](Layer& L, int extra = 0) {
       std::vector<std::pair<float, int>> screen;
-      for (int tl : cands_of(L)) screen.emplace_back(time_layer(*m, L, *w, x, tl, L.splitk, reps, st, t), tl);
+      for (int tl : cands_of(L)) {
+        if (extra && !((tl & PPS_TILE_H2) && h2_tile_ok(L, tl | extra))) continue;
+        tl |= extra;
+        screen.emplace_back(time_layer(*m, L, *w, x, tl, L.splitk, reps, st, t), tl);
+      }
       std::sort(screen.begin(), screen.end());
       // finalists, each also on the chunk-tiled weight copy and / or in
       // column-major tile order; timed in interleaved rounds (min per
@@ -1640,8 +1731,13 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         for (size_t v = 0; v < var.size(); ++v)
           tmin[v] = std::min(tmin[v], time_layer(*m, L, *w, x, var[v], L.splitk, final_reps, st, t));
       float best = 1e30f;
-      for (size_t v = 0; v < var.size(); ++v)
+      auto& rk = ranked[&L];
+      rk.clear();
+      for (size_t v = 0; v < var.size(); ++v) {
+        rk.emplace_back(tmin[v], var[v]);
         if (tmin[v] < best) { best = tmin[v]; L.tile = var[v]; }
+      }
+      std::sort(rk.begin(), rk.end());
       return best;
     };
     const bool tune_planes = (flags & PPS_AUTOTUNE_NO_PLANES) == 0 && m->act_planes;
@@ -1721,30 +1817,40 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       }
     }
     if (try_h2 && !(flags & PPS_AUTOTUNE_NO_H2E)) {
-      // f16x2 planes from the producer's epilogue (PPS_TILE_H2E): kept if
-      // the producer + consumer pair is > 2 % faster
+      // f16x2 planes from the producer's epilogue (PPS_TILE_H2E): the
+      // consumer re-tuned over the f16x2 tiles reading them (the planes
+      // input favours other tiles than f32 does), kept if the producer +
+      // consumer pair is > 2 % faster
       for (size_t ci = 0; ci < m->layers.size(); ++ci) {
         Layer& C = m->layers[ci];
-        if (!(C.tile & PPS_TILE_H2) || C.planes_in) continue;
+        if (!C.w2 || C.planes_in || C.planes_out || C.splitk != 1) continue;
         const int pi = h2e_producer(*m, C);
         if (pi < 0) continue;
         Layer& P = m->layers[pi];
         if (P.planes_in || P.planes_out || P.splitk != 1 || (P.tile & PPS_TILE_SEAM)) continue;
+        int first = -1;   // an f16x2 tile of C, so P writes the planes from here on
+        for (int tl : cands_of(C))
+          if ((tl & PPS_TILE_H2) && h2_tile_ok(C, tl | PPS_TILE_H2E)) { first = tl; break; }
+        if (first < 0) continue;
         const int save = C.tile;
-        C.tile = (save & ~PPS_TILE_H2P) | PPS_TILE_H2E;
-        float tp = 1e30f, tc = 1e30f;
-        for (int r = 0; r < final_rounds; ++r) {
+        const auto save_rank = ranked[&C];
+        C.tile = first | PPS_TILE_H2E;
+        run_layer(*m, P, *w, x, nullptr, false, P.tile, 1, st);
+        const float tc = tune(C, PPS_TILE_H2E);
+        float tp = 1e30f;
+        for (int r = 0; r < final_rounds; ++r)
           tp = std::min(tp, time_layer(*m, P, *w, x, P.tile, 1, final_reps, st, t));
-          tc = std::min(tc, time_layer(*m, C, *w, x, C.tile, 1, final_reps, st, t));
-        }
         if (tp + tc < 0.98f * (cost[pi] + cost[ci])) {
           cost[pi] = tp;
           cost[ci] = tc;
         } else {
           C.tile = save;
+          ranked[&C] = save_rank;
+          run_layer(*m, P, *w, x, nullptr, false, P.tile, 1, st);   // f32 output again
         }
       }
     }
+    if (!(flags & PPS_AUTOTUNE_NO_GROUPS)) group_pass(*m, *w, x, N, ranked, st, t);
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   });
 }

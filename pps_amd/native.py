@@ -22,7 +22,7 @@ from .config import cfg as _cfg
 
 MATH = {'x3': 0, 'f32': 1}
 AUTOTUNE_NO_PLANES, AUTOTUNE_SPLITK, AUTOTUNE_NO_SEAM, AUTOTUNE_NO_H2 = 1, 2, 4, 8
-AUTOTUNE_NO_H2E = 16
+AUTOTUNE_NO_H2E, AUTOTUNE_NO_GROUPS = 16, 32
 FWD_KEEP_AMAX = 1   # pps_abi.h PPS_FWD_KEEP_AMAX
 
 
