@@ -1823,7 +1823,9 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       // consumer pair is > 2 % faster
       for (size_t ci = 0; ci < m->layers.size(); ++ci) {
         Layer& C = m->layers[ci];
-        if (!C.w2 || C.planes_in || C.planes_out || C.splitk != 1) continue;
+        // (a seam launch keeps its pair: its cost also holds the next layer's)
+        if (!C.w2 || C.planes_in || C.planes_out || C.splitk != 1 || (C.tile & PPS_TILE_SEAM))
+          continue;
         const int pi = h2e_producer(*m, C);
         if (pi < 0) continue;
         Layer& P = m->layers[pi];
