@@ -1225,10 +1225,12 @@ float time_forward(const PpsModel& m, const float* x, int N, float* feat, int re
 // members' two best distinct tiles (their own f16x2-plane flags kept), each
 // applied to the whole group and timed as whole forwards in interleaved
 // rounds; the group moves to the best one if it beats the current
-// assignment by > 0.5 %.  Seam pairs keep their launch.
+// assignment by > 0.5 %.  A layer of its own shape tries its three best
+// variants as they are, and an f16x2-planes reader also its pick without
+// the planes (pre_h2e).  Seam pairs keep their launch.
 void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
                 const std::map<const Layer*, std::vector<std::pair<float, int>>>& ranked,
-                hipStream_t st, Timer& t) {
+                const std::map<const Layer*, int>& pre_h2e, hipStream_t st, Timer& t) {
   constexpr int kKeep = PPS_TILE_H2E | PPS_TILE_H2P;
   std::map<std::string, std::vector<int>> groups;
   for (size_t i = 0; i < m.layers.size(); ++i) {
@@ -1249,22 +1251,36 @@ void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
   constexpr int reps = 6, rounds = 3;
   for (const auto& g : groups) {
     const std::vector<int>& mem = g.second;
-    if (mem.size() < 2) continue;
+    const bool single = mem.size() == 1;
     std::vector<int> cands;
     for (int i : mem) {
       int taken = 0;
       for (const auto& r : ranked.at(&m.layers[i])) {
-        const int c = r.second & ~kKeep;
+        const int c = single ? r.second : r.second & ~kKeep;
         if (std::find(cands.begin(), cands.end(), c) == cands.end()) cands.push_back(c);
-        if (++taken == 2) break;
+        if (++taken == (single ? 3 : 2)) break;
       }
     }
-    if (cands.size() < 2) continue;
+    if (single && pre_h2e.count(&m.layers[mem[0]])) {
+      const int c = pre_h2e.at(&m.layers[mem[0]]);
+      if (std::find(cands.begin(), cands.end(), c) == cands.end()) cands.push_back(c);
+    }
+    if (single) {   // (the current tile is times[0])
+      const int cur = m.layers[mem[0]].tile;
+      cands.erase(std::remove(cands.begin(), cands.end(), cur), cands.end());
+      if (cands.empty()) continue;
+    } else if (cands.size() < 2) {
+      continue;
+    }
     std::vector<int> save;
     for (int i : mem) save.push_back(m.layers[i].tile);
     auto apply = [&](int c) {
       for (size_t j = 0; j < mem.size(); ++j) {
         Layer& L = m.layers[mem[j]];
+        if (single) {
+          L.tile = c;
+          continue;
+        }
         L.tile = c | ((c & PPS_TILE_H2) ? (save[j] & kKeep) : 0);
         if ((L.tile & PPS_TILE_H2P) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2P;
         if ((L.tile & PPS_TILE_H2E) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2E;
@@ -1700,8 +1716,10 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
       if (c.empty()) c.push_back(0);
       return c;
     };
-    // every tuned layer's finalists, best first (the in-forward group pass)
+    // every tuned layer's finalists, best first, and an f16x2-planes reader's
+    // pick before the planes (the in-forward group pass)
     std::map<const Layer*, std::vector<std::pair<float, int>>> ranked;
+    std::map<const Layer*, int> pre_h2e;
     // extra: flags or-ed into every candidate (PPS_TILE_H2E: the f16x2 tiles
     // only, reading the planes the producer wrote)
     auto tune = [&](Layer& L, int extra = 0) {
@@ -1845,6 +1863,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         if (tp + tc < 0.98f * (cost[pi] + cost[ci])) {
           cost[pi] = tp;
           cost[ci] = tc;
+          pre_h2e[&C] = save;
         } else {
           C.tile = save;
           ranked[&C] = save_rank;
@@ -1852,7 +1871,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         }
       }
     }
-    if (!(flags & PPS_AUTOTUNE_NO_GROUPS)) group_pass(*m, *w, x, N, ranked, st, t);
+    if (!(flags & PPS_AUTOTUNE_NO_GROUPS)) group_pass(*m, *w, x, N, ranked, pre_h2e, st, t);
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   });
 }
