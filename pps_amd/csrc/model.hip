@@ -1223,14 +1223,16 @@ float time_forward(const PpsModel& m, const float* x, int N, float* feat, int re
 
 // The in-forward pass of pps_model_autotune over layers of one shape: the
 // members' two best distinct tiles (their own f16x2-plane flags kept), each
-// applied to the whole group and timed as whole forwards in interleaved
-// rounds; the group moves to the best one if it beats the current
-// assignment by > 0.5 %.  A layer of its own shape tries its three best
-// variants as they are, and an f16x2-planes reader also its pick without
-// the planes (pre_h2e).  Seam pairs keep their launch.
+// applied to the whole group, and the group's planes edges all on (each
+// reader on its best planes variant, h2e_best) or all off (pre_h2e), timed
+// as whole forwards in interleaved rounds; the group moves to the best
+// assignment if it beats the current one by > 0.5 %.  A layer of its own
+// shape tries its three best variants as they are.  Seam pairs keep their
+// launch.
 void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
                 const std::map<const Layer*, std::vector<std::pair<float, int>>>& ranked,
-                const std::map<const Layer*, int>& pre_h2e, hipStream_t st, Timer& t) {
+                const std::map<const Layer*, int>& pre_h2e,
+                const std::map<const Layer*, int>& h2e_best, hipStream_t st, Timer& t) {
   constexpr int kKeep = PPS_TILE_H2E | PPS_TILE_H2P;
   std::map<std::string, std::vector<int>> groups;
   for (size_t i = 0; i < m.layers.size(); ++i) {
@@ -1252,59 +1254,57 @@ void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
   for (const auto& g : groups) {
     const std::vector<int>& mem = g.second;
     const bool single = mem.size() == 1;
-    std::vector<int> cands;
+    std::vector<int> save;
+    for (int i : mem) save.push_back(m.layers[i].tile);
+    // candidate assignments (one tile per member); [0] = the current one
+    std::vector<std::vector<int>> cands{save};
+    auto add = [&](const std::vector<int>& a) {
+      if (std::find(cands.begin(), cands.end(), a) == cands.end()) cands.push_back(a);
+    };
+    std::vector<int> bases;
     for (int i : mem) {
       int taken = 0;
       for (const auto& r : ranked.at(&m.layers[i])) {
         const int c = single ? r.second : r.second & ~kKeep;
-        if (std::find(cands.begin(), cands.end(), c) == cands.end()) cands.push_back(c);
+        if (std::find(bases.begin(), bases.end(), c) == bases.end()) bases.push_back(c);
         if (++taken == (single ? 3 : 2)) break;
       }
     }
-    if (single && pre_h2e.count(&m.layers[mem[0]])) {
-      const int c = pre_h2e.at(&m.layers[mem[0]]);
-      if (std::find(cands.begin(), cands.end(), c) == cands.end()) cands.push_back(c);
-    }
-    if (single) {   // (the current tile is times[0])
-      const int cur = m.layers[mem[0]].tile;
-      cands.erase(std::remove(cands.begin(), cands.end(), cur), cands.end());
-      if (cands.empty()) continue;
-    } else if (cands.size() < 2) {
-      continue;
-    }
-    std::vector<int> save;
-    for (int i : mem) save.push_back(m.layers[i].tile);
-    auto apply = [&](int c) {
+    for (int c : bases) {   // one tile for the whole group (members' plane flags kept)
+      std::vector<int> a(mem.size());
       for (size_t j = 0; j < mem.size(); ++j) {
-        Layer& L = m.layers[mem[j]];
-        if (single) {
-          L.tile = c;
-          continue;
-        }
-        L.tile = c | ((c & PPS_TILE_H2) ? (save[j] & kKeep) : 0);
-        if ((L.tile & PPS_TILE_H2P) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2P;
-        if ((L.tile & PPS_TILE_H2E) && !h2_tile_ok(L, L.tile)) L.tile &= ~PPS_TILE_H2E;
+        const Layer& L = m.layers[mem[j]];
+        int tl = single ? c : c | ((c & PPS_TILE_H2) ? (save[j] & kKeep) : 0);
+        if ((tl & PPS_TILE_H2P) && !h2_tile_ok(L, tl)) tl &= ~PPS_TILE_H2P;
+        if ((tl & PPS_TILE_H2E) && !h2_tile_ok(L, tl)) tl &= ~PPS_TILE_H2E;
+        a[j] = tl;
       }
+      add(a);
+    }
+    // the f16x2-planes edges into the group: every reader on its best planes
+    // variant, and every reader back on its pick without them
+    std::vector<int> on = save, off = save;
+    for (size_t j = 0; j < mem.size(); ++j) {
+      const Layer* L = &m.layers[mem[j]];
+      if (h2e_best.count(L)) on[j] = h2e_best.at(L);
+      if (pre_h2e.count(L) && (save[j] & PPS_TILE_H2E)) off[j] = pre_h2e.at(L);
+    }
+    add(on);
+    add(off);
+    if (cands.size() < 2) continue;
+    auto apply = [&](const std::vector<int>& a) {
+      for (size_t j = 0; j < mem.size(); ++j) m.layers[mem[j]].tile = a[j];
     };
-    // times[0]: the current assignment
-    std::vector<float> tmin(cands.size() + 1, 1e30f);
+    std::vector<float> tmin(cands.size(), 1e30f);
     for (int r = 0; r < rounds; ++r)
-      for (size_t v = 0; v <= cands.size(); ++v) {
-        if (v == 0) {
-          for (size_t j = 0; j < mem.size(); ++j) m.layers[mem[j]].tile = save[j];
-        } else {
-          apply(cands[v - 1]);
-        }
+      for (size_t v = 0; v < cands.size(); ++v) {
+        apply(cands[v]);
         tmin[v] = std::min(tmin[v], time_forward(m, x, N, feat.as<float>(), reps, st, t));
       }
     size_t best = 0;
-    for (size_t v = 1; v <= cands.size(); ++v)
+    for (size_t v = 1; v < cands.size(); ++v)
       if (tmin[v] < tmin[best]) best = v;
-    if (best > 0 && tmin[best] < 0.995f * tmin[0]) {
-      apply(cands[best - 1]);
-    } else {
-      for (size_t j = 0; j < mem.size(); ++j) m.layers[mem[j]].tile = save[j];
-    }
+    apply(best > 0 && tmin[best] < 0.995f * tmin[0] ? cands[best] : save);
   }
 }
 
@@ -1719,7 +1719,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
     // every tuned layer's finalists, best first, and an f16x2-planes reader's
     // pick before the planes (the in-forward group pass)
     std::map<const Layer*, std::vector<std::pair<float, int>>> ranked;
-    std::map<const Layer*, int> pre_h2e;
+    std::map<const Layer*, int> pre_h2e, h2e_best;   // (h2e_best: kept or not)
     // extra: flags or-ed into every candidate (PPS_TILE_H2E: the f16x2 tiles
     // only, reading the planes the producer wrote)
     auto tune = [&](Layer& L, int extra = 0) {
@@ -1857,6 +1857,7 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         C.tile = first | PPS_TILE_H2E;
         run_layer(*m, P, *w, x, nullptr, false, P.tile, 1, st);
         const float tc = tune(C, PPS_TILE_H2E);
+        h2e_best[&C] = C.tile;
         float tp = 1e30f;
         for (int r = 0; r < final_rounds; ++r)
           tp = std::min(tp, time_layer(*m, P, *w, x, P.tile, 1, final_reps, st, t));
@@ -1871,7 +1872,8 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         }
       }
     }
-    if (!(flags & PPS_AUTOTUNE_NO_GROUPS)) group_pass(*m, *w, x, N, ranked, pre_h2e, st, t);
+    if (!(flags & PPS_AUTOTUNE_NO_GROUPS))
+      group_pass(*m, *w, x, N, ranked, pre_h2e, h2e_best, st, t);
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   });
 }
