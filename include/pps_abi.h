@@ -862,7 +862,7 @@ int pps_model_set_planes(PpsModel* model, const char* producer, int on);
 /* Time every tile per layer on this device (then plane edges, optionally
  * split-K, seams, f16x2-plane edges) with x [N][H][W][4] as input; last, the
  * layers of one shape (e.g. the five res4 3x3 convs) are tried on each of
- * their members' two best tiles inside whole forwards, with their f16x2-plane
+ * their members' three best tiles inside whole forwards, with their f16x2-plane
  * edges all on and all off, and a layer of its own shape on its three best
  * variants, so the pick holds where the layer actually runs (isolated
  * repeats of one launch can rank near-equal tiles differently).  Not

@@ -1222,7 +1222,7 @@ float time_forward(const PpsModel& m, const float* x, int N, float* feat, int re
 }
 
 // The in-forward pass of pps_model_autotune over layers of one shape: the
-// members' two best distinct tiles (their own f16x2-plane flags kept), each
+// members' three best distinct tiles (their own f16x2-plane flags kept), each
 // applied to the whole group, and the group's planes edges all on (each
 // reader on its best planes variant, h2e_best) or all off (pre_h2e), timed
 // as whole forwards in interleaved rounds; the group moves to the best
@@ -1267,7 +1267,7 @@ void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
       for (const auto& r : ranked.at(&m.layers[i])) {
         const int c = single ? r.second : r.second & ~kKeep;
         if (std::find(bases.begin(), bases.end(), c) == bases.end()) bases.push_back(c);
-        if (++taken == (single ? 3 : 2)) break;
+        if (++taken == 3) break;
       }
     }
     for (int c : bases) {   // one tile for the whole group (members' plane flags kept)
