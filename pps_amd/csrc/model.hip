@@ -1308,6 +1308,36 @@ void group_pass(PpsModel& m, Workspace& w, const float* x, int N,
   }
 }
 
+// The bottleneck seams judged inside whole forwards too: each seam-capable
+// branch2c with its launch toggled (on: the seam tile; off: its best tile of
+// its own, ranked), kept if the forward gets > 0.5 % faster.  The seam pass
+// before it judged the pair's two isolated launches.
+void seam_forward_pass(PpsModel& m, Workspace& w, const float* x, int N,
+                       const std::map<const Layer*, std::vector<std::pair<float, int>>>& ranked,
+                       hipStream_t st, Timer& t) {
+  DevBuf feat((size_t)N * m.plan.feat_dim * sizeof(float));
+  constexpr int reps = 6, rounds = 3;
+  for (Layer& L : m.layers) {
+    if (!seam_ok(m, L) || !ranked.count(&L)) continue;
+    const int save = L.tile;
+    int alt = GEMM_TILE_WS | PPS_TILE_SEAM;
+    if (save & PPS_TILE_SEAM) {   // off: the layer's best variant of its own
+      alt = -1;
+      for (const auto& r : ranked.at(&L))
+        if (!(r.second & PPS_TILE_SEAM)) { alt = r.second; break; }
+      if (alt < 0) continue;
+    }
+    float t0 = 1e30f, t1 = 1e30f;
+    for (int r = 0; r < rounds; ++r) {
+      L.tile = save;
+      t0 = std::min(t0, time_forward(m, x, N, feat.as<float>(), reps, st, t));
+      L.tile = alt;
+      t1 = std::min(t1, time_forward(m, x, N, feat.as<float>(), reps, st, t));
+    }
+    L.tile = t1 < 0.995f * t0 ? alt : save;
+  }
+}
+
 float time_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, int tile,
                  int sk, int reps, hipStream_t st, Timer& t) {
   for (int i = 0; i < 2; ++i) run_layer(m, L, w, x, nullptr, false, tile, sk, st);
@@ -1872,8 +1902,10 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         }
       }
     }
-    if (!(flags & PPS_AUTOTUNE_NO_GROUPS))
+    if (!(flags & PPS_AUTOTUNE_NO_GROUPS)) {
       group_pass(*m, *w, x, N, ranked, pre_h2e, h2e_best, st, t);
+      if (!(flags & PPS_AUTOTUNE_NO_SEAM)) seam_forward_pass(*m, *w, x, N, ranked, st, t);
+    }
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   });
 }
