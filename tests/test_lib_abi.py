@@ -76,3 +76,32 @@ def test_pipelined_tile_shapes():
               ops.tile_shape(t, True)[1] <= 256]
     assert pps_f32 == [30, 32, 35, 37, 39, 41, 46, 47, 48, 52]
     assert pps_pl == [30, 32, 37, 39, 41, 46, 47, 48, 52]
+
+
+def _defines():
+    with open(os.path.join(ROOT, 'include', 'pps_abi.h')) as f:
+        src = f.read()
+    return {k: int(v, 0) for k, v in re.findall(r'^#define\s+(PPS_\w+)\s+(0x[0-9a-fA-F]+|\d+)\b',
+                                                 src, re.M)}
+
+
+def test_python_flag_constants_match_the_header():
+    """The or-ed tile flags, the autotune flags and the slot size the Python
+    side passes across the ABI are the header's values (a drift would run a
+    different launch without an error)."""
+    from pps_amd import native, ops
+    d = _defines()
+    pairs = {'PPS_TILE_B_TILED': ops.TILE_B_TILED, 'PPS_TILE_COL_ORDER': ops.TILE_COL_ORDER,
+             'PPS_TILE_SEAM': ops.TILE_SEAM, 'PPS_TILE_H2': ops.TILE_H2,
+             'PPS_TILE_H2P': ops.TILE_H2P, 'PPS_TILE_H2E': ops.TILE_H2E,
+             'PPS_AMAX_SLOT_FLOATS': ops.AMAX_SLOT_FLOATS,
+             'PPS_AUTOTUNE_NO_PLANES': native.AUTOTUNE_NO_PLANES,
+             'PPS_AUTOTUNE_SPLITK': native.AUTOTUNE_SPLITK,
+             'PPS_AUTOTUNE_NO_SEAM': native.AUTOTUNE_NO_SEAM,
+             'PPS_AUTOTUNE_NO_H2': native.AUTOTUNE_NO_H2,
+             'PPS_AUTOTUNE_NO_H2E': native.AUTOTUNE_NO_H2E,
+             'PPS_AUTOTUNE_NO_GROUPS': native.AUTOTUNE_NO_GROUPS}
+    for name, value in pairs.items():
+        assert d[name] == value, (name, d.get(name), value)
+    flags = [v for k, v in d.items() if k.startswith('PPS_TILE_') and k in pairs]
+    assert ops.TILE_FLAGS == sum(flags)
