@@ -34,7 +34,7 @@ PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 # f16x2 distance path (csrc/gemm_h2.hip): 3 f16 MFMA terms per f32-level
 # product (f16 MFMA: the bf16 rate) -> its roof in f32-equivalent TFLOP/s
 PEAK_H2_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
-TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r05', 'pmc_traffic.json')
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'r06', 'pmc_traffic.json')
 PEAK_HBM_GBPS = 8000.0          # MI355X HBM3E spec
 Q_MARKET, G_MARKET, D_FEAT = 3368, 15913, 3968
 
@@ -63,6 +63,10 @@ def parse():
     p.add_argument('--no-autotune', action='store_true')
     p.add_argument('--dry-run', action='store_true',
                    help='no GPU work: exercise the launch / rendezvous / reporting path only')
+    p.add_argument('--sharded-legs', action='store_true',
+                   help='also run the config_cuhk03 / config_1m legs at N = 1 (they run by '
+                        'default at N > 1)')
+    p.add_argument('--no-sharded-legs', action='store_true')
     p.add_argument('--tiles-file', default=None,
                    help='JSON {layer: tile}: reuse (if present) or save the autotune result, '
                         'so profiling passes run the same kernels as the timed run')
@@ -103,57 +107,68 @@ def market_cfg():
     return cfg
 
 
-def synth_features(n, ids, gen, noise=4.0, n_ids=750):
+def synth_features(n, ids, gen, noise=4.0, n_ids=750, dim=D_FEAT, device='cuda'):
     """SURVEY §8(d) recipe on the device: centroid[id] + noise*N(0,1), L2 norm."""
-    cent = torch.randn((n_ids + 1, D_FEAT), generator=gen, device='cuda')
-    x = cent[ids] + noise * torch.randn((n, D_FEAT), generator=gen, device='cuda')
+    cent = torch.randn((n_ids + 1, dim), generator=gen, device=device)
+    x = cent[ids] + noise * torch.randn((n, dim), generator=gen, device=device)
     return (x / x.norm(dim=1, keepdim=True)).contiguous()
 
 
+def retrieval_inputs(nq, ng, n_distractors, n_ids, dim=D_FEAT, device='cuda'):
+    """Seeded ids / cams and the [nq + ng, dim] features (queries first) of a
+    retrieval workload: the same global data on every rank."""
+    rng = np.random.RandomState(0)
+    qid = rng.randint(1, n_ids + 1, nq)
+    gid = np.concatenate([rng.randint(1, n_ids + 1, ng - n_distractors),
+                          np.zeros(n_distractors, int)])
+    qcam = rng.randint(1, 7, nq)
+    gcam = rng.randint(1, 7, ng)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(0)
+    allf = synth_features(nq + ng, torch.from_numpy(np.concatenate([qid, gid])).to(device), gen,
+                          n_ids=n_ids, dim=dim, device=device)
+    return qid, gid, qcam, gcam, allf
+
+
 def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
-                    n_distractors=2793, n_ids=750):
-    """Distance matrix + mAP/CMC (default: Market sizes; scripts/
-    bench_retrieval_sharded.py passes the CUHK03 / Duke splits).  Gallery
+                    n_distractors=2793, n_ids=750, backend=None, device='cuda', dim=D_FEAT):
+    """Distance matrix + mAP/CMC (default: Market sizes; the config_cuhk03
+    leg and scripts/bench_retrieval_sharded.py pass other splits).  Gallery
     sharded over ranks, queries all-gathered.  Returns timings
-    (ms) and scores."""
+    (ms) and scores.  backend / device: the product HipBackend on the GPU, or
+    (tests/test_distributed_cpu.py) the oracle's CpuBackend on CPU with gloo,
+    which runs the same collective code with host timers and no rooflines."""
     from pps_amd import distributed as pdist
     Q_MARKET, G_MARKET = nq, ng   # local names: the sizes of this run
-    rng = np.random.RandomState(0)
-    qid = rng.randint(1, n_ids + 1, Q_MARKET)
-    gid = np.concatenate([rng.randint(1, n_ids + 1, G_MARKET - n_distractors),
-                          np.zeros(n_distractors, int)])
-    qcam = rng.randint(1, 7, Q_MARKET)
-    gcam = rng.randint(1, 7, G_MARKET)
-    gen = torch.Generator(device='cuda')
-    gen.manual_seed(0)
-    # same global features on every rank (seeded), each rank keeps its shards
-    allf = synth_features(Q_MARKET + G_MARKET,
-                          torch.from_numpy(np.concatenate([qid, gid])).cuda(), gen,
-                          n_ids=n_ids)
+    qid, gid, qcam, gcam, allf = retrieval_inputs(nq, ng, n_distractors, n_ids, dim, device)
     qsl = pdist.shard_range(Q_MARKET, rank, world)
     gsl = pdist.shard_range(G_MARKET, rank, world)
     q_local = allf[qsl[0]:qsl[1]].contiguous()
     g_local = allf[Q_MARKET + gsl[0]:Q_MARKET + gsl[1]].contiguous()
     del allf
-    ev = pdist.ShardedEvaluator(qid, qcam, gid, gcam, rank, world)
+    ev = pdist.ShardedEvaluator(qid, qcam, gid, gcam, rank, world, backend=backend)
+    gpu = device == 'cuda'
+    tune = tune and gpu
     if tune:
         # distance-GEMM tile choice on this shard's shape (outside the timed runs)
         from pps_amd import ops
-        qa = torch.empty((Q_MARKET, D_FEAT), device='cuda').normal_(generator=gen)
+        gen = torch.Generator(device='cuda')
+        gen.manual_seed(1)
+        qa = torch.empty((Q_MARKET, dim), device='cuda').normal_(generator=gen)
         # gallery index and query planes prepared once: the tiles compete on the
         # GEMM alone (what roofline_distmat times)
-        h2 = ops.dist_math() == 'h2' and D_FEAT % 32 == 0
+        h2 = ops.dist_math() == 'h2' and dim % 32 == 0
         if h2:   # f16x2 split of both operands; the h2 tiles compete
             gidx = ops.GalleryIndex(g_local, math='h2')
             q2, qrs, qsq = ops.split_h2_tiled(qa)
             qt = None
             cands = [(t, False) for t in range(1, ops.h2_num_tiles())]
         else:
-            gidx = ops.GalleryIndex(g_local, tiled=D_FEAT % 32 == 0, math='x3')
-            qt, qsq = ops.split_sqnorm_tiled(qa) if D_FEAT % 32 == 0 else (None, None)
+            gidx = ops.GalleryIndex(g_local, tiled=dim % 32 == 0, math='x3')
+            qt, qsq = ops.split_sqnorm_tiled(qa) if dim % 32 == 0 else (None, None)
             # (the 3x3-patch ids 56+ run tile 38 on a distance matrix)
             cands = [(t, False) for t in range(1, ops.TILE_C16_FIRST)]
-            if ops.dist_math() == 'x3' and D_FEAT % 32 == 0:  # queries as planes too
+            if ops.dist_math() == 'x3' and dim % 32 == 0:  # queries as planes too
                 cands += [(t, True) for t in range(ops.TILE_P_FIRST, ops.TILE_C16_FIRST)]
         dout = ops.dist_buffer(Q_MARKET, g_local.shape[0], 'cuda')
 
@@ -162,7 +177,7 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
                 ops.distmat_h2(q2, qrs, qsq, gidx, dout, tile=t)
             elif qp:
                 ops.distmat_planes(None, qsq, gidx, dout, tile=t, q_tiled=qt, Q=Q_MARKET,
-                                   D=D_FEAT)
+                                   D=dim)
             else:
                 ops.compute_dist(qa, gidx, out=dout, tile=t)
 
@@ -190,27 +205,35 @@ def retrieval_stage(rank, world, reps, tune=True, nq=Q_MARKET, ng=G_MARKET,
         pdist.HipBackend.distmat_tile = best[0]
         pdist.HipBackend.distmat_qplanes = best[1]
         del qa, gidx, qt, dout
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     # warm-up
     res = ev.run(q_local, g_local)
-    torch.cuda.synchronize()
-    t_dist, t_rank, t_total = [], [], []
+    sync()
+    t_gather, t_dist, t_rank, t_total = [], [], [], []
     for _ in range(reps):
         pdist.barrier(world)
-        torch.cuda.synchronize()
+        sync()
+        t0 = time.perf_counter()
         res = ev.run(q_local, g_local, timed=True, keep_dist=True)
-        torch.cuda.synchronize()
-        t_dist.append(res['t_distmat_ms'])
-        t_rank.append(res['t_rank_ms'])
-        t_total.append(res['t_total_ms'])
-    rank_roof = rank_roofline(ev, res['dist'])
-    argsort_roof = argsort_roofline(res['dist'])
-    dist_roof = distmat_roofline(q_local, g_local, world)
+        sync()
+        if gpu:
+            t_gather.append(res['t_gather_ms'])
+            t_dist.append(res['t_distmat_ms'])
+            t_rank.append(res['t_rank_ms'])
+            t_total.append(res['t_total_ms'])
+        else:   # host timers: the whole run only
+            t_total.append((time.perf_counter() - t0) * 1e3)
+    rank_roof = rank_roofline(ev, res['dist']) if gpu else None
+    argsort_roof = argsort_roofline(res['dist']) if gpu else None
+    dist_roof = distmat_roofline(q_local, g_local, world) if gpu else None
     del res['dist']
+    med = lambda v: float(np.median(v)) if v else None   # noqa: E731
+    be = ev.backend
     out = dict(rank_roofline=rank_roof, dist_roofline=dist_roof, argsort_roofline=argsort_roof,
-               distmat_tile=pdist.HipBackend.distmat_tile,
-               distmat_qplanes=pdist.HipBackend.distmat_qplanes,
-               distmat_ms=float(np.median(t_dist)), rank_eval_ms=float(np.median(t_rank)),
-               retrieval_ms=float(np.median(t_total)), mAP=res['mAP'],
+               distmat_tile=getattr(be, 'distmat_tile', None),
+               distmat_qplanes=getattr(be, 'distmat_qplanes', None),
+               gather_ms=med(t_gather), distmat_ms=med(t_dist), rank_eval_ms=med(t_rank),
+               retrieval_ms=med(t_total), mAP=res['mAP'], cmc=[float(c) for c in res['cmc']],
                cmc1=float(res['cmc'][0]), cmc5=float(res['cmc'][4]),
                cmc10=float(res['cmc'][9]), G_local=gsl[1] - gsl[0])
     return out
@@ -326,9 +349,209 @@ def argsort_roofline(dist, reps=10):
                 avg_launch_us=round(us, 2), algorithmic_bytes_per_launch=byt, rows=Q, cols=G)
 
 
+# BASELINE configs[3] / configs[4]: CUHK03-detected (new
+# protocol) and the synthetic 1M-gallery x 10k-query, 2048-d shard stress
+CUHK03 = dict(nq=1400, ng=5332, n_distractors=0, n_ids=700)
+SHARD_1M = dict(nq=10000, ng=1000000, dim=2048, k=100)
+
+
+class _Stamps(object):
+    """Stage boundaries: HIP events on the GPU (read after one sync), host
+    clocks on the CPU rehearsal."""
+
+    def __init__(self, gpu):
+        self.gpu, self.t = gpu, []
+
+    def mark(self):
+        if self.gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.t.append(e)
+        else:
+            self.t.append(time.perf_counter())
+
+    def ms(self):
+        if self.gpu:
+            self.t[-1].synchronize()
+            return [a.elapsed_time(b) for a, b in zip(self.t, self.t[1:])]
+        return [(b - a) * 1e3 for a, b in zip(self.t, self.t[1:])]
+
+
+def config_cuhk03(rank, world, reps=5, backend=None, device='cuda', sizes=None):
+    """BASELINE configs[3]: CUHK03-detected retrieval, 1400 queries x 5332
+    gallery, the gallery sharded over the ranks, queries
+    all-gathered over RCCL, each rank's distance block + per-shard match
+    lists (all-gathered) + additive counts (all-reduced), mAP / CMC -- the
+    product path of pps_amd/distributed.py (replaces the reference's
+    subprocess fan-out + one-host evaluation, utils/subprocess.py:39-103,
+    core/test_engine.py:184-229).  Stage times are medians over `reps`, the
+    max over ranks."""
+    from pps_amd import distributed as pdist
+    sz = dict(CUHK03, **(sizes or {}))
+    dim = sz.pop('dim', D_FEAT)
+    ret = retrieval_stage(rank, world, reps, tune=True, backend=backend, device=device, dim=dim,
+                          **sz)
+    mx = lambda v: None if v is None else round(pdist.max_over_ranks(v, world), 4)  # noqa: E731
+    nq, ng = sz['nq'], sz['ng']
+    total_ms = mx(ret['retrieval_ms'])
+    out = dict(workload='CUHK03-detected retrieval, %dq x %dg, D=%d, L2, gallery-sharded over %d '
+                        'rank(s), queries all-gathered, counts all-reduced' % (nq, ng, dim, world),
+               n_ranks=world, G_local_rank0=ret['G_local'],
+               query_allgather_ms=mx(ret['gather_ms']), distmat_ms=mx(ret['distmat_ms']),
+               rank_eval_ms=mx(ret['rank_eval_ms']), retrieval_ms=total_ms,
+               queries_per_s=round(nq / (total_ms * 1e-3), 1) if total_ms else None,
+               distmat_GBps=(round(((nq + ng) * dim * 4 + nq * ng * 4) /
+                                   (mx(ret['distmat_ms']) * 1e-3) / 1e9, 2)
+                             if ret['distmat_ms'] else None),
+               mAP_synthetic=round(ret['mAP'], 9), cmc=ret['cmc'],
+               cmc1_synthetic=ret['cmc1'], cmc5_synthetic=ret['cmc5'],
+               roofline_distmat_rank0=ret['dist_roofline'],
+               roofline_rank_rank0=ret['rank_roofline'],
+               timing='median of %d runs per rank (HIP events: all-gather / GEMM / lists + '
+                      'counts + all-reduce + AP), max over ranks' % reps,
+               data='synthetic (SURVEY §8(d) recipe: 700 centroids + noise 4.0, L2 norm)')
+    return out
+
+
+def synth_rows(a, b, dim, seed, device='cuda', chunk=8192):
+    """Rows [a, b) of a seeded, L2-normalised Gaussian [*, dim] matrix whose
+    rows do not depend on how it is sharded: chunk c of `chunk` rows is drawn
+    from seed * 1000003 + c."""
+    out = torch.empty((max(b - a, 0), dim), dtype=torch.float32, device=device)
+    gen = torch.Generator(device=device)
+    for c in range(a // chunk, (b + chunk - 1) // chunk):
+        lo, hi = max(a, c * chunk), min(b, (c + 1) * chunk)
+        if lo >= hi:
+            continue
+        gen.manual_seed(seed * 1000003 + c)
+        blk = torch.randn((chunk, dim), generator=gen, device=device)
+        out[lo - a:hi - a] = blk[lo - c * chunk:hi - c * chunk]
+    out /= out.norm(dim=1, keepdim=True)
+    return out
+
+
+def config_1m(rank, world, reps=3, backend=None, device='cuda', sizes=None, keep=False):
+    """BASELINE configs[4]: the synthetic 1M-gallery x 10k-query, 2048-d
+    sharded distance matrix (the HBM-roofline stress):
+    rank r owns gallery rows shard_range(1M, r, world) (a [10k, 1M/world]
+    block), the query shards are all-gathered, each rank takes the stable
+    top-100 of its block (pps_topk), the lists are all-gathered and merged
+    by (distance, global index) (pps_topk_merge) into the global top-100 of
+    every query -- the reference's np.argsort(distmat, axis=1)[:, :100]
+    (reid_dataset_evaluator.py:319,420) over the unsharded matrix.  Features:
+    synth_rows (seeded normalised Gaussian, sharding-independent).  keep:
+    also return the merged (vals, idx) (the CPU rehearsal checks them)."""
+    from pps_amd import distributed as pdist
+    be = backend or pdist.HipBackend
+    sz = dict(SHARD_1M, **(sizes or {}))
+    nq, ng, dim, k = sz['nq'], sz['ng'], sz['dim'], sz['k']
+    gpu = device == 'cuda'
+    qa, qb = pdist.shard_range(nq, rank, world)
+    ga, gb = pdist.shard_range(ng, rank, world)
+    q_sizes = [b - a for a, b in (pdist.shard_range(nq, r, world) for r in range(world))]
+    offsets = [pdist.shard_range(ng, r, world)[0] for r in range(world)]
+    q_local = synth_rows(qa, qb, dim, 1, device)
+    g_local = synth_rows(ga, gb, dim, 2, device)
+    G = gb - ga
+    kin = min(k, G)
+    st = _Stamps(gpu)
+    if gpu:
+        from pps_amd import ops
+        st.mark()
+        index = ops.GalleryIndex(g_local)   # the gallery prepared once per shard
+        st.mark()
+        index_ms = st.ms()[0]
+        dist = ops.dist_buffer(nq, G, device)
+    else:
+        index, index_ms, dist = g_local, None, None
+
+    def once():
+        s = _Stamps(gpu)
+        s.mark()
+        q_all = pdist.all_gather_rows(q_local, q_sizes)
+        s.mark()
+        if gpu:
+            from pps_amd import ops
+            d = ops.compute_dist(q_all, index, out=dist, tile=be.distmat_tile)
+        else:
+            d = be.distmat(q_all, index, 'euclidean')
+        s.mark()
+        vals, idx = be.topk(d, kin)
+        if kin < k:   # a shard shorter than k: pad its list with (+inf, -1)
+            pv = torch.full((nq, k), float('inf'), dtype=torch.float32, device=vals.device)
+            pi = torch.full((nq, k), -1, dtype=torch.int32, device=vals.device)
+            pv[:, :kin], pi[:, :kin] = vals, idx
+            vals, idx = pv, pi
+        s.mark()
+        av = pdist.all_gather_rows(vals.contiguous()[None], [1] * world)
+        ai = pdist.all_gather_rows(idx.contiguous()[None], [1] * world)
+        mv, mi = be.topk_merge(av.contiguous(), ai.contiguous(), offsets, k)
+        s.mark()
+        return s.ms(), (mv, mi)
+
+    once()   # warm-up
+    times = []
+    for _ in range(reps):
+        pdist.barrier(world)
+        if gpu:
+            torch.cuda.synchronize()
+        t, merged = once()
+        times.append(t)
+    med = [float(np.median([t[i] for t in times])) for i in range(4)]
+    mx = [pdist.max_over_ranks(v, world) for v in med]
+    total = pdist.max_over_ranks(float(np.median([sum(t) for t in times])), world)
+    out = dict(workload='synthetic %dq x %dg, D=%d, L2, gallery-sharded over %d rank(s) (%d rows '
+                        'each), per-rank stable top-%d + all-gather + merge'
+                        % (nq, ng, dim, world, G, k),
+               n_ranks=world, G_local_rank0=G,
+               gallery_index_ms_rank0=round(index_ms, 3) if index_ms is not None else None,
+               query_allgather_ms=round(mx[0], 3), distmat_ms=round(mx[1], 3),
+               topk_ms=round(mx[2], 3), list_allgather_merge_ms=round(mx[3], 3),
+               total_ms=round(total, 3), queries_per_s=round(nq / (total * 1e-3), 1),
+               distmat_GBps=round(((nq + ng) * dim * 4 + nq * ng * 4) / (mx[1] * 1e-3) / 1e9, 2),
+               timing='median of %d runs per rank, stage boundaries by %s, max over ranks'
+                      % (reps, 'HIP events' if gpu else 'host clock'),
+               data='synthetic (seeded normalised Gaussian rows, synth_rows)')
+    if gpu:
+        from pps_amd import ops
+        # the two kernels of the leg on their own, rank 0's shard: the
+        # distance GEMM (f16x2 roof) and the stable top-k stream (HBM)
+        n = 3
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        q_all = pdist.all_gather_rows(q_local, q_sizes)
+        e0.record()
+        for _ in range(n):
+            ops.compute_dist(q_all, index, out=dist, tile=be.distmat_tile)
+        e1.record()
+        for _ in range(n):
+            be.topk(dist, kin)
+        e2.record()
+        e2.synchronize()
+        gemm_us = e0.elapsed_time(e1) * 1e3 / n
+        topk_us = e1.elapsed_time(e2) * 1e3 / n
+        flops = 2.0 * nq * G * dim
+        h2 = getattr(index, 'math', None) == 'h2'
+        peak = PEAK_H2_TFLOPS if h2 else PEAK_X3_TFLOPS
+        tb = nq * G * 4 + nq * kin * 8
+        out['roofline_distmat_rank0'] = dict(
+            bound='mfma', achieved=round(flops / gemm_us / 1e6, 2), peak=round(peak, 1),
+            unit='TFLOP/s', frac=round(flops / gemm_us / 1e6 / peak, 4),
+            math='h2' if h2 else 'x3', avg_launch_us=round(gemm_us, 1),
+            note='compute_dist on the prepared GalleryIndex (query split + GEMM)')
+        out['roofline_topk_rank0'] = dict(
+            bound='hbm', achieved=round(tb / topk_us / 1e3, 1),
+            peak=PEAK_HBM_GBPS, unit='GB/s',
+            frac=round(tb / topk_us / 1e3 / PEAK_HBM_GBPS, 4), avg_launch_us=round(topk_us, 1),
+            algorithmic_bytes_per_launch=tb,
+            kernel='topk_wave_kernel (stable top-%d, one stream over the block)' % kin)
+    if keep:
+        out['merged'] = merged
+    return out
+
+
 def _pmc_traffic(key, math, batch):
     """HBM bytes per launch measured by rocprofv3 PMC passes of this bench
-    (scripts/pmc_traffic.py -> profiles/r05/pmc_traffic.json): FETCH_SIZE x 2
+    (scripts/pmc_traffic.py -> profiles/r06/pmc_traffic.json): FETCH_SIZE x 2
     (gfx950 reports half of wide streaming reads) + WRITE_SIZE, per launch.
     None unless the file was measured for the same math and batch."""
     try:
@@ -337,23 +560,28 @@ def _pmc_traffic(key, math, batch):
     except (OSError, ValueError):
         return None
     e = t.get(key)
-    if not e or (e.get('math', math) != math) or \
+    # conv entries carry the model's base arithmetic as model_math (their
+    # `math` names the f16x2 / bf16x3 launch mix)
+    if not e or (e.get('model_math', e.get('math', math)) != math) or \
             (batch is not None and e.get('batch', batch) != batch):
         return None
     return e.get('bytes_per_launch')
 
 
 def _pmc_mfma(math, batch):
-    """Conv stack's effective clock and MFMA-busy fraction from the committed
-    PMC pass (GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES), same math and batch."""
+    """Conv stack's MFMA-busy fraction from the committed PMC pass
+    (SQ_VALU_MFMA_BUSY_CYCLES over the launches' trace durations, at 2.4 GHz
+    and at the DPM clock the bench sampled; scripts/pmc_traffic.py), same
+    model arithmetic and batch."""
     try:
         with open(TRAFFIC_FILE) as f:
             e = json.load(f).get('conv_mfma')
     except (OSError, ValueError):
         return None
-    if not e or e.get('math') != math or e.get('batch') != batch:
+    if not e or e.get('model_math', e.get('math')) != math or e.get('batch') != batch:
         return None
-    return {k: e[k] for k in ('clock_GHz', 'mfma_busy_frac', 'mfma_busy_frac_at_2p4GHz')}
+    return {k: e[k] for k in ('mfma_busy_frac_at_2p4GHz', 'mfma_busy_frac_at_dpm_clock',
+                              'dpm_clock_MHz', 'math') if k in e}
 
 
 def conv_roofline(nm, x, reps=20):
@@ -926,7 +1154,19 @@ def main():
         'metric': 'gallery images/sec + distmat GB/s; mAP/Rank-1 parity on Market-1501',
         'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        # f32 operands and outputs; the products run as exact-split f16 / bf16
+        # MFMA terms with f32 accumulation
+        'dtype': ('f32 (f16x2 3-term / bf16x3 6-term MFMA emulation, f32 accumulate)'
+                  if nm.math == 'x3' else 'f32 (f32 MFMA)'),
+        'math': dict(conv_launches=dict(
+                         f16x2=sum(1 for v in per_layer.values()
+                                   if v['gemm'] and v['tile'] & ops.TILE_H2),
+                         bf16x3=sum(1 for v in per_layer.values()
+                                    if v['gemm'] and not v['tile'] & ops.TILE_H2)),
+                     distance=ops.dist_math(), accumulate='f32',
+                     note='f16x2: each f32 operand as two f16 terms on a power-of-two scale, '
+                          'three f16 MFMA products; bf16x3: three bf16 terms, six products'),
         'data': 'synthetic (uint8 images, seeded weights of the PPS R-50 architecture)',
         'config': {'workload': 'Market-1501 ResNet-50 PPS (stride-1 res5, 31 part subsets), '
                                'batch %d/GPU, 384x128, 3368q x 15913g L2 distmat' % B,
@@ -973,6 +1213,14 @@ def main():
                         ', queries and gallery as chunk-tiled bf16x3 planes '
                         '(pps_distmat_x3p_tiled)' if ret['distmat_qplanes'] else ''))),
     }
+    if (world > 1 or args.sharded_legs) and not args.no_sharded_legs:
+        # BASELINE configs[3] and configs[4] on the ranks this run has (the
+        # driver's N = 2 / 4 / 8 runs): gallery-sharded, RCCL collectives
+        torch.cuda.empty_cache()
+        out['config_cuhk03'] = config_cuhk03(rank, world)
+        torch.cuda.empty_cache()
+        out['config_1m'] = config_1m(rank, world)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_duke:
         # BASELINE configs[2] (Duke sizes, cosine + k-reciprocal re-ranking),
         # timed after the headline workload: distance / re-ranking / rank

@@ -1132,6 +1132,15 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
       if (!L.conv_output.empty()) made.insert(L.conv_output);
       if (L.seam_next >= 0 && (L.tile & PPS_TILE_SEAM)) made.insert(m.layers[L.seam_next].output);
     }
+    // and the tensors it produces start from zero, as in a whole forward:
+    // their producers combine into the slot with atomicMax, so a larger max
+    // left by an earlier call would otherwise set a stale scale
+    for (const std::string& t : made) {
+      if (!m.slot.count(t)) continue;
+      float* slot = w.amax->as<float>() + (size_t)m.slot.at(t) * PPS_AMAX_SLOT_FLOATS;
+      hip_check(hipMemsetAsync(slot, 0, PPS_AMAX_SLOT_FLOATS * sizeof(float), st),
+                "hipMemsetAsync");
+    }
   }
   for (int i = first; i < last; ++i) {
     const Layer& L = m.layers[i];
@@ -1176,10 +1185,15 @@ double layer_bytes(const PpsModel& m, const Layer& L, const std::map<std::string
              wb * L.cout * pps_stem_k();
     case Op::Conv: case Op::ConvDual: {
       const Shape& y = s.at(L.output);
-      double b = 4.0 * s.at(L.input).numel() + 4.0 * y.numel() +
-                 wb * L.cout * ((double)L.k * L.k * L.cin + L.shortcut_cin);
+      const double pix = (double)y.d[0] * y.d[1] * y.d[2];
+      // a 1x1 (k < stride) conv reads only the pixels under its taps: one
+      // input pixel per output position and tap, not the whole tensor
+      const double in = L.k < L.stride ? 4.0 * pix * L.k * L.k * L.cin
+                                       : 4.0 * s.at(L.input).numel();
+      double b = in + 4.0 * y.numel() + wb * L.cout * ((double)L.k * L.k * L.cin + L.shortcut_cin);
       if (!L.residual.empty()) b += 4.0 * y.numel();
-      if (L.op == Op::ConvDual) b += 4.0 * s.at(L.input2).numel();
+      if (L.op == Op::ConvDual)  // the 1x1 shortcut, stride2
+        b += L.stride2 > 1 ? 4.0 * pix * L.shortcut_cin : 4.0 * s.at(L.input2).numel();
       return b;
     }
     case Op::ConvPps: {

@@ -289,6 +289,7 @@ class ShardedEvaluator(object):
         if keep_dist:
             res['dist'] = dist
         if use_ev:
+            res['t_gather_ms'] = evs[0].elapsed_time(evs[1])   # the query all-gather
             res['t_distmat_ms'] = evs[1].elapsed_time(evs[2])
             res['t_rank_ms'] = evs[2].elapsed_time(evs[3])
             res['t_total_ms'] = evs[0].elapsed_time(evs[3])

@@ -547,12 +547,18 @@ class PPSModel(object):
                                    wbytes * L['cout'] * ops.stem_k())
             elif L['op'] in ('conv', 'conv_dual'):
                 n, ho, wo, co = shapes[L['output']]
-                b = 4 * np.prod(shapes[L['input']]) + 4 * n * ho * wo * co
+                # a 1x1 (k < stride) conv reads only the pixels under its taps
+                if L['k'] < L['stride']:
+                    b = 4 * n * ho * wo * L['k'] * L['k'] * L['cin']
+                else:
+                    b = 4 * np.prod(shapes[L['input']])
+                b += 4 * n * ho * wo * co
                 b += wbytes * co * (L['k'] * L['k'] * L['cin'] + L.get('shortcut_cin', 0))
                 if L.get('residual'):
                     b += 4 * n * ho * wo * co
-                if L['op'] == 'conv_dual':
-                    b += 4 * np.prod(shapes[L['input2']])
+                if L['op'] == 'conv_dual':   # the 1x1 shortcut at stride2
+                    b += (4 * n * ho * wo * L['shortcut_cin'] if L['stride2'] > 1 else
+                          4 * np.prod(shapes[L['input2']]))
                 L['bytes'] = float(b)
             elif L['op'] == 'conv_pps':
                 # input + residual + weights read, the part subsets written (the

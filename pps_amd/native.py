@@ -264,9 +264,8 @@ class NativeModel(object):
             raw = (ctypes.c_uint16 * (2 * n))()
             _memcpy_d2h(raw, p.value, 4 * n)
             h = np.frombuffer(raw, np.float16).astype(np.float64).reshape(2, n).sum(0)
-            bnd = np.float32(self.tensor_amax(N, blob))
-            e = int(np.frexp(bnd)[1]) if bnd > 0 else 0
-            return (h * 2.0 ** (e - 15)).astype(np.float32).reshape(tuple(shape))
+            inv = h2_inv_scale(self.tensor_amax(N, blob))
+            return (h * inv).astype(np.float32).reshape(tuple(shape))
         if pl.value:
             raw = (ctypes.c_uint16 * (3 * n))()
             _memcpy_d2h(raw, p.value, 6 * n)
@@ -284,6 +283,21 @@ class NativeModel(object):
         v = ctypes.c_float()
         call('pps_model_tensor_amax', self._h, int(N), blob.encode(), ctypes.addressof(v))
         return float(v.value)
+
+
+def h2_inv_scale(amax):
+    """2^-s for the f16x2 scale 2^s the kernels derive from a tensor's max
+    (pps_internal.hpp h2_scale_of): s = 15 - (biased exponent - 126), so
+    max|x 2^s| lies in [2^14, 2^15); a zero max keeps scale 1, a denormal one
+    takes s = 126, and s is clamped to [-126, 126]."""
+    a = np.float32(amax)
+    ebits = (int(a.view(np.uint32)) >> 23) & 0xff
+    if ebits == 0:
+        sh = 126 if a > 0 else 0
+    else:
+        sh = 15 - (ebits - 126)
+    sh = max(-126, min(126, sh))
+    return 2.0 ** (-sh)
 
 
 _HIP = None

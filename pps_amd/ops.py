@@ -236,7 +236,12 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
     work); None = whenever q IS g's data, D % 32 == 0 and (x3) the tile is a
     square one (SELF_TILES)."""
     if isinstance(g, GalleryIndex):
-        math = g.math
+        # the index fixes the arithmetic; an explicit request for another one
+        # is an error (f32 reads the index's features as they are)
+        if math not in (None, 'f32', g.math):
+            raise RuntimeError("compute_dist: math=%r but the GalleryIndex holds a %r split"
+                               % (math, g.math))
+        math = math or g.math
     math = math or dist_math()
     if q.dim() != 2 or len(g.shape) != 2 or q.shape[1] != g.shape[1]:
         raise RuntimeError('compute_dist expects [m1,n] and [m2,n], got %s %s'
@@ -270,8 +275,10 @@ def compute_dist(q, g, metric='euclidean', out=None, tile=0, math=None, q_planes
                  int(tile), _stream())
             out._pps_symmetric = True   # mirrored tiles: exactly symmetric
             return out
+        # a strided raw gallery (e.g. big[:, :D]) is made contiguous first: the
+        # f16x2 index needs whole rows
         idx = g if isinstance(g, GalleryIndex) and g.h2 is not None else \
-            GalleryIndex(f, math='h2')
+            GalleryIndex(f if f.is_contiguous() else f.contiguous(), math='h2')
         q2, qrs, qsq = split_h2_tiled(q)
         return distmat_h2(q2, qrs, qsq, idx, out, metric, tile, Q=Q)
     if math == 'h2':

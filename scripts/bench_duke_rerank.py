@@ -17,13 +17,13 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 
 Q, G, D = 2228, 17661, 3968
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'profiles', 'r05',
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'profiles', 'r06',
                             'pmc_duke.json')
 
 
 def _traffic(key, math):
     """Memory-side bytes per call measured by the PMC passes of this script
-    (scripts/gpu_duke_pmc.sh -> profiles/r05/pmc_duke.json), None unless
+    (scripts/gpu_duke_pmc.sh -> profiles/r06/pmc_duke.json), None unless
     measured for the same distance arithmetic."""
     try:
         with open(TRAFFIC_FILE) as f:

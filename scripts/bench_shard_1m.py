@@ -1,11 +1,11 @@
 """BASELINE.json configs[4] at the size one GPU owns: the synthetic 1M-gallery x
 10k-query, D=2048 sharded distance matrix is split
 8 ways, 125,000 gallery rows per GPU.  This times ONE shard on one GPU:
-build the gallery index (bf16x3 planes + norms), the [10k, 125k] L2 block
+build the gallery index (f16x2 planes + scales + norms; x3: bf16x3 planes), the [10k, 125k] L2 block
 (5.0 GB fp32) and the stable top-100 per query (the per-GPU output the
 8-way merge consumes).  Features: normalised Gaussian, seed 0 (§8(d)).
 
-  python scripts/bench_shard_1m.py [--queries 10000] [--shard 125000] [--math x3|f32]
+  python scripts/bench_shard_1m.py [--queries 10000] [--shard 125000] [--math h2|x3|f32]
 """
 import argparse
 import json
@@ -23,7 +23,7 @@ def main():
     ap.add_argument('--shard', type=int, default=125000)
     ap.add_argument('--dim', type=int, default=2048)
     ap.add_argument('--topk', type=int, default=100)
-    ap.add_argument('--math', default='x3')
+    ap.add_argument('--math', default='h2', choices=('h2', 'x3', 'f32'))
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--tile', type=int, default=-1,
                     help='distance-GEMM tile (-1: time the pipelined tiles once, keep the best)')
@@ -42,9 +42,11 @@ def main():
 
     tile = a.tile
     if tile < 0:
-        idx0 = ops.GalleryIndex(gal) if a.math == 'x3' else gal
+        idx0 = ops.GalleryIndex(gal, math=a.math) if a.math != 'f32' else gal
         best = None
-        for t in [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)):
+        cands = (range(ops.h2_num_tiles()) if a.math == 'h2' else
+                 [0] + list(range(ops.TILE_P_FIRST, ops.num_tiles() + 1)))
+        for t in cands:
             ops.compute_dist(q, idx0, out=out, math=a.math, tile=t)
             e0, e1 = ev(), ev()
             e0.record()
@@ -60,7 +62,7 @@ def main():
     for rep in range(a.reps + 1):
         e = [ev() for _ in range(4)]
         e[0].record()
-        idx = ops.GalleryIndex(gal) if a.math == 'x3' else gal
+        idx = ops.GalleryIndex(gal, math=a.math) if a.math != 'f32' else gal
         e[1].record()
         ops.compute_dist(q, idx, out=out, math=a.math, tile=tile)
         e[2].record()

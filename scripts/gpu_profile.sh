@@ -3,14 +3,14 @@
 #   1. bench (autotune; tiles saved)            -> gpurun_out/bench_tuned.log
 #   2. rocprofv3 --kernel-trace --stats (same tiles, no e2e stage: its ragged
 #      last batch would be the "last forward") -> gpurun_out/prof/
-#   3. PMC passes FETCH_SIZE / WRITE_SIZE / GRBM_GUI_ACTIVE+MFMA busy (same tiles)
+#   3. PMC passes FETCH_SIZE / WRITE_SIZE / MFMA busy (same tiles)
 #      -> gpurun_out/pmc_traffic.json
 #   4. bench again (same tiles, traffic filled)  -> gpurun_out/bench_final.log
 # Each GPU step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out
-R=${ROUND_DIR:-profiles/r05}
+R=${ROUND_DIR:-profiles/r06}
 mkdir -p $OUT $R
 TILES=$OUT/tiles.json
 rm -f $TILES
@@ -30,7 +30,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o r
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --no-duke --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
 # MFMA launches per forward: 50 layers, one fewer per bottleneck seam pair
 NCONV=$(python -c "import json; t = json.load(open('$TILES')); print(50 - sum(1 for k, v in t.items() if not k.startswith('__') and isinstance(v, int) and v & 0x400))")
-python scripts/pmc_traffic.py $OUT/pmcb $MATH 64 $NCONV > $OUT/pmc_traffic.json || exit 1
+CLK=$OUT/bench_tuned.log; [ -f $CLK ] || CLK=$OUT/prof.log
+python scripts/pmc_traffic.py $OUT/pmcb $MATH 64 $NCONV $TILES --clock-from $CLK > $OUT/pmc_traffic.json || exit 1
 cat $OUT/pmc_traffic.json
 cp $OUT/pmc_traffic.json $R/pmc_traffic.json   # bench-final reads it (box copy)
 step bench-final

@@ -1,6 +1,7 @@
 """Per-layer roofline table of the forward's MFMA launches:
-GFLOP, algorithmic MB, us, TF, fraction of the x3 roof, MFMA busy, effective
-clock, memory-side FETCH/WRITE MB per launch.
+GFLOP, algorithmic MB, us, TF, fraction of the x3 roof, MFMA busy (over the
+launch's trace duration at 2.4 GHz: a lower bound; no GRBM-derived clock, see
+pmc_traffic.py), memory-side FETCH/WRITE MB per launch.
 
   python scripts/layer_table.py <layers.json (bench.py PPS_BENCH_LAYERS)> <pmcb dir> > table.md
 
@@ -38,10 +39,10 @@ def main():
     w = [v for nm, v in load(glob.glob(os.path.join(d, 'p2', '*counter_collection.csv'))[0],
                              'WRITE_SIZE') if is_mfma(nm)][-n:]
     p3 = [r for r in load_all(glob.glob(os.path.join(d, 'p3', '*counter_collection.csv'))[0])
-          if is_mfma(r[0]) and 'GRBM_GUI_ACTIVE' in r[1]][-n:]
+          if is_mfma(r[0]) and 'SQ_VALU_MFMA_BUSY_CYCLES' in r[1]][-n:]
     print('| layer | op | tile | math | GFLOP | alg. MB | us | TF | frac of its roof | frac of x3 '
-          'roof | MFMA busy | clock GHz | fetch MB | write MB | traffic / alg. |')
-    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|')
+          'roof | MFMA busy at 2.4 GHz | fetch MB | write MB | traffic / alg. |')
+    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|---|')
     tot = dict(fl=0.0, ms=0.0, by=0.0, tr=0.0, roof_ms=0.0)
     for i, (name, v) in enumerate(gemm):
         fl, ms, by = v['flops'], v['ms'], v['bytes']
@@ -50,11 +51,9 @@ def main():
         wb = 1024 * w[i] if i < len(w) else float('nan')
         if i < len(p3):
             nm, c, dur = p3[i]
-            act = c['GRBM_GUI_ACTIVE'] / 8.0
-            busy = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) / (1024.0 * act) if act else 0.0
-            clk = act / dur if dur else 0.0
+            busy = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) / (1024.0 * dur * 2.4) if dur else 0.0
         else:
-            busy = clk = float('nan')
+            busy = float('nan')
         h2 = bool(v.get('tile', 0) & H2)
         peak = PEAK_H2 if h2 else PEAK_X3
         tot['fl'] += fl
@@ -62,13 +61,13 @@ def main():
         tot['by'] += by
         tot['tr'] += fb + wb
         tot['roof_ms'] += fl / (peak * 1e12) * 1e3
-        print('| %s | %s | %#x | %s | %.2f | %.1f | %.1f | %.1f | %.3f | %.3f | %.3f | %.2f | %.1f '
+        print('| %s | %s | %#x | %s | %.2f | %.1f | %.1f | %.1f | %.3f | %.3f | %.3f | %.1f '
               '| %.1f | %.2f |' % (name, v['op'], v.get('tile', 0), 'f16x2' if h2 else 'bf16x3',
                                    fl / 1e9, by / 1e6, ms * 1e3, tf, tf / peak, tf / PEAK_X3,
-                                   busy, clk, fb / 1e6, wb / 1e6,
+                                   busy, fb / 1e6, wb / 1e6,
                                    (fb + wb) / by if by else float('nan')))
     tf = tot['fl'] / (tot['ms'] * 1e-3) / 1e12
-    print('| **all %d** | | | | %.1f | %.1f | %.1f | %.1f | %.3f | %.3f | | | | | %.2f |'
+    print('| **all %d** | | | | %.1f | %.1f | %.1f | %.1f | %.3f | %.3f | | | | %.2f |'
           % (n, tot['fl'] / 1e9, tot['by'] / 1e6, tot['ms'] * 1e3, tf,
              tot['roof_ms'] / tot['ms'], tf / PEAK_X3, tot['tr'] / tot['by']))
 

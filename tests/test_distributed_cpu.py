@@ -131,3 +131,80 @@ def test_shard_range_is_array_split():
                 [(int(p[0]) if len(p) else sum(len(x) for x in parts[:i]),
                   (int(p[-1]) + 1) if len(p) else sum(len(x) for x in parts[:i]))
                  for i, p in enumerate(parts)]
+
+
+_LEG_CUHK = dict(nq=60, ng=300, n_distractors=0, n_ids=20, dim=64)
+_LEG_1M = dict(nq=24, ng=500, dim=32, k=10)
+
+
+def _legs_worker(rank, world, port, out):
+    if world > 1:
+        _init(rank, world, port)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle.rank_counts import CpuBackend
+    c = bench.config_cuhk03(rank, world, reps=1, backend=CpuBackend, device='cpu',
+                            sizes=_LEG_CUHK)
+    m = bench.config_1m(rank, world, reps=1, backend=CpuBackend, device='cpu', sizes=_LEG_1M,
+                        keep=True)
+    mv, mi = m.pop('merged')
+    out[rank] = (c['mAP_synthetic'], c['cmc'], c['G_local_rank0'], mv.numpy().tolist(),
+                 mi.numpy().tolist(), m['G_local_rank0'], sorted(c), sorted(m))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [1, 2])
+def test_bench_sharded_legs_rehearsal(world):
+    """bench.py's config_cuhk03 / config_1m legs (BASELINE configs[3] and
+    [4], run by the driver's N > 1 benches) driven through their collective
+    code on CPU with gloo and the oracle backend, at reduced sizes: the
+    sharded mAP / CMC equal the one-process oracle evaluation of the same
+    features, and the merged top-k of the 1M leg equals the stable argsort of
+    the unsharded matrix."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle import evaluator as ev
+    mgr = mp.Manager()
+    out = mgr.dict()
+    if world > 1:
+        mp.spawn(_legs_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    else:
+        _legs_worker(0, 1, None, out)
+    s = _LEG_CUHK
+    qid, gid, qcam, gcam, f = bench.retrieval_inputs(s['nq'], s['ng'], s['n_distractors'],
+                                                     s['n_ids'], s['dim'], 'cpu')
+    f = f.numpy()
+    d = ev.compute_dist(f[:s['nq']], f[s['nq']:])
+    ref_map = ev.mean_ap(d, qid, gid, qcam, gcam)
+    ref_cmc = ev.cmc(d, qid, gid, qcam, gcam, topk=10, first_match_break=True)
+    t = _LEG_1M
+    q = bench.synth_rows(0, t['nq'], t['dim'], 1, 'cpu').numpy()
+    g = bench.synth_rows(0, t['ng'], t['dim'], 2, 'cpu').numpy()
+    full = ev.compute_dist(q, g)
+    order = np.argsort(full, axis=1, kind='stable')[:, :t['k']]
+    for r in range(world):
+        mAP, cmc, gl, mv, mi, gl1, ckeys, mkeys = out[r]
+        assert gl == s['ng'] // world + (1 if r < s['ng'] % world else 0)   # this rank's shard
+        assert gl1 == t['ng'] // world + (1 if r < t['ng'] % world else 0)
+        assert abs(mAP - ref_map) < 1e-9, (mAP, ref_map)
+        np.testing.assert_allclose(cmc, ref_cmc, atol=1e-12)
+        np.testing.assert_array_equal(np.array(mi), order)
+        np.testing.assert_allclose(np.array(mv, np.float32), np.take_along_axis(full, order, 1),
+                                   rtol=0, atol=1e-6)
+        assert {'distmat_ms', 'query_allgather_ms', 'retrieval_ms', 'mAP_synthetic'} <= set(ckeys)
+        assert {'distmat_ms', 'topk_ms', 'list_allgather_merge_ms', 'total_ms'} <= set(mkeys)
+
+
+def test_synth_rows_do_not_depend_on_sharding():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from pps_amd.distributed import shard_range
+    full = bench.synth_rows(0, 1000, 16, 7, 'cpu', chunk=96)
+    for w in (1, 3, 8):
+        parts = [bench.synth_rows(*shard_range(1000, r, w), 16, 7, 'cpu', chunk=96)
+                 for r in range(w)]
+        assert torch.equal(torch.cat(parts), full)

@@ -111,6 +111,31 @@ def test_h2_gallery_index_and_padded_output():
     assert float(full[:, :50].abs().sum()) == 0 and float(full[:, 351:].abs().sum()) == 0
 
 
+def test_h2_strided_gallery_and_math_mismatch():
+    """A row-strided raw gallery (big[:, :D], D % 32 == 0) takes the h2 path
+    with the bits of its contiguous copy (it used to reach the h2 GEMM with
+    no h2 index); an explicit math that disagrees with a GalleryIndex's split
+    is an error, not silently overridden."""
+    from pps_amd import ops
+    rng = np.random.RandomState(11)
+    q = _cuda(rng.randn(40, 96))
+    big = _cuda(rng.randn(130, 160))
+    g = big[:, :96]
+    assert not g.is_contiguous()
+    a = ops.compute_dist(q, g, math='h2')
+    b = ops.compute_dist(q, g.contiguous(), math='h2')
+    assert torch.equal(a, b)
+    ref = ev.compute_dist(q.cpu().numpy(), g.cpu().numpy())
+    assert np.abs(a.cpu().numpy() - ref).max() < 1e-4
+    idx = ops.GalleryIndex(g.contiguous(), math='h2')
+    with pytest.raises(RuntimeError, match='GalleryIndex'):
+        ops.compute_dist(q, idx, math='x3')
+    assert torch.equal(ops.compute_dist(q, idx, math='h2'), a)
+    # f32 reads the index's features as they are
+    f = ops.compute_dist(q, idx, math='f32').cpu().numpy()
+    assert np.abs(f - ref).max() < 1e-4
+
+
 @pytest.mark.parametrize('N,D', [(1000, 3968), (700, 256), (301, 64), (17, 32), (513, 2048)])
 @pytest.mark.parametrize('metric', ['euclidean', 'cosine'])
 def test_h2_self_distance_symmetric(N, D, metric):

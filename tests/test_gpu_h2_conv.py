@@ -37,20 +37,23 @@ def _h2_tiles():
     return [0] + [t for t in range(ops.TILE_P16_FIRST, ops.num_tiles() + 1) if t != 54]
 
 
-@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p', [
+_SHAPES = [
     (2, 24, 8, 256, 256, 3, 1, 1),     # res4 branch2b (patch tiles apply)
     (1, 24, 8, 512, 512, 3, 1, 1),     # res5 branch2b
     (2, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
     (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1 (STRIDE_1X1 branch2a)
     (2, 96, 32, 64, 64, 3, 1, 1),      # res2 branch2b
     (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
-])
-@pytest.mark.parametrize('residual', [False, True])
-@pytest.mark.parametrize('mag', [1.0, 1e-20, 1e20])
+]
+# every shape with and without the residual at unit magnitude, plus the
+# magnitude sweep (inputs x 1e-20 and x 1e20) on the res4 3x3 shape
+_CASES = [sh + (res, 1.0) for sh in _SHAPES for res in (False, True)] + \
+    [_SHAPES[0] + (False, mag) for mag in (1e-20, 1e20)]
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,k,s,p,residual,mag', _CASES)
 def test_conv_h2_error_tiles_amax(N, H, W, Cin, Cout, k, s, p, residual, mag):
     from pps_amd import model, ops
-    if mag != 1.0 and (k != 3 or Cin != 256 or residual):
-        pytest.skip('magnitude sweep on one shape')
     rng = np.random.RandomState(N + H + Cin + Cout + k)
     x = (rng.randn(N, Cin, H, W) * mag).astype(np.float32)
     w = (rng.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).astype(np.float32)

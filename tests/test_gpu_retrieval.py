@@ -580,6 +580,15 @@ def test_sharded_evaluator_tiled_query_planes(golden, case):
                                    rtol=0, atol=1e-5)
     for o in outs:
         assert abs(o['mAP'] - float(g['mAP'])) < 1e-6
+        # CMC of every arithmetic (the default h2 included) vs the reference's
+        # own evaluation (the golden cmc covers topk = 10 here too)
+        np.testing.assert_allclose(o['cmc'], np.asarray(g['cmc'])[:len(o['cmc'])], rtol=0,
+                                   atol=1e-9)
+    # runs of one arithmetic on the same bits: identical scores
+    for a, b in ((outs[1], outs[2]), (outs[3], outs[4]), (outs[0], outs[3])):
+        if torch.equal(a['dist'], b['dist']):
+            assert a['mAP'] == b['mAP']
+            np.testing.assert_array_equal(a['cmc'], b['cmc'])
 
 
 def test_rank_prepare_beyond_lds_merge_cap():

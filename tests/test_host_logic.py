@@ -92,3 +92,19 @@ def test_decode_pool_matches_in_process_decode(tmp_path):
         want = decode_pool.decode_bgr(p)
         assert g.dtype == np.uint8 and g.shape == want.shape and np.array_equal(g, want)
     assert decode_pool.default_workers(share=1000) == 1
+
+
+def test_h2_inv_scale_mirrors_the_kernel_scale():
+    """native.h2_inv_scale (the f16x2-planes decode of NativeModel.tensor)
+    follows pps_internal.hpp h2_scale_of: normal maxima land in [2^14, 2^15)
+    after scaling, a zero max keeps scale 1, a denormal max takes 2^126, and
+    the shift is clamped to [-126, 126]."""
+    from pps_amd.native import h2_inv_scale
+    rng = np.random.RandomState(0)
+    for a in np.exp(rng.uniform(-70, 80, 200)).astype(np.float32):
+        s = a / h2_inv_scale(a)
+        assert 2.0 ** 14 <= s < 2.0 ** 15, (a, s)
+    assert h2_inv_scale(0.0) == 1.0
+    assert h2_inv_scale(np.float32(1e-40)) == 2.0 ** -126      # denormal
+    assert h2_inv_scale(np.float32(1e-37)) == 2.0 ** -126      # shift clamped
+    assert h2_inv_scale(np.float32(3e38)) == 2.0 ** 113
