@@ -457,11 +457,20 @@ def config_1m(rank, world, reps=3, backend=None, device='cuda', sizes=None, keep
     st = _Stamps(gpu)
     if gpu:
         from pps_amd import ops
+        # the gallery prepared once per shard, in sub-blocks whose f16x2 planes
+        # stay under the 2 GiB a buffer resource addresses (1M / 2 ranks =
+        # 500k rows of 2048-d: 4 GB of planes), each scored into its columns
+        sub = max(4, min(G, ((2 ** 31 - 2 ** 20) // (dim * 4)) // 4 * 4))
         st.mark()
-        index = ops.GalleryIndex(g_local)   # the gallery prepared once per shard
+        index = [(a, ops.GalleryIndex(g_local[a:a + sub])) for a in range(0, G, sub)]
         st.mark()
         index_ms = st.ms()[0]
         dist = ops.dist_buffer(nq, G, device)
+
+        def gemm(q_all):
+            for a, ix in index:
+                ops.compute_dist(q_all, ix, out=dist[:, a:a + ix.shape[0]], tile=be.distmat_tile)
+            return dist
     else:
         index, index_ms, dist = g_local, None, None
 
@@ -471,8 +480,7 @@ def config_1m(rank, world, reps=3, backend=None, device='cuda', sizes=None, keep
         q_all = pdist.all_gather_rows(q_local, q_sizes)
         s.mark()
         if gpu:
-            from pps_amd import ops
-            d = ops.compute_dist(q_all, index, out=dist, tile=be.distmat_tile)
+            d = gemm(q_all)
         else:
             d = be.distmat(q_all, index, 'euclidean')
         s.mark()
@@ -521,7 +529,7 @@ def config_1m(rank, world, reps=3, backend=None, device='cuda', sizes=None, keep
         q_all = pdist.all_gather_rows(q_local, q_sizes)
         e0.record()
         for _ in range(n):
-            ops.compute_dist(q_all, index, out=dist, tile=be.distmat_tile)
+            gemm(q_all)
         e1.record()
         for _ in range(n):
             be.topk(dist, kin)
@@ -530,14 +538,15 @@ def config_1m(rank, world, reps=3, backend=None, device='cuda', sizes=None, keep
         gemm_us = e0.elapsed_time(e1) * 1e3 / n
         topk_us = e1.elapsed_time(e2) * 1e3 / n
         flops = 2.0 * nq * G * dim
-        h2 = getattr(index, 'math', None) == 'h2'
+        h2 = index[0][1].math == 'h2'
         peak = PEAK_H2_TFLOPS if h2 else PEAK_X3_TFLOPS
         tb = nq * G * 4 + nq * kin * 8
         out['roofline_distmat_rank0'] = dict(
             bound='mfma', achieved=round(flops / gemm_us / 1e6, 2), peak=round(peak, 1),
             unit='TFLOP/s', frac=round(flops / gemm_us / 1e6 / peak, 4),
             math='h2' if h2 else 'x3', avg_launch_us=round(gemm_us, 1),
-            note='compute_dist on the prepared GalleryIndex (query split + GEMM)')
+            note='compute_dist on the prepared GalleryIndex sub-blocks (%d; query split + '
+                 'GEMM per sub-block)' % len(index))
         out['roofline_topk_rank0'] = dict(
             bound='hbm', achieved=round(tb / topk_us / 1e3, 1),
             peak=PEAK_HBM_GBPS, unit='GB/s',

@@ -42,6 +42,10 @@ namespace pps {
 // (l & 15) and gallery columns 4 (l >> 4) + e, e = 0..3.
 __device__ inline f32x4 mfma_h2t(const f16x8& a0, const f16x8& a1, const f16x8& b0,
                                  const f16x8& b1, f32x4 c) {
+#if H2_ABL == 2
+  asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
+  return c;
+#endif
   c = mfma16_f16(b0, a0, c);
   c = mfma16_f16(b1, a0, c);
   c = mfma16_f16(b0, a1, c);
@@ -205,6 +209,10 @@ __device__ inline void h2_dist_epilogue(const GemmParams& p, f32x4 (&acc)[BM / W
   }
 }
 
+#ifndef H2_ABL
+#define H2_ABL 0  // probes: 1 = no DMA after the prologue, 2 = no MFMAs (timing ablations)
+#endif
+
 template <int BM, int BN, int WM, int WN, int NS>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
@@ -241,13 +249,13 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // ---- DMA pieces.  Piece q of a chunk: A plane q / ABLK, block q % ABLK
   // (q < 2 ABLK), else B; its LDS image is stage + q KiB.  Lane l fills row
   // l >> 2 of the 16-row block, physical 16-byte slot l & 3 with logical slot
-  // (l & 3) ^ ((row >> 2) & 3) (bank-conflict swizzle on the source address).
+  // (l & 3) ^ sw64(row) (bank-conflict swizzle on the source address).
   const rsrc_t ra = make_rsrc(p.a3, p.a_bytes);
   const rsrc_t rb = make_rsrc(p.b3, p.b_bytes);
   const int ablocks = (int)(p.a_plane / (16 * (int64_t)p.Kloop));
   const int bblocks = (int)(p.b_plane / (16 * (int64_t)p.Kloop));
   const int lr = lane >> 2;
-  const int loff = lr * 64 + (((lane & 3) ^ ((lr >> 2) & 3)) << 4);
+  const int loff = lr * 64 + (((lane & 3) ^ sw64(lr)) << 4);
   int src[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -272,6 +280,7 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
     src[i] = blk < nblk ? (int)(pbase + (int64_t)blk * nkc * 1024 + loff) : (int)0x80000000;
   }
   auto issue = [&](int kc, int stage) {
+    if (H2_ABL == 1 && kc >= NS) return;
     const unsigned char* st = lds + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -286,7 +295,7 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // ---- fragments: lane l reads row l & 15 of a block, logical 16-byte slot
   // l >> 4 (K elements 8 (l >> 4) .. + 7), at its swizzled position
   const int r16 = lane & 15;
-  const int foff = r16 * 64 + (((lane >> 4) ^ ((r16 >> 2) & 3)) << 4);
+  const int foff = r16 * 64 + (((lane >> 4) ^ sw64(r16)) << 4);
   auto readA = [&](const unsigned char* st, int i, f16x8 (&f)[2]) {
     const unsigned char* a = st + (wm * (BM / WM / 16) + i) * 1024 + foff;
     f[0] = *reinterpret_cast<const f16x8*>(a);

@@ -79,7 +79,7 @@ seam_kernel(SeamParams p, int ntiles) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, h = lane >> 4;
-  const int bsw = (r16 >> 2) & 3;
+  const int bsw = sw64(r16);
   float* scr = reinterpret_cast<float*>(lds + 2 * C::STAGE) + wave * (C::SCR / 4);
   float* s_s2c = reinterpret_cast<float*>(lds + 2 * C::STAGE + kSeamWaves * C::SCR);
   float* s_t2c = s_s2c + N1;
@@ -109,13 +109,13 @@ seam_kernel(SeamParams p, int ntiles) {
     if (u * 16 < C::W2C) {   // W2c: [kc][pl][n][32]
       const int n = rest % CG, pk = rest / CG, kc = pk / 3, pl = pk - 3 * kc;
       goff = pl * N1 * K1 + (cg * CG + n) * K1 + kc * 32 + slot * 8;
-      loff = (pk * CG + n) * 64 + ((slot ^ ((n >> 2) & 3)) << 4);
+      loff = (pk * CG + n) * 64 + ((slot ^ sw64(n)) << 4);
       return p.w2c;
     }
     const int r2 = rest - C::W2C / 64;   // W2a: [kc2][pl][n][32]
     const int n = r2 % N2, pk = r2 / N2, kc = pk / 3, pl = pk - 3 * kc;
     goff = pl * N2 * N1 + n * N1 + cg * CG + kc * 32 + slot * 8;
-    loff = C::W2C + (pk * N2 + n) * 64 + ((slot ^ ((n >> 2) & 3)) << 4);
+    loff = C::W2C + (pk * N2 + n) * 64 + ((slot ^ sw64(n)) << 4);
     return p.w2a;
   };
   // the slab in two halves of PPT / 2 pieces: the W2c half (read by 2c) and

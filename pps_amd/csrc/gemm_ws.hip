@@ -60,7 +60,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
 
   // 1) this block's weight columns [n0, n0 + BN2) and scale / shift -> LDS;
   // 16-byte slot c of a column's 64-byte chunk row lands in slot
-  // c ^ ((col >> 2) & 3), the pipelined kernel's B swizzle
+  // c ^ sw64(col), the pipelined kernel's B swizzle (gemm_common.hpp)
   for (int u = threadIdx.x; u < NCH * 3 * BN2 * 4; u += 64 * kWsWaves) {
     const int slot = u & 3;
     const int rest = u >> 2;
@@ -72,7 +72,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
     if (gcol < p.Ncol)
       v = *reinterpret_cast<const u32x4*>(p.b3 + pl * p.b_plane + (int64_t)gcol * p.ldb +
                                          kc * 32 + slot * 8);
-    *reinterpret_cast<u32x4*>(ws_lds + (pk * BN2 + col) * 64 + ((slot ^ ((col >> 2) & 3)) << 4)) = v;
+    *reinterpret_cast<u32x4*>(ws_lds + (pk * BN2 + col) * 64 + ((slot ^ sw64(col)) << 4)) = v;
   }
   for (int c = threadIdx.x; c < BN2; c += 64 * kWsWaves) {
     const bool ok = n0 + c < p.Ncol;
@@ -95,7 +95,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   const int nch1 = DUAL ? p.Kloop1 / 32 : NCH;
   const int rt0 = g / n_cb;
   const int my = rt0 < n_rt ? (n_rt - rt0 + rg - 1) / rg : 0;
-  const int bsw = (r16 >> 2) & 3;
+  const int bsw = sw64(r16);
   const int hw = p.Ho * p.Wo;
 
   // One tile's operands of this lane: activation vectors (chunk kc, K

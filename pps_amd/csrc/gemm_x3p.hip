@@ -40,6 +40,9 @@ namespace pps {
 #ifndef X3P_PRIO
 #define X3P_PRIO 0  // probes: 1 = s_setprio(1) around every MFMA cluster, 2 = younger half raised
 #endif
+#ifndef X3P_ABL
+#define X3P_ABL 0  // probes: 1 = no DMA after the prologue, 2 = no MFMAs (timing ablations)
+#endif
 #ifndef X3P_CLK
 #define X3P_CLK 0  // diagnostic builds: per-workgroup shader clocks / 100 MHz ticks
 #endif
@@ -256,7 +259,9 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     for (int i = 0; i < AI; ++i) {
       const int rt = A3 ? apiece(i) * 16 + (lane >> 2) : apiece(i) * 8 + (lane >> 3);
       // first element (of the 32-wide K chunk) this lane fetches
-      const int ce = A3 ? 8 * ((lane & 3) ^ ((rt >> 2) & 3)) : 4 * ((lane & 7) ^ ((rt >> 1) & 7));
+      // (16x16x32 tiles: the group-aware swizzles of gemm_common.hpp)
+      const int ce = A3 ? 8 * ((lane & 3) ^ (S == 16 ? sw64(rt) : ((rt >> 2) & 3)))
+                        : 4 * ((lane & 7) ^ (S == 16 ? sw128(rt) : ((rt >> 1) & 7)));
       const int row = m0 + rt;
       const int rowc = row < p.M ? row : 0;
       const int n = rowc / hw;
@@ -290,7 +295,7 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   const rsrc_t rb0 = make_rsrc(b3, p.b_bytes);
   const rsrc_t rb1 = make_rsrc(b3 + p.b_plane, p.b_bytes);
   const rsrc_t rb2 = make_rsrc(b3 + 2 * p.b_plane, p.b_bytes);
-  const int bcl = (lane & 3) ^ ((lane >> 4) & 3);
+  const int bcl = (lane & 3) ^ (S == 16 ? sw64(lane >> 2) : ((lane >> 4) & 3));
   int boff[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
@@ -319,6 +324,11 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   int kiss = 0;  // next chunk to request
   int siss = 0;  // its LDS stage
   auto issue = [&]() {
+    if (X3P_ABL == 1 && kiss >= NS) {  // probe: keep the counters, skip the DMA
+      ++kiss;
+      siss = siss + 1 == NS ? 0 : siss + 1;
+      return;
+    }
     const unsigned char* st = lds + siss * STAGE;
     if (DUAL && kiss >= nch1) {
       const int kofs = (kiss - nch1) * BK * 4;
@@ -380,8 +390,8 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
   if constexpr ((EPI & EPI_F_H2OUT) != 0) bnd_pre = h2o_bound(p);
   // Fragment reads: the rows of this lane are r32 mod S, so both swizzles
   // are per-lane constants.
-  const int asw = (r32 >> 1) & 7;
-  const int bsw = (r32 >> 2) & 3;
+  const int asw = S == 16 ? sw128(r32) : (r32 >> 1) & 7;
+  const int bsw = S == 16 ? sw64(r32) : (r32 >> 2) & 3;
   // chunk kc has landed for every wave once each wave saw its own pieces
   // retire (counted vmcnt: the NS-2 younger chunks stay in flight) and all
   // waves passed the barrier; the barrier also retires every wave's reads of
@@ -507,9 +517,14 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int jj = 0; jj < TNH; ++jj)
+        for (int jj = 0; jj < TNH; ++jj) {
+          if (X3P_ABL == 2) {  // probe: fragments kept live, no MFMA
+            asm volatile("" ::"v"(fa[i][0]), "v"(fa[i][1]), "v"(fb[jj][0]), "v"(fb[jj][1]));
+            continue;
+          }
           acc[i][half * TNH + jj] = H2 ? mfma16_h2t(fa[i], fb[jj], acc[i][half * TNH + jj])
                                        : mfma16_x3t(fa[i], fb[jj], acc[i][half * TNH + jj]);
+        }
       if (X3P_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     };
     bf16x8 fa0[TM][3], fa1[TM][3], fb0[TNH][3], fb1[TNH][3];
