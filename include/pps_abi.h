@@ -94,8 +94,11 @@ int pps_gemm_num_tiles(void);
 /* Whole-network plan only, or-ed into a conv / fused-shortcut / conv_pps
  * layer's tile: run the layer in the f16x2 arithmetic of
  * pps_conv2d_bn_act_h2 (three f16 MFMA terms per product) on base tile 0,
- * 38..53, 55 or, for stride-1 3x3 convs, 56..59 (conv_pps: its 192-row
- * tiles >= 38), optionally with PPS_TILE_COL_ORDER; f32 activations at both
+ * 38..53, 55, 54 for a 1x1 / stride-1 conv or fused-shortcut conv with K =
+ * 64 / 128 / 256 (the weight-stationary kernel with the f16x2 weight planes
+ * in LDS; f32 input, no PPS_TILE_H2P / H2E) or, for stride-1 3x3 convs,
+ * 56..59 (conv_pps: its 192-row tiles >= 38), optionally with
+ * PPS_TILE_COL_ORDER; f32 activations at both
  * ends (no plane edge), no split-K.  The handle keeps the f16x2 weight split
  * beside the bf16x3 one; each forward zeroes its per-tensor activation maxima
  * and every producer reports max|y| from its epilogue (the f16x2 layers'
@@ -233,9 +236,11 @@ int pps_h2_num_tiles(void);
  * through its amax_y, or by pps_amax), and splits them into two f16 terms
  * after the LDS fragment read.  amax_y (a zeroed slot or NULL) receives
  * max|y|.  Cin % 32 == 0,
- * Kpad == KH*KW*Cin; tile 0 (= 38), the 16x16x32 pipelined tiles 38..53, 55
- * and the patch tiles 56..59, or-ed with PPS_TILE_COL_ORDER; no planes, no
- * split-K.  Same f32-level error as the x3 entries (tests/test_gpu_h2_conv.py). */
+ * Kpad == KH*KW*Cin; tile 0 (= 38), the 16x16x32 pipelined tiles 38..53, 55,
+ * the weight-stationary tile 54 (1x1 / stride 1 / K = 64, 128, 256; other
+ * shapes run 38) and the patch tiles 56..59, or-ed with PPS_TILE_COL_ORDER;
+ * no planes, no split-K.  Every tile gives the same bits; the same f32-level
+ * error as the x3 entries (tests/test_gpu_h2_conv.py). */
 int pps_conv2d_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx,
                          const uint16_t* w2t, const float* wrs, int Cout, int Kpad, int KH,
                          int KW, int stride, int pad, int dil, const float* scale,
@@ -243,7 +248,9 @@ int pps_conv2d_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx,
                          int Wo, int ldy, const float* amax_x, float* amax_y, int tile,
                          void* stream);
 /* pps_conv2d_dual_bn_act_x3 (projection shortcut K-concatenated) in f16x2:
- * both inputs share the scale of max(*amax_x, *amax_x2); Cin2 % 32 == 0. */
+ * both inputs share the scale of max(*amax_x, *amax_x2); Cin2 % 32 == 0;
+ * tiles 0, 38..55 (54: the weight-stationary kernel when K = Cin + Cin2 is
+ * 64, 128 or 256) or 60. */
 int pps_conv2d_dual_bn_act_h2(const float* x, int N, int H, int W, int Cin, int ldx, int KH,
                               int KW, int stride, int pad, const float* x2, int H2, int W2,
                               int Cin2, int ldx2, int stride2, const uint16_t* w2t,

@@ -694,9 +694,9 @@ int conv_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     PPS_ENFORCE(amax_in != nullptr, "f16x2 conv: the input tensor's max (amax_x) is required");
     PPS_ENFORCE(Cin % 32 == 0 && Kpad == KH * KW * Cin,
                 "f16x2 conv: Cin % 32 == 0 and Kpad == KH*KW*Cin");
-    PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile != GEMM_TILE_WS &&
-                              tile < GEMM_NUM_TILES),
-                "f16x2 conv: tile 0, 38..53 or 55..60");
+    PPS_ENFORCE(tile == 0 || (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_NUM_TILES),
+                "f16x2 conv: tile 0 or 38..60 (54: the weight-stationary 1x1 where it "
+                "applies, else 38)");
     p.b3 = static_cast<const uint16_t*>(w);
     p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * Kpad;
     p.b_bytes = (uint32_t)(p.b_plane * 2);
@@ -1061,9 +1061,8 @@ int dual_impl(const float* x, int N, int H, int W, int Cin, int ldx,
     PPS_ENFORCE(Cin % 32 == 0 && Kpad1 == KH * KW * Cin && Kpad2 % 32 == 0,
                 "f16x2 conv: Cin % 32 == 0, Kpad1 == KH*KW*Cin, Cin2 % 32 == 0");
     PPS_ENFORCE(tile == 0 || tile == GEMM_TILE_P16_192x128W41 ||
-                    (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_TILE_C16_FIRST &&
-                     tile != GEMM_TILE_WS),
-                "f16x2 fused-shortcut conv: tile 0, 38..53, 55 or 60");
+                    (tile >= GEMM_TILE_P16_FIRST && tile < GEMM_TILE_C16_FIRST),
+                "f16x2 fused-shortcut conv: tile 0, 38..55 or 60");
     p.b3 = static_cast<const uint16_t*>(w);
     p.b_plane = (int64_t)(Cout + 15) / 16 * 16 * (Kpad1 + Kpad2);
     p.b_bytes = (uint32_t)(p.b_plane * 2);

@@ -23,6 +23,15 @@
 // Arithmetic: the six terms of mfma16_x3t per 32-wide K chunk, chunks in
 // order, then fma(acc, scale, shift) [+ residual] [ReLU] -- the S = 16
 // pipelined tiles' sequence, so this tile's results equal theirs bit for bit.
+// EPI_F_H2 (round 6): the f16x2 arithmetic of the pipelined kernel's
+// PPS_TILE_H2 tiles -- activations split after the load on their tensor's
+// power-of-two scale (split8_h2), the two chunk-tiled f16 weight planes in
+// LDS (4 B per weight instead of 6, so a 256-column block of a K = 128
+// layer fits and its activation rows are read once), the three terms of
+// mfma16_h2t, the column scale (scale * 2^-s_w) * 2^-s_a in the epilogue:
+// bit for bit the f16x2 pipelined tiles' results.
+#include <cstdlib>
+
 #include "gemm_x3_common.hpp"
 
 namespace pps {
@@ -47,12 +56,20 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   constexpr bool HAS_RES = (EPI & EPI_F_RES) != 0;
   constexpr bool RELU = (EPI & EPI_F_RELU) != 0;
   constexpr bool DUAL = (EPI & EPI_F_DUAL) != 0;
-  constexpr int WBYTES = NCH * 3 * BN2 * 64;  // weights: [chunk][plane][column][32 bf16]
+  constexpr bool H2 = (EPI & EPI_F_H2) != 0;
+  // f16x2 planes out (PPS_TILE_H2E producer): the two f16 planes its f16x2
+  // reader would split, on the scale of the output bound (conv_epilogue_t)
+  constexpr bool H2O = (EPI & EPI_F_H2OUT) != 0;
+  static_assert(!H2O || (H2 && !HAS_RES && !DUAL), "planes out: f16x2 conv + BN + ReLU");
+  constexpr int NBP = H2 ? 2 : 3;  // weight planes
+  constexpr int WBYTES = NCH * NBP * BN2 * 64;  // weights: [chunk][plane][column][32 x 2 B]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, h = lane >> 4;
   const int wr = wave / WC, wcol = 64 * (wave - wr * WC);  // row group, first column
-  const int g = blockIdx.x;
+  // f16x2: the workgroups of one row tile's column blocks on one XCD (their
+  // activation rows shared through its L2)
+  const int g = H2 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int cb = g % n_cb;
   const int n0 = cb * BN2;
   float* s_sc = reinterpret_cast<float*>(ws_lds + WBYTES);
@@ -61,22 +78,37 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   // 1) this block's weight columns [n0, n0 + BN2) and scale / shift -> LDS;
   // 16-byte slot c of a column's 64-byte chunk row lands in slot
   // c ^ sw64(col), the pipelined kernel's B swizzle (gemm_common.hpp)
-  for (int u = threadIdx.x; u < NCH * 3 * BN2 * 4; u += 64 * kWsWaves) {
+  // (f16x2: chunk-tiled planes [2][col / 16][K / 32][16][32], the layout the
+  // pipelined tiles stream)
+  for (int u = threadIdx.x; u < NCH * NBP * BN2 * 4; u += 64 * kWsWaves) {
     const int slot = u & 3;
     const int rest = u >> 2;
     const int col = rest % BN2;
-    const int pk = rest / BN2;  // chunk * 3 + plane
-    const int kc = pk / 3, pl = pk - 3 * kc;
+    const int pk = rest / BN2;  // chunk * NBP + plane
+    const int kc = pk / NBP, pl = pk - NBP * kc;
     const int gcol = n0 + col;
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (gcol < p.Ncol)
-      v = *reinterpret_cast<const u32x4*>(p.b3 + pl * p.b_plane + (int64_t)gcol * p.ldb +
-                                         kc * 32 + slot * 8);
+    if (gcol < p.Ncol) {
+      const int64_t e = H2 ? ((int64_t)(gcol >> 4) * (p.ldb / 32) + kc) * 512 + (gcol & 15) * 32
+                           : (int64_t)gcol * p.ldb + kc * 32;
+      v = *reinterpret_cast<const u32x4*>(p.b3 + pl * p.b_plane + e + slot * 8);
+    }
     *reinterpret_cast<u32x4*>(ws_lds + (pk * BN2 + col) * 64 + ((slot ^ sw64(col)) << 4)) = v;
+  }
+  // f16x2: the activations' scale 2^s_a (and 2^-s_a for the epilogue); planes
+  // out: the output bound and its scale
+  float h2s = 1.f, inv_a = 1.f, bnd = 0.f, so = 1.f;
+  if constexpr (H2) h2s = h2_act_scale(p, DUAL, &inv_a);
+  if constexpr (H2O) {
+    float inv;
+    bnd = h2o_bound(p);
+    so = h2_scale_of(bnd, &inv);
   }
   for (int c = threadIdx.x; c < BN2; c += 64 * kWsWaves) {
     const bool ok = n0 + c < p.Ncol;
-    s_sc[c] = (ok && !DUAL) ? p.scale[n0 + c] : 1.f;
+    float sc = (ok && !DUAL) ? p.scale[n0 + c] : 1.f;
+    if (H2 && ok) sc = sc * p.rs_b[n0 + c] * inv_a;  // conv_epilogue_t's order
+    s_sc[c] = sc;
     s_sh[c] = ok ? p.shift[n0 + c] : 0.f;
   }
   __syncthreads();
@@ -91,7 +123,8 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
   const rsrc_t ra2 = DUAL ? make_rsrc(p.a2, p.a2_bytes) : ra;
   const rsrc_t rres = make_rsrc(HAS_RES ? p.residual : p.a,
                                 HAS_RES ? (uint32_t)((int64_t)p.M * p.ldr * 4) : 0u);
-  const rsrc_t rout = make_rsrc(p.out, (uint32_t)((int64_t)p.M * p.ldo * 4));
+  const rsrc_t rout = H2O ? make_rsrc(p.out3, (uint32_t)((p.out_plane + (int64_t)p.M * p.ldo) * 2))
+                          : make_rsrc(p.out, (uint32_t)((int64_t)p.M * p.ldo * 4));
   const int nch1 = DUAL ? p.Kloop1 / 32 : NCH;
   const int rt0 = g / n_cb;
   const int my = rt0 < n_rt ? (n_rt - rt0 + rg - 1) / rg : 0;
@@ -151,16 +184,19 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
 #pragma unroll
     for (int kc = 0; kc < NCH; ++kc) {
       bf16x8 fa[3];
-      split8(o.a[kc][0], o.a[kc][1], fa[0], fa[1], fa[2]);
+      if (H2)
+        split8_h2(o.a[kc][0], o.a[kc][1], h2s, fa[0], fa[1]);
+      else
+        split8(o.a[kc][0], o.a[kc][1], fa[0], fa[1], fa[2]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bf16x8 fb[3];
         const unsigned char* bp =
-            ws_lds + ((kc * 3) * BN2 + wcol + 16 * j + r16) * 64 + ((h ^ bsw) << 4);
+            ws_lds + ((kc * NBP) * BN2 + wcol + 16 * j + r16) * 64 + ((h ^ bsw) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NBP; ++pl)
           fb[pl] = *reinterpret_cast<const bf16x8*>(bp + pl * BN2 * 64);
-        acc[j] = mfma16_x3t(fa, fb, acc[j]);
+        acc[j] = H2 ? mfma16_h2t(fa, fb, acc[j]) : mfma16_x3t(fa, fb, acc[j]);
       }
       // one chunk's weight fragments live at a time (the compiler would hoist
       // every chunk's LDS reads and run out of registers)
@@ -193,7 +229,16 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
         m4 = fmaxf(m4, fabsf(v[e]));
       }
       amx = oo != kOOB ? fmaxf(amx, m4) : amx;  // rows of this launch only
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, kStAux);
+      if constexpr (H2O) {  // 2-byte elements: the f32 offset halved, plane 1 a plane further
+        u32x2 hi, lo;
+        split4_h2(v, so, hi, lo);
+        const int oh = oo == kOOB ? kOOB : oo / 2;
+        __builtin_amdgcn_raw_buffer_store_b64(hi, rout, oh, 0, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b64(lo, rout, oh == kOOB ? kOOB : oh + (int)(p.out_plane * 2),
+                                              0, kStAux);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, oo, 0, kStAux);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next park
   };
@@ -210,7 +255,7 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
       process(rt0 + t * rg, t < my, ring[u]);
     }
   }
-  if (p.amax_out) amax_commit(p.amax_out, amx);
+  if (p.amax_out) amax_commit(p.amax_out, H2O ? bnd : amx);
 }
 
 // Shapes this kernel takes: a 1x1 / stride-1 / unpadded conv on f32 NHWC
@@ -218,13 +263,26 @@ gemm_ws_kernel(GemmParams p, int n_cb, int n_rt, int rg) {
 // f32 output, the conv epilogues C [| RELU] [| RES] [| DUAL].
 bool ws_eligible(const GemmParams& p, int epi, int batch) {
   if (batch != 1 || p.splitk != 1 || p.ksplit_conv || p.a3 || !p.a || !p.b3 || p.sym) return false;
-  if (epi & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES | EPI_F_PPS | EPI_F_H2OUT)) return false;
+  // f16x2: chunk-tiled two-plane weights, their column scales and the inputs' maxima
+  if ((epi & EPI_F_H2) && (!(p.tiled & 2) || !p.rs_b || !p.amax_a ||
+                           ((epi & EPI_F_DUAL) && !p.amax_a2)))
+    return false;
+  if (!(epi & EPI_F_H2) && (p.tiled & 2)) return false;
+  if (epi & (EPI_DIST | EPI_F_RAW | EPI_F_PLANES | EPI_F_PPS)) return false;
+  // f16x2 planes out: an f16x2 conv + BN + ReLU, planes within the 2 GiB a
+  // buffer resource addresses
+  if ((epi & EPI_F_H2OUT) &&
+      (!(epi & EPI_F_H2) || (epi & (EPI_F_RES | EPI_F_DUAL)) || !p.out3 || !p.h2o_in ||
+       (reinterpret_cast<uintptr_t>(p.out3) & 7) || (p.out_plane + (int64_t)p.M * p.ldo) * 2 >= kMaxBufBytes ||
+       p.out_plane * 2 >= (1ll << 31)))
+    return false;
   if (p.KH != 1 || p.KW != 1 || p.stride != 1 || p.pad != 0 || p.H != p.Ho || p.W != p.Wo)
     return false;
   const int K = p.Kloop;
   if (K % 32 || (K != 64 && K != 128 && K != 256) || p.kb_valid < K || p.ldb % 8) return false;
   if (p.a2 ? (p.Kloop1 % 32 || p.lda2 % 4 || p.Cin != p.Kloop1) : p.Cin != K) return false;
   if (p.lda % 4 || p.Ncol % 64 || p.ldo % 4 || (reinterpret_cast<uintptr_t>(p.out) & 15)) return false;
+  if (!(epi & EPI_F_H2OUT) && !p.out) return false;
   if (p.residual && (p.ldr % 4 || (reinterpret_cast<uintptr_t>(p.residual) & 15))) return false;
   if ((int64_t)p.M * p.lda * 4 >= kMaxBufBytes || (int64_t)p.M * p.ldo * 4 >= kMaxBufBytes ||
       (p.residual && (int64_t)p.M * p.ldr * 4 >= kMaxBufBytes))
@@ -233,14 +291,39 @@ bool ws_eligible(const GemmParams& p, int epi, int batch) {
 }
 
 template <int NCH, int BN2, int W>
+constexpr size_t ws_lds_bytes(bool h2) {
+  return (size_t)NCH * (h2 ? 2 : 3) * BN2 * 64 + 2 * BN2 * sizeof(float) +
+         (size_t)W * 16 * kWsLd * sizeof(float);
+}
+
+template <int NCH, int BN2, int W>
 static int launch_ws_cfg(const GemmParams& p, int epi, hipStream_t stream) {
   const int n_cb = (p.Ncol + BN2 - 1) / BN2;
   const int n_rt = (p.M + ws_rows<BN2, W>() - 1) / ws_rows<BN2, W>();
   const int rg = n_cb >= kWsCUs ? 1 : (kWsCUs / n_cb < n_rt ? kWsCUs / n_cb : n_rt);
-  const size_t lds = (size_t)NCH * 3 * BN2 * 64 + 2 * BN2 * sizeof(float) +
-                     (size_t)W * 16 * kWsLd * sizeof(float);
+  const size_t lds = ws_lds_bytes<NCH, BN2, W>((epi & EPI_F_H2) != 0);
+  if (lds > 160 * 1024) {
+    set_error("weight-stationary GEMM: column block does not fit in LDS");
+    return PPS_ERR_INVALID_ARG;
+  }
   const dim3 grid((unsigned)(n_cb * rg)), block(64 * W);
   constexpr int C = EPI_CONV, RL = EPI_F_RELU, RS = EPI_F_RES, DU = EPI_F_DUAL;
+  if (epi & EPI_F_H2) {
+    constexpr int H = EPI_F_H2;
+    switch (epi & ~H) {
+      case C | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL | H, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+      case C | RS | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RS | RL | H, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+      case C | RL | DU: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL | DU | H, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
+      case C | RL | EPI_F_H2OUT:
+        hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL | EPI_F_H2OUT | H, W>), grid, block, lds, stream, p, n_cb, n_rt, rg);
+        break;
+      default:
+        set_error("weight-stationary f16x2 GEMM: conv + BN + ReLU [+ residual | shortcut] only");
+        return PPS_ERR_INVALID_ARG;
+    }
+    PPS_CHECK_LAUNCH("gemm_ws_kernel");
+    return PPS_OK;
+  }
   switch (epi) {
     case C: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
     case C | RL: hipLaunchKernelGGL((gemm_ws_kernel<NCH, BN2, C | RL, W>), grid, block, lds, stream, p, n_cb, n_rt, rg); break;
@@ -258,8 +341,34 @@ static int launch_ws_cfg(const GemmParams& p, int epi, hipStream_t stream) {
 
 // The column block is the widest of 256 / 128 / 64 columns whose bf16x3
 // weights (BN2 * K * 6 bytes) fit in 96 KB and that divides into Ncol.
+// f16x2 (4 B per weight): the widest block whose weights and eight waves'
+// epilogue scratch fit (a K = 64 layer's 256 columns: every activation row
+// read once).  PPS_WS_H2_WIDE=1 (probes): also the blocks that fit only with
+// four waves (K = 128: 256 columns, K = 256: 128) -- measured slower on
+// res3 / res4 2c (54.7 vs 45.8 us, 49.2 vs 35.4 on the pipelined tile 45).
+static bool ws_h2_wide() {
+  static const bool on = [] {
+    const char* e = getenv("PPS_WS_H2_WIDE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 int launch_gemm_ws(const GemmParams& p, int epi, hipStream_t stream) {
   const int K = p.Kloop;
+  if (epi & EPI_F_H2) {
+    if (K == 64) {
+      if (p.Ncol % 256 == 0) return launch_ws_cfg<2, 256, 8>(p, epi, stream);
+      if (p.Ncol % 128 == 0) return launch_ws_cfg<2, 128, 8>(p, epi, stream);
+      return launch_ws_cfg<2, 64, 8>(p, epi, stream);
+    }
+    if (K == 128) {
+      if (ws_h2_wide() && p.Ncol % 256 == 0) return launch_ws_cfg<4, 256, 4>(p, epi, stream);
+      if (p.Ncol % 128 == 0) return launch_ws_cfg<4, 128, 8>(p, epi, stream);
+      return launch_ws_cfg<4, 64, 8>(p, epi, stream);
+    }
+    if (ws_h2_wide() && p.Ncol % 128 == 0) return launch_ws_cfg<8, 128, 4>(p, epi, stream);
+    return launch_ws_cfg<8, 64, 8>(p, epi, stream);
+  }
   if (K == 64) {
     if (p.Ncol % 256 == 0) return launch_ws_cfg<2, 256, 8>(p, epi, stream);
     if (p.Ncol % 128 == 0) return launch_ws_cfg<2, 128, 8>(p, epi, stream);

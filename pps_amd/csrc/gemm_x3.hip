@@ -299,13 +299,14 @@ int launch_gemm_x3(const GemmParams& p, int epi, int batch, hipStream_t stream) 
     return PPS_ERR_INVALID_ARG;
   }
   if (epi & EPI_F_H2) {
-    // f16x2 convs: the patch tiles (56..59) where they apply, else the
-    // 16x16x32 pipelined tiles (38..53, 55; tile 38 for the patch ids'
-    // fallback and for 0)
+    // f16x2 convs: the patch tiles (56..59) and the weight-stationary 1x1
+    // tile (54) where they apply, else the 16x16x32 pipelined tiles (38..53,
+    // 55; tile 38 for the patch / weight-stationary ids' fallback and for 0)
     if (p.tile >= GEMM_TILE_C16_FIRST && x3c_eligible(p, epi, batch, p.tile))
       return launch_gemm_x3c(p, epi, stream, p.tile);
-    const int t = (p.tile == 0 || (p.tile >= GEMM_TILE_C16_FIRST &&
-                                   p.tile != GEMM_TILE_P16_192x128W41))
+    if (p.tile == GEMM_TILE_WS && ws_eligible(p, epi, batch)) return launch_gemm_ws(p, epi, stream);
+    const int t = (p.tile == 0 || p.tile == GEMM_TILE_WS ||
+                   (p.tile >= GEMM_TILE_C16_FIRST && p.tile != GEMM_TILE_P16_192x128W41))
                       ? GEMM_TILE_P16_FIRST
                       : p.tile;
     if (t < GEMM_TILE_P16_FIRST || t == GEMM_TILE_WS || batch != 1 || p.splitk != 1 ||

@@ -677,6 +677,16 @@ bool seam_ok(const PpsModel& m, const Layer& L) {
   return !L.planes_in && !L.planes_out && !X.planes_out && L.splitk == 1 && X.splitk == 1;
 }
 
+// A layer the f16x2 weight-stationary kernel takes (gemm_ws.hip ws_eligible):
+// a 1x1 / stride-1 / unpadded conv, or the fused shortcut conv, whose K =
+// Cin (+ the shortcut's Cin) is 64, 128 or 256
+bool ws_h2_layer(const Layer& L) {
+  if (L.op != Op::Conv && L.op != Op::ConvDual) return false;
+  if (L.k != 1 || L.stride != 1 || L.pad != 0 || L.kpad != L.cin_eff) return false;
+  const int K = L.cin_eff + (L.op == Op::ConvDual ? L.shortcut_cin : 0);
+  return (K == 64 || K == 128 || K == 256) && L.cout % 64 == 0;
+}
+
 // A PPS_TILE_H2 tile this layer can run (structure only; planes and split-K
 // are checked at run time, since they may change after the tile is set)
 bool h2_tile_ok(const Layer& L, int tile) {
@@ -688,7 +698,9 @@ bool h2_tile_ok(const Layer& L, int tile) {
   if (L.op != Op::Conv && L.op != Op::ConvDual && L.op != Op::ConvPps) return false;
   if (!L.relu && L.op == Op::Conv) return false;  // the f16x2 epilogues end in a ReLU
   if (base == 0) return true;
-  if (base < GEMM_TILE_P16_FIRST || base == GEMM_TILE_WS || base >= GEMM_NUM_TILES) return false;
+  if (base == GEMM_TILE_WS)  // the weight-stationary 1x1 (f32 input, K = 64 / 128 / 256)
+    return ws_h2_layer(L) && !(tile & (PPS_TILE_H2P | PPS_TILE_H2E));
+  if (base < GEMM_TILE_P16_FIRST || base >= GEMM_NUM_TILES) return false;
   return L.op == Op::Conv || base < GEMM_TILE_C16_FIRST || base == GEMM_TILE_P16_192x128W41;
 }
 
@@ -1750,9 +1762,11 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         const bool pipelined_only = L.planes_in || L.planes_out;
         for (int tl = pipelined_only ? GEMM_TILE_P_FIRST : 1; tl < GEMM_NUM_TILES; ++tl)
           if (tl != GEMM_TILE_P16_192x128W41) c.push_back(tl);   // (f16x2 only)
+        // (PPS_AUTOTUNE_NO_WSH2=1, A/B runs: no f16x2 weight-stationary tile)
+        static const bool no_wsh2 = getenv_flag_on("PPS_AUTOTUNE_NO_WSH2");
         if (h2ok)
           for (int tl = GEMM_TILE_P16_FIRST; tl < GEMM_NUM_TILES; ++tl)
-            if (h2_tile_ok(L, tl | PPS_TILE_H2) &&
+            if (h2_tile_ok(L, tl | PPS_TILE_H2) && !(no_wsh2 && tl == GEMM_TILE_WS) &&
                 !(tl >= GEMM_TILE_C16_FIRST && tl != GEMM_TILE_P16_192x128W41 &&
                   (L.k != 3 || L.stride != 1)))
               c.push_back(tl | PPS_TILE_H2);

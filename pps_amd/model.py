@@ -601,6 +601,18 @@ class PPSModel(object):
                 (L['op'] != 'conv_dual' or L['shortcut_cin'] % 32 == 0) and
                 (L['op'] != 'conv' or L['relu']))
 
+    @staticmethod
+    def ws_h2_layer(L):
+        """The layers the f16x2 weight-stationary tile (54) takes (the C
+        plan's ws_h2_layer): a 1x1 / stride-1 / unpadded conv or fused
+        shortcut conv with K = 64, 128 or 256 and Cout % 64 == 0."""
+        if L['op'] not in ('conv', 'conv_dual'):
+            return False
+        if L['k'] != 1 or L['stride'] != 1 or L['pad'] != 0 or L['kpad'] != L['cin_eff']:
+            return False
+        K = L['cin_eff'] + (L.get('shortcut_cin', 0) if L['op'] == 'conv_dual' else 0)
+        return K in (64, 128, 256) and L['cout'] % 64 == 0
+
     def _run_h2(self, L, bufs, tile):
         """PPS_TILE_H2: the layer in f16x2 arithmetic (ops.conv2d_bn_act_h2 and
         siblings); the input's max comes from ops.amax (the C plan's producers
@@ -1017,13 +1029,17 @@ class PPSModel(object):
                              % name)
         if tile & ops.TILE_H2:
             base = tile & 0xff
-            if not self.h2_capable(L) or not (
-                    base == 0 or (ops.TILE_P16_FIRST <= base <= ops.num_tiles() and
-                                  base != ops.TILE_WS and
-                                  (L['op'] == 'conv' or base < ops.TILE_C16_FIRST or
-                                   base == ops.TILE_H2_WIDE))):
+            if base == ops.TILE_WS:   # the weight-stationary 1x1, f32 input (h2_tile_ok)
+                ok = (self.ws_h2_layer(L) and
+                      not tile & (ops.TILE_H2P | ops.TILE_H2E))
+            else:
+                ok = base == 0 or (ops.TILE_P16_FIRST <= base <= ops.num_tiles() and
+                                   (L['op'] == 'conv' or base < ops.TILE_C16_FIRST or
+                                    base == ops.TILE_H2_WIDE))
+            if not self.h2_capable(L) or not ok:
                 raise ValueError("PPS_TILE_H2: '%s' has no f16x2 arithmetic or the base tile "
-                                 "%d is not 0, 38..53, 55, 60 or (convs) 56..59" % (name, base))
+                                 "%d is not 0, 38..55, 60, (convs) 56..59 or 54 on a "
+                                 "weight-stationary 1x1" % (name, base))
 
     def set_tiles(self, tiles):
         """Apply a tiles() mapping (e.g. a saved autotune result).  Seam and

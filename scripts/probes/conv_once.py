@@ -16,6 +16,8 @@ SHAPES = {   # H, W, Cin, Cout, k
     'res5c': (24, 8, 512, 2048, 1), 'res4b': (24, 8, 256, 256, 3),
     'res4a': (24, 8, 1024, 256, 1), 'res4c': (24, 8, 256, 1024, 1),
     'res3b': (48, 16, 128, 128, 3), 'res2b': (96, 32, 64, 64, 3),
+    'res3c': (48, 16, 128, 512, 1), 'res2c': (96, 32, 64, 256, 1),
+    'res2a': (96, 32, 256, 64, 1), 'res3a': (48, 16, 512, 128, 1),
 }
 
 

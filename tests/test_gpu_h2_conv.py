@@ -33,8 +33,9 @@ def _rel_err(got, ref):
 
 
 def _h2_tiles():
+    # (54: the weight-stationary 1x1 kernel where it applies, else tile 38)
     from pps_amd import ops
-    return [0] + [t for t in range(ops.TILE_P16_FIRST, ops.num_tiles() + 1) if t != 54]
+    return [0] + list(range(ops.TILE_P16_FIRST, ops.num_tiles() + 1))
 
 
 _SHAPES = [
@@ -44,6 +45,13 @@ _SHAPES = [
     (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1 (STRIDE_1X1 branch2a)
     (2, 96, 32, 64, 64, 3, 1, 1),      # res2 branch2b
     (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+    # the f16x2 weight-stationary 1x1 shapes (tile 54): res2 2c / 2a, res3 2c,
+    # res4 2c, and a ragged row count
+    (1, 96, 32, 64, 256, 1, 1, 0),
+    (1, 96, 32, 256, 64, 1, 1, 0),
+    (2, 48, 16, 128, 512, 1, 1, 0),
+    (2, 24, 8, 256, 1024, 1, 1, 0),
+    (3, 7, 5, 128, 192, 1, 1, 0),
 ]
 # every shape with and without the residual at unit magnitude, plus the
 # magnitude sweep (inputs x 1e-20 and x 1e20) on the res4 3x3 shape
@@ -122,7 +130,7 @@ def test_conv_dual_h2(N, H, W, C1, C2, Cout, s2):
                            True, y, tile=ops.TILE_P16_FIRST)
     e_x3 = _rel_err(y.cpu().numpy(), ref)
     wq, wrs = ops.split_weights_h2(_cuda(w))
-    tiles = [0] + [t for t in range(ops.TILE_P16_FIRST, 56) if t != 54] + [60]
+    tiles = [0] + list(range(ops.TILE_P16_FIRST, 56)) + [60]
     outs = []
     for tile in tiles:
         y = torch.full(ref.shape, float('nan'), device='cuda')
@@ -188,6 +196,7 @@ def test_conv_h2_enforces():
     (2, 24, 8, 1024, 256, 1, 1, 0),    # res4 branch2a
     (2, 48, 16, 256, 128, 1, 2, 0),    # strided 1x1
     (3, 7, 5, 64, 40, 3, 1, 1),        # ragged M and N
+    (2, 48, 16, 128, 512, 1, 1, 0),    # a weight-stationary shape (tile 54 -> 38 on planes)
 ])
 @pytest.mark.parametrize('residual', [False, True])
 def test_conv_h2_activation_planes_same_bits(N, H, W, Cin, Cout, k, s, p, residual):
