@@ -212,6 +212,9 @@ __device__ inline void h2_dist_epilogue(const GemmParams& p, f32x4 (&acc)[BM / W
 #ifndef H2_ABL
 #define H2_ABL 0  // probes: 1 = no DMA after the prologue, 2 = no MFMAs (timing ablations)
 #endif
+#ifndef H2_SPREAD
+#define H2_SPREAD 1  // DMA pieces spread over the chunk's MFMA blocks (NS >= 3 tiles); 0: a burst after the barrier
+#endif
 
 template <int BM, int BN, int WM, int WN, int NS>
 __global__ void __launch_bounds__(64 * WM * WN)
@@ -279,17 +282,19 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
     // out-of-range blocks: an offset >= 2^31 > num_records reads zeros
     src[i] = blk < nblk ? (int)(pbase + (int64_t)blk * nkc * 1024 + loff) : (int)0x80000000;
   }
+  // piece i of this wave for chunk kc into its stage
+  auto issue_piece = [&](int kc, int stage, int i) {
+    const unsigned char* st = lds + stage * STAGE;
+    const int q = wave * PPW + i;
+    if (EVEN || q < NPIECE)
+      glds16(q < 2 * ABLK ? ra : rb, st + q * 1024, src[i] + kc * 1024);
+    else
+      glds16(rb, lds + NS * STAGE, (int)0x80000000);
+  };
   auto issue = [&](int kc, int stage) {
     if (H2_ABL == 1 && kc >= NS) return;
-    const unsigned char* st = lds + stage * STAGE;
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int q = wave * PPW + i;
-      if (EVEN || q < NPIECE)
-        glds16(q < 2 * ABLK ? ra : rb, st + q * 1024, src[i] + kc * 1024);
-      else
-        glds16(rb, lds + NS * STAGE, (int)0x80000000);
-    }
+    for (int i = 0; i < PPW; ++i) issue_piece(kc, stage, i);
   };
 
   // ---- fragments: lane l reads row l & 15 of a block, logical 16-byte slot
@@ -336,10 +341,22 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   // DMA, the request two chunks ahead into this stage, and the next chunk's B
   // fragments and first A block beside the last block's MFMAs.
   int scur = 0;  // stage of chunk kc
+  // SPREAD (three or more stages): chunk kc - 1 + NS goes into the stage the
+  // previous chunk's barrier freed, its pieces spread over this chunk's
+  // first TM - 1 blocks (an MFMA block between two DMA pieces) instead of a
+  // burst right after the barrier, where both waves of a SIMD stall on
+  // their DMA issue at once; all pieces are out before the chunk's wait
+  constexpr bool SPREAD = H2_SPREAD && NS >= 3 && H2_ABL == 0;
   auto chunk = [&](int kc, f16x8 (&fbc)[TN][2], f16x8 (&fbn)[TN][2]) {
     const unsigned char* st = lds + scur * STAGE;
+    const int sprev = scur == 0 ? NS - 1 : scur - 1;
 #pragma unroll
     for (int i = 0; i < TM - 1; ++i) {
+      if (SPREAD && kc >= 1) {
+#pragma unroll
+        for (int j = i * PPW / (TM - 1); j < (i + 1) * PPW / (TM - 1); ++j)
+          issue_piece(kc - 1 + NS, sprev, j);
+      }
       if (i & 1) {
         readA(st, i + 1, fa0);
 #pragma unroll
@@ -357,7 +374,7 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
       wait_vmcnt<PPW * (NS - 2)>();  // chunk kc + 1 landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      issue(kc + NS, scur);
+      if (!SPREAD) issue(kc + NS, scur);
       scur = scur + 1 == NS ? 0 : scur + 1;
       const unsigned char* sn = lds + scur * STAGE;
       readB(sn, fbn);

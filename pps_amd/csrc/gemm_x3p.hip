@@ -907,8 +907,13 @@ int launch_gemm_x3p(const GemmParams& p, int epi, int batch, hipStream_t stream,
 #endif
   if (variant == GEMM_TILE_P16_128x128W42S3 - GEMM_TILE_P_FIRST)
     return launch_tile_p<128, 128, 4, 2, X3P_DEEP ? 4 : 3, 3, 16>(p, epi, batch, stream);
-  if (variant == GEMM_TILE_P16_192x128W42S3 - GEMM_TILE_P_FIRST)
+#ifndef X3P_DEEP52
+#define X3P_DEEP52 0  // probes: 1 = four LDS stages (160 KB) on tile 52
+#endif
+  if (variant == GEMM_TILE_P16_192x128W42S3 - GEMM_TILE_P_FIRST) {
+    if (X3P_DEEP52 && (epi & EPI_F_H2)) return launch_tile_h2<192, 128, 4, 2, 4>(p, epi, batch, stream);
     return launch_tile_p<192, 128, 4, 2, 3, 2, 16>(p, epi, batch, stream);
+  }
   // 96x128 as 2 x 4 waves with three stages (uneven pieces, per-wave waits)
   if (variant == GEMM_TILE_P16_96x128W24S3 - GEMM_TILE_P_FIRST)
     return launch_tile_p<96, 128, 2, 4, X3P_DEEP ? 4 : 3, 3, 16>(p, epi, batch, stream);

@@ -27,7 +27,7 @@ step pmc
 rm -rf $OUT/pmcb
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmcb/p1 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --no-duke --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc1.log 2>&1 || { tail -5 $OUT/pmc1.log; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmcb/p2 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --no-duke --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc2.log 2>&1 || { tail -5 $OUT/pmc2.log; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --no-duke --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT -d $OUT/pmcb/p3 -o run --output-format csv -- python3 bench.py --tiles-file $TILES --no-cpu-baseline --no-e2e --no-duke --steps 2 --warmup 1 --dist-reps 1 > $OUT/pmc3.log 2>&1 || { tail -5 $OUT/pmc3.log; exit 1; }
 # MFMA launches per forward: 50 layers, one fewer per bottleneck seam pair
 NCONV=$(python -c "import json; t = json.load(open('$TILES')); print(50 - sum(1 for k, v in t.items() if not k.startswith('__') and isinstance(v, int) and v & 0x400))")
 CLK=$OUT/bench_tuned.log; [ -f $CLK ] || CLK=$OUT/prof.log

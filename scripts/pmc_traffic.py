@@ -164,9 +164,11 @@ def main():
         if len(rows) == nconv:
             dur = sum(r[2] for r in rows)
             busy = sum(r[1].get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) for r in rows)
+            lds_cf = sum(r[1].get('SQ_LDS_BANK_CONFLICT', 0.0) for r in rows)
             out['conv_mfma'] = dict(
                 math=out.get('conv', {}).get('math', math), model_math=math, batch=batch,
                 launches=nconv, duration_us=round(dur / 1e3, 1),
+                lds_bank_conflict_cycles_per_forward=lds_cf,
                 source='rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES (third pass)',
                 **busy_fields(busy, dur, mhz))
         # the same for the last distance-matrix launch (the distmat roofline's kernel)
