@@ -809,7 +809,7 @@ def table_digest(nm):
     planes = set(nm.planes())
     rows, groups = [], {}
     for L in layers:
-        if L['op'] not in ('conv', 'conv_dual', 'heads', 'conv_pps'):
+        if L['op'] not in ('conv', 'conv_dual', 'heads', 'conv_pps', 'stem_pool'):
             continue
         t = L['tile']
         rows.append('%s:%d:%d:%d' % (L['name'], t, int(L['name'] in planes), L['splitk']))
@@ -818,6 +818,10 @@ def table_digest(nm):
              'x16' if base < ops.TILE_C16_FIRST else 'patch')
         if t & ops.TILE_H2:   # f16x2 arithmetic: its own rounding groups
             g = 'h2_' + ('x16' if base < ops.TILE_C16_FIRST else 'patch')
+        if L['op'] == 'stem_pool':
+            g = 'stem_h2' if t & ops.TILE_H2 else 'stem'
+            if t & ops.TILE_H2:
+                rows[-1] += ':h2'   # (the stem's tile alone, 0 / 0x800, would collide with nothing)
         groups[g] = groups.get(g, 0) + 1
     return dict(sha1=hashlib.sha1('\n'.join(rows).encode()).hexdigest()[:16],
                 layers_per_rounding_group=groups, plane_edges=len(planes),

@@ -696,6 +696,15 @@ int pps_stem_variant(int v);
 int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w3,
                           const float* scale, const float* shift, float* y, int Hp, int Wp,
                           void* stream);
+/* The same stem in the f16x2 arithmetic (round 6): the input split into two
+ * f16 planes on the power-of-two scale of its max (amax_x: an activation-max
+ * slot, PPS_AMAX_SLOT_FLOATS floats, as pps_amax fills it), the weights as
+ * pps_stem_split_h2 leaves them (w2 [2][64][pps_stem_k()] f16, w_inv [64] the
+ * per-channel 2^-s), three f16 MFMA terms per product; f32 accumulation. */
+int pps_stem_split_h2(const float* w, uint16_t* w2, float* w_inv, void* stream);
+int pps_stem_conv_pool_h2(const float* x, int N, int H, int W, const uint16_t* w2,
+                          const float* w_inv, const float* amax_x, const float* scale,
+                          const float* shift, float* y, int Hp, int Wp, void* stream);
 
 /* The last res5 conv with the part pooling fused into its epilogue
  * (ResNet.py:276-333 res5_2 branch2c + Sum + Relu feeding bpm_heads.py:18-55

@@ -145,6 +145,9 @@ SIGNATURES = {
                           ctypes.c_double, c_int, c_ptr, c_i64, c_ptr, c_ptr],
     'pps_stem_conv_pool_x3': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int,
                               c_int, c_ptr],
+    'pps_stem_split_h2': [c_ptr, c_ptr, c_ptr, c_ptr],
+    'pps_stem_conv_pool_h2': [c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                              c_ptr, c_int, c_int, c_ptr],
     'pps_maxpool2d': [c_ptr, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ptr,
                       c_int, c_int, c_ptr],
     'pps_part_power_set': [c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_int, c_ptr,

@@ -24,8 +24,6 @@ int part_power_set(const float*, int, int, int, int, const int32_t*, int, int, f
                    hipStream_t);
 int l2_normalize(const float*, int64_t, int, float*, hipStream_t);
 int group_mean(const float*, int, const int32_t*, const int32_t*, int, float*, hipStream_t);
-int preprocess_bgr(const uint8_t*, int, int, int, const int64_t*, const int32_t*,
-                   const int32_t*, const float*, int, int, float*, hipStream_t);
 int collect_positives(const float*, int64_t, int64_t, int64_t, const int32_t*,
                       const int32_t*, const int32_t*, const int32_t*, int64_t, int, float*,
                       int32_t*, int32_t*, hipStream_t);

@@ -554,8 +554,9 @@ __global__ void __launch_bounds__(256)
 preprocess_sep_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
                       const int64_t* __restrict__ offsets, const int32_t* __restrict__ heights,
                       const int32_t* __restrict__ widths, Means mean, int Ho, int Wo, int kcap,
-                      float* __restrict__ y) {
+                      float* __restrict__ y, float* __restrict__ amax) {
   extern __shared__ float hrow[];  // [kcap][Wo][3]
+  float amx = 0.f;  // max |y| of this thread's outputs (amax: the f16x2 stem's input scale)
   const int nb = (Ho + kPrepRows - 1) / kPrepRows;
   const int n = blockIdx.x / nb;
   const int oy0 = (blockIdx.x - n * nb) * kPrepRows;
@@ -597,7 +598,9 @@ preprocess_sep_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
       }
       *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oy) * Wo + ox) * 4) =
           f32x4{acc[0], acc[1], acc[2], 0.f};
+      amx = fmaxf(amx, fmaxf(fabsf(acc[0]), fmaxf(fabsf(acc[1]), fabsf(acc[2]))));
     }
+    if (amax) amax_commit(amax, amx);
     return;
   }
   // pass 1: horizontal filter of source rows ys..ye
@@ -637,12 +640,14 @@ preprocess_sep_kernel(const uint8_t* __restrict__ blob, int N, int Hi0, int Wi0,
     }
     *reinterpret_cast<f32x4*>(y + (((int64_t)n * Ho + oy) * Wo + ox) * 4) =
         f32x4{acc[0], acc[1], acc[2], 0.f};
+    amx = fmaxf(amx, fmaxf(fabsf(acc[0]), fmaxf(fabsf(acc[1]), fabsf(acc[2]))));
   }
+  if (amax) amax_commit(amax, amx);
 }
 
 int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* offsets,
                    const int32_t* heights, const int32_t* widths, const float* means,
-                   int Ho, int Wo, float* y, hipStream_t st) {
+                   int Ho, int Wo, float* y, hipStream_t st, float* amax) {
   Means m;
   for (int c = 0; c < 3; ++c) m.m[c] = means[c];
   if ((int64_t)N * Ho == 0 || Wo == 0) return PPS_OK;
@@ -657,9 +662,15 @@ int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* off
     const int64_t nblk = (int64_t)N * ((Ho + kPrepRows - 1) / kPrepRows);
     hipLaunchKernelGGL(preprocess_sep_kernel, dim3((unsigned)nblk), dim3(256),
                        (size_t)kcap * Wo * 12, st, img, N, Hi, Wi, offsets, heights, widths, m,
-                       Ho, Wo, kcap, y);
+                       Ho, Wo, kcap, y, amax);
     PPS_CHECK_LAUNCH("preprocess_sep_kernel");
     return PPS_OK;
+  }
+  if (amax) {  // (wide outputs: the direct kernel, then a max pass)
+    hipLaunchKernelGGL(preprocess_bgr_kernel, dim3((unsigned)(N * Ho), (Wo + 127) / 128),
+                       dim3(128), 0, st, img, N, Hi, Wi, offsets, heights, widths, m, Ho, Wo, y);
+    PPS_CHECK_LAUNCH("preprocess_bgr_kernel");
+    return amax_of(y, (int64_t)N * Ho * Wo * 4, amax, st);
   }
   hipLaunchKernelGGL(preprocess_bgr_kernel, dim3((unsigned)(N * Ho), (Wo + 127) / 128),
                      dim3(128), 0, st, img, N, Hi, Wi, offsets, heights, widths, m, Ho, Wo, y);

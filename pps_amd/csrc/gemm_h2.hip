@@ -33,6 +33,8 @@
 // grouped query panels for q x g, upper-triangle super-blocks + mirror for the
 // self-distance.  The epilogue parks the accumulators in LDS (column passes
 // when the tile's f32 image exceeds it) and writes whole row segments.
+#include <type_traits>
+
 #include "gemm_x3p_common.hpp"
 
 namespace pps {
@@ -212,6 +214,16 @@ __device__ inline void h2_dist_epilogue(const GemmParams& p, f32x4 (&acc)[BM / W
 #ifndef H2_ABL
 #define H2_ABL 0  // probes: 1 = no DMA after the prologue, 2 = no MFMAs (timing ablations)
 #endif
+// A blocks multiplied after the chunk barrier by waves 0 .. NW/2 - 1 (O) and
+// NW/2 .. NW - 1 (Y); -1: 2 / 4 on the three-stage tiles (Market 3368 x 15913:
+// tile 6 1061 / 1067 -> 1049 / 1058 us, tiles 3 / 4 1114-1130 -> 1101-1105;
+// the two-stage 256-row tiles would spill), 1 / 1 on the others
+#ifndef H2_STAG_O
+#define H2_STAG_O -1
+#endif
+#ifndef H2_STAG_Y
+#define H2_STAG_Y -1
+#endif
 #ifndef H2_SPREAD
 #define H2_SPREAD 1  // DMA pieces spread over the chunk's MFMA blocks (NS >= 3 tiles); 0: a burst after the barrier
 #endif
@@ -333,63 +345,141 @@ gemm_h2_kernel(GemmParams p, int tiles_m, int tiles_n) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  f16x8 fb0[TN][2], fb1[TN][2], fa0[2], fa1[2];
-  readB(lds, fb0);
-  readA(lds, 0, fa0);
-  // One chunk: block i's MFMAs beside block i + 1's A reads; before the last
-  // block, the barrier that retires this stage's reads and the next chunk's
-  // DMA, the request two chunks ahead into this stage, and the next chunk's B
-  // fragments and first A block beside the last block's MFMAs.
-  int scur = 0;  // stage of chunk kc
-  // SPREAD (three or more stages): chunk kc - 1 + NS goes into the stage the
-  // previous chunk's barrier freed, its pieces spread over this chunk's
-  // first TM - 1 blocks (an MFMA block between two DMA pieces) instead of a
-  // burst right after the barrier, where both waves of a SIMD stall on
-  // their DMA issue at once; all pieces are out before the chunk's wait
   constexpr bool SPREAD = H2_SPREAD && NS >= 3 && H2_ABL == 0;
-  auto chunk = [&](int kc, f16x8 (&fbc)[TN][2], f16x8 (&fbn)[TN][2]) {
-    const unsigned char* st = lds + scur * STAGE;
-    const int sprev = scur == 0 ? NS - 1 : scur - 1;
+  constexpr int SO = H2_STAG_O >= 0 ? H2_STAG_O : (NS >= 3 ? 2 : 1);
+  constexpr int SY = H2_STAG_Y >= 0 ? H2_STAG_Y : (NS >= 3 ? 4 : 1);
+  constexpr int DO = SO < TM ? SO : TM - 1;
+  constexpr int DY = SY < TM ? SY : TM - 1;
+  if constexpr (DO == 1 && DY == 1) {
+    f16x8 fb0[TN][2], fb1[TN][2], fa0[2], fa1[2];
+    readB(lds, fb0);
+    readA(lds, 0, fa0);
+    // One chunk: block i's MFMAs beside block i + 1's A reads; before the last
+    // block, the barrier that retires this stage's reads and the next chunk's
+    // DMA, the request two chunks ahead into this stage, and the next chunk's B
+    // fragments and first A block beside the last block's MFMAs.
+    int scur = 0;  // stage of chunk kc
+    // SPREAD (three or more stages): chunk kc - 1 + NS goes into the stage the
+    // previous chunk's barrier freed, its pieces spread over this chunk's
+    // first TM - 1 blocks (an MFMA block between two DMA pieces) instead of a
+    // burst right after the barrier, where both waves of a SIMD stall on
+    // their DMA issue at once; all pieces are out before the chunk's wait
+    auto chunk = [&](int kc, f16x8 (&fbc)[TN][2], f16x8 (&fbn)[TN][2]) {
+      const unsigned char* st = lds + scur * STAGE;
+      const int sprev = scur == 0 ? NS - 1 : scur - 1;
 #pragma unroll
-    for (int i = 0; i < TM - 1; ++i) {
-      if (SPREAD && kc >= 1) {
+      for (int i = 0; i < TM - 1; ++i) {
+        if (SPREAD && kc >= 1) {
 #pragma unroll
-        for (int j = i * PPW / (TM - 1); j < (i + 1) * PPW / (TM - 1); ++j)
-          issue_piece(kc - 1 + NS, sprev, j);
+          for (int j = i * PPW / (TM - 1); j < (i + 1) * PPW / (TM - 1); ++j)
+            issue_piece(kc - 1 + NS, sprev, j);
+        }
+        if (i & 1) {
+          readA(st, i + 1, fa0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = mfma_h2t(fa1[0], fa1[1], fbc[j][0], fbc[j][1], acc[i][j]);
+        } else {
+          readA(st, i + 1, fa1);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = mfma_h2t(fa0[0], fa0[1], fbc[j][0], fbc[j][1], acc[i][j]);
+        }
       }
-      if (i & 1) {
-        readA(st, i + 1, fa0);
+      if (kc + 1 < nkc) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_vmcnt<PPW * (NS - 2)>();  // chunk kc + 1 landed
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!SPREAD) issue(kc + NS, scur);
+        scur = scur + 1 == NS ? 0 : scur + 1;
+        const unsigned char* sn = lds + scur * STAGE;
+        readB(sn, fbn);
+        readA(sn, 0, fa0);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[TM - 1][j] = mfma_h2t(fa1[0], fa1[1], fbc[j][0], fbc[j][1], acc[TM - 1][j]);
+    };
+    int kc = 0;
+    for (; kc + 1 < nkc; kc += 2) {
+      chunk(kc, fb0, fb1);
+      chunk(kc + 1, fb1, fb0);
+    }
+    if (kc < nkc) chunk(kc, fb0, fb1);
+  } else {
+    // One chunk, D blocks deferred: blocks 0 .. TM-1-D multiply before the
+    // chunk's barrier (each beside the A read of a later block), every A block
+    // of the chunk is in registers by the barrier; after it (the barrier that
+    // retires this stage's reads and the next chunk's DMA), the next chunk's B
+    // fragments and first A block are read beside the last D blocks' MFMAs.
+    // The two halves of the workgroup run different D (H2_STAG_O for waves
+    // 0 .. NW/2-1, H2_STAG_Y for the rest): the two waves of a SIMD then carry
+    // different amounts of MFMA work across the barrier, so the one that
+    // reaches it first leaves the matrix pipe to its partner instead of both
+    // idling there together (MI355X_MICROARCH "try a stagger").
+    // SPREAD (three or more stages): chunk kc - 1 + NS goes into the stage the
+    // previous chunk's barrier freed, its pieces spread over this chunk's
+    // pre-barrier blocks (an MFMA block between two DMA pieces) instead of a
+    // burst right after the barrier, where both waves of a SIMD stall on
+    // their DMA issue at once; all pieces are out before the chunk's wait
+    f16x8 fb0[TN][2], fb1[TN][2];
+    f16x8 fa[TM + 1][2];  // the chunk's A blocks; [TM]: the next chunk's block 0
+    readB(lds, fb0);
+    readA(lds, 0, fa[0]);
+    int scur = 0;  // stage of chunk kc
+    auto chunk = [&](auto dtag, int kc, f16x8 (&fbc)[TN][2], f16x8 (&fbn)[TN][2]) {
+      constexpr int D = decltype(dtag)::value;
+      constexpr int PRE = TM - D;  // blocks multiplied before the barrier
+      constexpr int SPB = PRE > 0 ? PRE : 1;  // blocks the DMA pieces spread over
+      const unsigned char* st = lds + scur * STAGE;
+      const int sprev = scur == 0 ? NS - 1 : scur - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (SPREAD && kc >= 1 && i < SPB) {
+#pragma unroll
+          for (int j = i * PPW / SPB; j < (i + 1) * PPW / SPB; ++j)
+            issue_piece(kc - 1 + NS, sprev, j);
+        }
+        if (i + 1 < TM) readA(st, i + 1, fa[i + 1]);
+        if (i < PRE) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = mfma_h2t(fa[i][0], fa[i][1], fbc[j][0], fbc[j][1], acc[i][j]);
+        }
+      }
+      if (kc + 1 < nkc) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_vmcnt<PPW * (NS - 2)>();  // chunk kc + 1 landed
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!SPREAD) issue(kc + NS, scur);
+        scur = scur + 1 == NS ? 0 : scur + 1;
+        const unsigned char* sn = lds + scur * STAGE;
+        readB(sn, fbn);
+        readA(sn, 0, fa[TM]);
+      }
+#pragma unroll
+      for (int i = PRE; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = mfma_h2t(fa1[0], fa1[1], fbc[j][0], fbc[j][1], acc[i][j]);
-      } else {
-        readA(st, i + 1, fa1);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = mfma_h2t(fa0[0], fa0[1], fbc[j][0], fbc[j][1], acc[i][j]);
+          acc[i][j] = mfma_h2t(fa[i][0], fa[i][1], fbc[j][0], fbc[j][1], acc[i][j]);
+      fa[0][0] = fa[TM][0];
+      fa[0][1] = fa[TM][1];
+    };
+    auto loop = [&](auto dtag) {
+      int kc = 0;
+      for (; kc + 1 < nkc; kc += 2) {
+        chunk(dtag, kc, fb0, fb1);
+        chunk(dtag, kc + 1, fb1, fb0);
       }
-    }
-    if (kc + 1 < nkc) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_vmcnt<PPW * (NS - 2)>();  // chunk kc + 1 landed
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (!SPREAD) issue(kc + NS, scur);
-      scur = scur + 1 == NS ? 0 : scur + 1;
-      const unsigned char* sn = lds + scur * STAGE;
-      readB(sn, fbn);
-      readA(sn, 0, fa0);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      acc[TM - 1][j] = mfma_h2t(fa1[0], fa1[1], fbc[j][0], fbc[j][1], acc[TM - 1][j]);
-  };
-  int kc = 0;
-  for (; kc + 1 < nkc; kc += 2) {
-    chunk(kc, fb0, fb1);
-    chunk(kc + 1, fb1, fb0);
+      if (kc < nkc) chunk(dtag, kc, fb0, fb1);
+    };
+    if (DO == DY || wave < NW / 2)
+      loop(std::integral_constant<int, DO>{});
+    else
+      loop(std::integral_constant<int, DY>{});
   }
-  if (kc < nkc) chunk(kc, fb0, fb1);
   wait_vmcnt<0>();
 
   h2_dist_epilogue<BM, BN, WM, WN, HB>(p, acc, lds, m0, n0, wm, wn, lane);

@@ -43,6 +43,11 @@ namespace pps {
 #ifndef X3P_ABL
 #define X3P_ABL 0  // probes: 1 = no DMA after the prologue, 2 = no MFMAs (timing ablations)
 #endif
+#ifndef X3P_STAG
+#define X3P_STAG -1  // 1 / 2: waves NW/2.. / ..NW/2-1 of 8-wave tiles multiply a chunk's two
+                     // column halves before its barrier (the others: one before, one after);
+                     // -1: 1 on tile 52, 0 elsewhere; 0: never (probes)
+#endif
 #ifndef X3P_CLK
 #define X3P_CLK 0  // diagnostic builds: per-workgroup shader clocks / 100 MHz ticks
 #endif
@@ -544,22 +549,50 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
       readB16(lds + scur * STAGE, 0, fb0);
       mfmas16(fc, fb1, 1);
     };
+    // the same chunk with both column halves multiplied before the barrier:
+    // with X3P_STAG one half of an 8-wave workgroup runs it, so the two waves
+    // of a SIMD carry different amounts of MFMA work across the barrier and
+    // the one that reaches it first leaves the matrix pipe to its partner
+    // (MI355X_MICROARCH "try a stagger")
+    auto step_pre = [&](bf16x8 (&fc)[TM][3], bf16x8 (&fn)[TM][3]) {
+      const unsigned char* st = lds + scur * STAGE;
+      scur = scur + 1 == NS ? 0 : scur + 1;
+      readB16(st, 1, fb1);
+      mfmas16(fc, fb0, 0);
+      mfmas16(fc, fb1, 1);
+      chunk_barrier();
+      issue();
+      readA16(lds + scur * STAGE, fn);
+      readB16(lds + scur * STAGE, 0, fb0);
+    };
     auto tail = [&](bf16x8 (&fc)[TM][3]) {
       readB16(lds + scur * STAGE, 1, fb1);
       mfmas16(fc, fb0, 0);
       mfmas16(fc, fb1, 1);
     };
-    int kc = 0;
-    for (; kc + 2 < nchunks; kc += 2) {
-      step(fa0, fa1);
-      step(fa1, fa0);
-    }
-    if (kc + 1 < nchunks) {
-      step(fa0, fa1);
-      tail(fa1);
-    } else {
-      tail(fa0);
-    }
+    auto run = [&](auto&& stp) {
+      int kc = 0;
+      for (; kc + 2 < nchunks; kc += 2) {
+        stp(fa0, fa1);
+        stp(fa1, fa0);
+      }
+      if (kc + 1 < nchunks) {
+        stp(fa0, fa1);
+        tail(fa1);
+      } else {
+        tail(fa0);
+      }
+    };
+    // tile 52 (192 x 128, 4 x 2 waves, three stages): res5 3x3 166.8 / 171.7
+    // -> 155.1 / 160.0 us with the younger half staggered; the 128 x 128 8-wave
+    // tile (two workgroups per CU, <= 128 VGPRs) loses 50 % with it, tiles 47
+    // and 53 are level (scripts/gpu_r6_stagger.sh)
+    constexpr int STAG = X3P_STAG >= 0 ? X3P_STAG
+                                       : (BM == 192 && BN == 128 && WM == 4 && WN == 2 && NS == 3);
+    if (STAG != 0 && NW == 8 && (STAG == 1 ? wave >= NW / 2 : wave < NW / 2))
+      run(step_pre);
+    else
+      run(step);
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup retires
 #if X3P_CLK

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <set>
@@ -522,7 +523,13 @@ void compile(PpsModel& m, const std::map<std::string, Blob>& blobs, hipStream_t 
           count_readers(m, L.output, false) == 1) {
         Layer F = L;
         F.op = Op::StemPool; F.output = P.output; F.conv_output = L.output;
-        F.w = split3(upload(pack_stem(blobs.at(L.name + "_w")), st), 64LL * pps_stem_k(), 1, st);
+        const Buf wf = upload(pack_stem(blobs.at(L.name + "_w")), st);
+        F.w = split3(wf, 64LL * pps_stem_k(), 1, st);
+        // and the f16x2 split (PPS_TILE_H2 on the stem): [2][64][K] f16 + 2^-s per channel
+        F.w2 = std::make_shared<DevBuf>((size_t)2 * 64 * pps_stem_k() * sizeof(uint16_t));
+        F.wrs = std::make_shared<DevBuf>((size_t)64 * sizeof(float));
+        rc_check(stem_split_h2(wf->as<float>(), F.w2->as<uint16_t>(), F.wrs->as<float>(), st));
+        hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
         m.layers[i] = F;
         m.layers.erase(m.layers.begin() + i + 1);
         done = true;
@@ -692,6 +699,8 @@ bool ws_h2_layer(const Layer& L) {
 bool h2_tile_ok(const Layer& L, int tile) {
   const int base = tile & 0xff;
   if (!L.w2 || (tile & PPS_TILE_SEAM)) return false;
+  // the fused stem: its own kernel, no tile id, no planes at either end
+  if (L.op == Op::StemPool) return tile == PPS_TILE_H2;
   // activation planes: plain convs and conv_pps (the fused shortcut reads f32)
   if ((tile & (PPS_TILE_H2P | PPS_TILE_H2E)) && L.op == Op::ConvDual) return false;
   if ((tile & PPS_TILE_H2P) && (tile & PPS_TILE_H2E)) return false;
@@ -1022,6 +1031,15 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
       const Shape ys = w.shapes.at(L.output);
       // pps_stem_conv_pool_x3 (shapes checked when the stem was fused), max |y| reported
       const int Hin = (int)a.s.d[1];
+      if (h2) {  // pps_stem_conv_pool_h2: the input's max from its slot
+        PPS_MCHECK(slotp(L.input), "layer '" + L.name + "': the f16x2 stem needs its input's "
+                                   "activation-max slot");
+        rc_check(stem_conv_pool_h2(a.f, (int)a.s.d[0], Hin, L.w2->as<uint16_t>(),
+                                   L.wrs->as<float>(), sc, sh, fbuf(L.output),
+                                   (Hin + 2 * 3 - 7) / 2 + 1, (int)ys.d[1], st, slotp(L.output),
+                                   slotp(L.input)));
+        return;
+      }
       rc_check(stem_conv_pool_x3(a.f, (int)a.s.d[0], Hin, w3, sc, sh, fbuf(L.output),
                                  (Hin + 2 * 3 - 7) / 2 + 1, (int)ys.d[1], st, slotp(L.output)));
       return;
@@ -1098,8 +1116,12 @@ void run_layer(const PpsModel& m, const Layer& L, Workspace& w, const float* x, 
   }
 }
 
+// pre (whole forwards only): writes x before the layers run -- the
+// preprocessing of pps_forward_bgr -- and reports max|x| into the slot it is
+// given (null when no f16x2 layer reads the input)
 void forward_range(const PpsModel& m, const float* x, int N, float* feat, int first, int last,
-                   hipStream_t st, bool keep_amax = false) {
+                   hipStream_t st, bool keep_amax = false,
+                   const std::function<void(float*)>* pre = nullptr) {
   Workspace& w = workspace(m, N, st, true);
   // the tensors whose maxima this forward needs
   const bool all = m.amax_all || getenv_flag_on("PPS_AMAX_ALL");
@@ -1115,8 +1137,16 @@ void forward_range(const PpsModel& m, const float* x, int N, float* feat, int fi
           w.amax_need[m.slot.at(m.layers[pi].input)] = 1;
       }
   if (first == 0 && !keep_amax) {
-    // a forward: every producer reports its output's max afresh
+    // a forward: every producer reports its output's max afresh, and the
+    // input's max is measured when an f16x2 layer (the stem) reads it
     hip_check(hipMemsetAsync(w.amax->p, 0, w.amax->bytes, st), "hipMemsetAsync");
+    const auto ds = m.slot.find("data");
+    float* dslot = ds != m.slot.end() && ds->second < (int)w.amax_need.size() &&
+                           w.amax_need[ds->second]
+                       ? w.amax->as<float>() + (size_t)ds->second * PPS_AMAX_SLOT_FLOATS
+                       : nullptr;
+    if (pre) (*pre)(dslot);  // the producer of x reports its max
+    else if (dslot) rc_check(amax_of(x, w.shapes.at("data").numel(), dslot, st));
   } else if (!keep_amax) {
     // a layer range: the f32 tensors it reads but does not produce are
     // measured afresh (their producers ran in an earlier call)
@@ -1531,6 +1561,13 @@ int pps_model_layer_info(const PpsModel* m, int i, int N, PpsLayerInfo* info) {
 int pps_model_set_tile(PpsModel* m, const char* layer, int tile) {
   return guarded([&] {
     Layer* L = find_layer(m, layer);
+    // the fused stem takes 0 (bf16x3) or PPS_TILE_H2 (f16x2) only
+    if (L->op == Op::StemPool) {
+      PPS_MCHECK(tile == 0 || (tile == PPS_TILE_H2 && h2_tile_ok(*L, tile)),
+                 std::string("stem '") + layer + "': tile 0 or PPS_TILE_H2 (f16x2) only");
+      L->tile = tile;
+      return;
+    }
     PPS_MCHECK(tunable(*L), std::string("layer '") + layer + "' has no GEMM tile");
     const int base = tile & ~(PPS_TILE_B_TILED | PPS_TILE_COL_ORDER | PPS_TILE_SEAM | PPS_TILE_H2 |
                               PPS_TILE_H2P | PPS_TILE_H2E);
@@ -1705,9 +1742,14 @@ int pps_forward_bgr(const PpsModel* m, const uint8_t* img, int N, int Hi, int Wi
     const hipStream_t st = as_stream(stream);
     Workspace& w = workspace(*m, N, st, true);
     float* x = nhwc4_buffer(*m, w, st);
-    rc_check(pps_preprocess_bgr(img, N, Hi, Wi, m->cfg.pixel_means, m->cfg.height, m->cfg.width,
-                                x, st));
-    forward_range(*m, x, N, feat, 0, (int)m->layers.size(), st);
+    PPS_MCHECK(Hi > 0 && Wi > 0, "bad image shape");
+    // preprocessing inside the forward, after the maxima slots are zeroed:
+    // it reports max|x| for an f16x2 stem (no separate pass over x)
+    const std::function<void(float*)> pre = [&](float* slot) {
+      rc_check(preprocess_bgr(img, N, Hi, Wi, nullptr, nullptr, nullptr, m->cfg.pixel_means,
+                              m->cfg.height, m->cfg.width, x, st, slot));
+    };
+    forward_range(*m, x, N, feat, 0, (int)m->layers.size(), st, false, &pre);
   });
 }
 
@@ -1797,7 +1839,10 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
         var.push_back(tl);
         // f16x2 finalists also with the input split once into planes
         if ((tl & PPS_TILE_H2) && h2_tile_ok(L, tl | PPS_TILE_H2P)) var.push_back(tl | PPS_TILE_H2P);
-        if (L.splitk == 1 && L.op != Op::Heads && tl >= GEMM_TILE_P_FIRST && tl != GEMM_TILE_WS)
+        // (base tile: the flags of an f16x2 candidate are or-ed in already;
+        // the weight-stationary kernel has no tile order to choose)
+        const int tb = tl & 0xff;
+        if (L.splitk == 1 && L.op != Op::Heads && tb >= GEMM_TILE_P_FIRST && tb != GEMM_TILE_WS)
           for (int f : {PPS_TILE_B_TILED, PPS_TILE_COL_ORDER,
                         PPS_TILE_B_TILED | PPS_TILE_COL_ORDER})
             if (!(f & PPS_TILE_B_TILED) || (L.wt && !(tl & PPS_TILE_H2))) var.push_back(tl | f);
@@ -1822,6 +1867,29 @@ int pps_model_autotune(PpsModel* m, const float* x, int N, int flags, void* stre
     std::vector<float> cost(m->layers.size(), 0.f);
     for (size_t i = 0; i < m->layers.size(); ++i)
       if (tunable(m->layers[i])) cost[i] = tune(m->layers[i]);
+    // the fused stem: f16x2 (plus the pass that measures the input's max, run
+    // by every forward that takes it) against bf16x3, interleaved rounds
+    for (Layer& L : m->layers)
+      if (L.op == Op::StemPool) L.tile = 0;
+    if (try_h2)
+      for (Layer& L : m->layers) {
+        if (L.op != Op::StemPool || !h2_tile_ok(L, PPS_TILE_H2) || !m->slot.count("data")) continue;
+        float* ds = w->amax->as<float>() + (size_t)m->slot.at("data") * PPS_AMAX_SLOT_FLOATS;
+        const int64_t n = w->shapes.at("data").numel();
+        float tx = 1e30f, th = 1e30f, ta = 1e30f;
+        for (int r = 0; r < final_rounds; ++r) {
+          tx = std::min(tx, time_layer(*m, L, *w, x, 0, 1, final_reps, st, t));
+          th = std::min(th, time_layer(*m, L, *w, x, PPS_TILE_H2, 1, final_reps, st, t));
+          hip_check(hipEventRecord(t.e0, st), "hipEventRecord");
+          for (int i = 0; i < final_reps; ++i) rc_check(amax_of(x, n, ds, st));  // same max again
+          hip_check(hipEventRecord(t.e1, st), "hipEventRecord");
+          hip_check(hipEventSynchronize(t.e1), "hipEventSynchronize");
+          float ms = 0.f;
+          hip_check(hipEventElapsedTime(&ms, t.e0, t.e1), "hipEventElapsedTime");
+          ta = std::min(ta, ms / final_reps);
+        }
+        L.tile = th + ta < 0.98f * tx ? PPS_TILE_H2 : 0;
+      }
     if (tune_planes) {
       for (auto& e : m->edges) {
         Layer& P = m->layers[e.first];

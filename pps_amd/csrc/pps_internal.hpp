@@ -318,6 +318,15 @@ int conv_pps_impl(const float* x, const uint16_t* x3, int64_t x_plane, int N, in
                   const float* amax_in);
 int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const float* scale,
                       const float* shift, float* y, int Hc, int Hp, hipStream_t st, float* amax);
+int stem_conv_pool_h2(const float* x, int N, int H, const uint16_t* w2, const float* w_inv,
+                      const float* scale, const float* shift, float* y, int Hc, int Hp,
+                      hipStream_t st, float* amax, const float* amax_in);
+int stem_split_h2(const float* w, uint16_t* w2, float* w_inv, hipStream_t st);
+// image preprocessing (pps_preprocess_bgr[_ragged]); amax (may be null)
+// receives max |y| (the f16x2 stem's input scale)
+int preprocess_bgr(const uint8_t* img, int N, int Hi, int Wi, const int64_t* offsets,
+                   const int32_t* heights, const int32_t* widths, const float* means, int Ho,
+                   int Wo, float* y, hipStream_t st, float* amax = nullptr);
 int maxpool2d(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
               int Ho, int Wo, hipStream_t st, float* amax);
 // max |x| of n floats into *amax (atomic max on the float bits; zero it first)

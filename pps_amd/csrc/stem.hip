@@ -235,10 +235,29 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
 #define RING_ABL 0  // probes only, bit mask: 1 = no epilogue, 2 = no ring staging, 4 = no
                     // barrier, 8 = no MFMA, 16 = no fragment reads in the K loop
 #endif
+// Two floats scaled by S -> their f16x2 split as two packed f16 pairs
+// (split8_h2's arithmetic): x S = hi + lo + r, |r| <= 2^-22 |x S|.
+__device__ inline void split2_h2(float x0, float x1, float S, unsigned& hi, unsigned& lo) {
+  const float y0 = x0 * S, y1 = x1 * S;  // exact (a power of two)
+  const _Float16 h0 = (_Float16)y0, h1 = (_Float16)y1;
+  const _Float16 l0 = (_Float16)(y0 - (float)h0), l1 = (_Float16)(y1 - (float)h1);
+  hi = (unsigned)__builtin_bit_cast(uint16_t, h0) | ((unsigned)__builtin_bit_cast(uint16_t, h1) << 16);
+  lo = (unsigned)__builtin_bit_cast(uint16_t, l0) | ((unsigned)__builtin_bit_cast(uint16_t, l1) << 16);
+}
+
+// The three f16x2 terms a0 b0 + a1 b0 + a0 b1 on v_mfma_f32_32x32x16_f16
+// (fragments kept in bf16x8 storage, as the x3 ring's)
+__device__ inline f32x16 mfma32_h2(const bf16x8 (&a)[3], const bf16x8 (&b)[2], f32x16 c) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[0]), __builtin_bit_cast(h8, b[0]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[1]), __builtin_bit_cast(h8, b[0]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[0]), __builtin_bit_cast(h8, b[1]), c, 0, 0, 0);
+  return c;
+}
+
 constexpr int kRingPR = 6;                    // pooled rows per workgroup
 constexpr int kRingCR = 2 * kRingPR + 1;      // conv rows per workgroup
 constexpr int kRingSlots = 10;                // 7 read by row i + 1 in flight + 2 written
-constexpr int kRingRow = 3 * kStemCols;       // bf16 elements per (channel, slot): 3 planes
 
 #ifndef RING_STREAMS
 #define RING_STREAMS 2  // row streams per workgroup (2: 4-wave workgroups)
@@ -248,18 +267,29 @@ constexpr int kRingThreads = 128 * RING_STREAMS;
 #define RING_CLK 0
 #endif
 
+// H2: the f16x2 arithmetic (round 6) -- the input split into two f16 planes
+// on the scale of its max (amax_in: the activation-max slot of the stem's
+// input), two-plane f16 weights with per-channel inverse scales w_inv, three
+// product terms (v_mfma_f32_32x32x16_f16) instead of six; the scales fold
+// into the BN scale of the epilogue (exact powers of two).
+template <bool H2>
 __global__ void __launch_bounds__(kRingThreads, 2)
-stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
-                    const uint16_t* __restrict__ w3, const float* __restrict__ scale,
-                    const float* __restrict__ shift, float* __restrict__ y, int Hc, int Hp,
-                    float* __restrict__ amax) {
-  __shared__ __attribute__((aligned(16))) uint16_t ring[RING_STREAMS * 3 * kRingSlots * kRingRow];
+stem_ring_kernel(const float* __restrict__ x, int H, int tiles_h,
+                 const uint16_t* __restrict__ w3, const float* __restrict__ scale,
+                 const float* __restrict__ shift, float* __restrict__ y, int Hc, int Hp,
+                 float* __restrict__ amax, const float* __restrict__ amax_in,
+                 const float* __restrict__ w_inv) {
+  constexpr int NP = H2 ? 2 : 3;             // planes per staged row
+  constexpr int RR = NP * kStemCols;         // elements per (channel, slot)
+  __shared__ __attribute__((aligned(16))) uint16_t ring[RING_STREAMS * 3 * kRingSlots * RR];
   float amx = 0.f;  // max of this thread's pooled outputs (ReLU: >= 0)
+  float S = 1.f, inv_a = 1.f;  // f16x2: the input's scale 2^s and 2^-s
+  if (H2) S = h2_scale_of(amax_read(amax_in), &inv_a);
   const int n = blockIdx.x / tiles_h;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nb = wid & 1;        // channel half
   const int stream = wid >> 1;   // row stream: its own pooled rows and ring
-  uint16_t* tile = ring + stream * (3 * kRingSlots * kRingRow);
+  uint16_t* tile = ring + stream * (3 * kRingSlots * RR);
   const int ph0 = (blockIdx.x - n * tiles_h) * (kRingPR * RING_STREAMS) + stream * kRingPR;
   const int r0 = 4 * ph0 - 5;  // input row of ring row ri = 0
   const int lane = threadIdx.x & 63;
@@ -267,7 +297,7 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
   const float* xin = x + (int64_t)n * H * kStemW * 4;
 
   // staged columns 0, 1 and 132..135 (input columns -3, -2, 129..132) stay zero
-  for (int e = threadIdx.x; e < RING_STREAMS * 9 * kRingSlots; e += kRingThreads) {
+  for (int e = threadIdx.x; e < RING_STREAMS * 3 * NP * kRingSlots; e += kRingThreads) {
     uint16_t* row = ring + e * kStemCols;
     *reinterpret_cast<unsigned*>(row) = 0u;
     *reinterpret_cast<u32x2*>(row + kStemW + 4) = (u32x2){0u, 0u};
@@ -289,20 +319,32 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
   };
   auto put = [&](int ri, const f32x4& a, const f32x4& b, const f32x4& c, int ok) {
     const int slot = (ri + nb) % kRingSlots;
-    unsigned* t = reinterpret_cast<unsigned*>(tile + slot * kRingRow + 2 * lane + 2);
+    unsigned* t = reinterpret_cast<unsigned*>(tile + slot * RR + 2 * lane + 2);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      unsigned hh, mm, ll;
-      split2((ok & 1) ? a[ch] : 0.f, (ok & 2) ? b[ch] : 0.f, hh, mm, ll);
-      unsigned* tc = t + ch * (kRingSlots * kRingRow / 2);
-      tc[0] = hh;
-      tc[kStemCols / 2] = mm;
-      tc[kStemCols] = ll;
-      if (lane == 63) {
-        split2((ok & 4) ? c[ch] : 0.f, 0.f, hh, mm, ll);
-        tc[1] = hh;
-        tc[kStemCols / 2 + 1] = mm;
-        tc[kStemCols + 1] = ll;
+      unsigned* tc = t + ch * (kRingSlots * RR / 2);
+      if constexpr (H2) {
+        unsigned hh, ll;
+        split2_h2((ok & 1) ? a[ch] : 0.f, (ok & 2) ? b[ch] : 0.f, S, hh, ll);
+        tc[0] = hh;
+        tc[kStemCols / 2] = ll;
+        if (lane == 63) {
+          split2_h2((ok & 4) ? c[ch] : 0.f, 0.f, S, hh, ll);
+          tc[1] = hh;
+          tc[kStemCols / 2 + 1] = ll;
+        }
+      } else {
+        unsigned hh, mm, ll;
+        split2((ok & 1) ? a[ch] : 0.f, (ok & 2) ? b[ch] : 0.f, hh, mm, ll);
+        tc[0] = hh;
+        tc[kStemCols / 2] = mm;
+        tc[kStemCols] = ll;
+        if (lane == 63) {
+          split2((ok & 4) ? c[ch] : 0.f, 0.f, hh, mm, ll);
+          tc[1] = hh;
+          tc[kStemCols / 2 + 1] = mm;
+          tc[kStemCols + 1] = ll;
+        }
       }
     }
   };
@@ -316,15 +358,17 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
     }
   }
   // this lane's B fragments (weights) for all chunks: channel 32 nb + r32
-  bf16x8 b[kStemChunks][3];
+  bf16x8 b[kStemChunks][NP];
   const int co = 32 * nb + r32;
 #pragma unroll
   for (int k = 0; k < kStemChunks; ++k)
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NP; ++p)
       b[k][p] = *reinterpret_cast<const bf16x8*>(w3 + ((int64_t)p * kStemCout + co) * kStemK +
                                                   16 * k + 8 * h);
-  const float sc = scale[co], sh = shift[co];
+  // (f16x2: the product carries 2^(s_a + s_w); BN scale times 2^-(s_a + s_w)
+  // is exact, so fma(acc, sc', sh) rounds as fma(acc 2^-(s_a + s_w), sc, sh))
+  const float sc = H2 ? scale[co] * (inv_a * w_inv[co]) : scale[co], sh = shift[co];
   __syncthreads();
 
   float cur[16];
@@ -356,12 +400,12 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
       int s0 = rs + kh0, s1 = rs + kh1;
       s0 = s0 >= kRingSlots ? s0 - kRingSlots : s0;
       s1 = s1 >= kRingSlots ? s1 - kRingSlots : s1;
-      const int o0 = (c0 * kRingSlots + s0) * kRingRow, o1 = (c1 * kRingSlots + s1) * kRingRow;
+      const int o0 = (c0 * kRingSlots + s0) * RR, o1 = (c1 * kRingSlots + s1) * RR;
       return tile + (h ? o1 : o0) + 2 * r32;
     };
     auto frag = [&](const uint16_t* src, int blk, bf16x8 (&a)[3]) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
         u32x4 u;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -379,11 +423,13 @@ stem_ring_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
       if (!(RING_ABL & 16)) frag(src_of(k), 1, fb);
       __builtin_amdgcn_sched_barrier(0);
       if (RING_ABL & 8) asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]));
+      else if constexpr (H2) acc0 = mfma32_h2(fa, b[k], acc0);
       else acc0 = mfma_x3(fa, b[k], acc0);
       __builtin_amdgcn_sched_barrier(0);
       if (k + 1 < kStemChunks && !(RING_ABL & 16)) frag(src_of(k + 1), 0, fa);
       __builtin_amdgcn_sched_barrier(0);
       if (RING_ABL & 8) asm volatile("" ::"v"(fb[0]), "v"(fb[1]), "v"(fb[2]));
+      else if constexpr (H2) acc1 = mfma32_h2(fb, b[k], acc1);
       else acc1 = mfma_x3(fb, b[k], acc1);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -472,16 +518,57 @@ int stem_conv_pool_x3(const float* x, int N, int H, const uint16_t* w3, const fl
   if (N <= 0) return PPS_OK;
   if (g_stem_variant == 0) {
     const int tiles_h = (Hp + kRingPR * RING_STREAMS - 1) / (kRingPR * RING_STREAMS);
-    hipLaunchKernelGGL(stem_ring_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(kRingThreads), 0,
-                       st, x,
-                       H, tiles_h, w3, scale, shift, y, Hc, Hp, amax);
-    PPS_CHECK_LAUNCH("stem_ring_x3_kernel");
+    hipLaunchKernelGGL(stem_ring_kernel<false>, dim3((unsigned)(N * tiles_h)), dim3(kRingThreads),
+                       0, st, x, H, tiles_h, w3, scale, shift, y, Hc, Hp, amax, nullptr, nullptr);
+    PPS_CHECK_LAUNCH("stem_ring_kernel<x3>");
     return PPS_OK;
   }
   const int tiles_h = (Hp + kStemPR - 1) / kStemPR;
   hipLaunchKernelGGL(stem_conv_pool_x3_kernel, dim3((unsigned)(N * tiles_h)), dim3(256),
                      kStemLdsBytes, st, x, H, tiles_h, w3, scale, shift, y, Hc, Hp, amax);
   PPS_CHECK_LAUNCH("stem_conv_pool_x3_kernel");
+  return PPS_OK;
+}
+
+// f16x2 stem (ring-staged kernel only): w2 = [2][64][kStemK] f16 planes of the
+// packed weights, w_inv = their per-channel inverse scales, amax_in = the
+// activation-max slot of x
+int stem_conv_pool_h2(const float* x, int N, int H, const uint16_t* w2, const float* w_inv,
+                      const float* scale, const float* shift, float* y, int Hc, int Hp,
+                      hipStream_t st, float* amax, const float* amax_in) {
+  if (N <= 0) return PPS_OK;
+  const int tiles_h = (Hp + kRingPR * RING_STREAMS - 1) / (kRingPR * RING_STREAMS);
+  hipLaunchKernelGGL(stem_ring_kernel<true>, dim3((unsigned)(N * tiles_h)), dim3(kRingThreads), 0,
+                     st, x, H, tiles_h, w2, scale, shift, y, Hc, Hp, amax, amax_in, w_inv);
+  PPS_CHECK_LAUNCH("stem_ring_kernel<h2>");
+  return PPS_OK;
+}
+
+// Per output channel (one wave per row of the packed [64][kStemK] f32
+// weights): max |w| -> 2^s (h2_scale_of), the planes f16(w 2^s) and
+// f16(w 2^s - hi), and 2^-s.
+__global__ void stem_split_h2_kernel(const float* __restrict__ w, uint16_t* __restrict__ w2,
+                                     float* __restrict__ w_inv) {
+  const int co = blockIdx.x, lane = threadIdx.x;
+  const float* r = w + (int64_t)co * kStemK;
+  float mx = 0.f;
+  for (int k = lane; k < kStemK; k += 64) mx = fmaxf(mx, fabsf(r[k]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float inv;
+  const float S = h2_scale_of(mx, &inv);
+  for (int k = lane; k < kStemK; k += 64) {
+    const float v = r[k] * S;
+    const _Float16 hi = (_Float16)v, lo = (_Float16)(v - (float)hi);
+    w2[(int64_t)co * kStemK + k] = __builtin_bit_cast(uint16_t, hi);
+    w2[((int64_t)kStemCout + co) * kStemK + k] = __builtin_bit_cast(uint16_t, lo);
+  }
+  if (lane == 0) w_inv[co] = inv;
+}
+
+int stem_split_h2(const float* w, uint16_t* w2, float* w_inv, hipStream_t st) {
+  hipLaunchKernelGGL(stem_split_h2_kernel, dim3(kStemCout), dim3(64), 0, st, w, w2, w_inv);
+  PPS_CHECK_LAUNCH("stem_split_h2_kernel");
   return PPS_OK;
 }
 
@@ -512,6 +599,27 @@ int pps_stem_conv_pool_x3(const float* x, int N, int H, int W, const uint16_t* w
   PPS_ENFORCE(aligned16(x) && aligned16(w3) && aligned16(y), "16-byte aligned pointers");
   PPS_ENFORCE((int64_t)N * H * W * 4 < (1ll << 31), "input larger than 2^31 floats");
   return stem_conv_pool_x3(x, N, H, w3, scale, shift, y, Hc, Hp, as_stream(stream), nullptr);
+}
+
+int pps_stem_split_h2(const float* w, uint16_t* w2, float* w_inv, void* stream) {
+  PPS_ENFORCE(w && w2 && w_inv, "null pointer");
+  return stem_split_h2(w, w2, w_inv, as_stream(stream));
+}
+
+int pps_stem_conv_pool_h2(const float* x, int N, int H, int W, const uint16_t* w2,
+                          const float* w_inv, const float* amax_x, const float* scale,
+                          const float* shift, float* y, int Hp, int Wp, void* stream) {
+  PPS_ENFORCE(x && w2 && w_inv && amax_x && scale && shift && y, "null pointer");
+  PPS_ENFORCE(W == kStemW, "the fused stem is built for input width " +
+                               std::to_string(kStemW) + ", got " + std::to_string(W));
+  PPS_ENFORCE(N >= 0 && H >= 7, "bad shape");
+  const int Hc = (H + 2 * 3 - 7) / 2 + 1;
+  PPS_ENFORCE(Hp == (Hc + 2 - 3) / 2 + 1 && Wp == kStemWp,
+              "output must be the 3x3/2 pad 1 max pool of the 7x7/2 pad 3 conv");
+  PPS_ENFORCE(aligned16(x) && aligned16(w2) && aligned16(y), "16-byte aligned pointers");
+  PPS_ENFORCE((int64_t)N * H * W * 4 < (1ll << 31), "input larger than 2^31 floats");
+  return stem_conv_pool_h2(x, N, H, w2, w_inv, scale, shift, y, Hc, Hp, as_stream(stream),
+                           nullptr, amax_x);
 }
 
 }  // extern "C"

@@ -408,8 +408,9 @@ class PPSModel(object):
                     P['stride'] == 2 and P['pad'] == 1 and
                     sum(1 for M in self.layers if M.get('input') == L['output']) == 1):
                 w = pack_stem_weight(blobs[L['name'] + '_w'])
+                wd = torch.from_numpy(w).to(self.device)
                 F = dict(L, op='stem_pool', output=P['output'], conv_output=L['output'],
-                         w=ops.split_bf16x3(torch.from_numpy(w).to(self.device)))
+                         w=ops.split_bf16x3(wd), w32s=wd)
                 self.layers[i:i + 2] = [F]
                 return
 
@@ -748,6 +749,13 @@ class PPSModel(object):
         tile &= ~ops.TILE_SEAM   # one layer alone (forward() runs the seam pairs)
         if op == 'conv' and self._h2e_consumer(L) is not None:
             return self._run_h2out(L, bufs, tile)
+        if op == 'stem_pool' and tile & ops.TILE_H2:   # f16x2 stem, the input's max measured here
+            if '_w2s' not in L:
+                L['_w2s'] = ops.stem_split_h2(L['w32s'])
+            w2, winv = L['_w2s']
+            x = bufs[L['input']]
+            return ops.stem_conv_pool_h2(x, w2, winv, ops.amax(x), L['scale'], L['shift'],
+                                         bufs[L['output']])
         if tile & ops.TILE_H2:
             return self._run_h2(L, bufs, tile)
         sk = L.get('splitk', 1) if splitk is None else splitk
@@ -998,7 +1006,7 @@ class PPSModel(object):
     def tiles(self):
         """{layer name: tile id} of the GEMM layers (0 = heuristic)."""
         return {L.get('name', L['output']): int(L.get('tile', 0)) for L in self.layers
-                if L['op'] in ('conv', 'conv_dual', 'heads', 'conv_pps')}
+                if L['op'] in ('conv', 'conv_dual', 'heads', 'conv_pps', 'stem_pool')}
 
     def _check_tile(self, i, tile):
         """The C plan's set_tile / seam_ok / h2_tile_ok conditions: a table
@@ -1006,6 +1014,10 @@ class PPSModel(object):
         must not run a wrong launch silently)."""
         L = self.layers[i]
         name = L.get('name', L['output'])
+        if L['op'] == 'stem_pool':   # 0 (bf16x3) or PPS_TILE_H2 (f16x2) only
+            if tile not in (0, ops.TILE_H2) or (tile and 'w32s' not in L):
+                raise ValueError("stem '%s': tile 0 or PPS_TILE_H2 (f16x2) only" % name)
+            return
         if tile & ops.TILE_SEAM:
             X = self.layers[i + 1] if i + 1 < len(self.layers) else None
 

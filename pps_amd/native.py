@@ -133,7 +133,7 @@ class NativeModel(object):
 
     def tiles(self):
         return {L['name']: L['tile'] for L in self.layers() if L['op'] in
-                ('conv', 'conv_dual', 'heads', 'conv_pps')}
+                ('conv', 'conv_dual', 'heads', 'conv_pps', 'stem_pool')}
 
     def set_tiles(self, tiles):
         names = {L['name'] for L in self.layers()}

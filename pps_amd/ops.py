@@ -1082,6 +1082,35 @@ def stem_conv_pool_x3(x, w3, scale, shift, y):
     return y
 
 
+def stem_split_h2(w):
+    """The f16x2 split of the packed stem weight [64, stem_k()] f32
+    (pps_stem_split_h2): (w2 [2, 64, stem_k()] f16 planes as int16, w_inv [64]
+    the per-channel 2^-s)."""
+    if tuple(w.shape) != (64, stem_k()):
+        raise RuntimeError('stem weight must be [64, %d]' % stem_k())
+    w = w.contiguous()
+    w2 = torch.empty((2, 64, stem_k()), dtype=torch.int16, device=w.device)
+    winv = torch.empty(64, dtype=torch.float32, device=w.device)
+    call('pps_stem_split_h2', _dev(w, 'w'), _dev(w2, 'w2', torch.int16), _dev(winv, 'w_inv'),
+         _stream())
+    return w2, winv
+
+
+def stem_conv_pool_h2(x, w2, winv, amax_x, scale, shift, y):
+    """The fused stem in f16x2 arithmetic (pps_stem_conv_pool_h2): as
+    stem_conv_pool_x3, the input split on the scale of its max (amax_x: an
+    activation-max slot, e.g. amax(x)), stem_split_h2 weights."""
+    N, H, W, C = x.shape
+    _, Hp, Wp, Co = y.shape
+    if C != 4 or Co != 64 or tuple(w2.shape) != (2, 64, stem_k()):
+        raise RuntimeError('stem: x must be NHWC4, y 64 channels, w2 [2, 64, %d]' % stem_k())
+    _amax_arg(amax_x, 'amax_x')
+    call('pps_stem_conv_pool_h2', _dev(x, 'x'), N, H, W, _dev(w2, 'w2', torch.int16),
+         _dev(winv, 'w_inv'), _dev(amax_x, 'amax_x'), _dev(scale, 'scale'), _dev(shift, 'shift'),
+         _dev(y, 'y'), Hp, Wp, _stream())
+    return y
+
+
 def maxpool2d(x, k, stride, pad, y):
     N, H, W, C = x.shape
     _, Ho, Wo, _ = y.shape

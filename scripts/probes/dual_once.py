@@ -1,7 +1,9 @@
-"""The res2_0 branch2c fused-shortcut conv of the batch-64 forward (1x1 64 ->
-256 on res2_0_branch2b's output + the 1x1 64 -> 256 projection of pool1, K =
-128), alone, f16x2: python scripts/probes/dual_once.py TILE [--reps N]
-(PPS_WS_H2_WIDE=1: the 256-column weight-stationary block)."""
+"""A branch2c fused-shortcut conv of the batch-64 forward, alone, f16x2:
+python scripts/probes/dual_once.py TILE [--reps N] [--shape res2|res5]
+res2: 1x1 64 -> 256 on res2_0_branch2b's output + the 1x1 64 -> 256
+projection of pool1 (K = 128; PPS_WS_H2_WIDE=1: the 256-column
+weight-stationary block); res5: 1x1 512 -> 2048 + the stride-1 1024 -> 2048
+projection of res4's output on 24 x 8 (K = 1536)."""
 import os
 import sys
 
@@ -15,7 +17,9 @@ from pps_amd import model, ops  # noqa: E402
 def main():
     tile = int(sys.argv[1])
     reps = int(sys.argv[sys.argv.index('--reps') + 1]) if '--reps' in sys.argv else 20
-    N, H, W, C1, C2, Cout = 64, 96, 32, 64, 64, 256
+    shape = sys.argv[sys.argv.index('--shape') + 1] if '--shape' in sys.argv else 'res2'
+    N, H, W, C1, C2, Cout = {'res2': (64, 96, 32, 64, 64, 256),
+                             'res5': (64, 24, 8, 512, 1024, 2048)}[shape]
     rng = np.random.RandomState(0)
     x = torch.from_numpy(np.maximum(rng.randn(N, H, W, C1), 0).astype(np.float32)).cuda()
     x2 = torch.from_numpy(np.maximum(rng.randn(N, H, W, C2), 0).astype(np.float32)).cuda()
@@ -39,8 +43,10 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     byt = 4.0 * N * H * W * (C1 + C2 + Cout)
-    print('dual res2_0 tile %d (wide %s): %.1f us, %.2f TB/s algorithmic'
-          % (tile, os.environ.get('PPS_WS_H2_WIDE', '0'), us, byt / us / 1e6))
+    fl = 2.0 * N * H * W * Cout * (C1 + C2)
+    print('dual %s tile %d (wide %s, GM %s): %.1f us, %.2f TB/s algorithmic, %.1f TF'
+          % (shape, tile, os.environ.get('PPS_WS_H2_WIDE', '0'), os.environ.get('PPS_CONV_GM', '0'),
+             us, byt / us / 1e6, fl / us / 1e6))
 
 
 if __name__ == '__main__':

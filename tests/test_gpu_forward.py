@@ -325,6 +325,38 @@ def test_fused_stem_vs_fp64(N, H):
         ops.stem_conv_pool_x3(_cuda(xin[:, :, :64]), w3, _cuda(scale), _cuda(shift), y)
 
 
+@pytest.mark.parametrize('N,H,mag', [(2, 384, 1.0), (3, 100, 1.0), (1, 30, 1e-20), (2, 7, 1.0),
+                                     (1, 390, 1e20)])
+def test_fused_stem_h2_vs_fp64(N, H, mag):
+    """The fused stem in f16x2 arithmetic (pps_stem_conv_pool_h2: input split
+    on the scale of its max, two-plane weights with per-channel scales, three
+    f16 MFMA terms) vs a float64 reference, also for inputs far from 1."""
+    from pps_amd import model, ops
+    rng = np.random.RandomState(H + N + 7)
+    x = (rng.randn(N, 3, H, 128) * 50 * mag).astype(np.float32)
+    w = (rng.randn(64, 3, 7, 7) / np.sqrt(147)).astype(np.float32)
+    scale = rng.uniform(0.5, 1.5, 64).astype(np.float32)
+    shift = (rng.randn(64) * 0.1 * mag).astype(np.float32)
+    ref = F.conv2d(torch.from_numpy(x).double(), torch.from_numpy(w).double(), stride=2,
+                   padding=3)
+    ref = ref * torch.from_numpy(scale).double()[None, :, None, None] + \
+        torch.from_numpy(shift).double()[None, :, None, None]
+    ref = F.max_pool2d(torch.clamp_min(ref, 0), 3, 2, 1).numpy().transpose(0, 2, 3, 1)
+    xin = np.zeros((N, H, 128, 4), np.float32)
+    xin[..., :3] = x.transpose(0, 2, 3, 1)
+    xd = _cuda(xin)
+    w2, winv = ops.stem_split_h2(_cuda(model.pack_stem_weight(w)))
+    y = torch.full(ref.shape, float('nan'), dtype=torch.float32, device='cuda')
+    ops.stem_conv_pool_h2(xd, w2, winv, ops.amax(xd), _cuda(scale), _cuda(shift), y)
+    got = y.cpu().numpy()
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    print('f16x2 stem N=%d H=%d mag %g: max rel err %.3g' % (N, H, mag, err))
+    assert err < 2e-6, err
+    with pytest.raises(RuntimeError, match='width'):
+        ops.stem_conv_pool_h2(_cuda(xin[:, :, :64]), w2, winv, ops.amax(xd), _cuda(scale),
+                              _cuda(shift), y)
+
+
 def test_fused_stem_model_matches_two_kernel_stem():
     from pps_amd import model
     _market_cfg()

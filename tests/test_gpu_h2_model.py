@@ -71,10 +71,13 @@ def _h2_table(nm, N):
     t = {}
     k = 0
     for L in nm.layers(N):
-        if L['op'] in ('conv', 'conv_dual', 'conv_pps'):
+        if L['op'] in ('conv', 'conv_dual', 'conv_pps', 'stem_pool'):
             t[L['name']] = L['tile']
     for name in list(t):
         L = next(M for M in nm.layers(N) if M['name'] == name)
+        if L['op'] == 'stem_pool':   # the fused stem: its own kernel, f16x2 or not
+            t[name] = ops.TILE_H2
+            continue
         base = fam[k % len(fam)]
         k += 1
         if L['op'] == 'conv_dual' and base >= 56:
@@ -115,6 +118,7 @@ def test_h2_table_c_plan_equals_twin_and_oracle():
     pm.set_planes([])
     ok = _apply(nm, _h2_table(nm, N))   # the layers the plan accepts (Cin % 32 == 0)
     assert len(ok) >= 45, len(ok)
+    assert ok.get('conv1') == ops.TILE_H2, ok.get('conv1')   # the f16x2 fused stem
     assert sum(1 for t in ok.values() if (t & 0xff) == ops.TILE_WS) >= 4   # f16x2 ws 1x1s
     assert sum(1 for t in ok.values() if t & ops.TILE_H2P) >= 12
     pm.set_tiles(ok)
