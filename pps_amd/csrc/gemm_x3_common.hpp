@@ -108,34 +108,46 @@ __device__ inline f32x4 mfma16_f16(const f16x8& a, const f16x8& b, const f32x4& 
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// Two floats (a, b), scaled by the wave-uniform power of two S, -> their f16
+// terms packed in pairs: hi = (f16(a S), f16(b S)), lo = (f16(a S - hi_a),
+// f16(b S - hi_b)).  a S is exact and so is a S - hi_a (<= 24 significant
+// bits), so each term is ONE rounding to f16 -- what (_Float16)(a * S) and
+// (_Float16)(a * S - (float)hi) give.  Four v_fma_mix per pair: the
+// compiler's own sequence (v_mul + v_cvt_pk for the hi pair, and the hi
+// terms again as v_fma_mixlo for the remainders) took seven, and the split is
+// the f16x2 main loops' VALU cost (an MFMA 16x16x32 gap leaves 8 issue
+// cycles).
+__device__ inline void h2_pair(float a, float b, float S, unsigned& hi, unsigned& lo) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, -0\n\t"   // (+ -0: a S exactly, its zero sign too)
+      "v_fma_mixhi_f16 %0, %3, %4, -0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(a), "v"(b), "s"(S));
+}
+
 // Eight consecutive-K floats, scaled by S, -> the two f16x8 MFMA fragments
 // (kept in bf16x8 storage so the bf16x3 kernels' fragment arrays hold them).
 __device__ inline void split8_h2(const f32x4& x0, const f32x4& x1, float S, bf16x8& f0,
                                  bf16x8& f1) {
-  f16x8 h0, h1;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float y = (e < 4 ? x0[e] : x1[e - 4]) * S;  // exact (a power of two)
-    h0[e] = (_Float16)y;
-    h1[e] = (_Float16)(y - (float)h0[e]);                // the remainder is exact in f32
-  }
-  f0 = __builtin_bit_cast(bf16x8, h0);
-  f1 = __builtin_bit_cast(bf16x8, h1);
+  unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+  h2_pair(x0[0], x0[1], S, h0, l0);
+  h2_pair(x0[2], x0[3], S, h1, l1);
+  h2_pair(x1[0], x1[1], S, h2, l2);
+  h2_pair(x1[2], x1[3], S, h3, l3);
+  f0 = __builtin_bit_cast(bf16x8, (u32x4){h0, h1, h2, h3});
+  f1 = __builtin_bit_cast(bf16x8, (u32x4){l0, l1, l2, l3});
 }
 
 // Four outputs as f16x2 planes on the scale S (EPI_F_H2OUT): split8_h2's
 // split, so a consumer reading the planes gets the fragments it would split
 // from the f32 values on that scale.
 __device__ inline void split4_h2(const f32x4& v, float S, u32x2& hi, u32x2& lo) {
-  f16x4 h0, h1;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float y = v[e] * S;
-    h0[e] = (_Float16)y;
-    h1[e] = (_Float16)(y - (float)h0[e]);
-  }
-  hi = __builtin_bit_cast(u32x2, h0);
-  lo = __builtin_bit_cast(u32x2, h1);
+  unsigned h0, l0, h1, l1;
+  h2_pair(v[0], v[1], S, h0, l0);
+  h2_pair(v[2], v[3], S, h1, l1);
+  hi = (u32x2){h0, h1};
+  lo = (u32x2){l0, l1};
 }
 
 // The bound B >= max|y| of an EPI_F_H2OUT conv output (GemmParams::h2o_*)

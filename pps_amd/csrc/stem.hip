@@ -236,13 +236,9 @@ stem_conv_pool_x3_kernel(const float* __restrict__ x, int H, int tiles_h,
                     // barrier, 8 = no MFMA, 16 = no fragment reads in the K loop
 #endif
 // Two floats scaled by S -> their f16x2 split as two packed f16 pairs
-// (split8_h2's arithmetic): x S = hi + lo + r, |r| <= 2^-22 |x S|.
+// (h2_pair: split8_h2's arithmetic), x S = hi + lo + r, |r| <= 2^-22 |x S|.
 __device__ inline void split2_h2(float x0, float x1, float S, unsigned& hi, unsigned& lo) {
-  const float y0 = x0 * S, y1 = x1 * S;  // exact (a power of two)
-  const _Float16 h0 = (_Float16)y0, h1 = (_Float16)y1;
-  const _Float16 l0 = (_Float16)(y0 - (float)h0), l1 = (_Float16)(y1 - (float)h1);
-  hi = (unsigned)__builtin_bit_cast(uint16_t, h0) | ((unsigned)__builtin_bit_cast(uint16_t, h1) << 16);
-  lo = (unsigned)__builtin_bit_cast(uint16_t, l0) | ((unsigned)__builtin_bit_cast(uint16_t, l1) << 16);
+  h2_pair(x0, x1, S, hi, lo);
 }
 
 // The three f16x2 terms a0 b0 + a1 b0 + a0 b1 on v_mfma_f32_32x32x16_f16
