@@ -102,7 +102,9 @@ int pps_gemm_num_tiles(void);
  * ends (no plane edge), no split-K.  The handle keeps the f16x2 weight split
  * beside the bf16x3 one; each forward zeroes its per-tensor activation maxima
  * and every producer reports max|y| from its epilogue (the f16x2 layers'
- * input scales). */
+ * input scales).  On the fused stem (`stem_pool` layer) PPS_TILE_H2 alone
+ * (tile 0x800) selects pps_stem_conv_pool_h2; the forward then measures its
+ * input's max (pps_forward_bgr: reported by the preprocessing kernel). */
 #define PPS_TILE_H2 0x800
 /* With PPS_TILE_H2 on a conv / conv_pps layer: the layer's input is split
  * into f16x2 activation planes by one pass (pps_split_f16x2_act) just before
