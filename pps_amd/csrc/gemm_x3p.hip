@@ -587,8 +587,12 @@ gemm_x3p_kernel(GemmParams p, int tiles_m, int tiles_n) {
     // -> 155.1 / 160.0 us with the younger half staggered; the 128 x 128 8-wave
     // tile (two workgroups per CU, <= 128 VGPRs) loses 50 % with it, tiles 47
     // and 53 are level (scripts/gpu_r6_stagger.sh)
+#ifndef X3P_STAG51
+#define X3P_STAG51 0  // probes: 1 = the stagger on tile 51 (128 x 128, 4 x 2 waves, three stages) too
+#endif
     constexpr int STAG = X3P_STAG >= 0 ? X3P_STAG
-                                       : (BM == 192 && BN == 128 && WM == 4 && WN == 2 && NS == 3);
+                                       : ((BM == 192 || (X3P_STAG51 && BM == 128)) && BN == 128 &&
+                                          WM == 4 && WN == 2 && NS == 3);
     if (STAG != 0 && NW == 8 && (STAG == 1 ? wave >= NW / 2 : wave < NW / 2))
       run(step_pre);
     else
