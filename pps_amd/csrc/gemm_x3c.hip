@@ -45,10 +45,13 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   constexpr int TNH = TN / 2;
   static_assert(TN % 2 == 0 && TM >= 1 && (BM / WM) % S == 0, "wave tile");
   // EPI_F_H2: f16x2 arithmetic (f32 patch split into two f16 terms after the
-  // fragment read, two chunk-tiled f16 weight planes, three MFMA terms)
+  // fragment read, two chunk-tiled f16 weight planes, three MFMA terms); with
+  // A3 the patch is the two f16x2 activation planes (a PPS_TILE_H2E / H2P
+  // edge): no split in the loop, the same fragments
   constexpr bool H2 = (EPI & EPI_F_H2) != 0;
-  static_assert(!H2 || (!A3 && !(EPI & (EPI_F_PLANES | EPI_F_RAW))), "f16x2: f32 activations");
+  static_assert(!H2 || !(EPI & (EPI_F_PLANES | EPI_F_RAW)), "f16x2: plain epilogues");
   constexpr int NBP = H2 ? 2 : 3;  // weight planes
+  constexpr int NAP = H2 ? 2 : 3;  // activation planes (A3)
   constexpr int B_PLANE = BN * BK * 2;
   constexpr int B_STAGE = NBP * B_PLANE;
   constexpr int NPB = BN / 16;  // weight pieces per plane and chunk
@@ -59,11 +62,11 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
   constexpr int PMR = (PMAX + PXP - 1) / PXP * PXP;   // pixels, whole pieces
   constexpr int PX_BYTES = A3 ? 64 : 128;             // per pixel (and plane)
   constexpr int P_PLANE = PMR * 64;                   // A3: plane stride in a buffer
-  constexpr int P_BYTES = A3 ? 3 * P_PLANE : PMR * 128;
+  constexpr int P_BYTES = A3 ? NAP * P_PLANE : PMR * 128;
   constexpr int NPT = PMR / PXP;                      // patch pieces (per plane)
   constexpr int SL = kX3cTaps - NS + 2;               // issue slots per patch
   constexpr int NPPW = (NPT + NW * SL - 1) / (NW * SL);  // patch pieces per wave and slot
-  constexpr int LA = A3 ? 3 : 1;
+  constexpr int LA = A3 ? NAP : 1;
   constexpr int NLOAD = NBP * BPW + LA * NPPW;        // DMA instructions per wave and issue
   static_assert(NS >= 2 && NS <= 4 && NLOAD * (NS - 2) <= 63, "stages / vmcnt range");
   constexpr int OFF_P = NS * B_STAGE;                 // patch buffers
@@ -146,7 +149,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
       unsigned char* d = buf + q * 1024;
       glds16(ra, d, off);
       glds16(ra1, d + P_PLANE, off);
-      glds16(ra2, d + 2 * P_PLANE, off);
+      if (!H2) glds16(ra2, d + 2 * P_PLANE, off);
     } else {
       glds16(ra, buf + q * 1024, ok ? e * 4 : kOOB);
     }
@@ -230,7 +233,7 @@ gemm_x3c_kernel(GemmParams p, int tiles_n) {
       if (A3) {
         const unsigned char* ap = buf + pix * 64 + ((h ^ ((pix >> 2) & 3)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NAP; ++pl)
           fa[i][pl] = *reinterpret_cast<const bf16x8*>(ap + pl * P_PLANE);
       } else {
         const unsigned char* rp = buf + pix * PX_BYTES;
@@ -336,15 +339,7 @@ static int launch_c(const GemmParams& p, int epi, hipStream_t stream) {
     X3C_CASE(C | RS | RL)
     X3C_CASE(C | PL)
     X3C_CASE(C | RL | PL)
-    case C | RL | EPI_F_H2:
-      if constexpr (!A3) {
-        hipLaunchKernelGGL((gemm_x3c_kernel<BM, BN, WM, WN, C | RL | EPI_F_H2, NS, A3, PMAX>), grid,
-                           block, 0, stream, p, tiles_n);
-        break;
-      } else {
-        set_error("f16x2 patch tiles take f32 activations");
-        return PPS_ERR_INVALID_ARG;
-      }
+    X3C_CASE(C | RL | EPI_F_H2)
     default:
       set_error("patch-staged 3x3 GEMM: epilogue not built");
       return PPS_ERR_INVALID_ARG;
@@ -386,7 +381,7 @@ bool x3c_eligible(const GemmParams& p, int epi, int batch, int tile) {
   if (epi != C && epi != (C | RL) && epi != (C | RS) && epi != (C | RS | RL) && epi != (C | PL) &&
       epi != (C | RL | PL) && epi != (C | RL | EPI_F_H2))
     return false;  // the epilogues launch_c builds
-  if ((epi & EPI_F_H2) && (p.a3 || !(p.tiled & 2) || !p.rs_b || !p.amax_a)) return false;
+  if ((epi & EPI_F_H2) && (!(p.tiled & 2) || !p.rs_b || !p.amax_a)) return false;
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.dil < 1 || p.pad != p.dil) return false;
   if (p.Ho != p.H || p.Wo != p.W || p.Cin % 32 != 0 || p.Kloop != 9 * p.Cin) return false;
   if (bm % p.Wo != 0 || (p.Ho * p.Wo) % bm != 0 || p.M % bm != 0) return false;

@@ -202,7 +202,8 @@ def test_conv_h2_enforces():
 def test_conv_h2_activation_planes_same_bits(N, H, W, Cin, Cout, k, s, p, residual):
     """f16x2 activation planes (pps_split_f16x2_act, once per element) in
     place of the f32 input: the same fragments reach the MFMAs, so every tile
-    gives the f32-input kernel's bits, and the same max|y|."""
+    gives the f32-input kernel's bits, and the same max|y| -- the patch tiles
+    56-59 too (round 6: their planes patch; stride-1 3x3 shapes, no residual)."""
     from pps_amd import model, ops
     rng = np.random.RandomState(Cin + Cout + k + s)
     x = rng.randn(N, H, W, Cin).astype(np.float32)
@@ -216,7 +217,7 @@ def test_conv_h2_activation_planes_same_bits(N, H, W, Cin, Cout, k, s, p, residu
     xd = _cuda(x)
     amx = ops.amax(xd)
     planes = ops.split_act_h2(xd, amx)
-    for tile in (0, 38, 45, 47, 52, 60):
+    for tile in (0, 38, 45, 47, 52, 60, 56, 57, 58, 59):
         y1 = torch.full((N, Ho, Wo, Cout), float('nan'), device='cuda')
         y2 = torch.full((N, Ho, Wo, Cout), float('nan'), device='cuda')
         a1, a2 = ops.amax_slot(), ops.amax_slot()
