@@ -117,7 +117,8 @@ int pps_gemm_num_tiles(void);
  * the scale of its output bound (pps_conv2d_bn_act_h2out; P in either
  * arithmetic, on a pipelined 16x16x32 tile) and C reads them -- no split in
  * C's main loop and no split pass, same bits as C splitting the f32 output on
- * that scale. */
+ * that scale (C on a pipelined tile or, round 6, a patch tile 56-59; the same
+ * for PPS_TILE_H2P). */
 #define PPS_TILE_H2E 0x2000
 
 /* ---- retrieval: distance matrix ------------------------------------------
