@@ -330,33 +330,71 @@ __device__ void sort_core(Each each, int n, u64 lo, u64 hi, u64* dst, unsigned* 
   each([&](u64 v) { dst[packed_take(off, fm.fine(v))] = v; }, 1);
   lds_barrier();
   SORT_PHASE(4);
-  // 4) buckets of <= kNet words: one lane's sorting network
-  for (int f = t; f < kNF; f += kT) {
-    const int s = f ? packed_get(off, f - 1) : 0, m = packed_get(off, f) - s;
-    if (m >= 2 && m <= 8) {
-      u64 r[kNet];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = j < m ? dst[s + j] : ~0ull;
-      net8(r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < m) dst[s + j] = r[j];
-    } else if (m > 8 && m <= kNet) {
-      u64 r[kNet];
-#pragma unroll
-      for (int j = 0; j < kNet; ++j) r[j] = j < m ? dst[s + j] : ~0ull;
-      net16(r);
-#pragma unroll
-      for (int j = 0; j < kNet; ++j)
-        if (j < m) dst[s + j] = r[j];
-    }
-  }
-  SORT_PHASE(5);
-  // larger buckets (ties, words the float map cannot separate): a wave each
+  // 4) buckets of <= kNet words, one lane each.  Buckets hold ~2.6 words on
+  //    average: the 2..4-word ones take a 5-comparator network in place;
+  //    the 5..kNet-word ones (~12 %) are listed per wave (in cb, free after
+  //    the scatter) and sorted in batches of up to kList, one per lane -- so
+  //    a wave runs the 8- / 16-input networks once per batch instead of once
+  //    per 64 buckets with most lanes idle (the per-bucket branches used to
+  //    diverge inside every wave).  Larger buckets (ties, words the float
+  //    map cannot separate) are sorted by a wave's bitonic network.
+  constexpr int kList = (kNC + 1) / kW;   // per-wave list entries (s | m << 16)
+  static_assert(kList >= 32, "medium-bucket lists");
   const int lane = t & 63, wave = t >> 6;
+  unsigned* wl = cb + wave * kList;
+  auto sort_listed = [&](int n) {   // lanes j < n: listed bucket j
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < n) {
+      const unsigned e = wl[lane];
+      const int s = (int)(e & 0xffffu), m = (int)(e >> 16);
+      u64 r[kNet];
+      if (m <= 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = j < m ? dst[s + j] : ~0ull;
+        net8(r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < m) dst[s + j] = r[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < kNet; ++j) r[j] = j < m ? dst[s + j] : ~0ull;
+        net16(r);
+#pragma unroll
+        for (int j = 0; j < kNet; ++j)
+          if (j < m) dst[s + j] = r[j];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  int nl = 0;   // listed, not yet sorted (wave-uniform)
   for (int base = wave * 64; base < kNF; base += kT) {
     const int f = base + lane;
     const int s = f ? packed_get(off, f - 1) : 0, m = packed_get(off, f) - s;
+    if (m >= 2 && m <= 4) {
+      u64 r0 = dst[s], r1 = dst[s + 1], r2 = m > 2 ? dst[s + 2] : ~0ull,
+          r3 = m > 3 ? dst[s + 3] : ~0ull;
+      ce(r0, r1); ce(r2, r3); ce(r0, r2); ce(r1, r3); ce(r1, r2);
+      dst[s] = r0;
+      dst[s + 1] = r1;
+      if (m > 2) dst[s + 2] = r2;
+      if (m > 3) dst[s + 3] = r3;
+    }
+    const bool med = m > 4 && m <= kNet;
+    const unsigned long long mb = __ballot(med);
+    // up to 64 new entries: list them in order, sorting each full batch
+    // (a batch never takes more than kList; pre < 0 once a lane is listed)
+    int cnt = __popcll(mb), pre = med ? __popcll(mb & ((1ull << lane) - 1ull)) : -1;
+    while (cnt) {   // wave-uniform
+      if (nl == kList) {   // the batch is full: sort it first
+        sort_listed(nl);
+        nl = 0;
+      }
+      const int take = cnt < kList - nl ? cnt : kList - nl;
+      if (pre >= 0 && pre < take) wl[nl + pre] = (unsigned)s | ((unsigned)m << 16);
+      nl += take;
+      cnt -= take;
+      pre = pre >= take ? pre - take : -1;
+    }
     unsigned long long big = __ballot(m > kNet);
     while (big) {
       const int j = __builtin_ctzll(big);
@@ -364,6 +402,8 @@ __device__ void sort_core(Each each, int n, u64 lo, u64 hi, u64* dst, unsigned* 
       wave_bitonic(dst + __shfl(s, j), __shfl(m, j));
     }
   }
+  if (nl) sort_listed(nl);
+  SORT_PHASE(5);
   lds_barrier();
   SORT_PHASE(6);
 }
