@@ -656,7 +656,8 @@ def test_rank_prepare_beyond_lds_merge_cap():
                                       (37, 1, 'plain'), (5, 4099, 'degenerate'),
                                       (40, 18432, 'plain'), (300, 19889, 'market'),
                                       (24, 19889, 'ties'), (5, 30001, 'degenerate'),
-                                      (12, 125000, 'market'), (6, 125000, 'ties')])
+                                      (12, 125000, 'market'), (6, 125000, 'ties'),
+                                      (48, 15913, 'groups'), (12, 30001, 'groups')])
 def test_argsort_rows_equals_stable_argsort(Q, G, kind):
     """pps_argsort_rows == np.argsort(kind='stable') on every row (VERDICT
     r03 item 8): Market-sized rows of L2 distances (the reference's full rank
@@ -664,7 +665,10 @@ def test_argsort_rows_equals_stable_argsort(Q, G, kind):
     negative zeros, all-equal and two-valued rows (one bucket: the wave
     bitonic path), the one-pass kernel's longest row (18,432), and longer
     rows through the segmented kernel: Duke-plus (19,889) and a 1M-config
-    gallery shard (125,000)."""
+    gallery shard (125,000).  'groups': every value repeated 5..16 times
+    (row q: 5 + q % 12), so most buckets hold 5..16 words -- the per-wave
+    lists of those buckets fill several times per step (over 32 new entries
+    in one 64-bucket step, the case that once overran a list)."""
     from pps_amd import ops
     rng = np.random.RandomState(G + Q)
     if kind == 'market':
@@ -675,6 +679,9 @@ def test_argsort_rows_equals_stable_argsort(Q, G, kind):
         d[2, ::3] = 0.0
         d[3] = np.float32(np.inf)
         d[3, 7] = 1.0
+    elif kind == 'groups':
+        d = np.stack([(rng.permutation(G) // (5 + q % 12)).astype(np.float32)
+                      for q in range(Q)])
     elif kind == 'degenerate':
         d = np.ones((Q, G), np.float32)
         d[1, ::2] = 2.0
