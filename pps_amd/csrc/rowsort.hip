@@ -41,7 +41,10 @@ constexpr int kW = kT / 64;
 constexpr int kNC = 512;     // coarse slices (equalisation)
 constexpr int kNF = 6144;    // fine buckets (16-bit counters, two per word)
 constexpr int kNF2 = kNF / 2;
-constexpr int kSample = 4;   // the coarse histogram counts every kSample-th word
+#ifndef PPS_SORT_SAMPLE
+#define PPS_SORT_SAMPLE 2
+#endif
+constexpr int kSample = PPS_SORT_SAMPLE;   // the coarse histogram counts every kSample-th word
 constexpr int kNet = 16;     // buckets up to this size: one lane's sorting network
 constexpr int kLds = 160 * 1024;
 constexpr int kFixed = 4 * (kNC + 1) + 4 * kNF2 + 8 * 2 * kW + 64;
