@@ -38,7 +38,10 @@ typedef unsigned long long u64;
 
 constexpr int kT = 1024;     // threads per workgroup (16 waves)
 constexpr int kW = kT / 64;
-constexpr int kNC = 512;     // coarse slices (equalisation)
+#ifndef PPS_SORT_NC
+#define PPS_SORT_NC 512
+#endif
+constexpr int kNC = PPS_SORT_NC;   // coarse slices (equalisation)
 constexpr int kNF = 6144;    // fine buckets (16-bit counters, two per word)
 constexpr int kNF2 = kNF / 2;
 #ifndef PPS_SORT_SAMPLE

@@ -1,14 +1,15 @@
 #!/bin/bash
-# Row argsort: coarse-histogram sample density (probe_libs/libpps_hip_sN.so =
-# PPS_SORT_SAMPLE=N builds, made by hand, not tracked; product = every 4th
-# word).  Tests per library, then interleaved timings on uniform and
-# Market-like rows.
+# Row argsort parameter A/B: probe_libs/ builds made by hand with
+# scripts/build_variant.sh, not tracked -- libpps_hip_sN.so = PPS_SORT_SAMPLE=N
+# (coarse histogram of every N-th word), libpps_hip_ncN.so = PPS_SORT_NC=N
+# coarse slices; LIBS picks them (default: the sample-density set).  Tests per
+# library, then interleaved timings on uniform and Market-like rows.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out
 mkdir -p $OUT
-L=$OUT/r6_sample.log
+L=$OUT/r6_${TAG:-sample}.log
 : > $L
-LIBS="probe_libs/libpps_hip_s1.so probe_libs/libpps_hip_s2.so probe_libs/libpps_hip_s3.so"
+LIBS=${LIBS:-"probe_libs/libpps_hip_s1.so probe_libs/libpps_hip_s2.so probe_libs/libpps_hip_s3.so"}
 for lib in $LIBS; do
   echo "tests lib=$lib" >> $L
   PPS_LIB_PATH=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_retrieval.py -k "argsort" -q \
