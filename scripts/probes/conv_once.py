@@ -1,7 +1,8 @@
 """One conv layer of the batch-64 forward, alone, for profiling
 (scripts/probes/conv_pmc.sh):  python scripts/probes/conv_once.py SHAPE MATH TILE [--reps N]
 SHAPE: res5b (3x3 512->512, 24x8), res5a (1x1 2048->512), res5c (1x1 512->2048),
-res4b (3x3 256->256), res4a (1x1 1024->256), res4c (1x1 256->1024), res3b, res2b."""
+res4b (3x3 256->256), res4a (1x1 1024->256), res4c (1x1 256->1024), res3b, res2b,
+res2a0 (res2_0_branch2a: 1x1 64->64 on 96x32)."""
 import os
 import sys
 
@@ -18,6 +19,7 @@ SHAPES = {   # H, W, Cin, Cout, k
     'res3b': (48, 16, 128, 128, 3), 'res2b': (96, 32, 64, 64, 3),
     'res3c': (48, 16, 128, 512, 1), 'res2c': (96, 32, 64, 256, 1),
     'res2a': (96, 32, 256, 64, 1), 'res3a': (48, 16, 512, 128, 1),
+    'res2a0': (96, 32, 64, 64, 1),
 }
 
 
@@ -66,7 +68,9 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     fl = 2.0 * N * H * W * Cout * Cin * k * k
-    print('%s %s tile %d: %.1f us, %.1f TF' % (shape, math, tile, us, fl / us / 1e6))
+    nb = 4.0 * N * H * W * (Cin + Cout)
+    print('%s %s tile %d: %.1f us, %.1f TF, %.2f TB/s in + out' % (shape, math, tile, us,
+                                                                 fl / us / 1e6, nb / us / 1e6))
 
 
 if __name__ == '__main__':
