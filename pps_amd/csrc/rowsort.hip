@@ -292,9 +292,9 @@ __device__ void wave_bitonic(u64* a, int n) {
 // f(word) for the calling thread's words; every k-th of them when k > 1) in
 // range [lo, hi] -> dst[0, n) ascending (n < 65536).  cb: kNC + 1 words,
 // off: kNF2 words, red: 2 * kW words.
-template <class Each>
+template <class Each, class After>
 __device__ void sort_core(Each each, int n, u64 lo, u64 hi, u64* dst, unsigned* cb,
-                          unsigned* off, unsigned* red PROBE_PARAMS) {
+                          unsigned* off, unsigned* red, After after_scatter PROBE_PARAMS) {
   const int t = threadIdx.x;
   for (int i = t; i <= kNC; i += kT) cb[i] = 0u;
   for (int i = t; i < kNF2; i += kT) off[i] = 0u;
@@ -335,6 +335,7 @@ __device__ void sort_core(Each each, int n, u64 lo, u64 hi, u64* dst, unsigned* 
   SORT_PHASE(3);
   each([&](u64 v) { dst[packed_take(off, fm.fine(v))] = v; }, 1);
   lds_barrier();
+  after_scatter();   // the caller's words are in LDS now (their registers free)
   SORT_PHASE(4);
   // 4) buckets of <= kNet words, one lane each.  Buckets hold ~2.6 words on
   //    average: the 2..4-word ones take a 5-comparator network in place;
@@ -452,7 +453,6 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
       }
     }
     block_minmax(mn, mx, red64);
-    load(q + gridDim.x, nxt);   // the next row's loads fly under this row's sort
     auto each = [&](auto f, int k) {
 #pragma unroll
       for (int u = 0; u < kSortU; ++u) {
@@ -460,7 +460,11 @@ argsort_rows_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_t ld
         if (i < G && u % k == 0) f(word_of(cur[u], i));
       }
     };
-    sort_core(each, G, mn << 32, (mx << 32) | (u64)(G - 1), pk, cb, off, red PROBE_ARGS);
+    // the next row's loads fly under this row's bucket sort, issued once
+    // this row's values are scattered: the two never hold registers at once
+    // (the kernel is at the 128-VGPR cap of 16 waves per CU)
+    sort_core(each, G, mn << 32, (mx << 32) | (u64)(G - 1), pk, cb, off, red,
+              [&] { load(q + gridDim.x, nxt); } PROBE_ARGS);
     // the sorted row out, coalesced
     int32_t* orow = idx + q * ldi;
     float* vrow = vals ? vals + q * ldv : nullptr;
@@ -646,7 +650,7 @@ argsort_rows_big_kernel(const float* __restrict__ dist, int64_t Q, int G, int64_
       auto each = [&](auto f, int k) {
         for (int i = t; i < n; i += kT * k) f(src[i]);
       };
-      sort_core(each, n, mn, mx, dst, cb, off, red PROBE_ARGS);
+      sort_core(each, n, mn, mx, dst, cb, off, red, [] {} PROBE_ARGS);
       int32_t* orow = idx + q * ldi + out0;
       float* vrow = vals ? vals + q * ldv + out0 : nullptr;
       for (int p = t; p < n; p += kT) {
